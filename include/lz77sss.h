@@ -1,0 +1,134 @@
+/*
+ * lz77sss.h -- C-ABI of liblz77sss_hip.so, the MI355X-native LZ77-SSS engine.
+ *
+ * This is the drop-in boundary for the reference's approximate-factorization
+ * path.  Each entry point names the reference interface it replaces
+ * (paths relative to LukasNalbach/lz77-sss):
+ *
+ *   lz77sss_factorize_approx_u32  <- lz77_sss<uint32_t>::factorize_approximate
+ *                                    <fact_mode, phr_mode, tau>(input, n, output, params)
+ *                                    include/lz77_sss/lz77_sss.hpp:176-186
+ *   lz77sss_decode_u32            <- lz77_sss<uint32_t>::decode(fact_it, out_it, n)
+ *                                    include/lz77_sss/lz77_sss.hpp:202-203,
+ *                                    include/lz77_sss/algorithms/common.cpp:31-54
+ *   lz77sss_factor32              <- lz77_sss<uint32_t>::factor {src, len}
+ *                                    include/lz77_sss/lz77_sss.hpp:129-147 (8-byte layout;
+ *                                    literal <=> len == 0, src = (uint8_t)char)
+ *   lz77sss_params                <- struct parameters {num_threads, log}
+ *                                    include/lz77_sss/lz77_sss.hpp:67-70, plus the knobs the
+ *                                    reference leaves to std::random_device / malloc_count
+ *
+ * The session API keeps the text resident in HBM (bench / repeated calls);
+ * the one-shot API uploads, factorizes and streams factors to a callback in
+ * text order, batched, on the calling thread (the reference calls `output`
+ * once per factor on the calling thread: greedy.cpp:91,127).
+ *
+ * Errors: every function returns 0 on success or a negative LZ77SSS_E* code
+ * and never throws across the ABI; lz77sss_last_error() gives a message.
+ * There is no CPU fallback: without a usable gfx950 device every compute
+ * entry point fails with LZ77SSS_ENODEV.
+ */
+#ifndef LZ77SSS_H
+#define LZ77SSS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* enum phrase_mode, lz77_sss.hpp:48-53 (same numeric values) */
+enum { LZ77SSS_LPF_NAIVE = 0, LZ77SSS_LPF_LNF_NAIVE = 1, LZ77SSS_LPF_OPT = 2, LZ77SSS_LPF_LNF_OPT = 3 };
+/* enum factorize_mode, lz77_sss.hpp:55-59 (same numeric values) */
+enum { LZ77SSS_GREEDY_NAIVE = 0, LZ77SSS_GREEDY = 1, LZ77SSS_SKIP_PHRASES = 2 };
+
+enum {
+    LZ77SSS_OK = 0,
+    LZ77SSS_EINVAL = -1,      /* bad argument (unsupported mode, tau, n too large for pos_t) */
+    LZ77SSS_ENODEV = -2,      /* no HIP device / HIP runtime error at init */
+    LZ77SSS_EHIP = -3,        /* HIP runtime error during a launch / copy */
+    LZ77SSS_ENOMEM = -4,      /* device or host allocation failed */
+    LZ77SSS_ECALLBACK = -5,   /* the emit callback returned non-zero (output aborted) */
+    LZ77SSS_EINTERNAL = -6    /* internal consistency check failed */
+};
+
+typedef struct { uint32_t src; uint32_t len; } lz77sss_factor32;
+
+typedef struct {
+    int32_t phr_mode;        /* default LZ77SSS_LPF_OPT, lz77_sss.hpp:77 */
+    int32_t fact_mode;       /* default LZ77SSS_GREEDY, lz77_sss.hpp:78 */
+    uint32_t tau;            /* default 512, lz77_sss.hpp:82 (only 512 is supported) */
+    uint32_t rk_seed;        /* seeds the 5 gap-index rk_prime<107> bases (replaces the
+                                std::random_device of rolling_hash.hpp:127-130) */
+    int32_t index_log2_size; /* 0 = the reference formula with malloc_count == 0
+                                (lz77_sss.hpp:117-122, rolling_hash_index_107.hpp:59-70) */
+    int32_t device;          /* HIP device ordinal */
+    int32_t log;             /* parameters::log: print per-phase times to stderr */
+    uint16_t num_threads;    /* parameters::num_threads; accepted for API parity -- the
+                                output is always the p = 1 factorization */
+} lz77sss_params;
+
+/* Fills defaults (the reference's template defaults + rk_seed = 42). */
+void lz77sss_default_params(lz77sss_params* prm);
+
+/* Batched, in-order factor sink.  Return 0 to continue, non-zero to abort. */
+typedef int (*lz77sss_emit_fn)(const lz77sss_factor32* batch, uint64_t count, void* user);
+
+/* One-shot: factorize text[0..n) (host memory).  LPF/LNF modes do NOT modify
+ * `text` (the reference reverses the caller's buffer in place and restores
+ * it, lz77_sss.hpp:385-393; here the reversal happens in HBM).  No padding
+ * past n is required. */
+int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
+                                 lz77sss_emit_fn emit, void* user);
+
+/* Decode nf factors into out[0..n) (host memory), algorithms/common.cpp:31-54. */
+int lz77sss_decode_u32(const lz77sss_factor32* factors, uint64_t nf, uint8_t* out, uint64_t n);
+
+/* ---- device-resident session (text stays in HBM across calls) ---- */
+typedef struct lz77sss_session lz77sss_session;
+
+/* Creates a session on `device` able to hold texts of up to max_n bytes. */
+int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out);
+/* Copies text[0..n) host -> HBM (not part of the timed factorization). */
+int lz77sss_session_load(lz77sss_session* s, const uint8_t* text, uint64_t n);
+/* Factorizes the loaded text; factors stay in HBM. */
+int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_params* prm, uint64_t* num_factors);
+/* Copies the factors HBM -> host (cap >= num_factors). */
+int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32* out, uint64_t cap);
+/* Runs only the string-synchronizing-set pass (kernel 1) on the loaded text. */
+int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs);
+/* Copies the sync set of the last sss/factorize call HBM -> host. */
+int lz77sss_session_get_sss(lz77sss_session* s, uint32_t* out, uint64_t cap);
+/* Copies SA_S / LCP_S (suffix order of the sync positions) of the last call. */
+int lz77sss_session_get_sa_s(lz77sss_session* s, uint32_t* sa, uint32_t* lcp, uint64_t cap);
+/* Copies the LPF phrase list (beg,end,src triples) of the last factorize call. */
+int lz77sss_session_get_lpf(lz77sss_session* s, uint32_t* out3, uint64_t cap, uint64_t* count);
+/* Per-phase times (ms, hipEvent-timed) of the last call; returns the count. */
+int lz77sss_session_phase_times(lz77sss_session* s, double* ms, const char** names, int cap);
+/* Statistics of the last factorize call: [size_sss, has_runs, num_lpf, len_lpf_phr,
+ * num_gaps, patt_lens[5], roll_threshold, log2_size_h, greedy_rounds, fixups, ...]. */
+int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap);
+void lz77sss_session_destroy(lz77sss_session* s);
+
+/* Average duration (ms) of the dominant kernel (SSS main pass) over the
+ * last call, measured with hipEvents on its own stream; bytes = algorithmic
+ * bytes of that launch (n + 4|S|). */
+int lz77sss_session_sss_kernel_time(lz77sss_session* s, double* ms, uint64_t* bytes);
+
+/* ---- synthetic inputs (tests / bench) ---- */
+/* random_repetitive_string (utils.hpp:579-640) with a seed instead of
+ * std::random_device; knobs < 0 are drawn as in the reference. */
+int64_t lz77sss_gen_random_repetitive(uint32_t min_size, uint32_t max_size, uint32_t seed,
+                                      double rep_knob, double run_knob, uint8_t* out, uint64_t cap);
+/* chr19-style: random ACGT base block repeated with point mutations. */
+int64_t lz77sss_gen_genome(uint64_t n, uint64_t base_len, double mut_rate, uint32_t seed, uint8_t* out);
+
+const char* lz77sss_last_error(void);
+/* Number of visible HIP devices (0 if none); does not create a context. */
+int lz77sss_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LZ77SSS_H */

@@ -1,0 +1,315 @@
+// engine.hip -- session lifetime, phase orchestration and the C-ABI
+// (include/lz77sss.h).  The orchestration mirrors
+// factorizer::factorize / compute_approximation (include/lz77_sss/lz77_sss.hpp:285-491)
+// for fact_mode = greedy, phr_mode = lpf_opt, p = 1.
+#include "../../include/lz77sss.h"
+#include "../include/engine.h"
+
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+namespace lz {
+
+void engine::init(int dev, u64 maxn) {
+    device = dev;
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) throw error(LZ77SSS_ENODEV, "no HIP device available");
+    if (dev < 0 || dev >= cnt) throw error(LZ77SSS_EINVAL, "invalid device ordinal");
+    LZ_HIP(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    LZ_HIP(hipGetDeviceProperties(&prop, dev));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        throw error(LZ77SSS_ENODEV, std::string("device is not gfx950: ") + prop.gcnArchName);
+    LZ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    max_n = maxn;
+    LZ_HIP(hipMalloc(&d_text, max_n + TEXT_PAD));
+    LZ_HIP(hipMemsetAsync(d_text, 0, max_n + TEXT_PAD, st));
+    LZ_HIP(hipStreamSynchronize(st));
+}
+
+void engine::load(const u8* h_text, u64 n_) {
+    if (n_ > max_n) throw error(LZ77SSS_EINVAL, "text larger than the session capacity");
+    LZ_HIP(hipSetDevice(device));
+    n = n_;
+    if (n) LZ_HIP(hipMemcpyAsync(d_text, h_text, n, hipMemcpyHostToDevice, st));
+    LZ_HIP(hipMemsetAsync(d_text + n, 0, TEXT_PAD, st));
+    LZ_HIP(hipStreamSynchronize(st));
+}
+
+void engine::destroy() {
+    if (d_text) (void)hipFree(d_text);
+    if (d_text_rev) (void)hipFree(d_text_rev);
+    d_text = d_text_rev = nullptr;
+    if (st) (void)hipStreamDestroy(st);
+    st = nullptr;
+}
+
+u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log) {
+    LZ_HIP(hipSetDevice(device));
+    if (phr_mode != LZ77SSS_LPF_OPT) throw error(LZ77SSS_EINVAL, "unsupported phrase mode (lpf_opt only)");
+    if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
+    num_fact = 0;
+    stats.assign(24, 0);
+    if (n == 0) return 0;
+    timer.begin(st);
+    const bool dbg = debug_enabled();
+    auto trace = [&](const char* what) {
+        if (!dbg) return;
+        LZ_HIP(hipStreamSynchronize(st));
+        std::fprintf(stderr, "[lz77sss-debug] done %s (|S|=%u phrases=%u)\n", what, s, num_phr);
+    };
+    build_sss(d_text);
+    timer.mark("sss");
+    trace("sss");
+    build_sa_s(d_text);
+    timer.mark("sa_s");
+    trace("sa_s");
+    build_lcp_rmq(d_text);
+    timer.mark("lcp_rmq");
+    trace("lcp_rmq");
+    build_lpf_opt(d_text);
+    timer.mark("lpf");
+    trace("lpf");
+    num_fact = factorize_greedy(d_text, rk_seed, log2_override);
+    timer.mark("greedy");
+    trace("greedy");
+    LZ_HIP(hipStreamSynchronize(st));
+    if (log) {
+        for (auto& [name, ms] : timer.read()) std::fprintf(stderr, "[lz77sss] %-10s %9.3f ms\n", name.c_str(), ms);
+        std::fprintf(stderr, "[lz77sss] n=%llu |S|=%u phrases=%u factors=%llu outer=%llu rounds=%llu\n",
+                     (unsigned long long)n, s, num_phr, (unsigned long long)num_fact,
+                     (unsigned long long)stats[12], (unsigned long long)stats[13]);
+    }
+    return num_fact;
+}
+
+}  // namespace lz
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+struct lz77sss_session {
+    lz::engine E;
+};
+
+static thread_local std::string g_err;
+
+template <class F>
+static int guarded(F&& f) {
+    try {
+        f();
+        return LZ77SSS_OK;
+    } catch (const lz::error& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of memory";
+        return LZ77SSS_ENOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return LZ77SSS_EINTERNAL;
+    }
+}
+
+extern "C" {
+
+LZ77SSS_API const char* lz77sss_last_error(void) { return g_err.c_str(); }
+
+LZ77SSS_API int lz77sss_device_count(void) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+    return c;
+}
+
+LZ77SSS_API void lz77sss_default_params(lz77sss_params* prm) {
+    if (!prm) return;
+    std::memset(prm, 0, sizeof(*prm));
+    prm->phr_mode = LZ77SSS_LPF_OPT;
+    prm->fact_mode = LZ77SSS_GREEDY;
+    prm->tau = 512;
+    prm->rk_seed = 42;
+    prm->index_log2_size = 0;
+    prm->device = 0;
+    prm->log = 0;
+    prm->num_threads = 0;
+}
+
+static void check_params(const lz77sss_params* prm) {
+    if (!prm) throw lz::error(LZ77SSS_EINVAL, "params is NULL");
+    if (prm->tau != 512) throw lz::error(LZ77SSS_EINVAL, "only tau = 512 is supported");
+    if (prm->fact_mode != LZ77SSS_GREEDY) throw lz::error(LZ77SSS_EINVAL, "only fact_mode = greedy is supported");
+    if (prm->phr_mode != LZ77SSS_LPF_OPT) throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
+    if (prm->index_log2_size < 0 || prm->index_log2_size > 30) throw lz::error(LZ77SSS_EINVAL, "bad index_log2_size");
+}
+
+LZ77SSS_API int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out) {
+    if (!out) return LZ77SSS_EINVAL;
+    *out = nullptr;
+    lz77sss_session* s = new (std::nothrow) lz77sss_session();
+    if (!s) return LZ77SSS_ENOMEM;
+    int rc = guarded([&] { s->E.init(device, max_n); });
+    if (rc) {
+        s->E.destroy();
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return LZ77SSS_OK;
+}
+
+LZ77SSS_API int lz77sss_session_load(lz77sss_session* s, const uint8_t* text, uint64_t n) {
+    if (!s || (!text && n)) return LZ77SSS_EINVAL;
+    return guarded([&] { s->E.load(text, n); });
+}
+
+LZ77SSS_API int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_params* prm, uint64_t* num_factors) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        check_params(prm);
+        uint64_t z = s->E.factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0);
+        if (num_factors) *num_factors = z;
+    });
+}
+
+LZ77SSS_API int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32* out, uint64_t cap) {
+    if (!s || (!out && s->E.num_fact)) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (cap < s->E.num_fact) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (s->E.num_fact)
+            LZ_HIP(hipMemcpy(out, s->E.fact.p, s->E.num_fact * sizeof(lz77sss_factor32), hipMemcpyDeviceToHost));
+    });
+}
+
+LZ77SSS_API int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        LZ_HIP(hipSetDevice(s->E.device));
+        s->E.build_sss(s->E.d_text);
+        LZ_HIP(hipStreamSynchronize(s->E.st));
+        if (size_sss) *size_sss = s->E.s;
+        if (has_runs) *has_runs = s->E.has_runs;
+    });
+}
+
+LZ77SSS_API int lz77sss_session_get_sss(lz77sss_session* s, uint32_t* out, uint64_t cap) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (cap < s->E.s) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (s->E.s) LZ_HIP(hipMemcpy(out, s->E.S.p, (size_t)s->E.s * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+LZ77SSS_API int lz77sss_session_get_sa_s(lz77sss_session* s, uint32_t* sa, uint32_t* lcp, uint64_t cap) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (cap < s->E.s) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (!s->E.s) return;
+        if (sa) LZ_HIP(hipMemcpy(sa, s->E.SA.p, (size_t)s->E.s * 4, hipMemcpyDeviceToHost));
+        if (lcp) LZ_HIP(hipMemcpy(lcp, s->E.lcp_rmq[0].p, (size_t)s->E.s * 4, hipMemcpyDeviceToHost));
+    });
+}
+
+LZ77SSS_API int lz77sss_session_get_lpf(lz77sss_session* s, uint32_t* out3, uint64_t cap, uint64_t* count) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (count) *count = s->E.num_phr;
+        if (!out3) return;
+        if (cap < s->E.num_phr) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (s->E.num_phr) LZ_HIP(hipMemcpy(out3, s->E.lpf.p, (size_t)s->E.num_phr * 12, hipMemcpyDeviceToHost));
+    });
+}
+
+LZ77SSS_API int lz77sss_session_phase_times(lz77sss_session* s, double* ms, const char** names, int cap) {
+    if (!s) return LZ77SSS_EINVAL;
+    int k = 0;
+    int rc = guarded([&] {
+        static thread_local std::vector<std::string> keep;
+        auto v = s->E.timer.read();
+        keep.clear();
+        for (auto& x : v) keep.push_back(x.first);
+        for (auto& x : v) {
+            if (k >= cap) break;
+            if (ms) ms[k] = x.second;
+            if (names) names[k] = keep[k].c_str();
+            k++;
+        }
+    });
+    return rc ? rc : k;
+}
+
+LZ77SSS_API int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap) {
+    if (!s || !out) return LZ77SSS_EINVAL;
+    int k = 0;
+    for (; k < cap && k < (int)s->E.stats.size(); k++) out[k] = s->E.stats[k];
+    return k;
+}
+
+LZ77SSS_API int lz77sss_session_sss_kernel_time(lz77sss_session* s, double* ms, uint64_t* bytes) {
+    if (!s) return LZ77SSS_EINVAL;
+    if (ms) *ms = s->E.sss_kernel_ms;
+    if (bytes) *bytes = s->E.n + 4ull * s->E.s;
+    return LZ77SSS_OK;
+}
+
+LZ77SSS_API void lz77sss_session_destroy(lz77sss_session* s) {
+    if (!s) return;
+    s->E.destroy();
+    delete s;
+}
+
+LZ77SSS_API int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
+                                             lz77sss_emit_fn emit, void* user) {
+    if ((!text && n) || !emit) return LZ77SSS_EINVAL;
+    lz77sss_session* s = nullptr;
+    int rc = guarded([&] { check_params(prm); });
+    if (rc) return rc;
+    rc = lz77sss_session_create(prm->device, n, &s);
+    if (rc) return rc;
+    rc = lz77sss_session_load(s, text, n);
+    uint64_t z = 0;
+    if (!rc) rc = lz77sss_session_factorize(s, prm, &z);
+    if (!rc && z) {
+        std::vector<lz77sss_factor32> buf;
+        rc = guarded([&] {
+            buf.resize(z);
+            LZ_HIP(hipMemcpy(buf.data(), s->E.fact.p, z * sizeof(lz77sss_factor32), hipMemcpyDeviceToHost));
+        });
+        const uint64_t B = 1 << 16;
+        for (uint64_t o = 0; !rc && o < z; o += B) {
+            if (emit(buf.data() + o, std::min(B, z - o), user) != 0) {
+                g_err = "emit callback aborted";
+                rc = LZ77SSS_ECALLBACK;
+            }
+        }
+    }
+    lz77sss_session_destroy(s);
+    return rc;
+}
+
+// decode: algorithms/common.cpp:31-54 (sequential; forward byte copy allows overlap)
+LZ77SSS_API int lz77sss_decode_u32(const lz77sss_factor32* f, uint64_t nf, uint8_t* out, uint64_t n) {
+    if ((!f && nf) || (!out && n)) return LZ77SSS_EINVAL;
+    uint64_t pos = 0, k = 0;
+    while (pos < n && k < nf) {
+        const lz77sss_factor32 x = f[k++];
+        if (x.len == 0) {
+            out[pos++] = (uint8_t)x.src;
+        } else {
+            if ((uint64_t)x.src >= pos || pos + x.len > n) {
+                g_err = "invalid factor during decode";
+                return LZ77SSS_EINVAL;
+            }
+            for (uint32_t i = 0; i < x.len; i++) out[pos + i] = out[x.src + i];
+            pos += x.len;
+        }
+    }
+    if (pos != n) {
+        g_err = "factors do not cover the output length";
+        return LZ77SSS_EINVAL;
+    }
+    return LZ77SSS_OK;
+}
+
+}  // extern "C"

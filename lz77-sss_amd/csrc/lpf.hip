@@ -1,0 +1,253 @@
+// lpf.hip -- LPF candidate phrases at sync positions (build_LPF_opt,
+// include/lz77_sss/algorithms/approximate/lpf_lnf/lpf_opt.cpp:33-157, p = 1)
+// and the phrase statistics (get_phrase_info, approximate/common.cpp:98-157).
+//
+//  1. PSV/NSV over SA_S (nxv_pxv.cpp:33-92) by descending a min sparse table
+//     over SA_S (the reference uses a sequential stack).
+//  2. Per sync index i, both candidates (source, end = S[i] + LCE_R, and the
+//     left extension LCE_L up to the largest cap the sequential loop could
+//     ever apply: S[i]-S[i-1]).
+//  3. The loop's skip chain (lpf_opt.cpp:61-63) is a linked list: the next
+//     processed index after i depends only on E_i = max candidate end, so the
+//     processed set is the path from index 0, found by pointer doubling; the
+//     running max_end is an exclusive max-scan of E over that path.
+//  4. Phrases are then formed independently per processed index and compacted
+//     in text order.
+#include "../include/engine.h"
+#include "../include/lce_dev.h"
+
+#include <hipcub/hipcub.hpp>
+
+namespace lz {
+
+__global__ void k_sa_min_level(const u32* __restrict__ prev, u32 cnt, u32 half, u32* __restrict__ out) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < cnt) out[k] = min(prev[k], prev[k + half]);
+}
+
+struct sa_min_levels {
+    u32 nlev;
+    const u32* L[MAX_LV];
+};
+
+// PSV[r] = max r' < r with SA[r'] < SA[r] (or s); NSV[r] = min r' > r with SA[r'] < SA[r] (or s)
+__global__ void k_psv_nsv(const u32* __restrict__ SA, u32 s, sa_min_levels M, u32* __restrict__ PSV,
+                          u32* __restrict__ NSV) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= s) return;
+    const u32 v = SA[r];
+    u64 pos = r;
+    for (int lv = (int)M.nlev - 1; lv >= 0; lv--) {
+        const u64 w = 1ull << lv;
+        if (pos >= w && M.L[lv][pos - w] > v) pos -= w;
+    }
+    PSV[r] = pos == 0 ? s : (u32)(pos - 1);
+    pos = r + 1;
+    for (int lv = (int)M.nlev - 1; lv >= 0; lv--) {
+        const u64 w = 1ull << lv;
+        if (pos + w <= s && M.L[lv][pos] > v) pos += w;
+    }
+    NSV[r] = pos >= s ? s : (u32)pos;
+}
+
+// candidate record per sync index: [srcP, endP, lP, srcN, endN, lN, hasP|hasN<<1, E]
+constexpr int CREC = 8;
+
+__global__ void k_lpf_candidates(lce_view L, const u32* __restrict__ SA, const u32* __restrict__ PSV,
+                                 const u32* __restrict__ NSV, u32* __restrict__ cand) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 s = L.s;
+    if (i >= s) return;
+    const u32* S = L.S;
+    const u32 r = L.ISA[i];
+    const u32 Si = S[i];
+    const u32 capmax = i >= 2 ? Si - S[i - 1] : Si;
+    u32 rec[CREC] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u32 E = 0;
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+        const u32 nb = side == 0 ? PSV[r] : NSV[r];
+        if (nb == s) continue;
+        const u32 src = S[SA[nb]];
+        const u32 end = Si + (u32)dev_lce(L, src, Si);
+        u32 l = 0;
+        if (src != 0 && Si != 0) l = dev_lce_left(L.T, src - 1, Si - 1, capmax);
+        rec[side * 3 + 0] = src;
+        rec[side * 3 + 1] = end;
+        rec[side * 3 + 2] = l;
+        rec[6] |= 1u << side;
+        E = max(E, end);
+    }
+    rec[7] = E;
+#pragma unroll
+    for (int x = 0; x < CREC; x++) cand[i * CREC + x] = rec[x];
+}
+
+// next processed index after i (lpf_opt.cpp:61-63): max(i+1, last k: S[k] <= E_i)
+__global__ void k_next(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand, u32* __restrict__ nxt) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > s) return;
+    if (i == s) { nxt[s] = s; return; }
+    const u32 E = cand[i * CREC + 7];
+    u32 nx = (u32)i + 1;
+    if (i + 1 < s && S[i + 1] <= E) {
+        u32 lo = (u32)i + 1, hi = s;  // last k with S[k] <= E: first k with S[k] > E, minus 1
+        while (lo < hi) {
+            u32 mid = (lo + hi) >> 1;
+            if (S[mid] <= E) lo = mid + 1; else hi = mid;
+        }
+        nx = lo - 1;
+        if (nx < i + 1) nx = (u32)i + 1;
+    }
+    nxt[i] = nx;
+}
+__global__ void k_jump(const u32* __restrict__ prev, u32 m, u32* __restrict__ out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[i] = prev[prev[i]];
+}
+// top-down path expansion: out[2m] = C[m], out[2m+1] = J[C[m]]
+__global__ void k_expand(const u32* __restrict__ C, u32 cnt, const u32* __restrict__ J, u32* __restrict__ out) {
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= cnt) return;
+    const u32 c = C[m];
+    out[2 * m] = c;
+    out[2 * m + 1] = J[c];
+}
+__global__ void k_mark(const u32* __restrict__ C, u32 cnt, u32 s, u32* __restrict__ mark) {
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < cnt && C[m] < s) mark[C[m]] = 1;
+}
+__global__ void k_masked_E(const u32* __restrict__ cand, const u32* __restrict__ mark, u32 s, u32* __restrict__ Em) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < s) Em[i] = mark[i] ? cand[i * CREC + 7] : 0u;
+}
+
+// phrase of a processed index given lst_end (lpf_opt.cpp:65-144)
+__global__ void k_phrase(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand, const u32* __restrict__ mark,
+                         const u32* __restrict__ lst, u32* __restrict__ ph, u32* __restrict__ push) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= s) return;
+    u32 pu = 0;
+    u32 pb = 0, pe = 0, ps = 0;
+    if (mark[i]) {
+        const u32* c = cand + i * CREC;
+        const u32 lst_end = lst[i];
+        const u32 Si = S[i];
+        const u32 has = c[6];
+        for (int side = 0; side < 2; side++) {
+            if (!(has >> side & 1)) continue;
+            u32 src = c[side * 3 + 0];
+            const u32 end = c[side * 3 + 1];
+            if (end > lst_end) {
+                u32 beg = Si;
+                if (Si > lst_end && src != 0 && Si != 0) {
+                    const u32 l = min(c[side * 3 + 2], Si - lst_end);
+                    beg -= l;
+                    src -= l;
+                }
+                if (beg < lst_end) {
+                    const u32 exc = lst_end - beg;
+                    beg += exc;
+                    src += exc;
+                }
+                if (side == 0) {
+                    if (end - beg > 1) { pb = beg; pe = end; ps = src; }
+                } else {
+                    if (end - beg > pe - pb) { pb = beg; pe = end; ps = src; }
+                }
+            }
+            if (side == 1 && pe - pb > 1) pu = 1;  // pushed only in the NSV branch (lpf_opt.cpp:138-140)
+        }
+    }
+    ph[i * 3 + 0] = pb;
+    ph[i * 3 + 1] = pe;
+    ph[i * 3 + 2] = ps;
+    push[i] = pu;
+}
+__global__ void k_compact3(const u32* __restrict__ ph, const u32* __restrict__ push, const u32* __restrict__ off,
+                           u32 s, u32* __restrict__ out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= s || !push[i]) return;
+    const u32 o = off[i];
+    out[o * 3 + 0] = ph[i * 3 + 0];
+    out[o * 3 + 1] = ph[i * 3 + 1];
+    out[o * 3 + 2] = ph[i * 3 + 2];
+}
+
+struct max_op {
+    __device__ u32 operator()(const u32& a, const u32& b) const { return a > b ? a : b; }
+};
+
+void engine::build_lpf_opt(const u8* T) {
+    num_phr = 0;
+    if (s == 0) return;
+    const unsigned g = cdiv(s, 256);
+    // 1. PSV/NSV
+    u32 nl = 0;
+    {
+        sa_min_levels M{};
+        M.L[0] = SA.p;
+        nl = 1;
+        for (u32 lv = 1; (1ull << lv) <= s; lv++) {
+            const u32 cnt = s - (1u << lv) + 1;
+            u32* out = sa_min[lv].get(cnt);
+            k_sa_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(lv == 1 ? SA.p : sa_min[lv - 1].p, cnt, 1u << (lv - 1), out);
+            M.L[lv] = out;
+            nl = lv + 1;
+        }
+        M.nlev = nl;
+        k_psv_nsv<<<g, 256, 0, st>>>(SA.p, s, M, PSV.get(s), NSV.get(s));
+    }
+    // 2. candidates
+    u32* cd = cand.get((u64)s * CREC);
+    k_lpf_candidates<<<g, 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, cd);
+    // 3. skip chain: pointer doubling over next[], nodes 0..s (s = end)
+    const u32 m = s + 1;
+    u32 T_lv = 0;
+    while ((1ull << T_lv) < m) T_lv++;
+    k_next<<<cdiv(m, 256), 256, 0, st>>>(S.p, s, cd, jump[0].get(m));
+    for (u32 t = 1; t <= T_lv; t++) k_jump<<<cdiv(m, 256), 256, 0, st>>>(jump[t - 1].p, m, jump[t].get(m));
+    u32* C = u32a.get(2ull << T_lv);
+    u32* C2 = u32b.get(2ull << T_lv);
+    u32 zero = 0;
+    LZ_HIP(hipMemcpyAsync(C, &zero, 4, hipMemcpyHostToDevice, st));
+    u32 cnt = 1;
+    for (int t = (int)T_lv - 1; t >= 0; t--) {
+        k_expand<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, jump[t].p, C2);
+        std::swap(C, C2);
+        cnt *= 2;
+    }
+    u32* mark = u32c.get(s);
+    LZ_HIP(hipMemsetAsync(mark, 0, (size_t)s * 4, st));
+    k_mark<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, s, mark);
+    // running max_end before each processed index
+    u32* Em = u32d.get(s);
+    k_masked_E<<<g, 256, 0, st>>>(cd, mark, s, Em);
+    u32* lst = (C == u32a.p) ? u32b.p : u32a.p;  // reuse the free expansion buffer (>= s entries)
+    {
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, Em, lst, max_op{}, 0u, (int)s, st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(t, tb, Em, lst, max_op{}, 0u, (int)s, st));
+    }
+    // 4. phrases + compaction
+    u32* ph = PSV.p;  // PSV/NSV no longer needed: reuse as scratch (3 words per index needs 3s)
+    u32* ph3 = u32e.get((u64)s * 3);
+    (void)ph;
+    u32* push = Em;
+    k_phrase<<<g, 256, 0, st>>>(S.p, s, cd, mark, lst, ph3, push);
+    u32* off = mark;  // mark no longer needed after k_phrase
+    {
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, push, off, (int)s, st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, push, off, (int)s, st));
+    }
+    const u32 last_off = rd1(off + s - 1, st), last_push = rd1(push + s - 1, st);
+    num_phr = last_off + last_push;
+    u32* out = lpf.get((u64)(num_phr + 1) * 3);
+    k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);
+    LZ_HIP(hipGetLastError());
+}
+
+}  // namespace lz

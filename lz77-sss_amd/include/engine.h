@@ -1,0 +1,134 @@
+// engine.h -- the device-resident LZ77-SSS engine (one per session / GPU).
+// Data layout in HBM is documented in DESIGN.md section 5.
+#pragma once
+#include "lz77sss_internal.h"
+#include "lce_dev.h"
+
+#include <array>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace lz {
+
+struct lpf3 { u32 beg, end, src; };
+
+// greedy walk segments (csrc/greedy.hip)
+struct seg_in { u32 start, p, idxpos, zmask; };
+struct seg_out {
+    u32 next;        // start of the next gap (or n)
+    u32 e;           // end of this segment's gap walk (positions [start, e) inserted)
+    u32 nfact;
+    u32 idxpos;      // gap index position after the segment
+    u32 zmask;
+    u32 nsingle;     // extra inserted positions (LPF-start queries)
+    u32 single[4];
+    u32 flags;       // 1: reached the tail region, 2: single overflow
+};
+
+struct phase_timer {
+    hipStream_t st = nullptr;
+    std::vector<std::pair<std::string, hipEvent_t>> marks;
+    bool on = false;
+    void begin(hipStream_t s) {
+        st = s;
+        clear();
+        mark("start");
+    }
+    void mark(const char* name) {
+        hipEvent_t e;
+        LZ_HIP(hipEventCreate(&e));
+        LZ_HIP(hipEventRecord(e, st));
+        marks.emplace_back(name, e);
+    }
+    void clear() {
+        for (auto& m : marks) (void)hipEventDestroy(m.second);
+        marks.clear();
+    }
+    // (name, ms since previous mark)
+    std::vector<std::pair<std::string, double>> read() {
+        std::vector<std::pair<std::string, double>> out;
+        if (marks.empty()) return out;
+        LZ_HIP(hipEventSynchronize(marks.back().second));
+        for (size_t i = 1; i < marks.size(); i++) {
+            float ms = 0;
+            LZ_HIP(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));
+            out.emplace_back(marks[i].first, ms);
+        }
+        return out;
+    }
+    ~phase_timer() { clear(); }
+};
+
+struct engine {
+    int device = 0;
+    hipStream_t st = nullptr;
+    u64 max_n = 0, n = 0;
+    u8* d_text = nullptr;  // n + TEXT_PAD bytes (zero padded)
+    u8* d_text_rev = nullptr;  // reversed copy for LPF/LNF modes (lazily allocated)
+
+    // ---- string synchronizing set ----
+    dbuf<u16> q_info;          // per anchor: Q interval (start<<8 | end) of (a-128, a]
+    dbuf<u32> lane_out, lane_cnt, lane_flag;
+    dbuf<u32> S;               // sync positions (sorted)
+    dbuf<u32> counters;        // small scratch counters
+    u32 s = 0;
+    bool has_runs = false;
+    double sss_kernel_ms = 0;  // dominant kernel (SSS main pass) duration
+    u64 stats_fallback_lanes = 0;
+
+    // ---- suffix order of sync positions / LCE ----
+    dbuf<u32> SA, ISA, LCP, key_len;
+    dbuf<u32> rank_lv[MAX_LV];       // R_h per doubling level (for LCP binary lifting)
+    dbuf<u32> lcp_rmq[MAX_LV];       // sparse table levels over LCP
+    u32 nlev_rank = 0, nlev_rmq = 0;
+    dbuf<u32> succ_tab;              // bucket -> first sync index with S >= bucket*512
+    dbuf<u8> tmp_bytes, scan_tmp;
+    dbuf<u64> u64a, u64b;
+    dbuf<u32> u32a, u32b, u32c, u32d, u32e;
+
+    // ---- LPF phrases ----
+    dbuf<u32> sa_min[MAX_LV];        // sparse table over SA (PSV/NSV)
+    dbuf<u32> jump[MAX_LV];          // pointer-doubling tables (skip chain)
+    dbuf<u32> PSV, NSV;
+    dbuf<u32> cand;                  // per sync index candidate data
+    dbuf<u32> lpf;                   // phrases as (beg,end,src) triples + sentinel
+    u32 num_phr = 0;
+
+    // ---- greedy ----
+    dbuf<u32> fact;                  // output factors (src,len) pairs
+    dbuf<u8> tmp_greedy, chunk_buf;
+    dbuf<seg_in> seg_in_buf;
+    dbuf<seg_out> seg_out_buf;
+    dbuf<u32> seg_ids, ist, iend, irank, ekeys, evals, ekeys2, evals2, ipos_buf, occ_buf, tail_ins_buf;
+    dbuf<u64> seg_offs, counters64;
+    u64 num_fact = 0;
+    std::vector<u64> stats;
+
+    phase_timer timer;
+
+    void init(int dev, u64 maxn);
+    void load(const u8* h_text, u64 n_);
+    void destroy();
+
+    // pipeline phases (each enqueues on `st`)
+    void build_sss(const u8* T);
+    void build_sa_s(const u8* T);
+    void build_lcp_rmq(const u8* T);
+    void build_lpf_opt(const u8* T);
+    u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override);
+    u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log);
+    lce_view view(const u8* T) const;
+};
+
+// small host helpers
+template <class T>
+static inline T rd1(const T* dptr, hipStream_t st) {
+    T v;
+    LZ_HIP(hipMemcpyAsync(&v, dptr, sizeof(T), hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    return v;
+}
+static inline unsigned cdiv(u64 a, u64 b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace lz

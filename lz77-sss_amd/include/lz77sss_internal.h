@@ -1,0 +1,113 @@
+// Internal declarations shared by the host/device sources of liblz77sss_hip.so.
+#pragma once
+#define LZ77SSS_API __attribute__((visibility("default")))
+
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace lz {
+
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+using u128 = unsigned __int128;
+
+constexpr u32 TAU = 512;
+constexpr u32 QL = TAU / 3;  // period bound of Q (170)
+constexpr u32 QM = 2 * QL;   // anchor probe length (340)
+constexpr u32 QA = 128;      // anchor stride
+constexpr u64 P61 = (1ull << 61) - 1;
+constexpr u64 SSS_BASE = 296819;
+constexpr u64 INF64 = ~0ull;
+constexpr u32 NONE = 0xFFFFFFFFu;
+// zero bytes allocated past n in the HBM text buffer: lets vector loads and
+// the SSS lane streams run past the end without bounds checks
+constexpr u64 TEXT_PAD = 64 * 1024;
+
+inline bool debug_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("LZ77SSS_DEBUG");
+        v = (e && *e && *e != '0') ? 1 : 0;
+    }
+    return v == 1;
+}
+
+struct error : std::runtime_error {
+    int code;
+    error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define LZ_HIP(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess)                                                                      \
+            throw ::lz::error(-3, std::string(#x) + ": " + hipGetErrorString(e_) + " @" __FILE__ ":" \
+                                      + std::to_string(__LINE__));                                 \
+    } while (0)
+
+// grow-only device buffer
+template <class T>
+struct dbuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    dbuf() = default;
+    dbuf(const dbuf&) = delete;
+    dbuf& operator=(const dbuf&) = delete;
+    T* get(size_t n) {
+        if (n > cap) {
+            if (p) LZ_HIP(hipFree(p));
+            p = nullptr;
+            size_t c = std::max<size_t>(n, cap + cap / 4);
+            LZ_HIP(hipMalloc(&p, std::max<size_t>(c, 1) * sizeof(T)));
+            cap = c;
+        }
+        return p;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    ~dbuf() { release(); }
+};
+
+// ---------------------------------------------------------------------------
+// device helpers
+__device__ __forceinline__ u64 mod61_canon(u64 x) {  // x < 2^62
+    u64 c = (x & P61) + (x >> 61);
+    return c >= P61 ? c - P61 : c;
+}
+// unaligned 8-byte little-endian load from global memory
+__device__ __forceinline__ u64 ldu64(const u8* p) {
+    u64 a = (u64)(uintptr_t)p;
+    const u64* q = (const u64*)(a & ~7ull);
+    u32 sh = (u32)(a & 7) * 8;
+    u64 lo = q[0];
+    if (!sh) return lo;
+    u64 hi = q[1];
+    return (lo >> sh) | (hi << (64 - sh));
+}
+// forward LCE of T[a..] and T[b..], at most lim bytes (caller guarantees
+// a+lim, b+lim <= n + TEXT_PAD)
+__device__ __forceinline__ u64 dev_naive_lce(const u8* T, u64 a, u64 b, u64 lim) {
+    u64 k = 0;
+    while (k + 8 <= lim) {
+        u64 x = ldu64(T + a + k), y = ldu64(T + b + k);
+        if (x != y) return k + (__builtin_ctzll(x ^ y) >> 3);
+        k += 8;
+    }
+    while (k < lim && T[a + k] == T[b + k]) k++;
+    return k;
+}
+
+}  // namespace lz
+#endif

@@ -1,0 +1,229 @@
+"""Python mirror of the reference API over the C-ABI of liblz77sss_hip.so.
+
+Mirrors ``lz77_sss<uint32_t>`` (include/lz77_sss/lz77_sss.hpp:72-203 of
+LukasNalbach/lz77-sss):
+
+* ``factorize_approximate(text, fact_mode=GREEDY, phr_mode=LPF_OPT, ...)``
+  <- ``lz77_sss<>::factorize_approximate<fact_mode, phr_mode, tau>`` (:176-186)
+* ``decode(factors, n)`` <- ``lz77_sss<>::decode`` (:202-203, algorithms/common.cpp:31-54)
+* factors are an ``(z, 2)`` uint32 array of ``(src, len)`` = ``lz77_sss<>::factor``
+  (:129-147); a literal has ``len == 0`` and ``src`` = the byte.
+
+There is no CPU fallback: if the HIP library or a gfx950 device is missing,
+every compute call raises ``Lz77SssError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+LPF_NAIVE, LPF_LNF_NAIVE, LPF_OPT, LPF_LNF_OPT = 0, 1, 2, 3   # enum phrase_mode, lz77_sss.hpp:48-53
+GREEDY_NAIVE, GREEDY, SKIP_PHRASES = 0, 1, 2                 # enum factorize_mode, lz77_sss.hpp:55-59
+DEFAULT_TAU = 512
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("LZ77SSS_LIB", _HERE / "lib" / "liblz77sss_hip.so"))
+
+
+class Lz77SssError(RuntimeError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("phr_mode", ctypes.c_int32), ("fact_mode", ctypes.c_int32), ("tau", ctypes.c_uint32),
+                ("rk_seed", ctypes.c_uint32), ("index_log2_size", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("log", ctypes.c_int32), ("num_threads", ctypes.c_uint16)]
+
+
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+_SYMBOLS = {
+    # name: (restype, argtypes)
+    "lz77sss_default_params": (None, [ctypes.POINTER(Params)]),
+    "lz77sss_factorize_approx_u32": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), _P, _P]),
+    "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
+    "lz77sss_session_create": (ctypes.c_int, [ctypes.c_int, _U64, ctypes.POINTER(_P)]),
+    "lz77sss_session_load": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_factorize": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.POINTER(_U64)]),
+    "lz77sss_session_get_factors": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_sss": (ctypes.c_int, [_P, ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_int)]),
+    "lz77sss_session_get_sss": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_get_sa_s": (ctypes.c_int, [_P, _P, _P, _U64]),
+    "lz77sss_session_get_lpf": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    "lz77sss_session_phase_times": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "lz77sss_session_stats": (ctypes.c_int, [_P, _P, ctypes.c_int]),
+    "lz77sss_session_sss_kernel_time": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
+    "lz77sss_session_destroy": (None, [_P]),
+    "lz77sss_gen_random_repetitive": (ctypes.c_int64, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                       ctypes.c_double, ctypes.c_double, _P, _U64]),
+    "lz77sss_gen_genome": (ctypes.c_int64, [_U64, _U64, ctypes.c_double, ctypes.c_uint32, _P]),
+    "lz77sss_last_error": (ctypes.c_char_p, []),
+    "lz77sss_device_count": (ctypes.c_int, []),
+}
+
+_lib = None
+
+
+def load_library(path: Path | str | None = None):
+    """Loads liblz77sss_hip.so (raises Lz77SssError if it is missing)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise Lz77SssError(f"HIP library not built: {p} (run `make -C lz77-sss_amd`)")
+    lib = ctypes.CDLL(str(p))
+    for name, (res, args) in _SYMBOLS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load_library().lz77sss_last_error()
+        raise Lz77SssError(f"lz77sss error {rc}: {msg.decode() if msg else ''}")
+
+
+def _as_u8(text) -> np.ndarray:
+    if isinstance(text, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(text), dtype=np.uint8)
+    a = np.ascontiguousarray(text)
+    if a.dtype != np.uint8:
+        a = a.view(np.uint8)
+    return a
+
+
+def params(phr_mode=LPF_OPT, fact_mode=GREEDY, tau=DEFAULT_TAU, rk_seed=42, index_log2_size=0, device=0,
+           log=False, num_threads=0) -> Params:
+    p = Params()
+    load_library().lz77sss_default_params(ctypes.byref(p))
+    p.phr_mode, p.fact_mode, p.tau, p.rk_seed = phr_mode, fact_mode, tau, rk_seed
+    p.index_log2_size, p.device, p.log, p.num_threads = index_log2_size, device, int(log), num_threads
+    return p
+
+
+class Session:
+    """Device-resident session: the text stays in HBM across calls."""
+
+    def __init__(self, max_n: int, device: int = 0):
+        lib = load_library()
+        h = _P()
+        _check(lib.lz77sss_session_create(device, max_n, ctypes.byref(h)))
+        self._h = h
+        self.n = 0
+
+    def close(self):
+        if self._h:
+            load_library().lz77sss_session_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, text):
+        a = _as_u8(text)
+        _check(load_library().lz77sss_session_load(self._h, a.ctypes.data_as(_P), a.size))
+        self.n = a.size
+
+    def factorize(self, **kw) -> int:
+        p = params(**kw)
+        z = _U64()
+        _check(load_library().lz77sss_session_factorize(self._h, ctypes.byref(p), ctypes.byref(z)))
+        return z.value
+
+    def factors(self, z: int) -> np.ndarray:
+        out = np.empty((max(z, 1), 2), np.uint32)
+        _check(load_library().lz77sss_session_get_factors(self._h, out.ctypes.data_as(_P), z))
+        return out[:z]
+
+    def sss(self):
+        s, r = _U64(), ctypes.c_int()
+        _check(load_library().lz77sss_session_sss(self._h, ctypes.byref(s), ctypes.byref(r)))
+        out = np.empty(max(s.value, 1), np.uint32)
+        _check(load_library().lz77sss_session_get_sss(self._h, out.ctypes.data_as(_P), s.value))
+        return out[:s.value], bool(r.value)
+
+    def sync_set(self, s: int) -> np.ndarray:
+        out = np.empty(max(s, 1), np.uint32)
+        _check(load_library().lz77sss_session_get_sss(self._h, out.ctypes.data_as(_P), s))
+        return out[:s]
+
+    def sa_s(self, s: int):
+        sa, lcp = np.empty(max(s, 1), np.uint32), np.empty(max(s, 1), np.uint32)
+        _check(load_library().lz77sss_session_get_sa_s(self._h, sa.ctypes.data_as(_P), lcp.ctypes.data_as(_P), s))
+        return sa[:s], lcp[:s]
+
+    def lpf(self) -> np.ndarray:
+        c = _U64()
+        _check(load_library().lz77sss_session_get_lpf(self._h, None, 0, ctypes.byref(c)))
+        out = np.empty((max(c.value, 1), 3), np.uint32)
+        _check(load_library().lz77sss_session_get_lpf(self._h, out.ctypes.data_as(_P), c.value, ctypes.byref(c)))
+        return out[:c.value]
+
+    def stats(self) -> list[int]:
+        out = np.zeros(24, np.uint64)
+        k = load_library().lz77sss_session_stats(self._h, out.ctypes.data_as(_P), 24)
+        return [int(x) for x in out[:max(k, 0)]]
+
+    def phase_times(self) -> dict[str, float]:
+        ms = (ctypes.c_double * 32)()
+        names = (ctypes.c_char_p * 32)()
+        k = load_library().lz77sss_session_phase_times(self._h, ms, names, 32)
+        if k < 0:
+            _check(k)
+        return {names[i].decode(): ms[i] for i in range(k)}
+
+    def sss_kernel_time(self):
+        ms, b = ctypes.c_double(), _U64()
+        _check(load_library().lz77sss_session_sss_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(b)))
+        return ms.value, b.value
+
+
+def factorize_approximate(text, fact_mode=GREEDY, phr_mode=LPF_OPT, tau=DEFAULT_TAU, rk_seed=42, device=0,
+                          log=False) -> np.ndarray:
+    """lz77_sss<>::factorize_approximate: returns the (z, 2) uint32 factor array."""
+    a = _as_u8(text)
+    with Session(max(a.size, 1), device) as s:
+        s.load(a)
+        z = s.factorize(phr_mode=phr_mode, fact_mode=fact_mode, tau=tau, rk_seed=rk_seed, device=device, log=log)
+        return s.factors(z)
+
+
+def decode(factors: np.ndarray, n: int) -> np.ndarray:
+    """lz77_sss<>::decode (host, sequential as in the reference)."""
+    f = np.ascontiguousarray(factors, dtype=np.uint32)
+    out = np.empty(max(n, 1), np.uint8)
+    _check(load_library().lz77sss_decode_u32(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P), n))
+    return out[:n]
+
+
+def gen_random_repetitive(min_size: int, max_size: int, seed: int, rep: float = -1.0, run: float = -1.0) -> np.ndarray:
+    """random_repetitive_string (utils.hpp:579-640) with a seed instead of std::random_device."""
+    buf = np.empty(max_size + 16, np.uint8)
+    n = load_library().lz77sss_gen_random_repetitive(min_size, max_size, seed, rep, run, buf.ctypes.data_as(_P),
+                                                     max_size)
+    if n < 0:
+        raise Lz77SssError("generator failed")
+    return buf[:n].copy()
+
+
+def gen_genome(n: int, base_len: int, mut_rate: float, seed: int) -> np.ndarray:
+    buf = np.empty(max(n, 1), np.uint8)
+    load_library().lz77sss_gen_genome(n, base_len, mut_rate, seed, buf.ctypes.data_as(_P))
+    return buf[:n]

@@ -1,0 +1,130 @@
+// oracle/oracle_capi.cpp -- C entry points of the CPU oracle, for tests/ and
+// bench.py's cpu_baseline leg only (loaded with ctypes).  TEST INFRASTRUCTURE:
+// never linked into the product.  See oracle.hpp for what is restated and the
+// "parity unpinned" status.
+#include "oracle.hpp"
+
+#include <chrono>
+#include <cstdio>
+#include <exception>
+
+using namespace lzo;
+
+extern "C" {
+
+// Full 3-approximation (p = 1 semantics).  out: 2*cap uint32 (src,len pairs).
+// stats (optional, 16 x uint32): size_sss, has_runs, num_lpf, len_lpf_phr,
+//   num_gaps, patt_lens[5], roll_threshold, log2_size_h.
+// Returns number of factors, or -1 on error / capacity overflow.
+int64_t oracle_factorize_approx(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed,
+                                uint32_t* out, uint64_t cap, uint32_t* stats) {
+    try {
+        uint64_t k = 0;
+        bool overflow = false;
+        approx_stats st;
+        factorize_approximate(T, (u32)n, phr_mode, rk_seed, [&](factor f) {
+            if (k < cap) { out[2 * k] = f.src; out[2 * k + 1] = f.len; } else overflow = true;
+            k++;
+        }, &st);
+        if (stats) {
+            stats[0] = st.size_sss; stats[1] = st.has_runs; stats[2] = st.num_lpf;
+            stats[3] = st.len_lpf_phr; stats[4] = st.num_gaps;
+            for (int i = 0; i < 5; i++) stats[5 + i] = st.patt_lens[i];
+            stats[10] = st.roll_threshold; stats[11] = st.log2_size_h;
+        }
+        return overflow ? -1 : (int64_t)k;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -1;
+    }
+}
+
+// Factor count and wall time only (cpu_baseline); also returns an FNV-1a hash of the stream.
+int64_t oracle_factorize_timed(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed,
+                               double* seconds, uint64_t* stream_hash) {
+    uint64_t k = 0, h = 1469598103934665603ull;
+    auto t0 = std::chrono::steady_clock::now();
+    factorize_approximate(T, (u32)n, phr_mode, rk_seed, [&](factor f) {
+        k++;
+        uint32_t w[2] = {f.src, f.len};
+        const uint8_t* p = (const uint8_t*)w;
+        for (int i = 0; i < 8; i++) { h ^= p[i]; h *= 1099511628211ull; }
+    });
+    auto t1 = std::chrono::steady_clock::now();
+    if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+    if (stream_hash) *stream_hash = h;
+    return (int64_t)k;
+}
+
+// SSS only.  Returns |S| (or -1 if cap too small); *has_runs set.
+int64_t oracle_sss(const uint8_t* T, uint64_t n, uint32_t* out, uint64_t cap, int* has_runs) {
+    bool hr = false;
+    std::vector<u32> S = compute_sss(T, n, hr);
+    if (has_runs) *has_runs = hr;
+    if (S.size() > cap) return -1;
+    std::copy(S.begin(), S.end(), out);
+    return (int64_t)S.size();
+}
+
+// Q membership by brute force for j in [0, n-tau] (tests).  q: n-tau+1 bytes.
+void oracle_q_bruteforce(const uint8_t* T, uint64_t n, uint8_t* q) {
+    if (n < TAU) return;
+    for (u64 j = 0; j + TAU <= n; j++) q[j] = q_bruteforce(T, j);
+}
+// Phi' (tests): phi[j] for j in [0, n-tau], SSS_INF for Q
+void oracle_phi(const uint8_t* T, uint64_t n, uint64_t* phi) {
+    if (n < TAU) return;
+    u64 bp = pow61(SSS_BASE, TAU), neg = (P61 - bp) % P61, fp = 0;
+    for (u64 k = 0; k < TAU; k++) fp = mod61((u128)fp * SSS_BASE + T[k]);
+    for (u64 j = 0; j + TAU <= n; j++) {
+        phi[j] = q_bruteforce(T, j) ? SSS_INF : fp;
+        if (j + TAU < n) fp = mod61((u128)fp * SSS_BASE + T[j + TAU] + (u128)neg * T[j]);
+    }
+}
+
+// SA_S / ISA_S / LCP_S (tests).  Each array has cap entries.
+int64_t oracle_sa_s(const uint8_t* T, uint64_t n, uint32_t* S, uint32_t* SA, uint32_t* LCP, uint64_t cap) {
+    lce_structure L;
+    L.build(T, n);
+    if (L.s() > cap) return -1;
+    std::copy(L.S.begin(), L.S.end(), S);
+    std::copy(L.SA.begin(), L.SA.end(), SA);
+    std::copy(L.LCP.begin(), L.LCP.end(), LCP);
+    return L.s();
+}
+
+// Exact LCE for query pairs (tests).
+void oracle_lce(const uint8_t* T, uint64_t n, const uint32_t* qi, const uint32_t* qj, uint64_t nq, uint32_t* out) {
+    lce_structure L;
+    L.build(T, n);
+    for (u64 k = 0; k < nq; k++) out[k] = (u32)L.lce(qi[k], qj[k]);
+}
+
+// LPF phrase list after build_LPF_opt (tests); out: 3*cap (beg,end,src)
+int64_t oracle_lpf_opt(const uint8_t* T, uint64_t n, uint32_t* out, uint64_t cap) {
+    lce_structure L;
+    L.build(T, n);
+    auto P = build_lpf_opt(T, n, L);
+    if (P.size() > cap) return -1;
+    for (size_t k = 0; k < P.size(); k++) { out[3 * k] = P[k].beg; out[3 * k + 1] = P[k].end; out[3 * k + 2] = P[k].src; }
+    return (int64_t)P.size();
+}
+
+void oracle_decode(const uint32_t* f, uint64_t nf, uint8_t* out, uint64_t n) {
+    decode(reinterpret_cast<const factor*>(f), nf, out, n);
+}
+
+void oracle_gap_bases(uint32_t rk_seed, uint64_t* out5) {
+    auto b = gap_bases(rk_seed);
+    for (int i = 0; i < 5; i++) out5[i] = b[i];
+}
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+}  // extern "C"
