@@ -6,24 +6,26 @@
 //
 // The reference walks gaps sequentially against a hash table H that every
 // visited gap position writes (5 Karp-Rabin fingerprints mod 2^107-1).  A
-// query at position q only ever reads "the last position inserted into slot
-// s before q".  So, for a GIVEN set I of inserted positions, all lookups are
-// fixed by one stable radix sort of the (slot, position) entries of I.  The
-// engine therefore iterates:
+// query at q only ever reads "the last position inserted into slot s before
+// q".  For a GIVEN set I of inserted positions every lookup is therefore
+// fixed by a stable radix sort of the (slot, position) entries of I.  The
+// engine speculates I and iterates to a fixed point:
 //
-//   1. speculate I (initially: every gap position [phrase end, next phrase beg])
-//   2. k_slots + radix sort + k_occ  -> occ5[q][x] for every q in I
-//   3. k_walk (DRY): every walk segment (a gap walk + the LPF factors up to
-//      the next gap) runs in parallel from its assumed start state
-//   4. the host links segments into the chain starting at position 0; unknown
-//      start states become new segments (speculatively, all at once)
-//   5. I' = positions actually inserted along the chain.  I' == I means every
-//      lookup used in the chain was exact -> k_walk (WRITE) emits the factors.
-//      Otherwise I <- I' and repeat.
+//   base   : one full sort of the entries of a base set I_b
+//   delta  : I = I_b - R + A with R a bitmap over I_b and A a small sorted
+//            list of (slot, position, order) keys; lookups honour both
+//   walks  : a walk segment = one gap walk + the LPF factors up to the next
+//            gap; all segments run in parallel from their assumed start
+//   link   : the host links segments into the chain from position 0; unknown
+//            start states become new segments (speculatively, all at once)
+//   check  : I' = positions the chain actually inserted.  I' == I  =>  every
+//            lookup of the chain was exact -> a WRITE walk emits the factors.
+//            Otherwise only the segments holding the next same-slot insert
+//            after a changed position are re-walked (dirty), and I <- I'.
 //
-// The last 64 positions (the text tail, where the reference's stale / zeroed
-// fingerprints and conditional inserts live, rolling_hash_index_107.hpp:80-150)
-// are walked by one thread (k_tail) with an exact local model of the table.
+// The last 64 positions (where the reference's stale / zeroed fingerprints and
+// conditional inserts live, rolling_hash_index_107.hpp:80-150) are walked by
+// one thread (k_tail) with an exact local model of the table.
 #include "../include/engine.h"
 #include "../include/lce_dev.h"
 
@@ -31,17 +33,17 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <limits>
 #include <random>
-#include <unordered_map>
 
 namespace lz {
 
 // ---------------------------------------------------------------------------
-// 107-bit Mersenne arithmetic (rolling_hash.hpp uses mersenne::mod, absent
-// upstream; canonical residues in [0, 2^107-1))
+// 107-bit Mersenne arithmetic (rolling_hash.hpp relies on mersenne::mod, absent
+// upstream; residues are canonical in [0, 2^107-1))
 static constexpr u128 P107 = ((u128)1 << 107) - 1;
 __host__ __device__ static inline u128 mod107(u128 x) {
     x = (x & P107) + (x >> 107);
@@ -78,7 +80,7 @@ struct gap_cfg {
 __device__ __forceinline__ u128 kr_roll(u128 fp, u64 b, u128 negpow_out, u32 in) {
     return mod107(fp * b + mod107((u128)in + negpow_out));
 }
-// Phi_x(T[q..q+len)) mod P, direct evaluation (roll-ins only)
+// Phi_x(T[q..q+len)) mod P by direct evaluation (roll-ins only)
 __device__ __forceinline__ u128 kr_direct(const u8* T, u64 q, u32 len, u64 b) {
     u128 fp = 0;
     for (u32 j = 0; j < len; j++) fp = mod107(fp * b + T[q + j]);
@@ -86,7 +88,8 @@ __device__ __forceinline__ u128 kr_direct(const u8* T, u64 q, u32 len, u64 b) {
 }
 
 // ---------------------------------------------------------------------------
-// 2. entries of I: one thread per chunk of an interval
+// entries: e = 5*rank + (4 - x); entries of one position are generated in the
+// order of longest_prev_occ (x = 4 .. 0)
 struct ichunk { u32 q0, q1, rank0; };
 
 __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __restrict__ chunks, u32 nch,
@@ -99,12 +102,12 @@ __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __res
     for (int x = 0; x < 5; x++) fp[x] = kr_direct(T, ch.q0, G.lens[x], G.base[x]);
     for (u32 q = ch.q0; q < ch.q1; q++) {
         const u32 rank = ch.rank0 + (q - ch.q0);
-        ipos[rank] = q;
+        if (ipos) ipos[rank] = q;
 #pragma unroll
         for (int x = 4; x >= 0; x--) {
             const u32 e = 5 * rank + (4 - x);
             keys[e] = (u32)((u64)fp[x] & G.mask);
-            vals[e] = e;
+            if (vals) vals[e] = e;
         }
         if (q + 1 < ch.q1) {
 #pragma unroll
@@ -113,42 +116,51 @@ __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __res
         }
     }
 }
-
-__global__ void k_occ(const u32* __restrict__ skeys, const u32* __restrict__ svals, const u32* __restrict__ ipos,
-                      u64 m, u32* __restrict__ occ5) {
+// predecessor entry within the same slot (base set)
+__global__ void k_pred(const u32* __restrict__ skeys, const u32* __restrict__ svals, u64 m, u32* __restrict__ pred5) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= m) return;
-    const u32 e = svals[t];
-    u32 o = NONE;
-    if (t > 0 && skeys[t - 1] == skeys[t]) o = ipos[svals[t - 1] / 5];
-    occ5[e] = o;
+    pred5[svals[t]] = (t > 0 && skeys[t - 1] == skeys[t]) ? svals[t - 1] : NONE;
+}
+// added entries -> 64-bit keys (slot << 35 | pos << 3 | order)
+__global__ void k_pack_added(const u32* __restrict__ keys, const u32* __restrict__ ipos, u64 m, u64* __restrict__ out) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    out[e] = ((u64)keys[e] << 35) | ((u64)ipos[e / 5] << 3) | (e % 5);
+}
+__global__ void k_set_rem(u8* __restrict__ rem, const u32* __restrict__ ranks, u64 m, u8 v) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) rem[ranks[k]] = v;
 }
 
 // ---------------------------------------------------------------------------
-// 3. walks
 struct walk_ctx {
     const u8* T;
     gap_cfg G;
     const u32* P;        // phrases (beg,end,src) + sentinel
-    const u32* occ5;
-    const u32* istart;   // interval starts of I (sorted)
+    // base set
+    const u32* istart;   // interval starts (sorted)
     const u32* iend;     // interval ends (exclusive)
     const u32* irank;    // rank of istart
     u32 nint;
-    lce_view L;
-    // tail-model support
-    const u32* skeys;    // sorted slot keys
-    const u32* svals;
-    const u32* ipos;
+    const u32* keys;     // slot of entry e (position order)
+    const u32* skeys;    // sorted slots
+    const u32* svals;    // entry ids in sorted order
+    const u32* pred5;    // predecessor entry in the same slot
+    const u32* ipos;     // rank -> position
     u64 nentries;
+    // delta
+    const u8* rem;       // removed base ranks
+    const u64* akeys;    // sorted added keys
+    u64 nadd;
+    lce_view L;
 };
 
-__device__ __forceinline__ u32 interval_rank(const walk_ctx& W, u32 q, int& hint) {
-    // interval containing q; hint caches the last one
+__device__ __forceinline__ u32 base_rank(const walk_ctx& W, u32 q, int& hint) {
     if (hint >= 0 && q >= W.istart[hint] && q < W.iend[hint]) return W.irank[hint] + (q - W.istart[hint]);
     u32 lo = 0, hi = W.nint;
     while (lo < hi) {
-        u32 mid = (lo + hi) >> 1;
+        const u32 mid = (lo + hi) >> 1;
         if (W.istart[mid] <= q) lo = mid + 1; else hi = mid;
     }
     if (lo == 0) return NONE;
@@ -157,7 +169,79 @@ __device__ __forceinline__ u32 interval_rank(const walk_ctx& W, u32 q, int& hint
     hint = (int)k;
     return W.irank[k] + (q - W.istart[k]);
 }
+__device__ __forceinline__ u32 occ_max(u32 a, u32 b) {
+    if (a == NONE) return b;
+    if (b == NONE) return a;
+    return max(a, b);
+}
+__device__ __forceinline__ u32 occ_min(u32 a, u32 b) {
+    if (a == NONE) return b;
+    if (b == NONE) return a;
+    return min(a, b);
+}
+// last base entry strictly before (slot, q, ord) in processing order, skipping removed
+__device__ u32 base_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
+    u64 lo = 0, hi = W.nentries;  // first index with key > slot
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (W.skeys[mid] <= slot) lo = mid + 1; else hi = mid;
+    }
+    const u64 end = lo;
+    lo = 0;
+    hi = end;  // first index with key >= slot
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (W.skeys[mid] < slot) lo = mid + 1; else hi = mid;
+    }
+    const u64 beg = lo;
+    // within [beg, end) entries are in (position, order) order: first >= (q, ord)
+    lo = beg;
+    hi = end;
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        const u32 e = W.svals[mid];
+        const u32 pq = W.ipos[e / 5], po = e % 5;
+        if (pq < q || (pq == q && po < ord)) lo = mid + 1; else hi = mid;
+    }
+    for (u64 t = lo; t > beg; t--) {
+        const u32 rk = W.svals[t - 1] / 5;
+        if (!W.rem[rk] || W.ipos[rk] == q) return W.ipos[rk];
+    }
+    return NONE;
+}
+__device__ u32 added_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
+    if (!W.nadd) return NONE;
+    const u64 key = ((u64)slot << 35) | ((u64)q << 3) | ord;
+    u64 lo = 0, hi = W.nadd;  // first >= key
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (W.akeys[mid] < key) lo = mid + 1; else hi = mid;
+    }
+    if (lo == 0) return NONE;
+    const u64 k = W.akeys[lo - 1];
+    if ((k >> 35) != slot) return NONE;
+    return (u32)((k >> 3) & 0xFFFFFFFFull);
+}
+// H[slot of (q,x)] just before longest_prev_occ's advance_and_get_occ<x> at q
+__device__ u32 lookup(const walk_ctx& W, u32 q, int x, int& hint) {
+    const u32 ord = 4 - x;
+    const u32 rk = base_rank(W, q, hint);
+    u32 slot, cb;
+    if (rk != NONE) {
+        const u32 e = 5 * rk + ord;
+        slot = W.keys[e];
+        u32 p = W.pred5[e];
+        while (p != NONE && W.rem[p / 5] && W.ipos[p / 5] != q) p = W.pred5[p];
+        cb = p == NONE ? NONE : W.ipos[p / 5];
+    } else {
+        slot = (u32)((u64)kr_direct(W.T, q, W.G.lens[x], W.G.base[x]) & W.G.mask);
+        cb = base_last_before(W, slot, q, ord);
+    }
+    return occ_max(cb, added_last_before(W, slot, q, ord));
+}
 
+// ---------------------------------------------------------------------------
+// walks
 template <bool WRITE>
 __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fout) {
     const u8* T = W.T;
@@ -176,10 +260,8 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
     auto query = [&](u32 q, u32& fsrc, u32& flen) {
         fsrc = T[q];
         flen = 0;
-        const u32 rk = interval_rank(W, q, hint);
-        if (rk == NONE) return;  // q not in I: speculation miss, fixed by the next round
         for (int x = 4; x >= 0; x--) {
-            const u32 occ = W.occ5[5 * (u64)rk + (4 - x)];
+            const u32 occ = lookup(W, q, x, hint);
             if (occ != NONE && occ < q && T[occ] == T[q]) {
                 flen = (u32)dev_lce(W.L, occ, q);
                 fsrc = occ;
@@ -191,14 +273,14 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
         u32 gap_end = P[3 * p];
         if (i < gap_end) {
             if (idx < i) {
-                if (i - idx > W.G.thr) {  // reinit (only matters in the tail region)
+                if (i - idx > W.G.thr) {  // reinit (matters only in the tail region)
                     zm = 0;
                     for (int x = 0; x < 5; x++) zm |= ((u64)i + W.G.lens[x] >= n) ? (1u << x) : 0u;
                 }
                 idx = i;
             }
             do {
-                if (i >= nt) { flags |= 1; out.flags = flags; return; }
+                if (i >= nt) { out.flags = flags | 1; return; }
                 if (++guard > guard_max || i > n) { out.flags = flags | 4; return; }
                 u32 fsrc, flen;
                 query(i, fsrc, flen);
@@ -222,7 +304,7 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
         const u32 exc = i - gap_end;
         u32 lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
         if (idx == i) {
-            if (i >= nt) { flags |= 1; out.flags = flags; return; }
+            if (i >= nt) { out.flags = flags | 1; return; }
             u32 fsrc, flen;
             query(i, fsrc, flen);
             idx = i + 1;
@@ -245,38 +327,99 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
 }
 
 template <bool WRITE>
-__global__ void k_walk(walk_ctx W, const seg_in* __restrict__ segs, const u32* __restrict__ ids, u32 nseg,
-                       seg_out* __restrict__ outs, const u64* __restrict__ offs, u32* __restrict__ fact) {
+__global__ void k_walk(walk_ctx W, const seg_in* __restrict__ segs, u32 nseg, seg_out* __restrict__ outs,
+                       const u64* __restrict__ offs, u32* __restrict__ fact) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nseg) return;
-    const u32 g = ids ? ids[t] : (u32)t;
     seg_out o;
     o.flags = 0;
-    o.e = segs[g].start;
+    o.e = segs[t].start;
     o.nfact = 0;
-    walk_segment<WRITE>(W, segs[g], o, WRITE ? fact + 2 * offs[t] : nullptr);
-    if (!WRITE) outs[g] = o;
+    o.nsingle = 0;
+    walk_segment<WRITE>(W, segs[t], o, WRITE ? fact + 2 * offs[t] : nullptr);
+    if (!WRITE) outs[t] = o;
+}
+
+// successor insert (next position of the same slot after y) in the current set:
+// the only query whose lookup can change when y joins or leaves I
+__global__ void k_dirty(walk_ctx W, const u32* __restrict__ ys, u64 m, u32* __restrict__ out) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const u32 y = ys[k];
+#pragma unroll 1
+    for (int x = 0; x < 5; x++) {
+        const u32 slot = (u32)((u64)kr_direct(W.T, y, W.G.lens[x], W.G.base[x]) & W.G.mask);
+        u32 best = NONE;
+        u64 lo = 0, hi = W.nentries;  // first entry after (slot, y)
+        while (lo < hi) {
+            const u64 mid = (lo + hi) >> 1;
+            const u32 key = W.skeys[mid];
+            const u32 pq = W.ipos[W.svals[mid] / 5];
+            if (key < slot || (key == slot && pq <= y)) lo = mid + 1; else hi = mid;
+        }
+        for (u64 t = lo; t < W.nentries && W.skeys[t] == slot; t++) {
+            const u32 rk = W.svals[t] / 5;
+            if (!W.rem[rk]) { best = W.ipos[rk]; break; }
+        }
+        if (W.nadd) {
+            const u64 key = ((u64)slot << 35) | ((u64)(y + 1) << 3);
+            u64 a = 0, b = W.nadd;
+            while (a < b) {
+                const u64 mid = (a + b) >> 1;
+                if (W.akeys[mid] < key) a = mid + 1; else b = mid;
+            }
+            if (a < W.nadd && (W.akeys[a] >> 35) == slot) best = occ_min(best, (u32)((W.akeys[a] >> 3) & 0xFFFFFFFFull));
+        }
+        out[5 * k + x] = best;
+    }
+}
+
+// incremental delta: y joined (flag 1) or left (flag 0) I; base positions flip
+// their removed bit, others are reported as additions to maintain on the host
+__global__ void k_flip(walk_ctx W, const u32* __restrict__ ys, const u8* __restrict__ joined, u64 m,
+                       u8* __restrict__ rem, u8* __restrict__ in_base) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    int hint = -1;
+    const u32 rk = base_rank(W, ys[k], hint);
+    in_base[k] = rk != NONE;
+    if (rk != NONE) rem[rk] = joined[k] ? 0 : 1;
+}
+// rem[r] = (base position r is not in I); I given as sorted disjoint intervals
+__global__ void k_rem_from_set(const u32* __restrict__ ipos, u64 nb, const u32* __restrict__ ia,
+                               const u32* __restrict__ ib, u32 ni, u8* __restrict__ rem) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nb) return;
+    const u32 q = ipos[r];
+    u32 lo = 0, hi = ni;
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (ia[mid] <= q) lo = mid + 1; else hi = mid;
+    }
+    rem[r] = (lo == 0 || q >= ib[lo - 1]) ? 1 : 0;
+}
+// a walked segment is stale iff a dirty position lies in its covered range
+__global__ void k_stale(const u32* __restrict__ lo, const u32* __restrict__ hi, u64 nseg,
+                        const u32* __restrict__ dirty, u64 nd, u8* __restrict__ stale) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg) return;
+    const u32 a = lo[g], b = hi[g];
+    u64 l = 0, h = nd;
+    while (l < h) {
+        const u64 mid = (l + h) >> 1;
+        if (dirty[mid] < a) l = mid + 1; else h = mid;
+    }
+    stale[g] = (l < nd && dirty[l] <= b) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
-// exact single-thread walk from a segment start to the end of the text,
-// modelling the table in the tail region (last 64 positions)
+// exact single-thread walk from a segment start to the end of the text, with
+// a local model of the inserts in the tail region (last 64 positions)
 struct tail_ins { u32 slot, pos; };
 constexpr int TAIL_CAP = 64 * 5 + 8;
 
-__device__ u32 last_global_in_slot(const walk_ctx& W, u32 slot) {
-    // last entry with key == slot in the sorted key array
-    u64 lo = 0, hi = W.nentries;
-    while (lo < hi) {
-        u64 mid = (lo + hi) >> 1;
-        if (W.skeys[mid] <= slot) lo = mid + 1; else hi = mid;
-    }
-    if (lo == 0 || W.skeys[lo - 1] != slot) return NONE;
-    return W.ipos[W.svals[lo - 1] / 5];
-}
-
 __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u64* __restrict__ count_out,
-                       u32* __restrict__ ins_out /* [start, e) + singles, cap 8 */) {
+                       u32* __restrict__ ins_out /* [a, b) pairs below the tail region, cap 8 */) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const u8* T = W.T;
     const u32 n = W.G.n, nt = W.G.nt;
@@ -289,19 +432,15 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
     u32 nins = 0;
     auto fp_slot = [&](u32 q, int x) -> u32 {
         const u32 len = W.G.lens[x];
-        if (zm >> x & 1) return 0;
-        const u64 qq = ((u64)q + len <= n) ? q : (n >= len ? n - len : 0);
-        if ((u64)len > n) return 0;
+        if ((zm >> x & 1) || (u64)len > n) return 0;
+        const u64 qq = ((u64)q + len <= n) ? q : n - len;
         return (u32)((u64)kr_direct(T, qq, len, W.G.base[x]) & W.G.mask);
     };
-    auto lookup = [&](u32 q, int x, u32 slot) -> u32 {
+    auto tail_lookup = [&](u32 slot) -> u32 {
         for (int k = nloc - 1; k >= 0; k--)
             if (loc[k].slot == slot) return loc[k].pos;
-        if (q < nt) {
-            const u32 rk = interval_rank(W, q, hint);
-            return rk == NONE ? NONE : W.occ5[5 * (u64)rk + (4 - x)];
-        }
-        return last_global_in_slot(W, slot);
+        // every base / added entry lies below nt
+        return occ_max(base_last_before(W, slot, nt, 0), added_last_before(W, slot, nt, 0));
     };
     auto insert = [&](u32 q, u32 slot) {
         if (nloc < TAIL_CAP) loc[nloc++] = {slot, q};
@@ -311,17 +450,25 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
         flen = 0;
         bool hit = false;
         for (int x = 4; x >= 0; x--) {
-            if (!hit) {
-                const u32 slot = (q >= nt) ? fp_slot(q, x) : 0;
-                const u32 occ = lookup(q, x, slot);
-                if (q >= nt) insert(q, slot);
+            if (q < nt) {
+                if (hit) continue;
+                const u32 occ = lookup(W, q, x, hint);
                 if (occ != NONE && occ < q && T[occ] == T[q]) {
                     flen = (u32)dev_lce(W.L, occ, q);
                     fsrc = occ;
                     hit = true;
                 }
-            } else if (q >= nt && (u64)q + W.G.lens[x] < n) {
-                insert(q, fp_slot(q, x));
+            } else if (!hit) {
+                const u32 slot = fp_slot(q, x);
+                const u32 occ = tail_lookup(slot);
+                insert(q, slot);  // advance_and_get_occ always inserts
+                if (occ != NONE && occ < q && T[occ] == T[q]) {
+                    flen = (u32)dev_lce(W.L, occ, q);
+                    fsrc = occ;
+                    hit = true;
+                }
+            } else if ((u64)q + W.G.lens[x] < n) {
+                insert(q, fp_slot(q, x));  // advance<x> inserts only if cur_pos + len < n
             }
         }
     };
@@ -336,16 +483,15 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
         fact[2 * (off + nf) + 1] = len;
         nf++;
     };
-    // inserted intervals below the tail region (the only ones the speculated
-    // set I has to contain): recorded as [a, b) pairs, capacity 8
     auto record = [&](u32 a, u32 b) {
-        if (a >= nt || a >= b) return;
+        b = min(b, nt);
+        if (a >= b) return;
         if (nins > 0 && ins_out[2 * (nins - 1) + 1] >= a) {
             ins_out[2 * (nins - 1) + 1] = max(ins_out[2 * (nins - 1) + 1], b);
             return;
         }
         if (nins < 8) { ins_out[2 * nins] = a; ins_out[2 * nins + 1] = b; nins++; }
-        else count_out[2] = 1;  // overflow (cannot happen: see DESIGN.md 4.5)
+        else count_out[2] = 1;
     };
     count_out[2] = 0;
     u64 guard = 0;
@@ -399,6 +545,18 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
     count_out[1] = nins;
 }
 
+// phrase statistics (approximate/common.cpp:98-157, p = 1)
+__global__ void k_phrase_info(const u32* __restrict__ P, u32 m, u32 n, u32* __restrict__ acc) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const u32 b = P[3 * k], e = P[3 * k + 1];
+    atomicAdd(&acc[0], e - b);
+    u32 gaps = 0;
+    if (k == 0 ? b > 0 : b > P[3 * (k - 1) + 1]) gaps++;
+    if (k == m - 1 && e < n) gaps++;
+    if (gaps) atomicAdd(&acc[1], gaps);
+}
+
 // ---------------------------------------------------------------------------
 // host side
 struct gap_params_h {
@@ -436,23 +594,13 @@ static gap_params_h choose_gap_params(u32 n, u32 num_lpf, u32 len_lpf_phr, u32 n
     return g;
 }
 
-// phrase statistics (approximate/common.cpp:98-157, p = 1)
-__global__ void k_phrase_info(const u32* __restrict__ P, u32 m, u32 n, u32* __restrict__ acc) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m) return;
-    const u32 b = P[3 * k], e = P[3 * k + 1];
-    atomicAdd(&acc[0], e - b);
-    u32 gaps = 0;
-    if (k == 0 ? b > 0 : b > P[3 * (k - 1) + 1]) gaps++;
-    if (k == m - 1 && e < n) gaps++;
-    if (gaps) atomicAdd(&acc[1], gaps);
-}
-
 struct interval { u32 a, b; };  // [a, b)
+using ivec = std::vector<interval>;
 
-static void normalize(std::vector<interval>& v) {
+static void normalize(ivec& v) {
     std::sort(v.begin(), v.end(), [](const interval& x, const interval& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); });
-    std::vector<interval> out;
+    ivec out;
+    out.reserve(v.size());
     for (auto& x : v) {
         if (x.b <= x.a) continue;
         if (!out.empty() && x.a <= out.back().b) out.back().b = std::max(out.back().b, x.b);
@@ -460,12 +608,46 @@ static void normalize(std::vector<interval>& v) {
     }
     v.swap(out);
 }
-static void clip(std::vector<interval>& v, u32 nt) {
+static void clip(ivec& v, u32 nt) {
     for (auto& x : v) { x.a = std::min(x.a, nt); x.b = std::min(x.b, nt); }
     normalize(v);
 }
+// a \ b for normalized interval lists
+static ivec subtract(const ivec& a, const ivec& b) {
+    ivec out;
+    size_t j = 0;
+    for (auto x : a) {
+        u32 cur = x.a;
+        while (j < b.size() && b[j].b <= cur) j++;
+        for (size_t k = j; k < b.size() && b[k].a < x.b; k++) {
+            if (b[k].a > cur) out.push_back({cur, b[k].a});
+            cur = std::max(cur, b[k].b);
+            if (cur >= x.b) break;
+        }
+        if (cur < x.b) out.push_back({cur, x.b});
+    }
+    return out;
+}
+static u64 total_len(const ivec& v) {
+    u64 t = 0;
+    for (auto& x : v) t += x.b - x.a;
+    return t;
+}
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
+    const bool dbg = debug_enabled();
+    double t_mark = now_ms();
+    auto lap = [&](const char* what) {
+        if (!dbg) return;
+        LZ_HIP(hipStreamSynchronize(st));
+        const double t = now_ms();
+        std::fprintf(stderr, "[lz77sss-debug]   %-28s %9.3f ms\n", what, t - t_mark);
+        t_mark = t;
+    };
     const u32 N = (u32)n;
     const u32 m = num_phr;  // phrases; P[m] = sentinel
     u32* P = lpf.get((u64)(m + 1) * 3);
@@ -473,7 +655,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         const u32 sent[3] = {N, N + 1, 0};
         LZ_HIP(hipMemcpyAsync(P + 3 * (u64)m, sent, 12, hipMemcpyHostToDevice, st));
     }
-    // ---- phrase statistics -> parameters
+    // ---- phrase statistics -> parameters (lz77_sss.hpp:420-461)
     u32 num_lpf = m, len_lpf_phr = 0, num_gaps = 1;
     if (m > 0) {
         u32* acc = counters.get(16);
@@ -496,9 +678,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     std::vector<u128> negpow(5 * 256);
     for (int x = 0; x < 5; x++) {
         const u128 bp = powmod107_host(bases[x], gp.patt_lens[x]);
-        const u128 nb = (P107 - bp) % P107;
+        const u128 nbp = (P107 - bp) % P107;
         negpow[x * 256] = 0;
-        for (int o = 1; o < 256; o++) negpow[x * 256 + o] = mod107(negpow[x * 256 + o - 1] + nb);
+        for (int o = 1; o < 256; o++) negpow[x * 256 + o] = mod107(negpow[x * 256 + o - 1] + nbp);
     }
     u128* d_negpow = (u128*)tmp_greedy.get(5 * 256 * sizeof(u128));
     LZ_HIP(hipMemcpyAsync(d_negpow, negpow.data(), 5 * 256 * sizeof(u128), hipMemcpyHostToDevice, st));
@@ -516,14 +698,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     G.mask = (u32)((1ull << gp.log2_size_h) - 1);
     G.negpow = d_negpow;
 
-    // host copy of phrases (segment bookkeeping)
     std::vector<u32> hP((u64)(m + 1) * 3);
     LZ_HIP(hipMemcpyAsync(hP.data(), P, hP.size() * 4, hipMemcpyDeviceToHost, st));
     LZ_HIP(hipStreamSynchronize(st));
     auto first_phrase_after = [&](u32 i) -> u32 {  // smallest k with P[k].end > i
         u32 lo = 0, hi = m;
         while (lo < hi) {
-            u32 mid = (lo + hi) >> 1;
+            const u32 mid = (lo + hi) >> 1;
             if (hP[3 * mid + 1] <= i) lo = mid + 1; else hi = mid;
         }
         return lo;
@@ -531,45 +712,71 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     u32 zmask0 = 0;
     for (int x = 0; x < 5; x++) zmask0 |= (G.lens[x] >= N) ? (1u << x) : 0u;  // reinit(0) at construction
 
-    // ---- default segments and I_0
-    std::vector<u32> starts;   // segment start positions (sorted, unique)
-    std::vector<interval> I;
+    // ---- segments (flat arrays; ids in creation order)
+    std::vector<seg_in> hsegs;
+    std::vector<seg_out> houts;
+    std::vector<u8> valid;       // output exact for the current lookup state
+    std::vector<u32> seg_next;   // cached id of the segment starting at houts.next (NONE = unknown)
+    std::vector<std::pair<u32, u32>> by_start;  // (start, id), sorted
+    auto add_segment = [&](u32 a) {
+        hsegs.push_back({a, first_phrase_after(a), a, zmask0});
+        houts.push_back(seg_out{});
+        valid.push_back(0);
+        seg_next.push_back(NONE);
+    };
+    auto find_seg = [&](u32 a) -> u32 {
+        auto it = std::lower_bound(by_start.begin(), by_start.end(), std::make_pair(a, 0u));
+        return (it != by_start.end() && it->first == a) ? it->second : NONE;
+    };
+    // default segments and I_0 (every gap + the LPF-start query that follows it)
+    ivec I;
     {
         u32 prev_end = 0;
         for (u32 k = 0; k <= m; k++) {
             const u32 b = hP[3 * k], e = hP[3 * k + 1];
             if (prev_end < b) {
-                starts.push_back(prev_end);
+                add_segment(prev_end);
                 I.push_back({prev_end, std::min(b + 1, N)});
             }
             prev_end = std::max(prev_end, e);
         }
-        if (starts.empty() || starts[0] != 0) starts.insert(starts.begin(), 0u);
+        if (hsegs.empty() || hsegs[0].start != 0) add_segment(0);  // phrases begin at >= 1
+        for (u32 g = 0; g < hsegs.size(); g++) by_start.push_back({hsegs[g].start, g});
+        std::sort(by_start.begin(), by_start.end());
     }
     clip(I, G.nt);
+    // base superset: the speculated gaps plus the interiors of short phrases,
+    // where walk overruns insert (greedy.cpp:69-78); those start "removed"
+    ivec Isup = I;
+    for (u32 k = 0; k < m; k++) {
+        const u32 b = hP[3 * k], e = hP[3 * k + 1];
+        if (e - b <= 48) Isup.push_back({b, e});
+    }
+    clip(Isup, G.nt);
+    lap("greedy setup");
 
-    dbuf<seg_in>& d_segs = seg_in_buf;
-    dbuf<seg_out>& d_outs = seg_out_buf;
-    std::vector<seg_in> hsegs;
-    std::vector<seg_out> houts;
-    u64 total_fact = 0;
-    int outer = 0, rounds_total = 0;
-    for (;; outer++) {
-        if (outer > 64) throw error(-6, "greedy speculation did not converge");
-        // ---- 2. entries of I -> sort -> occ5
+    // ---- base build
+    ivec Ib;
+    std::vector<u32> h_is, h_ie, h_ir;
+    u64 nb = 0, ne = 0;
+    walk_ctx W{};
+    W.T = T;
+    W.G = G;
+    W.P = P;
+    W.L = view(T);
+    auto build_base = [&](const ivec& Inew) {
+        Ib = Inew;
+        h_is.clear(); h_ie.clear(); h_ir.clear();
         std::vector<ichunk> chunks;
-        std::vector<u32> h_is, h_ie, h_ir;
-        u64 nI = 0;
-        for (auto& iv : I) {
-            h_is.push_back(iv.a); h_ie.push_back(iv.b); h_ir.push_back((u32)nI);
-            for (u32 q = iv.a; q < iv.b; q += 1024) {
-                const u32 q1 = std::min<u32>(iv.b, q + 1024);
-                chunks.push_back({q, q1, (u32)(nI + (q - iv.a))});
-            }
-            nI += iv.b - iv.a;
+        nb = 0;
+        for (auto& iv : Ib) {
+            h_is.push_back(iv.a); h_ie.push_back(iv.b); h_ir.push_back((u32)nb);
+            for (u32 q = iv.a; q < iv.b; q += 1024)
+                chunks.push_back({q, std::min<u32>(iv.b, q + 1024), (u32)(nb + (q - iv.a))});
+            nb += iv.b - iv.a;
         }
-        if (5 * nI >= (1ull << 32)) throw error(-1, "gap region too large for 32-bit entry ids");
-        const u64 ne = 5 * nI;
+        if (5 * nb >= (1ull << 32)) throw error(-1, "gap region too large for 32-bit entry ids");
+        ne = 5 * nb;
         u32* d_is = ist.get(h_is.size() + 1);
         u32* d_ie = iend.get(h_ie.size() + 1);
         u32* d_ir = irank.get(h_ir.size() + 1);
@@ -581,10 +788,14 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         ichunk* d_ch = (ichunk*)chunk_buf.get(std::max<size_t>(1, chunks.size()) * sizeof(ichunk));
         if (!chunks.empty())
             LZ_HIP(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(ichunk), hipMemcpyHostToDevice, st));
-        u32* keys = ekeys.get(ne + 1), *vals = evals.get(ne + 1);
-        u32* skeys = ekeys2.get(ne + 1), *svals = evals2.get(ne + 1);
-        u32* ipos = ipos_buf.get(nI + 1);
-        u32* occ5 = occ_buf.get(ne + 1);
+        u32* keys = ekeys.get(ne + 1);
+        u32* vals = evals.get(ne + 1);
+        u32* skeys = ekeys2.get(ne + 1);
+        u32* svals = evals2.get(ne + 1);
+        u32* ipos = ipos_buf.get(nb + 1);
+        u32* pred5 = occ_buf.get(ne + 1);
+        u8* rem = rem_buf.get(nb + 1);
+        LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
         if (!chunks.empty()) {
             k_slots<<<cdiv(chunks.size(), 64), 64, 0, st>>>(T, G, d_ch, (u32)chunks.size(), keys, vals, ipos);
             size_t tb = 0;
@@ -593,107 +804,179 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             u8* t = scan_tmp.get(tb);
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, skeys, vals, svals, (int)ne, 0,
                                                       (int)gp.log2_size_h, st));
-            k_occ<<<cdiv(ne, 256), 256, 0, st>>>(skeys, svals, ipos, ne, occ5);
+            k_pred<<<cdiv(ne, 256), 256, 0, st>>>(skeys, svals, ne, pred5);
         }
-        walk_ctx W{};
-        W.T = T;
-        W.G = G;
-        W.P = P;
-        W.occ5 = occ5;
-        W.istart = d_is;
-        W.iend = d_ie;
-        W.irank = d_ir;
-        W.nint = (u32)h_is.size();
-        W.L = view(T);
-        W.skeys = skeys;
-        W.svals = svals;
-        W.ipos = ipos;
-        W.nentries = ne;
+        W.istart = d_is; W.iend = d_ie; W.irank = d_ir; W.nint = (u32)h_is.size();
+        W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne;
+        W.rem = rem; W.akeys = nullptr; W.nadd = 0;
+        lap("base build (slots+sort+pred)");
+    };
+    auto base_rank_host = [&](u32 q) -> u32 {
+        auto it = std::upper_bound(h_is.begin(), h_is.end(), q);
+        if (it == h_is.begin()) return NONE;
+        const size_t k = (it - h_is.begin()) - 1;
+        if (q >= h_ie[k]) return NONE;
+        return h_ir[k] + (q - h_is[k]);
+    };
+    std::vector<u32> A_pos;  // sorted positions of I outside the base set
+    // rebuild the added-entry list from A_pos
+    auto rebuild_added = [&]() {
+        W.nadd = 0;
+        W.akeys = nullptr;
+        if (A_pos.empty()) return;
+        std::vector<ichunk> chunks;
+        u64 na = 0;
+        for (size_t k = 0; k < A_pos.size();) {
+            size_t j = k + 1;
+            while (j < A_pos.size() && A_pos[j] == A_pos[j - 1] + 1 && j - k < 1024) j++;
+            chunks.push_back({A_pos[k], A_pos[j - 1] + 1, (u32)na});
+            na += j - k;
+            k = j;
+        }
+        ichunk* d_ch = (ichunk*)chunk_buf2.get(chunks.size() * sizeof(ichunk));
+        LZ_HIP(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(ichunk), hipMemcpyHostToDevice, st));
+        u32* akey32 = add_keys32.get(5 * na);
+        u32* apos = add_pos.get(na);
+        k_slots<<<cdiv(chunks.size(), 64), 64, 0, st>>>(T, G, d_ch, (u32)chunks.size(), akey32, nullptr, apos);
+        u64* ak = add_keys.get(5 * na);
+        u64* ak2 = add_keys2.get(5 * na);
+        k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, ak, ak2, (int)(5 * na), 0, 63, st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, ak, ak2, (int)(5 * na), 0, 63, st));
+        W.akeys = ak2;
+        W.nadd = 5 * na;
+    };
+    // full state for I (I must be a subset of the base set here)
+    auto set_state = [&](const ivec& Iset) {
+        std::vector<u32> ia(Iset.size()), ib(Iset.size());
+        for (size_t k = 0; k < Iset.size(); k++) { ia[k] = Iset[k].a; ib[k] = Iset[k].b; }
+        u32* d_a = dirty_in.get(ia.size() + 1);
+        u32* d_b = dirty_out.get(ib.size() + 1);
+        if (!ia.empty()) {
+            LZ_HIP(hipMemcpyAsync(d_a, ia.data(), ia.size() * 4, hipMemcpyHostToDevice, st));
+            LZ_HIP(hipMemcpyAsync(d_b, ib.data(), ib.size() * 4, hipMemcpyHostToDevice, st));
+        }
+        if (nb) k_rem_from_set<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, d_a, d_b, (u32)ia.size(), (u8*)W.rem);
+        A_pos.clear();
+        rebuild_added();
+        LZ_HIP(hipStreamSynchronize(st));
+    };
 
-        // ---- 3./4. walk all known segments, link the chain, add missing starts
-        std::unordered_map<u32, u32> id_of;
-        hsegs.clear();
-        for (u32 a : starts) {
-            id_of[a] = (u32)hsegs.size();
-            hsegs.push_back({a, first_phrase_after(a), a, zmask0});
+    build_base(Isup);
+    set_state(I);
+    std::vector<seg_in> tin;
+    std::vector<seg_out> tout;
+    auto walk_ids = [&](const std::vector<u32>& ids) {
+        if (ids.empty()) return;
+        tin.resize(ids.size());
+        for (size_t t = 0; t < ids.size(); t++) tin[t] = hsegs[ids[t]];
+        seg_in* ds = seg_in_buf.get(ids.size());
+        seg_out* dout = seg_out_buf.get(ids.size());
+        LZ_HIP(hipMemcpyAsync(ds, tin.data(), tin.size() * sizeof(seg_in), hipMemcpyHostToDevice, st));
+        k_walk<false><<<cdiv(ids.size(), 64), 64, 0, st>>>(W, ds, (u32)ids.size(), dout, nullptr, nullptr);
+        LZ_HIP(hipGetLastError());
+        tout.resize(ids.size());
+        LZ_HIP(hipMemcpyAsync(tout.data(), dout, tout.size() * sizeof(seg_out), hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        for (size_t t = 0; t < ids.size(); t++) {
+            const u32 g = ids[t];
+            houts[g] = tout[t];
+            valid[g] = 1;
+            seg_next[g] = NONE;
+            if (houts[g].flags & 2) throw error(-6, "greedy: too many LPF-start queries in one segment");
+            if (houts[g].flags & 4) throw error(-6, "greedy: walk guard tripped (internal error)");
         }
-        houts.assign(hsegs.size(), seg_out{});
-        std::vector<u32> todo(hsegs.size());
-        for (u32 g = 0; g < todo.size(); g++) todo[g] = g;
-        std::vector<u32> chain;
-        bool tail_reached = false;
+    };
+
+    std::vector<u32> chain;
+    bool tail_reached = false;
+    std::vector<u32> todo;
+    for (u32 g = 0; g < hsegs.size(); g++) todo.push_back(g);
+    u64 total_fact = 0;
+    int outer = 0, rounds_total = 0;
+    u64 walked_total = 0;
+    for (;; outer++) {
+        if (outer > 500) throw error(-6, "greedy speculation did not converge");
+        // ---- walk + link until the chain from position 0 is complete and exact
         for (int round = 0;; round++) {
             rounds_total++;
-            if (round > 256) throw error(-6, "greedy segment linking did not converge");
-            // walk the todo segments (compact arrays: dbuf growth does not preserve contents)
-            if (!todo.empty()) {
-                std::vector<seg_in> tin(todo.size());
-                for (size_t t = 0; t < todo.size(); t++) tin[t] = hsegs[todo[t]];
-                seg_in* ds = d_segs.get(todo.size());
-                seg_out* dout = d_outs.get(todo.size());
-                LZ_HIP(hipMemcpyAsync(ds, tin.data(), tin.size() * sizeof(seg_in), hipMemcpyHostToDevice, st));
-                k_walk<false><<<cdiv(todo.size(), 64), 64, 0, st>>>(W, ds, nullptr, (u32)todo.size(), dout, nullptr, nullptr);
-                LZ_HIP(hipGetLastError());
-                std::vector<seg_out> tout(todo.size());
-                LZ_HIP(hipMemcpyAsync(tout.data(), dout, tout.size() * sizeof(seg_out), hipMemcpyDeviceToHost, st));
-                LZ_HIP(hipStreamSynchronize(st));
-                for (size_t t = 0; t < todo.size(); t++) houts[todo[t]] = tout[t];
-            }
-            // link from position 0
+            if (round > 100000) throw error(-6, "greedy segment linking did not converge");
+            walk_ids(todo);
+            walked_total += todo.size();
+            lap("walk");
+            todo.clear();
             chain.clear();
             tail_reached = false;
-            std::vector<u32> missing;
-            u32 g = id_of.at(0);
+            u32 g = find_seg(0);
             u32 idxp = 0, zm = zmask0;
             bool complete = true;
             for (;;) {
                 if (chain.size() > hsegs.size()) throw error(-6, "greedy: segment chain has a cycle");
+                if (!valid[g]) { todo.push_back(g); complete = false; break; }
                 chain.push_back(g);
                 hsegs[g].idxpos = idxp;  // exact inputs of chain segments (used by the tail walk)
                 hsegs[g].zmask = zm;
                 const seg_out& o = houts[g];
-                if (o.flags & 2) throw error(-6, "greedy: too many LPF-start queries in one segment");
-                if (o.flags & 4) throw error(-6, "greedy: walk guard tripped (internal error)");
                 if (o.flags & 1) { tail_reached = true; break; }
                 if (o.next >= N) break;
                 idxp = o.idxpos;
                 zm = o.zmask;
-                auto it = id_of.find(o.next);
-                if (it == id_of.end()) { complete = false; break; }
-                g = it->second;
+                u32 nx = seg_next[g];
+                if (nx == NONE) {
+                    nx = find_seg(o.next);
+                    seg_next[g] = nx;
+                }
+                if (nx == NONE) { complete = false; break; }
+                g = nx;
             }
-            if (debug_enabled())
-                std::fprintf(stderr, "[lz77sss-debug] greedy outer=%d round=%d segs=%zu chain=%zu complete=%d tail=%d\n",
-                             outer, round, hsegs.size(), chain.size(), (int)complete, (int)tail_reached);
+            lap("link");
+            if (dbg)
+                std::fprintf(stderr,
+                             "[lz77sss-debug] greedy outer=%d round=%d segs=%zu chain=%zu complete=%d tail=%d |I|=%llu "
+                             "adds=%llu rems=%zu\n",
+                             outer, round, hsegs.size(), chain.size(), (int)complete, (int)tail_reached,
+                             (unsigned long long)total_len(I), (unsigned long long)(W.nadd / 5), A_pos.size());
             if (complete) break;
-            // speculatively add every unknown next state
-            todo.clear();
-            for (u32 h = 0; h < houts.size(); h++) {
-                const seg_out& o = houts[h];
-                if ((o.flags & 1) || o.next >= N) continue;
-                if (id_of.count(o.next)) continue;
-                const u32 a = o.next;
-                id_of[a] = (u32)hsegs.size();
-                todo.push_back((u32)hsegs.size());
-                hsegs.push_back({a, first_phrase_after(a), a, zmask0});
-                houts.push_back(seg_out{});
-                missing.push_back(a);
+            if (!todo.empty()) {
+                // batch: re-walk every stale segment, not only the one the link stopped at
+                todo.clear();
+                for (u32 h = 0; h < hsegs.size(); h++)
+                    if (!valid[h]) todo.push_back(h);
+                continue;
             }
-            if (missing.empty()) throw error(-6, "greedy: chain broken without new states");
+            // speculatively create every unknown next state of current segments
+            std::vector<u32> fresh;
+            for (u32 h = 0; h < houts.size(); h++) {
+                if (!valid[h]) continue;
+                const seg_out& o = houts[h];
+                if ((o.flags & 1) || o.next >= N || seg_next[h] != NONE) continue;
+                if (find_seg(o.next) != NONE) continue;
+                fresh.push_back(o.next);
+            }
+            std::sort(fresh.begin(), fresh.end());
+            fresh.erase(std::unique(fresh.begin(), fresh.end()), fresh.end());
+            if (fresh.empty()) throw error(-6, "greedy: chain broken without new states");
+            for (u32 a : fresh) {
+                todo.push_back((u32)hsegs.size());
+                by_start.push_back({a, (u32)hsegs.size()});
+                add_segment(a);
+            }
+            std::sort(by_start.begin(), by_start.end());
         }
-        // ---- tail: exact single-thread walk from the first chain segment in the tail region
+        // ---- tail: exact single-thread walk from the chain segment that enters the tail region
         u64 tail_count = 0;
-        std::vector<interval> tail_ins;
+        ivec tail_ins;
         u64 chain_fact = 0;
-        size_t nchain = chain.size() - (tail_reached ? 1 : 0);
+        const size_t nchain = chain.size() - (tail_reached ? 1 : 0);
         for (size_t c = 0; c < nchain; c++) chain_fact += houts[chain[c]].nfact;
-        u64* d_cnt = (u64*)counters64.get(4);
-        u32* d_tins = tail_ins_buf.get(16);
         const u64 tail_bound = tail_reached ? (u64)N - hsegs[chain.back()].start + 1 : 0;
         u32* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
         if (tail_reached) {
-            const seg_in tin = hsegs[chain.back()];
-            k_tail<<<1, 64, 0, st>>>(W, tin, fo, chain_fact, d_cnt, d_tins);
+            u64* d_cnt = counters64.get(4);
+            u32* d_tins = tail_ins_buf.get(16);
+            k_tail<<<1, 64, 0, st>>>(W, hsegs[chain.back()], fo, chain_fact, d_cnt, d_tins);
             LZ_HIP(hipGetLastError());
             u64 hc[3];
             u32 hti[16];
@@ -703,9 +986,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             if (hc[2]) throw error(-6, "greedy tail: insert overflow or guard tripped");
             tail_count = hc[0];
             for (u64 k = 0; k < hc[1]; k++) tail_ins.push_back({hti[2 * k], hti[2 * k + 1]});
+            lap("tail");
         }
-        // ---- 5. actual insert set along the chain
-        std::vector<interval> I2 = tail_ins;
+        // ---- the insert set the chain actually produced
+        ivec I2 = tail_ins;
+        I2.reserve(tail_ins.size() + 2 * nchain);
         for (size_t c = 0; c < nchain; c++) {
             const seg_in& si = hsegs[chain[c]];
             const seg_out& o = houts[chain[c]];
@@ -715,35 +1000,116 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         clip(I2, G.nt);
         bool same = I2.size() == I.size();
         for (size_t k = 0; same && k < I.size(); k++) same = I2[k].a == I[k].a && I2[k].b == I[k].b;
-        if (!same) {
-            I.swap(I2);
-            starts.clear();
-            for (auto& sg : hsegs) starts.push_back(sg.start);
-            std::sort(starts.begin(), starts.end());
-            starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+        lap("insert set");
+        if (same) {
+            // ---- every lookup of the chain was exact: emit the factors
+            if (nchain) {
+                std::vector<u64> offs(nchain);
+                std::vector<seg_in> cin(nchain);
+                u64 o = 0;
+                for (size_t c = 0; c < nchain; c++) { offs[c] = o; o += houts[chain[c]].nfact; cin[c] = hsegs[chain[c]]; }
+                u64* doffs = seg_offs.get(nchain);
+                seg_in* ds = seg_in_buf.get(nchain);
+                LZ_HIP(hipMemcpyAsync(ds, cin.data(), nchain * sizeof(seg_in), hipMemcpyHostToDevice, st));
+                LZ_HIP(hipMemcpyAsync(doffs, offs.data(), nchain * 8, hipMemcpyHostToDevice, st));
+                k_walk<true><<<cdiv(nchain, 64), 64, 0, st>>>(W, ds, (u32)nchain, nullptr, doffs, fo);
+                LZ_HIP(hipGetLastError());
+                lap("write");
+            }
+            total_fact = chain_fact + tail_count;
+            break;
+        }
+        // ---- I changed: the positions that joined (1) or left (0) it
+        const ivec joined_iv = subtract(I2, I), left_iv = subtract(I, I2);
+        std::vector<u32> ys;
+        std::vector<u8> yj;
+        for (auto& iv : joined_iv)
+            for (u32 q = iv.a; q < iv.b; q++) { ys.push_back(q); yj.push_back(1); }
+        for (auto& iv : left_iv)
+            for (u32 q = iv.a; q < iv.b; q++) { ys.push_back(q); yj.push_back(0); }
+        I.swap(I2);
+        const u64 outside = total_len(subtract(I, Ib));
+        if (outside * 50 > nb) {
+            // many positions outside the base set: rebuild it as I u I_b, re-walk everything
+            ivec Inew = I;
+            Inew.insert(Inew.end(), Ib.begin(), Ib.end());
+            normalize(Inew);
+            build_base(Inew);
+            set_state(I);
+            std::fill(valid.begin(), valid.end(), 0);
+            todo.clear();
+            for (u32 g = 0; g < hsegs.size(); g++) todo.push_back(g);
+            if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy rebuild: outside=%llu\n", (unsigned long long)outside);
             continue;
         }
-        // ---- write pass for the chain segments (before the tail segment)
-        if (nchain) {
-            std::vector<u64> offs(nchain);
-            std::vector<u32> ids(nchain);
-            u64 o = 0;
-            for (size_t c = 0; c < nchain; c++) { offs[c] = o; o += houts[chain[c]].nfact; ids[c] = chain[c]; }
-            u64* doffs = seg_offs.get(nchain);
-            std::vector<seg_in> cin(nchain);
-            for (size_t c = 0; c < nchain; c++) cin[c] = hsegs[chain[c]];
-            seg_in* ds = d_segs.get(nchain);
-            LZ_HIP(hipMemcpyAsync(ds, cin.data(), nchain * sizeof(seg_in), hipMemcpyHostToDevice, st));
-            LZ_HIP(hipMemcpyAsync(doffs, offs.data(), nchain * 8, hipMemcpyHostToDevice, st));
-            k_walk<true><<<cdiv(nchain, 64), 64, 0, st>>>(W, ds, nullptr, (u32)nchain, nullptr, doffs, fo);
-            LZ_HIP(hipGetLastError());
+        // dirty = changed positions + their same-slot successors before and after the update
+        const u64 ny = ys.size();
+        u32* d_y = dirty_in.get(ny + 1);
+        u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
+        u32* d_d = dirty_out.get(11 * ny + 1);
+        LZ_HIP(hipMemcpyAsync(d_y, ys.data(), ny * 4, hipMemcpyHostToDevice, st));
+        LZ_HIP(hipMemcpyAsync(d_j, yj.data(), ny, hipMemcpyHostToDevice, st));
+        LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * 4, hipMemcpyDeviceToDevice, st));
+        k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + ny);
+        k_flip<<<cdiv(ny, 256), 256, 0, st>>>(W, d_y, d_j, ny, (u8*)W.rem, d_j + ny);
+        std::vector<u8> inb(ny);
+        LZ_HIP(hipMemcpyAsync(inb.data(), d_j + ny, ny, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        bool a_changed = false;
+        {
+            std::vector<u32> add, del;
+            for (u64 k = 0; k < ny; k++)
+                if (!inb[k]) (yj[k] ? add : del).push_back(ys[k]);
+            if (!add.empty() || !del.empty()) {
+                a_changed = true;
+                std::sort(add.begin(), add.end());
+                std::sort(del.begin(), del.end());
+                std::vector<u32> tmp;
+                std::set_difference(A_pos.begin(), A_pos.end(), del.begin(), del.end(), std::back_inserter(tmp));
+                A_pos.clear();
+                std::merge(tmp.begin(), tmp.end(), add.begin(), add.end(), std::back_inserter(A_pos));
+            }
         }
-        total_fact = chain_fact + tail_count;
-        break;
+        if (a_changed) rebuild_added();
+        k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + 6 * ny);
+        // sort dirty positions (NONE entries sort last and are ignored)
+        u32* d_ds = dirty_sorted.get(11 * ny + 1);
+        {
+            size_t tb = 0;
+            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, d_d, d_ds, (int)(11 * ny), 0, 32, st));
+            u8* t = scan_tmp.get(tb);
+            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, d_d, d_ds, (int)(11 * ny), 0, 32, st));
+        }
+        // staleness of every walked segment
+        const u64 ns = hsegs.size();
+        std::vector<u32> lo(ns), hi(ns);
+        for (u64 g = 0; g < ns; g++) {
+            lo[g] = hsegs[g].start;
+            hi[g] = (houts[g].flags & 1) ? N : std::max(houts[g].next, houts[g].e + 1);
+        }
+        u32* d_lo = seg_lo.get(ns);
+        u32* d_hi = seg_hi.get(ns);
+        u8* d_st = (u8*)tmp_greedy3.get(ns);
+        LZ_HIP(hipMemcpyAsync(d_lo, lo.data(), ns * 4, hipMemcpyHostToDevice, st));
+        LZ_HIP(hipMemcpyAsync(d_hi, hi.data(), ns * 4, hipMemcpyHostToDevice, st));
+        k_stale<<<cdiv(ns, 256), 256, 0, st>>>(d_lo, d_hi, ns, d_ds, 11 * ny, d_st);
+        std::vector<u8> stale(ns);
+        LZ_HIP(hipMemcpyAsync(stale.data(), d_st, ns, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        todo.clear();
+        for (u64 g = 0; g < ns; g++) {
+            if (stale[g]) valid[g] = 0;
+            if (!valid[g]) todo.push_back((u32)g);
+        }
+        lap("delta + dirty");
+        if (dbg)
+            std::fprintf(stderr, "[lz77sss-debug] greedy delta: changed=%llu outside=%zu rewalk=%zu\n",
+                         (unsigned long long)ny, A_pos.size(), todo.size());
     }
     stats[12] = outer + 1;
     stats[13] = rounds_total;
     stats[14] = stats_fallback_lanes;
+    stats[15] = walked_total;
     return total_fact;
 }
 

@@ -97,7 +97,10 @@ struct engine {
 
     // ---- greedy ----
     dbuf<u32> fact;                  // output factors (src,len) pairs
-    dbuf<u8> tmp_greedy, chunk_buf;
+    dbuf<u8> tmp_greedy, chunk_buf, chunk_buf2, rem_buf;
+    dbuf<u32> add_keys32, add_pos, dirty_in, dirty_out, dirty_sorted, seg_lo, seg_hi;
+    dbuf<u8> tmp_greedy2, tmp_greedy3;
+    dbuf<u64> add_keys, add_keys2;
     dbuf<seg_in> seg_in_buf;
     dbuf<seg_out> seg_out_buf;
     dbuf<u32> seg_ids, ist, iend, irank, ekeys, evals, ekeys2, evals2, ipos_buf, occ_buf, tail_ins_buf;
