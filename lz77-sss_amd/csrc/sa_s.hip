@@ -120,6 +120,140 @@ __global__ void k_succ_table(const u32* __restrict__ S, u32 s, u64 nb, u32* __re
     tab[bkt] = lo;
 }
 
+// ---------------------------------------------------------------------------
+// key deduplication (exact: hash groups are verified by full comparison)
+__device__ __forceinline__ u64 mix64(u64 z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+// one wave per key: h = sum over 8-byte words w of mix(word_w + w*C) + mix(len)
+__global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, const u32* __restrict__ S,
+                                                  const u32* __restrict__ KL, u32 s, u64* __restrict__ H) {
+    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const u32 lane = threadIdx.x & 63;
+    if (k >= s) return;
+    const u64 beg = S[k], len = KL[k];
+    u64 h = 0;
+    for (u64 w = lane; 8 * w < len; w += 64) {
+        u64 x = ldu64(T + beg + 8 * w);
+        const u64 rem = len - 8 * w;
+        if (rem < 8) x &= (1ull << (8 * rem)) - 1;
+        h += mix64(x + w * 0x9e3779b97f4a7c15ull);
+    }
+    for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o);
+    if (lane == 0) H[k] = h + mix64(len ^ 0xd6e8feb86659fd93ull);
+}
+// wave-parallel exact comparison of two keys (all 64 lanes must call it)
+__device__ int wave_key_cmp(const u8* T, const u32* S, const u32* KL, u32 a, u32 b, u32 lane) {
+    const u64 la = KL[a], lb = KL[b], m = min(la, lb);
+    const u64 pa = S[a], pb = S[b];
+    for (u64 o = 0; o < m; o += 512) {
+        const u64 off = o + 8 * lane;
+        bool diff = false;
+        if (off < m) {
+            u64 x = ldu64(T + pa + off), y = ldu64(T + pb + off);
+            const u64 r = m - off;
+            if (r < 8) { const u64 msk = (1ull << (8 * r)) - 1; x &= msk; y &= msk; }
+            diff = x != y;
+        }
+        const u64 bal = __ballot(diff);
+        if (bal) {
+            const u32 first = __builtin_ctzll(bal);
+            const u64 fo = o + 8 * first;
+            const u64 x = ldu64(T + pa + fo), y = ldu64(T + pb + fo);
+            const u32 byte = __builtin_ctzll(x ^ y) >> 3;
+            return T[pa + fo + byte] < T[pb + fo + byte] ? -1 : 1;
+        }
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+// flags: new group where the hash changes; exact check of equal-hash neighbours
+__global__ __launch_bounds__(256) void k_group_verify(const u8* T, const u32* S, const u32* KL,
+                                                      const u64* __restrict__ Hs, const u32* __restrict__ idx,
+                                                      u32 s, u32* __restrict__ flag, u32* __restrict__ collide) {
+    const u64 t = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const u32 lane = threadIdx.x & 63;
+    if (t >= s) return;
+    if (t == 0 || Hs[t] != Hs[t - 1]) {
+        if (lane == 0) flag[t] = 1;
+        return;
+    }
+    const int c = wave_key_cmp(T, S, KL, idx[t - 1], idx[t], lane);
+    if (lane == 0) {
+        flag[t] = 0;
+        if (c != 0) atomicOr(collide, 1u);
+    }
+}
+__global__ void k_reps(const u32* __restrict__ flag, const u32* __restrict__ grp, const u32* __restrict__ idx, u32 s,
+                       u32* __restrict__ rep) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < s && flag[t]) rep[grp[t] - 1] = idx[t];
+}
+// bounded comparison (first CMP_BOUND bytes of each key)
+constexpr u64 CMP_BOUND = 2048;
+struct rep_less_bounded {
+    const u8* T;
+    const u32* S;
+    const u32* KL;
+    __device__ bool operator()(const u32& a, const u32& b) const {
+        const u64 la = min<u64>(KL[a], CMP_BOUND), lb = min<u64>(KL[b], CMP_BOUND), m = min(la, lb);
+        const u64 c = dev_naive_lce(T, S[a], S[b], m);
+        if (c < m) return T[(u64)S[a] + c] < T[(u64)S[b] + c];
+        // equal within the bound: stays in input order (stable sort), resolved exactly afterwards.
+        // NB: an explicit index tie-break here makes rocprim's merge sort hang on gfx950.
+        return la < lb;
+    }
+};
+__global__ void k_tie_flags(const u8* T, const u32* S, const u32* KL, const u32* __restrict__ srt, u32 d,
+                            u8* __restrict__ tie) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= d) return;
+    if (r == 0) { tie[0] = 0; return; }
+    const u32 a = srt[r - 1], b = srt[r];
+    const u64 la = min<u64>(KL[a], CMP_BOUND), lb = min<u64>(KL[b], CMP_BOUND);
+    tie[r] = (la == lb && dev_naive_lce(T, S[a], S[b], la) == la) ? 1 : 0;
+}
+// one wave per tie segment: insertion sort with exact wave comparisons
+__global__ __launch_bounds__(64) void k_sort_ties(const u8* T, const u32* S, const u32* KL, u32* __restrict__ srt,
+                                                  const u32* __restrict__ seg_beg, const u32* __restrict__ seg_len) {
+    const u32 lane = threadIdx.x;
+    u32* a = srt + seg_beg[blockIdx.x];
+    const u32 m = seg_len[blockIdx.x];
+    for (u32 i = 1; i < m; i++) {
+        const u32 x = a[i];
+        int j = (int)i - 1;
+        while (j >= 0 && wave_key_cmp(T, S, KL, a[j], x, lane) > 0) {
+            __syncthreads();
+            if (lane == 0) a[j + 1] = a[j];
+            __syncthreads();
+            j--;
+        }
+        __syncthreads();
+        if (lane == 0) a[j + 1] = x;
+        __syncthreads();
+    }
+}
+__global__ void k_rank_of_group(const u32* __restrict__ srt_grp, u32 d, u32* __restrict__ rank_of) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < d) rank_of[srt_grp[r]] = (u32)r + 1;
+}
+__global__ void k_r0_from_groups(const u32* __restrict__ idx, const u32* __restrict__ grp, const u32* __restrict__ rank_of,
+                                 u32 s, u32* __restrict__ R0) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < s) R0[idx[t]] = rank_of[grp[t] - 1];
+}
+__global__ void k_map_rep_to_group(const u32* __restrict__ srt_key, u32 d, const u32* __restrict__ key_to_grp,
+                                   u32* __restrict__ srt_grp) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < d) srt_grp[r] = key_to_grp[srt_key[r]];
+}
+__global__ void k_key_to_grp(const u32* __restrict__ flag, const u32* __restrict__ grp, const u32* __restrict__ idx,
+                             u32 s, u32* __restrict__ key_to_grp) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < s && flag[t]) key_to_grp[idx[t]] = grp[t] - 1;
+}
+
 static void scan_incl(u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
     size_t tb = 0;
     LZ_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out, (int)m, st));
@@ -134,25 +268,91 @@ void engine::build_sa_s(const u8* T) {
     u32* KL = key_len.get(s);
     const unsigned g = cdiv(s, 256);
     k_key_len<<<g, 256, 0, st>>>(dS, s, n, KL);
-    // ---- R_0: comparison merge sort of the keys
+    // ---- R_0: lexicographic rank of the keys (equal keys share a rank)
     u32* idx_in = u32a.get(s);
     u32* idx = u32b.get(s);
-    k_iota<<<g, 256, 0, st>>>(idx_in, s);
+    u32* flag = u32c.get(s);
+    u32* rank = u32d.get(s);
+    u32* R0 = rank_lv[0].get(s);
+    bool done_r0 = false;
     {
+        // 1. group identical keys by a wave-parallel hash, verified exactly
+        u64* H = u64a.get(s);
+        u64* Hs = u64b.get(s);
+        k_key_hash<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, dS, KL, s, H);
+        k_iota<<<g, 256, 0, st>>>(idx_in, s);
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, H, Hs, idx_in, idx, (int)s, 0, 64, st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, H, Hs, idx_in, idx, (int)s, 0, 64, st));
+        u32* ctr = counters.get(16);
+        LZ_HIP(hipMemsetAsync(ctr + 2, 0, 4, st));
+        k_group_verify<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, dS, KL, Hs, idx, s, flag, ctr + 2);
+        scan_incl(flag, rank, s, scan_tmp, st);  // rank[t] = group id + 1
+        const u32 collide = rd1(ctr + 2, st);
+        if (debug_enabled()) fprintf(stderr, "[sa_s] s=%u collide=%u\n", s, collide);
+        if (!collide) {
+            const u32 d = rd1(rank + s - 1, st);
+            u32* rep = sa_tmp1.get(d);
+            k_reps<<<g, 256, 0, st>>>(flag, rank, idx, s, rep);
+            // 2. sort distinct keys: bounded comparison, then exact wave sort of bounded ties
+            u32* srt = sa_tmp2.get(d);
+            {
+                size_t tb2 = 0;
+                rep_less_bounded cmp{T, dS, KL};
+                LZ_HIP(rocprim::merge_sort(nullptr, tb2, rep, srt, (size_t)d, cmp, st));
+                u8* t2 = scan_tmp.get(tb2);
+                LZ_HIP(rocprim::merge_sort(t2, tb2, rep, srt, (size_t)d, cmp, st));
+            }
+            u8* tie = tmp_bytes.get(d);
+            k_tie_flags<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, tie);
+            if (debug_enabled()) fprintf(stderr, "[sa_s] distinct=%u sorted\n", d);
+            std::vector<u8> htie(d);
+            LZ_HIP(hipMemcpyAsync(htie.data(), tie, d, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));
+            std::vector<u32> sb, sl;
+            for (u32 r = 1; r < d;) {
+                if (!htie[r]) { r++; continue; }
+                u32 e = r;
+                while (e < d && htie[e]) e++;
+                sb.push_back(r - 1);
+                sl.push_back(e - r + 1);
+                r = e;
+            }
+            if (debug_enabled()) fprintf(stderr, "[sa_s] tie segments=%zu\n", sb.size());
+            if (!sb.empty()) {
+                u32* dsb = sa_tmp3.get(2 * sb.size());
+                LZ_HIP(hipMemcpyAsync(dsb, sb.data(), sb.size() * 4, hipMemcpyHostToDevice, st));
+                LZ_HIP(hipMemcpyAsync(dsb + sb.size(), sl.data(), sl.size() * 4, hipMemcpyHostToDevice, st));
+                k_sort_ties<<<(unsigned)sb.size(), 64, 0, st>>>(T, dS, KL, srt, dsb, dsb + sb.size());
+            }
+            // 3. ranks: sorted distinct keys -> groups -> every key
+            u32* key_to_grp = idx_in;  // free now
+            k_key_to_grp<<<g, 256, 0, st>>>(flag, rank, idx, s, key_to_grp);
+            u32* srt_grp = sa_tmp1.p;  // rep no longer needed
+            k_map_rep_to_group<<<cdiv(d, 256), 256, 0, st>>>(srt, d, key_to_grp, srt_grp);
+            u32* rank_of = sa_tmp3.get(std::max<size_t>(2 * sb.size(), d));
+            k_rank_of_group<<<cdiv(d, 256), 256, 0, st>>>(srt_grp, d, rank_of);
+            k_r0_from_groups<<<g, 256, 0, st>>>(idx, rank, rank_of, s, R0);
+            stats_sa_distinct = d;
+            stats_sa_ties = sb.size();
+            done_r0 = true;
+        }
+    }
+    if (!done_r0) {
+        // hash collision between different keys: exact comparison sort of all keys
+        k_iota<<<g, 256, 0, st>>>(idx_in, s);
         size_t tb = 0;
         key_less cmp{T, dS, KL};
         LZ_HIP(rocprim::merge_sort(nullptr, tb, idx_in, idx, (size_t)s, cmp, st));
         u8* t = scan_tmp.get(tb);
         LZ_HIP(rocprim::merge_sort(t, tb, idx_in, idx, (size_t)s, cmp, st));
+        k_key_diff<<<g, 256, 0, st>>>(T, dS, KL, idx, s, flag);
+        scan_incl(flag, rank, s, scan_tmp, st);
+        k_scatter_rank<<<g, 256, 0, st>>>(idx, rank, s, R0);
     }
-    u32* flag = u32c.get(s);
-    u32* rank = u32d.get(s);
-    k_key_diff<<<g, 256, 0, st>>>(T, dS, KL, idx, s, flag);
-    scan_incl(flag, rank, s, scan_tmp, st);
-    u32* R0 = rank_lv[0].get(s);
-    k_scatter_rank<<<g, 256, 0, st>>>(idx, rank, s, R0);
     nlev_rank = 1;
-    u32 maxr = rd1(rank + s - 1, st);
+    u32 maxr = done_r0 ? (u32)stats_sa_distinct : rd1(rank + s - 1, st);
     // ---- prefix doubling over the sequence of key ranks
     u32 bits = 1;
     while (bits < 32 && (1ull << bits) <= s) bits++;

@@ -85,6 +85,8 @@ struct engine {
     dbuf<u32> succ_tab;              // bucket -> first sync index with S >= bucket*512
     dbuf<u8> tmp_bytes, scan_tmp;
     dbuf<u64> u64a, u64b;
+    dbuf<u32> sa_tmp1, sa_tmp2, sa_tmp3;
+    u64 stats_sa_distinct = 0, stats_sa_ties = 0;
     dbuf<u32> u32a, u32b, u32c, u32d, u32e;
 
     // ---- LPF phrases ----
