@@ -1,0 +1,207 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 3-approximate LZ77 factorization MB/s on a 1 GiB text.
+
+Metric (BASELINE.json): "factorization MB/s + factor count, 3-aprx on 1 GiB
+repetitive text".  One *step* = one full ``factorize_approximate<greedy,
+lpf_opt, 512>`` of the text (SSS -> SA_S/LCP/RMQ -> LPF_opt -> greedy emitter,
+factors left in HBM), the text already resident in HBM when the timed region
+starts.  MB = 10^6 bytes as the reference's
+``throughput`` helper (utils.hpp:88-91).
+
+Workloads:
+  rr      random_repetitive_string(2^30, 2^30) with repetition 0.5, run 0.05,
+          seed 42 (+rank) -- configs[1] of BASELINE.json (default)
+  genome  4-letter 64 MiB base block repeated with 0.1% point mutations, seed 7
+
+Multi-GPU (``--gpus N`` under torch.distributed.run): the texts are
+independent objects, one 1 GiB text per rank (seed 42 + rank); no data-path
+collective, the barrier/max-over-ranks timing only (weak scaling).
+
+Also reported:
+  roofline      the SSS kernel (k_sss_main), algorithmic bytes n + 4|S| per
+                launch over its HIP-event time on the library's own stream,
+                against the 8 TB/s HBM3E peak; ``traffic`` from the committed
+                rocprofv3 PMC summary (profiles/) when one exists for this
+                workload, else null.
+  cpu_baseline  the CPU oracle (a port of the reference algorithm, OpenMP) on
+                rank 0 at N=1, on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "lz77-sss_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+GIB = 1 << 30
+
+
+def make_text(lz, workload: str, n: int, rank: int):
+    if workload == "rr":
+        return lz.gen_random_repetitive(n, n, 42 + rank, 0.5, 0.05)
+    if workload == "genome":
+        return lz.gen_genome(n, 64 << 20, 0.001, 7 + rank)
+    raise SystemExit(f"unknown workload {workload}")
+
+
+def aggregate(dt_local: float, n_per_rank: int, world: int, dist=None, device="cpu"):
+    """Max step time over ranks and the whole-job MB/s (every rank processed its own n bytes)."""
+    dt = dt_local
+    if dist is not None and world > 1:
+        import torch
+
+        t = torch.tensor([dt_local], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, world * n_per_rank / dt / 1e6
+
+
+def pmc_traffic(workload: str, n: int):
+    """Per-launch HBM bytes of k_sss_main from profiles/*_pmc_sss.json (rocprofv3 --pmc passes)."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("*_pmc_sss.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and int(d.get("n", -1)) == n:
+            best = d
+    return None if best is None else best.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(lz, workload: str, sample_mib: int):
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle  # the CPU port (test/bench infrastructure only)
+
+    n = sample_mib << 20
+    T = make_text(lz, workload, n, 0)
+    z, sec, _ = oracle.factorize_timed(T)
+    desc = ("full 1 GiB workload text" if n == GIB else f"first {sample_mib} MiB-sized instance of the same generator")
+    return {"value": round(n / sec / 1e6, 2), "unit": "MB/s", "cores": oracle.num_threads(), "kind": "port",
+            "sample": f"{workload}: {desc} (n={n}, z={z}), oracle factorize_approximate<greedy,lpf_opt> p=1 "
+                      f"restatement with OpenMP stages, {sec:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="rr", choices=["rr", "genome"])
+    ap.add_argument("--size-mib", type=int, default=1024)
+    ap.add_argument("--cpu-sample-mib", type=int, default=-1,
+                    help="oracle sample size (default: full text for rr, 128 MiB for genome)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    import torch
+    import lz77sss as lz
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    n = args.size_mib << 20
+    T = make_text(lz, args.workload, n, rank)
+    sess = lz.Session(n, device=local_rank)
+    t_load0 = time.perf_counter()
+    sess.load(T)
+    t_load = time.perf_counter() - t_load0
+
+    for _ in range(args.warmup):
+        sess.factorize(device=local_rank)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    kern_ms, kern_bytes = [], []
+    barrier()
+    t0 = time.perf_counter()
+    z = 0
+    for _ in range(args.steps):
+        z = sess.factorize(device=local_rank)
+        ms, b = sess.sss_kernel_time()
+        kern_ms.append(ms)
+        kern_bytes.append(b)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    dt, value = aggregate((t1 - t0) / args.steps, n, world, dist, device="cuda")
+
+    phases = sess.phase_times()
+    st = sess.stats()
+    # PCIe-inclusive rate of one call (host text in, factors out), reported beside the HBM-resident value
+    t_out0 = time.perf_counter()
+    F = sess.factors(z)
+    t_out = time.perf_counter() - t_out0
+    del F
+
+    if rank == 0:
+        avg_ms = sum(kern_ms) / len(kern_ms)
+        bytes_launch = kern_bytes[-1]
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+        out = {
+            "metric": "factorization MB/s (3-aprx LZ77, greedy + lpf_opt, tau=512)",
+            "value": round(value, 2),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded restatement of the reference's random_repetitive_string)"
+            if args.workload == "rr" else "synthetic (genome-like: 64 MiB ACGT base block, 0.1% mutations)",
+            "config": {
+                "workload": f"{args.workload} n={n} ({args.size_mib} MiB) per GPU, pos_t=uint32",
+                "n": n, "tau": 512, "phr_mode": "lpf_opt", "fact_mode": "greedy", "virtual_p": 1,
+                "parallelism": f"independent-texts x{world}" if world > 1 else "single GPU",
+                "factors": int(z), "comp_ratio": round(n / max(z, 1), 2),
+                "sss_size": int(st[0]) if st else None, "has_runs": bool(st[1]) if st else None,
+                "lpf_phrases": int(st[2]) if st else None,
+                "phase_ms": {k: round(v, 3) for k, v in phases.items()},
+                "pcie_inclusive_mbps": round(n / (dt + t_load + t_out) / 1e6, 2),
+            },
+            "roofline": {
+                "kernel": "k_sss_main",
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic(args.workload, n),
+                "algorithmic_bytes_per_launch": int(bytes_launch),
+                "avg_launch_ms": round(avg_ms, 4),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else (
+                args.size_mib if args.workload == "rr" else min(128, args.size_mib))
+            out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample)
+        print(json.dumps(out), flush=True)
+    sess.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

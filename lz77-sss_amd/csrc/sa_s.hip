@@ -14,7 +14,6 @@
 #include "../include/lce_dev.h"
 
 #include <hipcub/hipcub.hpp>
-#include <rocprim/rocprim.hpp>
 
 namespace lz {
 
@@ -201,7 +200,6 @@ struct rep_less_bounded {
         const u64 c = dev_naive_lce(T, S[a], S[b], m);
         if (c < m) return T[(u64)S[a] + c] < T[(u64)S[b] + c];
         // equal within the bound: stays in input order (stable sort), resolved exactly afterwards.
-        // NB: an explicit index tie-break here makes rocprim's merge sort hang on gfx950.
         return la < lb;
     }
 };
@@ -254,6 +252,67 @@ __global__ void k_key_to_grp(const u32* __restrict__ flag, const u32* __restrict
     if (t < s && flag[t]) key_to_grp[idx[t]] = grp[t] - 1;
 }
 
+// ---------------------------------------------------------------------------
+// Stable comparison merge sort of u32 items (own implementation; the
+// comparator reads the text).  Pass 0: every thread insertion-sorts RUN
+// consecutive items; then merge-path passes double the run width.
+constexpr u32 RUN = 8;
+constexpr u32 MPT = 8;  // outputs per thread in a merge pass
+template <class C>
+__global__ void k_msort_runs(const u32* __restrict__ in, u32* __restrict__ out, u32 d, C cmp) {
+    const u64 b = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * RUN;
+    if (b >= d) return;
+    const u32 m = (u32)min<u64>(RUN, d - b);
+    u32 v[RUN];
+    for (u32 i = 0; i < m; i++) v[i] = in[b + i];
+    for (u32 i = 1; i < m; i++) {
+        const u32 x = v[i];
+        int j = (int)i - 1;
+        while (j >= 0 && cmp(x, v[j])) { v[j + 1] = v[j]; j--; }
+        v[j + 1] = x;
+    }
+    for (u32 i = 0; i < m; i++) out[b + i] = v[i];
+}
+template <class C>
+__global__ void k_msort_merge(const u32* __restrict__ in, u32* __restrict__ out, u32 d, u32 w, C cmp) {
+    const u64 p0 = ((u64)blockIdx.x * blockDim.x + threadIdx.x) * MPT;
+    if (p0 >= d) return;
+    const u64 base = p0 / (2ull * w) * (2ull * w);
+    const u64 a0 = base, a1 = min<u64>(base + w, d), b0 = a1, b1 = min<u64>(base + 2ull * w, d);
+    const u64 la = a1 - a0, lb = b1 - b0;
+    const u64 diag = p0 - base;
+    // merge path: i items from A, diag - i from B; A wins ties (stable)
+    u64 lo = diag > lb ? diag - lb : 0, hi = min(diag, la);
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        // take A[mid] before B[diag-1-mid] iff !(B < A)
+        if (!cmp(in[b0 + diag - 1 - mid], in[a0 + mid])) lo = mid + 1; else hi = mid;
+    }
+    u64 i = lo, j = diag - lo;
+    const u64 pend = min<u64>(p0 + MPT, b1);
+    for (u64 p = p0; p < pend; p++) {
+        bool takeA;
+        if (i >= la) takeA = false;
+        else if (j >= lb) takeA = true;
+        else takeA = !cmp(in[b0 + j], in[a0 + i]);
+        out[p] = takeA ? in[a0 + i++] : in[b0 + j++];
+    }
+}
+// sorts `a` (d items) stably; `tmp` has room for d items; result left in `a`
+template <class C>
+static void merge_sort_u32(u32* a, u32* tmp, u32 d, C cmp, hipStream_t st) {
+    if (d <= 1) return;
+    k_msort_runs<<<cdiv(cdiv(d, RUN), 256), 256, 0, st>>>(a, tmp, d, cmp);
+    u32* src = tmp;
+    u32* dst = a;
+    for (u64 w = RUN; w < d; w *= 2) {
+        k_msort_merge<<<cdiv(cdiv(d, MPT), 256), 256, 0, st>>>(src, dst, d, (u32)w, cmp);
+        std::swap(src, dst);
+    }
+    if (src != a) LZ_HIP(hipMemcpyAsync(a, src, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+    LZ_HIP(hipGetLastError());
+}
+
 static void scan_incl(u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
     size_t tb = 0;
     LZ_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out, (int)m, st));
@@ -296,14 +355,8 @@ void engine::build_sa_s(const u8* T) {
             u32* rep = sa_tmp1.get(d);
             k_reps<<<g, 256, 0, st>>>(flag, rank, idx, s, rep);
             // 2. sort distinct keys: bounded comparison, then exact wave sort of bounded ties
-            u32* srt = sa_tmp2.get(d);
-            {
-                size_t tb2 = 0;
-                rep_less_bounded cmp{T, dS, KL};
-                LZ_HIP(rocprim::merge_sort(nullptr, tb2, rep, srt, (size_t)d, cmp, st));
-                u8* t2 = scan_tmp.get(tb2);
-                LZ_HIP(rocprim::merge_sort(t2, tb2, rep, srt, (size_t)d, cmp, st));
-            }
+            u32* srt = rep;
+            merge_sort_u32(srt, sa_tmp2.get(d), d, rep_less_bounded{T, dS, KL}, st);
             u8* tie = tmp_bytes.get(d);
             k_tie_flags<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, tie);
             if (debug_enabled()) fprintf(stderr, "[sa_s] distinct=%u sorted\n", d);
@@ -329,9 +382,9 @@ void engine::build_sa_s(const u8* T) {
             // 3. ranks: sorted distinct keys -> groups -> every key
             u32* key_to_grp = idx_in;  // free now
             k_key_to_grp<<<g, 256, 0, st>>>(flag, rank, idx, s, key_to_grp);
-            u32* srt_grp = sa_tmp1.p;  // rep no longer needed
+            u32* srt_grp = sa_tmp2.p;  // merge scratch, free now
             k_map_rep_to_group<<<cdiv(d, 256), 256, 0, st>>>(srt, d, key_to_grp, srt_grp);
-            u32* rank_of = sa_tmp3.get(std::max<size_t>(2 * sb.size(), d));
+            u32* rank_of = srt;  // sorted reps consumed by k_map_rep_to_group (stream order)
             k_rank_of_group<<<cdiv(d, 256), 256, 0, st>>>(srt_grp, d, rank_of);
             k_r0_from_groups<<<g, 256, 0, st>>>(idx, rank, rank_of, s, R0);
             stats_sa_distinct = d;
@@ -341,12 +394,8 @@ void engine::build_sa_s(const u8* T) {
     }
     if (!done_r0) {
         // hash collision between different keys: exact comparison sort of all keys
-        k_iota<<<g, 256, 0, st>>>(idx_in, s);
-        size_t tb = 0;
-        key_less cmp{T, dS, KL};
-        LZ_HIP(rocprim::merge_sort(nullptr, tb, idx_in, idx, (size_t)s, cmp, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(rocprim::merge_sort(t, tb, idx_in, idx, (size_t)s, cmp, st));
+        k_iota<<<g, 256, 0, st>>>(idx, s);
+        merge_sort_u32(idx, idx_in, s, key_less{T, dS, KL}, st);
         k_key_diff<<<g, 256, 0, st>>>(T, dS, KL, idx, s, flag);
         scan_incl(flag, rank, s, scan_tmp, st);
         k_scatter_rank<<<g, 256, 0, st>>>(idx, rank, s, R0);

@@ -1,0 +1,172 @@
+"""ctypes wrapper of the CPU oracle (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module; the product path
+(``lz77-sss_amd/``) never does.  The oracle is a CPU restatement of the
+reference algorithm (see ``oracle.hpp``); parity is *unpinned* against the
+reference binary because the reference cannot be built here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "_build" / "liboracle.so"
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+_lib = None
+
+LPF_OPT, LPF_LNF_OPT = 2, 3
+
+
+def build(force: bool = False) -> Path:
+    src_newer = any(p.stat().st_mtime > LIB.stat().st_mtime for p in HERE.glob("oracle*.?pp")) if LIB.exists() else True
+    if force or src_newer:
+        subprocess.run(["make", "-s", "-C", str(HERE), f"-j{min(8, os.cpu_count() or 1)}"], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        L = ctypes.CDLL(str(LIB))
+        L.oracle_factorize_approx.restype = ctypes.c_int64
+        L.oracle_factorize_approx.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, _P, _U64, _P]
+        L.oracle_factorize_timed.restype = ctypes.c_int64
+        L.oracle_factorize_timed.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(_U64)]
+        L.oracle_sss.restype = ctypes.c_int64
+        L.oracle_sss.argtypes = [_P, _U64, _P, _U64, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_q_bruteforce.restype = None
+        L.oracle_q_bruteforce.argtypes = [_P, _U64, _P]
+        L.oracle_phi.restype = None
+        L.oracle_phi.argtypes = [_P, _U64, _P]
+        L.oracle_sa_s.restype = ctypes.c_int64
+        L.oracle_sa_s.argtypes = [_P, _U64, _P, _P, _P, _U64]
+        L.oracle_lce.restype = None
+        L.oracle_lce.argtypes = [_P, _U64, _P, _P, _U64, _P]
+        L.oracle_lpf_opt.restype = ctypes.c_int64
+        L.oracle_lpf_opt.argtypes = [_P, _U64, _P, _U64]
+        L.oracle_decode.restype = None
+        L.oracle_decode.argtypes = [_P, _U64, _P, _U64]
+        L.oracle_gap_bases.restype = None
+        L.oracle_gap_bases.argtypes = [ctypes.c_uint32, _P]
+        L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_num_threads.argtypes = []
+        _lib = L
+    return _lib
+
+
+def _u8(T) -> np.ndarray:
+    if isinstance(T, (bytes, bytearray)):
+        T = np.frombuffer(bytes(T), np.uint8)
+    return np.ascontiguousarray(T, dtype=np.uint8)
+
+
+def _padded(T) -> np.ndarray:
+    """Copy with zero padding (the oracle may read a few words past n, like the reference callers' padding)."""
+    T = _u8(T)
+    buf = np.zeros(T.size + 4096, np.uint8)
+    buf[:T.size] = T
+    return buf
+
+
+def factorize(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):
+    """lz77_sss<u32>::factorize_approximate<greedy, phr_mode, 512> at p=1 -> ((z,2) u32 factors, stats[16])."""
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros((n + 2, 2), np.uint32)
+    st = np.zeros(16, np.uint32)
+    z = lib().oracle_factorize_approx(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, out.ctypes.data_as(_P), n + 2,
+                                      st.ctypes.data_as(_P))
+    if z < 0:
+        raise RuntimeError("oracle factorization failed")
+    return out[:z].copy(), st
+
+
+def factorize_timed(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):
+    """Times the oracle factorization (output discarded into a running FNV-1a hash) -> (z, seconds, hash)."""
+    buf = _padded(T)
+    n = _u8(T).size
+    sec, h = ctypes.c_double(), _U64()
+    z = lib().oracle_factorize_timed(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, ctypes.byref(sec), ctypes.byref(h))
+    return int(z), sec.value, h.value
+
+
+def sss(T):
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros(n + 1, np.uint32)
+    hr = ctypes.c_int()
+    k = lib().oracle_sss(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), n + 1, ctypes.byref(hr))
+    return out[:k].copy(), bool(hr.value)
+
+
+def q_bruteforce(T) -> np.ndarray:
+    buf = _padded(T)
+    n = _u8(T).size
+    q = np.zeros(n + 1, np.uint8)
+    lib().oracle_q_bruteforce(buf.ctypes.data_as(_P), n, q.ctypes.data_as(_P))
+    return q[:max(n - 511, 0)]
+
+
+def phi(T) -> np.ndarray:
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros(n + 1, np.uint64)
+    lib().oracle_phi(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P))
+    return out[:max(n - 511, 0)]
+
+
+def sa_s(T):
+    """(S, SA_S, LCP) of the oracle's LCE structure."""
+    buf = _padded(T)
+    n = _u8(T).size
+    S, SA, LCP = (np.zeros(n + 1, np.uint32) for _ in range(3))
+    k = lib().oracle_sa_s(buf.ctypes.data_as(_P), n, S.ctypes.data_as(_P), SA.ctypes.data_as(_P),
+                          LCP.ctypes.data_as(_P), n + 1)
+    return S[:k].copy(), SA[:k].copy(), LCP[:k].copy()
+
+
+def lce(T, qi, qj) -> np.ndarray:
+    buf = _padded(T)
+    n = _u8(T).size
+    qi = np.ascontiguousarray(qi, np.uint32)
+    qj = np.ascontiguousarray(qj, np.uint32)
+    out = np.zeros(qi.size, np.uint32)
+    lib().oracle_lce(buf.ctypes.data_as(_P), n, qi.ctypes.data_as(_P), qj.ctypes.data_as(_P), qi.size,
+                     out.ctypes.data_as(_P))
+    return out
+
+
+def lpf_opt(T) -> np.ndarray:
+    """(beg, end, src) triples of build_LPF_opt at p=1."""
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros((n + 1, 3), np.uint32)
+    k = lib().oracle_lpf_opt(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), n + 1)
+    return out[:k].copy()
+
+
+def decode(F, n: int) -> np.ndarray:
+    F = np.ascontiguousarray(F, np.uint32)
+    out = np.zeros(max(n, 1), np.uint8)
+    lib().oracle_decode(F.ctypes.data_as(_P), F.shape[0], out.ctypes.data_as(_P), n)
+    return out[:n]
+
+
+def gap_bases(rk_seed: int) -> list[int]:
+    out = np.zeros(5, np.uint64)
+    lib().oracle_gap_bases(rk_seed, out.ctypes.data_as(_P))
+    return [int(x) for x in out]
+
+
+def num_threads() -> int:
+    return int(lib().oracle_num_threads())

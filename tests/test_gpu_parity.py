@@ -1,0 +1,156 @@
+"""GPU parity: the HIP path through the C-ABI against the oracle and the golden fixtures.
+
+Bit-exact on every intermediate the reference exposes (S, SA_S, LCP, LPF_opt
+phrases) and on the factor stream.  Full-size (1 GiB) inputs are checked by
+size-independent properties (decode round trip, factor validity) and, for the
+repetitive text, against the oracle stream itself.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def run(session, T, **kw):
+    s = session(max(T.size, 1))
+    s.load(T)
+    z = s.factorize(**kw)
+    return s, s.factors(z)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_factor_stream(session, name):
+    g = load_golden(name)
+    s, F = run(session, g["text"])
+    assert np.array_equal(F, g["factors"])
+    st = s.stats()
+    assert st[:12] == [int(x) for x in g["stats"][:12]]
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_intermediates(session, name):
+    g = load_golden(name)
+    s, _ = run(session, g["text"])
+    S, has_runs = s.sss()
+    assert np.array_equal(S, g["sss"]) and has_runs == bool(g["has_runs"][0])
+    if S.size:
+        SA, LCP = s.sa_s(S.size)
+        assert np.array_equal(SA, g["sa_s"]) and np.array_equal(LCP, g["lcp"])
+    assert np.array_equal(s.lpf(), g["lpf"])
+
+
+@pytest.mark.parametrize("seed", range(1, 17))
+def test_c1_seeds_vs_oracle(session, orc, lz, seed):
+    """Config C1: random_repetitive_string(10^4, 2·10^5), p = 1 stream."""
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    _, F = run(session, T)
+    F_ref, _ = orc.factorize(T)
+    assert np.array_equal(F, F_ref)
+    assert np.array_equal(lz.decode(F, T.size), T)
+
+
+@pytest.mark.parametrize("rk_seed", [0, 1, 7, 123456789])
+def test_gap_index_seeds(session, orc, lz, rk_seed):
+    T = lz.gen_random_repetitive(50000, 150000, 99)
+    _, F = run(session, T, rk_seed=rk_seed)
+    F_ref, _ = orc.factorize(T, rk_seed=rk_seed)
+    assert np.array_equal(F, F_ref)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 511, 512, 513, 1023, 1024, 1025, 1535, 1536, 1537, 2048, 4097, 65536,
+                               65537, 262144 + 3])
+def test_edge_sizes(session, orc, n):
+    rng = np.random.Generator(np.random.PCG64(n))
+    T = rng.integers(0, 3, n, dtype=np.uint8)
+    if n > 3000:
+        T[1000:2500] = T[100:1600]  # a long repeat -> LPF phrases
+    s, F = run(session, T)
+    F_ref, _ = orc.factorize(T)
+    assert np.array_equal(F, F_ref)
+
+
+@pytest.mark.parametrize("period", [1, 2, 5, 170, 171, 300])
+def test_runs(session, orc, period):
+    rng = np.random.Generator(np.random.PCG64(period))
+    unit = rng.integers(0, 256, period, dtype=np.uint8)
+    T = np.concatenate([rng.integers(0, 256, 3000, dtype=np.uint8), np.tile(unit, 200000 // period),
+                        rng.integers(0, 256, 5000, dtype=np.uint8), np.tile(unit, 3000 // period + 1)])
+    s, F = run(session, T)
+    F_ref, _ = orc.factorize(T)
+    assert np.array_equal(F, F_ref)
+    S, has_runs = s.sss()
+    S_ref, hr_ref = orc.sss(T)
+    assert np.array_equal(S, S_ref) and has_runs == hr_ref
+
+
+@pytest.mark.parametrize("kind,mib", [("genome", 16), ("rr", 64)])
+def test_medium_vs_oracle(session, orc, lz, kind, mib):
+    n = mib << 20
+    T = lz.gen_genome(n, 2 << 20, 0.001, 11) if kind == "genome" else lz.gen_random_repetitive(n, n, 5, 0.5, 0.05)
+    _, F = run(session, T)
+    F_ref, _ = orc.factorize(T)
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
+def test_one_shot_callback_api(lz, orc):
+    """lz77sss_factorize_approx_u32: factors arrive in order, batched, through the emit callback."""
+    T = lz.gen_random_repetitive(150000, 150000, 8)
+    got = []
+    EMIT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p)
+
+    def emit(ptr, count, user):
+        got.append(np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint32)), (count, 2)).copy())
+        return 0
+
+    cb = EMIT(emit)
+    p = lz.params()
+    rc = lz.load_library().lz77sss_factorize_approx_u32(T.ctypes.data_as(ctypes.c_void_p), T.size,
+                                                        ctypes.byref(p), cb, None)
+    assert rc == 0
+    F = np.concatenate(got)
+    assert np.array_equal(F, orc.factorize(T)[0])
+
+
+def test_invalid_parameters_fail_loudly(session, lz):
+    T = lz.gen_random_repetitive(20000, 20000, 1)
+    s = session(T.size)
+    s.load(T)
+    with pytest.raises(lz.Lz77SssError):
+        s.factorize(tau=256)
+    with pytest.raises(lz.Lz77SssError):
+        s.factorize(fact_mode=lz.SKIP_PHRASES)
+    small = lz.Session(1 << 10)
+    with pytest.raises(lz.Lz77SssError):
+        small.load(T)
+    small.close()
+
+
+def _check_valid(T, F):
+    """Vectorised factor validity: literals match, references point backwards, lengths sum to n."""
+    ln = F[:, 1].astype(np.int64)
+    pos = np.concatenate([[0], np.cumsum(np.maximum(ln, 1))[:-1]])
+    assert pos[-1] + max(ln[-1], 1) == T.size
+    lit = ln == 0
+    assert np.array_equal(F[lit, 0].astype(np.uint8), T[pos[lit]])
+    assert np.all(F[~lit, 0].astype(np.int64) < pos[~lit])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["rr", "genome"])
+def test_one_gib_properties(session, orc, lz, kind):
+    n = 1 << 30
+    T = lz.gen_random_repetitive(n, n, 42, 0.5, 0.05) if kind == "rr" else lz.gen_genome(n, 64 << 20, 0.001, 7)
+    s, F = run(session, T)
+    _check_valid(T, F)
+    assert np.array_equal(lz.decode(F, n), T)
+    st = s.stats()
+    assert st[0] <= 2 * n // 512 + 1024
+    if kind == "rr":  # the oracle finishes this one in seconds
+        F_ref, _ = orc.factorize(T)
+        assert np.array_equal(F, F_ref)

@@ -1,0 +1,242 @@
+"""CPU tests of the oracle restatement against independent numpy/Python definitions.
+
+The reference has no golden vectors for this path; these
+checks pin the oracle to the *definitions* it restates (τ-synchronizing set,
+true suffix order of S, LCE, LPF phrase validity, decode(factorize(T)) == T
+as in tests/test_lz77_sss.cpp:73-82 of the reference) and to the committed
+fixtures in tests/golden/ (regression pins of the oracle itself).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+TAU = 512
+P61 = (1 << 61) - 1
+BASE = 296819
+
+
+def phi_py(T):
+    """Φ(j) = Σ_k T[j+k]·b^(τ−1−k) mod 2^61−1 by a Python-int rolling hash."""
+    n = len(T)
+    if n < TAU:
+        return np.zeros(0, np.uint64)
+    bp = pow(BASE, TAU, P61)
+    out = np.zeros(n - TAU + 1, np.uint64)
+    h = 0
+    t = [int(x) for x in T]
+    for k in range(TAU):
+        h = (h * BASE + t[k]) % P61
+    out[0] = h
+    for j in range(1, n - TAU + 1):
+        h = (h * BASE + t[j + TAU - 1] - t[j - 1] * bp) % P61
+        out[j] = h
+    return out
+
+
+def q_numpy(T):
+    """Q[j] = T[j..j+τ) has a period p ≤ ⌊τ/3⌋ (window mismatch counts by prefix sums)."""
+    T = np.asarray(T, np.int16)
+    n = T.size
+    m = n - TAU + 1
+    if m <= 0:
+        return np.zeros(0, bool)
+    q = np.zeros(m, bool)
+    for p in range(1, TAU // 3 + 1):
+        d = np.zeros(n + 1, np.int64)
+        d[1:n - p + 1] = np.cumsum(T[:n - p] != T[p:])
+        d[n - p + 1:] = d[n - p]
+        # mismatches in [j, j+τ−p)
+        cnt = d[TAU - p:TAU - p + m] - d[:m]
+        q |= cnt == 0
+    return q
+
+
+def sss_numpy(T):
+    n = len(T)
+    if n < 2 * TAU:
+        return np.zeros(0, np.uint32)
+    ph = phi_py(T).astype(object)
+    q = q_numpy(T)
+    INF = 1 << 62
+    php = np.array([INF if q[j] else int(ph[j]) for j in range(len(ph))], dtype=np.int64)
+    out = []
+    for i in range(n - 2 * TAU + 1):
+        m = php[i:i + TAU + 1].min()
+        if m < INF and (php[i] == m or php[i + TAU] == m):
+            out.append(i)
+    return np.array(out, np.uint32)
+
+
+def planted_text(seed, n=6000, sigma=4):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    T = rng.integers(0, sigma, n, dtype=np.uint8)
+    for _ in range(4):
+        p = int(rng.integers(1, 260))
+        L = int(rng.integers(200, 1600))
+        a = int(rng.integers(0, n - L))
+        unit = rng.integers(0, sigma, p, dtype=np.uint8)
+        T[a:a + L] = np.tile(unit, L // p + 1)[:L]
+    return T
+
+
+@pytest.mark.parametrize("sigma", [256, 4])
+def test_phi_matches_python(orc, sigma):
+    """oracle_phi returns Φ' (Φ outside Q, all-ones on Q)."""
+    T = planted_text(1, 3000, sigma)
+    want = np.where(q_numpy(T), np.uint64(2**64 - 1), phi_py(T))
+    assert np.array_equal(orc.phi(T), want)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
+def test_q_anchor_detection_matches_definition(orc, seed):
+    T = planted_text(seed)
+    q = q_numpy(T)
+    assert np.array_equal(orc.q_bruteforce(T).astype(bool), q)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 7, 11])
+def test_sss_matches_definition(orc, seed):
+    T = planted_text(seed, 4000)
+    S, has_runs = orc.sss(T)
+    assert np.array_equal(S, sss_numpy(T))
+    assert has_runs == bool(q_numpy(T).any())
+
+
+def test_sss_all_equal_text(orc):
+    S, has_runs = orc.sss(np.zeros(5000, np.uint8))
+    assert S.size == 0 and has_runs
+
+
+@pytest.mark.parametrize("seed", [1, 2, 5])
+def test_sa_s_is_true_suffix_order(orc, seed):
+    T = planted_text(seed, 8000, 3)
+    S, SA, LCP = orc.sa_s(T)
+    b = T.tobytes()
+    order = sorted(range(S.size), key=lambda k: b[S[k]:])
+    assert list(SA) == order
+    assert LCP[0] == 0
+    for k in range(1, S.size):
+        x, y = int(S[SA[k]]), int(S[SA[k - 1]])
+        l = 0
+        while x + l < T.size and y + l < T.size and T[x + l] == T[y + l]:
+            l += 1
+        assert LCP[k] == l
+
+
+@pytest.mark.parametrize("seed", [1, 3])
+def test_lce_matches_naive(orc, seed):
+    T = planted_text(seed, 8000, 2)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    qi = rng.integers(0, T.size, 400).astype(np.uint32)
+    qj = rng.integers(0, T.size, 400).astype(np.uint32)
+    qj[:50] = qi[:50]
+    got = orc.lce(T, qi, qj)
+    for a, b, g in zip(qi, qj, got):
+        a, b = int(a), int(b)
+        if a == b:
+            want = T.size - a
+        else:
+            want = 0
+            while max(a, b) + want < T.size and T[a + want] == T[b + want]:
+                want += 1
+        assert g == want
+
+
+@pytest.mark.parametrize("name", ["c1_seed1", "c1_seed4", "periodic", "genome_small", "binary_30k"])
+def test_lpf_phrases_are_valid(orc, name):
+    g = load_golden(name)
+    T = g["text"]
+    P = orc.lpf_opt(T)
+    assert np.array_equal(P, g["lpf"])
+    prev_end = 0
+    for beg, end, src in P:
+        beg, end, src = int(beg), int(end), int(src)
+        assert end - beg > 1 and src < beg and beg >= prev_end
+        assert np.array_equal(T[src:src + end - beg], T[beg:end])
+        prev_end = end
+
+
+def check_factors(T, F):
+    pos = 0
+    for src, ln in F:
+        src, ln = int(src), int(ln)
+        if ln == 0:
+            assert src == T[pos]
+            pos += 1
+        else:
+            assert src < pos
+            for k in range(ln):  # overlapping copies allowed
+                assert T[src + k] == T[pos + k]
+            pos += ln
+    assert pos == T.size
+
+
+@pytest.mark.parametrize("seed", range(1, 17))
+def test_roundtrip_c1(orc, lz, seed):
+    """Reference test_lz77_sss.cpp:73-82: decode(factorize(T)) == T on random_repetitive_string(10^4, 2·10^5)."""
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    for mode in (orc.LPF_OPT, orc.LPF_LNF_OPT):
+        F, st = orc.factorize(T, phr_mode=mode)
+        assert np.array_equal(orc.decode(F, T.size), T)
+        assert st[0] <= 2 * T.size // TAU + 2 * TAU  # |S| density
+
+
+@pytest.mark.parametrize("name", ["c1_seed3", "periodic", "edge_n5000", "zeros_10k"])
+def test_factor_validity(name):
+    g = load_golden(name)
+    check_factors(g["text"], g["factors"])
+    check_factors(g["text"], g["factors_lnf"])
+
+
+def lz77_exact_z(T):
+    """Greedy (self-referential) LZ77 factor count by candidate filtering."""
+    n = T.size
+    i, z = 0, 0
+    while i < n:
+        cand = np.nonzero(T[:i] == T[i])[0]
+        l = 0
+        if cand.size:
+            l = 1
+            while i + l < n:
+                keep = cand[T[cand + l] == T[i + l]]
+                if keep.size == 0:
+                    break
+                cand = keep
+                l += 1
+        i += max(l, 1)
+        z += 1
+    return z
+
+
+@pytest.mark.parametrize("name", ["c1_seed3", "periodic", "genome_small"])
+def test_three_approximation_bound(name):
+    g = load_golden(name)
+    z = lz77_exact_z(g["text"])
+    assert g["factors"].shape[0] <= 3 * z
+    assert g["factors_lnf"].shape[0] <= 3 * z
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_oracle_matches_golden(orc, name):
+    g = load_golden(name)
+    T = g["text"]
+    F, st = orc.factorize(T)
+    assert np.array_equal(F, g["factors"]) and np.array_equal(st, g["stats"])
+    F3, st3 = orc.factorize(T, phr_mode=orc.LPF_LNF_OPT)
+    assert np.array_equal(F3, g["factors_lnf"]) and np.array_equal(st3, g["stats_lnf"])
+    S, hr = orc.sss(T)
+    assert np.array_equal(S, g["sss"]) and hr == bool(g["has_runs"][0])
+    _, SA, LCP = orc.sa_s(T)
+    assert np.array_equal(SA, g["sa_s"]) and np.array_equal(LCP, g["lcp"])
+
+
+def test_gap_bases_pinned(orc):
+    """rk_prime bases from mt19937_64(seed) + uniform_int_distribution(257, 2^20-1) (rolling_hash.hpp:31-37)."""
+    g = load_golden("c1_seed1")
+    b = orc.gap_bases(42)
+    assert b == [int(x) for x in g["gap_bases_seed42"]]
+    assert all(257 <= x < (1 << 20) for x in b)
+    assert orc.gap_bases(43) != b
