@@ -38,6 +38,7 @@
 #include <cstring>
 #include <limits>
 #include <random>
+#include <unordered_map>
 
 namespace lz {
 
@@ -248,9 +249,11 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
     const u32 n = W.G.n, nt = W.G.nt;
     const u32* P = W.P;
     u32 i = in.start, p = in.p, idx = in.idxpos, zm = in.zmask;
-    u32 nf = 0, ns = 0, flags = 0, e = in.start;
+    u32 nf = 0, ns = 0, flags = 0, e = in.start, nb = 0;
+    bool first_gap = true;
     int hint = -1;
     out.next = n;
+    out.nbnd = 0;
     u64 guard = 0;
     const u64 guard_max = 4ull * n + 1024;
     auto emit = [&](u32 src, u32 len) {
@@ -280,8 +283,20 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
                 idx = i;
             }
             do {
-                if (i >= nt) { out.flags = flags | 1; return; }
+                if (i >= in.lim) {  // chunk boundary reached: stop at the next factor start
+                    out.next = i;
+                    out.e = i;
+                    out.nfact = nf;
+                    out.idxpos = idx;
+                    out.zmask = zm;
+                    out.nsingle = ns;
+                    out.flags = flags;
+                    out.nbnd = nb;
+                    return;
+                }
+                if (i >= nt) { out.flags = flags | 1; out.nbnd = nb; return; }
                 if (++guard > guard_max || i > n) { out.flags = flags | 4; return; }
+                if (first_gap && nb < SEG_NBND) out.bnd[nb++] = i;
                 u32 fsrc, flen;
                 query(i, fsrc, flen);
                 idx = i + 1;
@@ -300,6 +315,7 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
             } while (i < gap_end);
             e = i;
         }
+        first_gap = false;
         if (i == n) break;
         const u32 exc = i - gap_end;
         u32 lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
@@ -324,6 +340,7 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
     out.zmask = zm;
     out.nsingle = ns;
     out.flags = flags;
+    out.nbnd = nb;
 }
 
 template <bool WRITE>
@@ -713,36 +730,79 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     for (int x = 0; x < 5; x++) zmask0 |= (G.lens[x] >= N) ? (1u << x) : 0u;  // reinit(0) at construction
 
     // ---- segments (flat arrays; ids in creation order)
+    // Long gaps are cut into chunks of GAP_CHUNK positions: a segment's gap walk
+    // stops at the first factor start at or after the next chunk boundary.  Every
+    // gap position is inserted whatever the factor boundaries are, so a chunk
+    // walk started at its boundary is exact from the first factor start it
+    // shares with the real chain (the chain enters through an alias segment).
+    const u32 GAP_CHUNK = std::getenv("LZ77SSS_NO_CHUNK") ? 0xFFFFFFF : 512;
+    std::vector<u32> cbv;  // chunk boundaries (sorted)
     std::vector<seg_in> hsegs;
     std::vector<seg_out> houts;
     std::vector<u8> valid;       // output exact for the current lookup state
     std::vector<u32> seg_next;   // cached id of the segment starting at houts.next (NONE = unknown)
-    std::vector<std::pair<u32, u32>> by_start;  // (start, id), sorted
+    std::unordered_map<u32, u32> seg_at;  // start -> id
     auto add_segment = [&](u32 a) {
-        hsegs.push_back({a, first_phrase_after(a), a, zmask0});
+        auto it = std::upper_bound(cbv.begin(), cbv.end(), a);
+        const u32 lim = it == cbv.end() ? N : *it;
+        seg_at[a] = (u32)hsegs.size();
+        hsegs.push_back({a, first_phrase_after(a), a, zmask0, lim});
         houts.push_back(seg_out{});
         valid.push_back(0);
         seg_next.push_back(NONE);
     };
     auto find_seg = [&](u32 a) -> u32 {
-        auto it = std::lower_bound(by_start.begin(), by_start.end(), std::make_pair(a, 0u));
-        return (it != by_start.end() && it->first == a) ? it->second : NONE;
+        auto it = seg_at.find(a);
+        return it == seg_at.end() ? NONE : it->second;
+    };
+    u64 n_alias = 0;
+    // segment starting at x: existing, or an alias entering a valid chunk walk at one
+    // of its recorded factor starts; NONE otherwise (*blocked: the chunk walk is stale)
+    auto resolve = [&](u32 x, bool* blocked) -> u32 {
+        u32 g = find_seg(x);
+        if (g != NONE) return g;
+        auto it = std::upper_bound(cbv.begin(), cbv.end(), x);
+        if (it == cbv.begin()) return NONE;
+        const u32 c = *(it - 1);
+        const u32 gc = find_seg(c);
+        if (gc == NONE) return NONE;
+        if (!valid[gc]) {
+            if (blocked) *blocked = true;
+            return NONE;
+        }
+        const seg_out& oc = houts[gc];
+        for (u32 k = 1; k < oc.nbnd; k++) {
+            if (oc.bnd[k] != x) continue;
+            seg_out oa = oc;
+            oa.nfact -= k;
+            oa.nbnd = 0;
+            add_segment(x);
+            g = (u32)hsegs.size() - 1;
+            houts[g] = oa;
+            valid[g] = 1;
+            n_alias++;
+            return g;
+        }
+        return NONE;
     };
     // default segments and I_0 (every gap + the LPF-start query that follows it)
     ivec I;
     {
         u32 prev_end = 0;
+        std::vector<u32> starts;
         for (u32 k = 0; k <= m; k++) {
             const u32 b = hP[3 * k], e = hP[3 * k + 1];
             if (prev_end < b) {
-                add_segment(prev_end);
+                starts.push_back(prev_end);
+                if (b - prev_end > 2 * (u64)GAP_CHUNK)
+                    for (u32 c = prev_end + GAP_CHUNK; c + GAP_CHUNK / 2 < b; c += GAP_CHUNK) cbv.push_back(c);
                 I.push_back({prev_end, std::min(b + 1, N)});
             }
             prev_end = std::max(prev_end, e);
         }
-        if (hsegs.empty() || hsegs[0].start != 0) add_segment(0);  // phrases begin at >= 1
-        for (u32 g = 0; g < hsegs.size(); g++) by_start.push_back({hsegs[g].start, g});
-        std::sort(by_start.begin(), by_start.end());
+        if (starts.empty() || starts[0] != 0) starts.insert(starts.begin(), 0);  // phrases begin at >= 1
+        for (u32 a : starts) add_segment(a);
+        for (u32 c : cbv) add_segment(c);
     }
     clip(I, G.nt);
     // base superset: the speculated gaps plus the interiors of short phrases,
@@ -810,13 +870,6 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne;
         W.rem = rem; W.akeys = nullptr; W.nadd = 0;
         lap("base build (slots+sort+pred)");
-    };
-    auto base_rank_host = [&](u32 q) -> u32 {
-        auto it = std::upper_bound(h_is.begin(), h_is.end(), q);
-        if (it == h_is.begin()) return NONE;
-        const size_t k = (it - h_is.begin()) - 1;
-        if (q >= h_ie[k]) return NONE;
-        return h_ir[k] + (q - h_is[k]);
     };
     std::vector<u32> A_pos;  // sorted positions of I outside the base set
     // rebuild the added-entry list from A_pos
@@ -925,8 +978,10 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
                 zm = o.zmask;
                 u32 nx = seg_next[g];
                 if (nx == NONE) {
-                    nx = find_seg(o.next);
+                    bool blocked = false;
+                    nx = resolve(o.next, &blocked);
                     seg_next[g] = nx;
+                    if (blocked) todo.push_back(g);  // a stale chunk walk: re-walk the invalid ones
                 }
                 if (nx == NONE) { complete = false; break; }
                 g = nx;
@@ -952,7 +1007,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
                 if (!valid[h]) continue;
                 const seg_out& o = houts[h];
                 if ((o.flags & 1) || o.next >= N || seg_next[h] != NONE) continue;
-                if (find_seg(o.next) != NONE) continue;
+                bool blocked = false;
+                if (resolve(o.next, &blocked) != NONE || blocked) continue;
                 fresh.push_back(o.next);
             }
             std::sort(fresh.begin(), fresh.end());
@@ -960,10 +1016,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             if (fresh.empty()) throw error(-6, "greedy: chain broken without new states");
             for (u32 a : fresh) {
                 todo.push_back((u32)hsegs.size());
-                by_start.push_back({a, (u32)hsegs.size()});
                 add_segment(a);
             }
-            std::sort(by_start.begin(), by_start.end());
         }
         // ---- tail: exact single-thread walk from the chain segment that enters the tail region
         u64 tail_count = 0;
@@ -1110,6 +1164,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     stats[13] = rounds_total;
     stats[14] = stats_fallback_lanes;
     stats[15] = walked_total;
+    stats[16] = n_alias;
+    stats[17] = cbv.size();
     return total_fact;
 }
 

@@ -71,7 +71,7 @@ __global__ void k_lpf_candidates(lce_view L, const u32* __restrict__ SA, const u
         const u32 src = S[SA[nb]];
         const u32 end = Si + (u32)dev_lce(L, src, Si);
         u32 l = 0;
-        if (src != 0 && Si != 0) l = dev_lce_left(L.T, src - 1, Si - 1, capmax);
+        if (src != 0 && Si != 0) l = dev_lce_left(L.T, L.R, src - 1, Si - 1, capmax);
         rec[side * 3 + 0] = src;
         rec[side * 3 + 1] = end;
         rec[side * 3 + 2] = l;

@@ -81,7 +81,7 @@ struct rank_levels {
 
 // LCP[r] = LCE(S[SA[r-1]], S[SA[r]]), r >= 1; LCP[0] = 0
 __global__ void k_lcp(const u8* __restrict__ T, u64 n, const u32* __restrict__ S, const u32* __restrict__ KL,
-                      const u32* __restrict__ SA, u32 s, rank_levels RL, u32* __restrict__ LCP) {
+                      const u32* __restrict__ SA, u32 s, rank_levels RL, run_tab R, u32* __restrict__ LCP) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= s) return;
     if (r == 0) { LCP[0] = 0; return; }
@@ -97,7 +97,7 @@ __global__ void k_lcp(const u8* __restrict__ T, u64 n, const u32* __restrict__ S
     else {
         const u32 ka = (u32)(a + c), kb = (u32)(b + c);
         const u64 m = min(KL[ka], KL[kb]);
-        v = ((u64)S[ka] - S[a]) + dev_naive_lce(T, S[ka], S[kb], m);
+        v = ((u64)S[ka] - S[a]) + dev_lce_fwd(T, R, S[ka], S[kb], m);
     }
     LCP[r] = (u32)v;
 }
@@ -212,25 +212,47 @@ __global__ void k_tie_flags(const u8* T, const u32* S, const u32* KL, const u32*
     const u64 la = min<u64>(KL[a], CMP_BOUND), lb = min<u64>(KL[b], CMP_BOUND);
     tie[r] = (la == lb && dev_naive_lce(T, S[a], S[b], la) == la) ? 1 : 0;
 }
-// one wave per tie segment: insertion sort with exact wave comparisons
-__global__ __launch_bounds__(64) void k_sort_ties(const u8* T, const u32* S, const u32* KL, u32* __restrict__ srt,
-                                                  const u32* __restrict__ seg_beg, const u32* __restrict__ seg_len) {
-    const u32 lane = threadIdx.x;
-    u32* a = srt + seg_beg[blockIdx.x];
-    const u32 m = seg_len[blockIdx.x];
-    for (u32 i = 1; i < m; i++) {
-        const u32 x = a[i];
-        int j = (int)i - 1;
-        while (j >= 0 && wave_key_cmp(T, S, KL, a[j], x, lane) > 0) {
-            __syncthreads();
-            if (lane == 0) a[j + 1] = a[j];
-            __syncthreads();
-            j--;
-        }
-        __syncthreads();
-        if (lane == 0) a[j + 1] = x;
-        __syncthreads();
+// Tie segments (keys equal within CMP_BOUND) are finished by a merge sort in
+// which every comparison is done by a whole wave (64 lanes x 8 bytes per step):
+// items are (segment << 32 | key); segments stay contiguous and ordered.
+__device__ __forceinline__ bool wave_less(const u8* T, const u32* S, const u32* KL, u64 x, u64 y, u32 lane) {
+    const u32 sx = (u32)(x >> 32), sy = (u32)(y >> 32);
+    if (sx != sy) return sx < sy;
+    return wave_key_cmp(T, S, KL, (u32)x, (u32)y, lane) < 0;
+}
+__global__ __launch_bounds__(256) void k_wmerge(const u8* T, const u32* S, const u32* KL, const u64* __restrict__ in,
+                                                u64* __restrict__ out, u32 m, u32 w, u32 opw) {
+    // each wave produces opw = min(64, 2w) outputs, so they never span two merges
+    const u64 wave = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const u32 lane = threadIdx.x & 63;
+    const u64 p0 = wave * opw;
+    if (p0 >= m) return;
+    const u64 base = p0 / (2ull * w) * (2ull * w);
+    const u64 a0 = base, a1 = min<u64>(base + w, m), b0 = a1, b1 = min<u64>(base + 2ull * w, m);
+    const u64 la = a1 - a0, lb = b1 - b0, diag = p0 - base;
+    u64 lo = diag > lb ? diag - lb : 0, hi = min(diag, la);
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (!wave_less(T, S, KL, in[b0 + diag - 1 - mid], in[a0 + mid], lane)) lo = mid + 1; else hi = mid;
     }
+    u64 i = lo, j = diag - lo;
+    const u64 pend = min<u64>(p0 + opw, b1);
+    for (u64 p = p0; p < pend; p++) {
+        bool takeA;
+        if (i >= la) takeA = false;
+        else if (j >= lb) takeA = true;
+        else takeA = !wave_less(T, S, KL, in[b0 + j], in[a0 + i], lane);
+        const u64 v = takeA ? in[a0 + i++] : in[b0 + j++];
+        if (lane == 0) out[p] = v;
+    }
+}
+__global__ void k_tie_items(const u32* __restrict__ srt, const u32* __restrict__ pos, u32 m, u64* __restrict__ items) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < m) items[t] |= srt[pos[t]];
+}
+__global__ void k_tie_scatter(const u64* __restrict__ items, const u32* __restrict__ pos, u32 m, u32* __restrict__ srt) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < m) srt[pos[t]] = (u32)items[t];
 }
 __global__ void k_rank_of_group(const u32* __restrict__ srt_grp, u32 d, u32* __restrict__ rank_of) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -313,6 +335,15 @@ static void merge_sort_u32(u32* a, u32* tmp, u32 d, C cmp, hipStream_t st) {
     LZ_HIP(hipGetLastError());
 }
 
+// debug builds of the phase: synchronize and name the step that faulted
+#define SA_DBG(what)                                                                  \
+    do {                                                                              \
+        if (debug_enabled()) {                                                        \
+            hipError_t se_ = hipStreamSynchronize(st);                                \
+            fprintf(stderr, "[sa_s] %-16s %s\n", what, se_ == hipSuccess ? "ok" : hipGetErrorString(se_)); \
+            LZ_HIP(se_);                                                              \
+        }                                                                             \
+    } while (0)
 static void scan_incl(u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
     size_t tb = 0;
     LZ_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out, (int)m, st));
@@ -356,29 +387,48 @@ void engine::build_sa_s(const u8* T) {
             k_reps<<<g, 256, 0, st>>>(flag, rank, idx, s, rep);
             // 2. sort distinct keys: bounded comparison, then exact wave sort of bounded ties
             u32* srt = rep;
+            SA_DBG("reps");
             merge_sort_u32(srt, sa_tmp2.get(d), d, rep_less_bounded{T, dS, KL}, st);
+            SA_DBG("bounded sort");
             u8* tie = tmp_bytes.get(d);
             k_tie_flags<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, tie);
             if (debug_enabled()) fprintf(stderr, "[sa_s] distinct=%u sorted\n", d);
             std::vector<u8> htie(d);
             LZ_HIP(hipMemcpyAsync(htie.data(), tie, d, hipMemcpyDeviceToHost, st));
             LZ_HIP(hipStreamSynchronize(st));
-            std::vector<u32> sb, sl;
+            // members of tie segments, in order, tagged with their segment
+            std::vector<u64> items;
+            std::vector<u32> ipos;
+            u32 nseg = 0;
             for (u32 r = 1; r < d;) {
                 if (!htie[r]) { r++; continue; }
                 u32 e = r;
                 while (e < d && htie[e]) e++;
-                sb.push_back(r - 1);
-                sl.push_back(e - r + 1);
+                for (u32 q = r - 1; q < e; q++) { items.push_back(((u64)nseg << 32)); ipos.push_back(q); }
+                nseg++;
                 r = e;
             }
-            if (debug_enabled()) fprintf(stderr, "[sa_s] tie segments=%zu\n", sb.size());
-            if (!sb.empty()) {
-                u32* dsb = sa_tmp3.get(2 * sb.size());
-                LZ_HIP(hipMemcpyAsync(dsb, sb.data(), sb.size() * 4, hipMemcpyHostToDevice, st));
-                LZ_HIP(hipMemcpyAsync(dsb + sb.size(), sl.data(), sl.size() * 4, hipMemcpyHostToDevice, st));
-                k_sort_ties<<<(unsigned)sb.size(), 64, 0, st>>>(T, dS, KL, srt, dsb, dsb + sb.size());
+            if (debug_enabled()) fprintf(stderr, "[sa_s] tie segments=%u members=%zu\n", nseg, items.size());
+            if (!items.empty()) {
+                const u32 mt = (u32)items.size();
+                u64* it_a = u64a.get(2 * (u64)mt);  // hashes no longer needed
+                u64* it_b = it_a + mt;
+                u32* dpos = sa_tmp3.get(mt);
+                LZ_HIP(hipMemcpyAsync(it_a, items.data(), (size_t)mt * 8, hipMemcpyHostToDevice, st));
+                LZ_HIP(hipMemcpyAsync(dpos, ipos.data(), (size_t)mt * 4, hipMemcpyHostToDevice, st));
+                k_tie_items<<<cdiv(mt, 256), 256, 0, st>>>(srt, dpos, mt, it_a);
+                SA_DBG("tie items");
+                for (u64 w = 1; w < mt; w *= 2) {
+                    const u32 opw = (u32)std::min<u64>(64, 2 * w);
+                    k_wmerge<<<cdiv((u64)cdiv(mt, opw) * 64, 256), 256, 0, st>>>(T, dS, KL, it_a, it_b, mt, (u32)w, opw);
+                    std::swap(it_a, it_b);
+                    SA_DBG("wmerge");
+                }
+                k_tie_scatter<<<cdiv(mt, 256), 256, 0, st>>>(it_a, dpos, mt, srt);
+                SA_DBG("tie scatter");
+                LZ_HIP(hipGetLastError());
             }
+            stats_sa_ties = nseg;
             // 3. ranks: sorted distinct keys -> groups -> every key
             u32* key_to_grp = idx_in;  // free now
             k_key_to_grp<<<g, 256, 0, st>>>(flag, rank, idx, s, key_to_grp);
@@ -387,8 +437,8 @@ void engine::build_sa_s(const u8* T) {
             u32* rank_of = srt;  // sorted reps consumed by k_map_rep_to_group (stream order)
             k_rank_of_group<<<cdiv(d, 256), 256, 0, st>>>(srt_grp, d, rank_of);
             k_r0_from_groups<<<g, 256, 0, st>>>(idx, rank, rank_of, s, R0);
+            SA_DBG("r0");
             stats_sa_distinct = d;
-            stats_sa_ties = sb.size();
             done_r0 = true;
         }
     }
@@ -420,6 +470,7 @@ void engine::build_sa_s(const u8* T) {
         scan_incl(flag, rank, s, scan_tmp, st);
         u32* Rn = rank_lv[nlev_rank].get(s);
         k_scatter_rank<<<g, 256, 0, st>>>(idx, rank, s, Rn);
+        SA_DBG("doubling");
         nlev_rank++;
         maxr = rd1(rank + s - 1, st);
     }
@@ -438,7 +489,7 @@ void engine::build_lcp_rmq(const u8* T) {
     RL.nlev = nlev_rank;
     for (u32 i = 0; i < nlev_rank; i++) RL.R[i] = rank_lv[i].p;
     u32* L0 = lcp_rmq[0].get(s);
-    k_lcp<<<g, 256, 0, st>>>(T, n, S.p, key_len.p, SA.p, s, RL, L0);
+    k_lcp<<<g, 256, 0, st>>>(T, n, S.p, key_len.p, SA.p, s, RL, runs(), L0);
     nlev_rmq = 1;
     for (u32 lv = 1; (1ull << lv) <= s; lv++) {
         const u32 cnt = s - (1u << lv) + 1;
@@ -459,6 +510,7 @@ lce_view engine::view(const u8* T) const {
     L.succ = succ_tab.p;
     L.nlev = nlev_rmq;
     for (u32 i = 0; i < nlev_rmq; i++) L.rmq[i] = lcp_rmq[i].p;
+    L.R = runs();
     return L;
 }
 

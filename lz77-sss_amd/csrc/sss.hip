@@ -26,13 +26,17 @@ namespace lz {
 // Q anchors
 constexpr int QT_ANCH = 128;                 // anchors per workgroup
 constexpr int QT_SPAN = QT_ANCH * QA;        // 16384 positions
-constexpr int QT_LDS = QT_SPAN + 128 + 1024; // [A0-128, A0+16384+1024)
+constexpr int QT_LDS = QT_SPAN + 256 + 1024; // [A0-256, A0+16384+1024)
+constexpr u32 RUN_HCAP = 640;                // local run extension: [a-256, a+640)
+constexpr u32 RUN_LCAP = 256;
 
 __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64 n, u64 nanch,
-                                                   u16* __restrict__ qinfo, u32* __restrict__ any_q) {
+                                                   u16* __restrict__ qinfo, u32* __restrict__ any_q,
+                                                   u8* __restrict__ run_p, u32* __restrict__ run_hi,
+                                                   u32* __restrict__ run_lo, u8* __restrict__ run_cap) {
     __shared__ __attribute__((aligned(16))) u8 buf[QT_LDS];
     const u64 A0 = (u64)blockIdx.x * QT_SPAN;
-    const int64_t base = (int64_t)A0 - 128;
+    const int64_t base = (int64_t)A0 - 256;
     for (int x = threadIdx.x * 16; x < QT_LDS; x += 128 * 16) {
         int64_t g = base + x;
         uint4 v = {0, 0, 0, 0};
@@ -44,6 +48,8 @@ __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64
     if (t >= nanch) return;
     const u64 a = t * QA;
     u16 res = 0xFF00;  // empty interval
+    u32 rp = 0, rhi = 0, rlo = 0;
+    u8 rcap = 0;
     if (a + QM <= n) {
         const int la = (int)(a - base);  // multiple of 4
         const u32* b32 = (const u32*)buf;
@@ -83,9 +89,54 @@ __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64
                 res = (u16)(((jlo - r0) << 8) | (jhi - r0));
                 atomicOr(any_q, 1u);
             }
+            // local extent of the p-periodic run around the window (for run-skipping LCE)
+            u64 h2 = hi;
+            const u64 h2_cap = min(a + RUN_HCAP - p, n - p);
+            while (h2 < h2_cap && buf[h2 - base] == buf[h2 + p - base]) h2++;
+            u64 l2 = lo;
+            const u64 l2_cap = a >= RUN_LCAP ? a - RUN_LCAP : 0;
+            while (l2 > l2_cap && buf[l2 - 1 - base] == buf[l2 - 1 + p - base]) l2--;
+            rp = p;
+            rhi = (u32)(h2 + p);
+            rlo = (u32)l2;
+            rcap = (h2 == a + RUN_HCAP - p ? 1 : 0) | (l2 == a - RUN_LCAP && a >= RUN_LCAP ? 2 : 0);
         }
     }
     qinfo[t] = res;
+    run_p[t] = (u8)rp;
+    run_hi[t] = rhi;
+    run_lo[t] = rlo;
+    run_cap[t] = rcap;
+}
+
+// run chains: anchor t continues into t+1 (same run) when both have period p
+// and t's run covers t+1's window; a chain's exact hi is its last anchor's local
+// hi (exact unless capped), its exact lo its first anchor's local lo.
+__global__ void k_run_elems(const u8* __restrict__ rp, const u32* __restrict__ rhi, const u32* __restrict__ rlo,
+                            const u8* __restrict__ rcap, u64 na, u64* __restrict__ ehi_rev, u64* __restrict__ elo) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= na) return;
+    const u32 p = rp[t];
+    const u64 a = t * QA;
+    const bool cont_f = p && t + 1 < na && rp[t + 1] == p && (u64)rhi[t] >= a + QA + QM;
+    const bool cont_b = p && t >= 1 && rp[t - 1] == p && (u64)rlo[t] + QA <= a;
+    u64 vh = 0, vl = 0xFFFFFFFFull;
+    if (p) {
+        vh = (!cont_f && (rcap[t] & 1)) ? 0 : rhi[t];
+        vl = (!cont_b && (rcap[t] & 2)) ? 0xFFFFFFFFull : rlo[t];
+    }
+    ehi_rev[na - 1 - t] = ((u64)(!cont_f) << 63) | vh;
+    elo[t] = ((u64)(!cont_b) << 63) | vl;
+}
+struct last_marked {
+    __device__ __forceinline__ u64 operator()(const u64& x, const u64& y) const { return (y >> 63) ? y : x; }
+};
+__global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restrict__ slo, u64 na,
+                             u32* __restrict__ rhi, u32* __restrict__ rlo) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= na) return;
+    rhi[t] = (u32)shi_rev[na - 1 - t];
+    rlo[t] = (u32)slo[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -303,6 +354,7 @@ static u64 pow61_host(u64 b, u64 e) {
 void engine::build_sss(const u8* T) {
     s = 0;
     has_runs = false;
+    runs_valid = false;
     sss_kernel_ms = 0;
     if (n < 2 * (u64)TAU) return;
     const u64 last_i = n - 2 * TAU;
@@ -310,8 +362,25 @@ void engine::build_sss(const u8* T) {
     u16* qi = q_info.get(nanch);
     u32* ctr = counters.get(16);
     LZ_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st));
-    k_q_anchors<<<cdiv(nanch, QT_ANCH), QT_ANCH, 0, st>>>(T, n, nanch, qi, ctr + 0);
+    u8* rp = run_p.get(nanch);
+    u32* rhi = run_hi.get(nanch);
+    u32* rlo = run_lo.get(nanch);
+    u8* rcap = tmp_bytes.get(nanch);
+    k_q_anchors<<<cdiv(nanch, QT_ANCH), QT_ANCH, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap);
     LZ_HIP(hipGetLastError());
+    {
+        u64* ea = run_scan_a.get(2 * nanch);
+        u64* eb = run_scan_b.get(2 * nanch);
+        k_run_elems<<<cdiv(nanch, 256), 256, 0, st>>>(rp, rhi, rlo, rcap, nanch, ea, ea + nanch);
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, ea, eb, last_marked{}, (int)nanch, st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ea, eb, last_marked{}, (int)nanch, st));
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ea + nanch, eb + nanch, last_marked{}, (int)nanch, st));
+        k_run_finish<<<cdiv(nanch, 256), 256, 0, st>>>(eb, eb + nanch, nanch, rhi, rlo);
+        LZ_HIP(hipGetLastError());
+        runs_valid = true;
+    }
 
     const u64 nlanes_need = last_i / SL + 1;
     const unsigned nwg = cdiv(nlanes_need, NLW);

@@ -14,7 +14,10 @@ namespace lz {
 struct lpf3 { u32 beg, end, src; };
 
 // greedy walk segments (csrc/greedy.hip)
-struct seg_in { u32 start, p, idxpos, zmask; };
+// walk segment input: start position, first phrase index, gap-index state, and
+// the position at or after which the gap walk stops (a chunk boundary; n = none)
+struct seg_in { u32 start, p, idxpos, zmask, lim; };
+constexpr int SEG_NBND = 16;  // factor starts recorded per gap walk (chunk convergence)
 struct seg_out {
     u32 next;        // start of the next gap (or n)
     u32 e;           // end of this segment's gap walk (positions [start, e) inserted)
@@ -24,6 +27,8 @@ struct seg_out {
     u32 nsingle;     // extra inserted positions (LPF-start queries)
     u32 single[4];
     u32 flags;       // 1: reached the tail region, 2: single overflow
+    u32 nbnd;        // recorded factor starts of the first gap walk
+    u32 bnd[SEG_NBND];
 };
 
 struct phase_timer {
@@ -76,6 +81,15 @@ struct engine {
     bool has_runs = false;
     double sss_kernel_ms = 0;  // dominant kernel (SSS main pass) duration
     u64 stats_fallback_lanes = 0;
+    dbuf<u8> run_p;            // periodic-run table per Q anchor (lce_dev.h run_tab)
+    dbuf<u32> run_hi, run_lo;
+    dbuf<u64> run_scan_a, run_scan_b;
+    bool runs_valid = false;
+    run_tab runs() const {
+        run_tab R;
+        if (runs_valid) { R.p = run_p.p; R.hi = run_hi.p; R.lo = run_lo.p; }
+        return R;
+    }
 
     // ---- suffix order of sync positions / LCE ----
     dbuf<u32> SA, ISA, LCP, key_len;

@@ -12,6 +12,73 @@ namespace lz {
 
 constexpr int MAX_LV = 32;
 
+// Periodic runs seen by the Q anchors (csrc/sss.hip): for anchor t (position
+// 128t) whose window T[128t..128t+340) has smallest period p <= 170: p[t] = p,
+// hi[t] = exclusive end and lo[t] = start of the maximal p-periodic run that
+// contains the window (hi = 0 / lo = ~0 when unknown); p[t] = 0 otherwise.
+// Long naive comparisons skip through runs with them: once 512 equal bytes
+// end inside runs of the same period on both sides, the two strings stay
+// equal until the first of the runs ends, and differ right there if the run
+// ends are at different offsets.
+struct run_tab {
+    const u8* p = nullptr;
+    const u32* hi = nullptr;
+    const u32* lo = nullptr;
+};
+
+// exact LCE of T[i..] and T[j..], at most lim (caller guarantees i+lim, j+lim <= n)
+__device__ inline u64 dev_lce_fwd(const u8* T, const run_tab& R, u64 i, u64 j, u64 lim) {
+    u64 k = 0;
+    while (k < lim) {
+        const u64 step = min<u64>(lim - k, 512);
+        const u64 c = dev_naive_lce(T, i + k, j + k, step);
+        k += c;
+        if (c < step || k >= lim || !R.p || k < 512) return min(k, lim);
+        const u64 x = i + k, y = j + k;  // T[x-512..x) == T[y-512..y)
+        const u64 ax = (x - 340) >> 7, by = (y - 340) >> 7;
+        const u32 pp = R.p[ax];
+        if (pp == 0 || R.p[by] != pp) continue;
+        const u64 hx = R.hi[ax], hy = R.hi[by];
+        if (hx < x || hy < y) continue;
+        const u64 dx = hx - x, dy = hy - y, d = min(dx, dy);
+        if (k + d >= lim) return lim;
+        k += d;
+        if (dx != dy) return k;
+    }
+    return lim;
+}
+// #equal chars going left from i and j (T[i-t] == T[j-t]), at most lim <= min(i,j)+1
+__device__ __forceinline__ u64 dev_naive_lce_left(const u8* T, u64 i, u64 j, u64 lim) {
+    u64 k = 0;
+    while (k + 8 <= lim) {
+        const u64 x = ldu64(T + (i - k - 7)), y = ldu64(T + (j - k - 7));
+        if (x != y) return k + (__builtin_clzll(x ^ y) >> 3);
+        k += 8;
+    }
+    while (k < lim && T[i - k] == T[j - k]) k++;
+    return k;
+}
+__device__ inline u64 dev_lce_bwd(const u8* T, const run_tab& R, u64 i, u64 j, u64 lim) {
+    u64 k = 0;
+    while (k < lim) {
+        const u64 step = min<u64>(lim - k, 512);
+        const u64 c = dev_naive_lce_left(T, i - k, j - k, step);
+        k += c;
+        if (c < step || k >= lim || !R.p || k < 512) return min(k, lim);
+        const u64 x = i - k + 1, y = j - k + 1;  // T[x..x+512) == T[y..y+512)
+        const u64 ax = (x + 127) >> 7, by = (y + 127) >> 7;
+        const u32 pp = R.p[ax];
+        if (pp == 0 || R.p[by] != pp) continue;
+        const u64 lx = R.lo[ax], ly = R.lo[by];
+        if (lx > x || ly > y) continue;
+        const u64 dx = x - lx, dy = y - ly, d = min(dx, dy);
+        if (k + d >= lim) return lim;
+        k += d;
+        if (dx != dy) return k;
+    }
+    return lim;
+}
+
 struct lce_view {
     const u8* T;
     u64 n;
@@ -21,6 +88,7 @@ struct lce_view {
     const u32* succ;  // bucket (x >> 9) -> first sync index with S >= bucket*512
     u32 nlev;
     const u32* rmq[MAX_LV];
+    run_tab R;
 };
 
 __device__ __forceinline__ u32 dev_succ(const lce_view& L, u64 x) {
@@ -47,34 +115,26 @@ __device__ __forceinline__ u64 dev_lce(const lce_view& L, u64 i, u64 j) {
     u64 c = dev_naive_lce(L.T, l, r, local);
     if (c < local || c == lmax) return c;
     const u32 kl = dev_succ(L, l), kr = dev_succ(L, r);
-    if (kl == L.s || kr == L.s) return c + dev_naive_lce(L.T, l + c, r + c, lmax - c);
+    if (kl == L.s || kr == L.s) return c + dev_lce_fwd(L.T, L.R, l + c, r + c, lmax - c);
     const u64 dl = L.S[kl] - l, dr = L.S[kr] - r;
     if (dl == dr) {
         if (dl > c) {
-            const u64 e = dev_naive_lce(L.T, l + c, r + c, dl - c);
+            const u64 e = dev_lce_fwd(L.T, L.R, l + c, r + c, dl - c);
             if (e < dl - c) return c + e;
         }
         return dl + dev_lce_sync(L, kl, kr);
     }
     const u64 bound = min(min(dl, dr) + 2 * TAU - 1, lmax);
-    if (bound > c) c += dev_naive_lce(L.T, l + c, r + c, bound - c);
+    if (bound > c) c += dev_lce_fwd(L.T, L.R, l + c, r + c, bound - c);
     return c;
 }
 
 // leftward LCE, exact semantics of lce_l_64 (include/lz77_sss/algorithms/lce_l.hpp:33-83):
 // min(cap', #equal chars going left from i and j), cap' = min(cap, min(i,j)+1)
-__device__ __forceinline__ u32 dev_lce_left(const u8* T, u32 i, u32 j, u32 cap) {
+__device__ __forceinline__ u32 dev_lce_left(const u8* T, const run_tab& R, u32 i, u32 j, u32 cap) {
     const u32 cp = min(cap, min(i, j) + 1);
     if (i == j) return cp;
-    u32 k = 0;
-    // 8 bytes at a time while possible
-    while (k + 8 <= cp) {
-        const u64 x = ldu64(T + (i - k - 7)), y = ldu64(T + (j - k - 7));
-        if (x != y) return k + (__builtin_clzll(x ^ y) >> 3);
-        k += 8;
-    }
-    while (k < cp && T[i - k] == T[j - k]) k++;
-    return k;
+    return (u32)dev_lce_bwd(T, R, i, j, cp);
 }
 
 }  // namespace lz
