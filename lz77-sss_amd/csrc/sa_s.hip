@@ -144,31 +144,15 @@ __global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, cons
     if (lane == 0) H[k] = h + mix64(len ^ 0xd6e8feb86659fd93ull);
 }
 // wave-parallel exact comparison of two keys (all 64 lanes must call it)
-__device__ int wave_key_cmp(const u8* T, const u32* S, const u32* KL, u32 a, u32 b, u32 lane) {
+__device__ int wave_key_cmp(const u8* T, const run_tab& R, const u32* S, const u32* KL, u32 a, u32 b, u32 lane) {
     const u64 la = KL[a], lb = KL[b], m = min(la, lb);
     const u64 pa = S[a], pb = S[b];
-    for (u64 o = 0; o < m; o += 512) {
-        const u64 off = o + 8 * lane;
-        bool diff = false;
-        if (off < m) {
-            u64 x = ldu64(T + pa + off), y = ldu64(T + pb + off);
-            const u64 r = m - off;
-            if (r < 8) { const u64 msk = (1ull << (8 * r)) - 1; x &= msk; y &= msk; }
-            diff = x != y;
-        }
-        const u64 bal = __ballot(diff);
-        if (bal) {
-            const u32 first = __builtin_ctzll(bal);
-            const u64 fo = o + 8 * first;
-            const u64 x = ldu64(T + pa + fo), y = ldu64(T + pb + fo);
-            const u32 byte = __builtin_ctzll(x ^ y) >> 3;
-            return T[pa + fo + byte] < T[pb + fo + byte] ? -1 : 1;
-        }
-    }
+    const u64 c = wave_lce_fwd(T, R, pa, pb, m, lane);
+    if (c < m) return T[pa + c] < T[pb + c] ? -1 : 1;
     return la < lb ? -1 : (la > lb ? 1 : 0);
 }
 // flags: new group where the hash changes; exact check of equal-hash neighbours
-__global__ __launch_bounds__(256) void k_group_verify(const u8* T, const u32* S, const u32* KL,
+__global__ __launch_bounds__(256) void k_group_verify(const u8* T, run_tab R, const u32* S, const u32* KL,
                                                       const u64* __restrict__ Hs, const u32* __restrict__ idx,
                                                       u32 s, u32* __restrict__ flag, u32* __restrict__ collide) {
     const u64 t = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -178,7 +162,7 @@ __global__ __launch_bounds__(256) void k_group_verify(const u8* T, const u32* S,
         if (lane == 0) flag[t] = 1;
         return;
     }
-    const int c = wave_key_cmp(T, S, KL, idx[t - 1], idx[t], lane);
+    const int c = wave_key_cmp(T, R, S, KL, idx[t - 1], idx[t], lane);
     if (lane == 0) {
         flag[t] = 0;
         if (c != 0) atomicOr(collide, 1u);
@@ -195,32 +179,34 @@ struct rep_less_bounded {
     const u8* T;
     const u32* S;
     const u32* KL;
+    run_tab R;
     __device__ bool operator()(const u32& a, const u32& b) const {
         const u64 la = min<u64>(KL[a], CMP_BOUND), lb = min<u64>(KL[b], CMP_BOUND), m = min(la, lb);
-        const u64 c = dev_naive_lce(T, S[a], S[b], m);
+        const u64 c = dev_lce_fwd(T, R, S[a], S[b], m);
         if (c < m) return T[(u64)S[a] + c] < T[(u64)S[b] + c];
         // equal within the bound: stays in input order (stable sort), resolved exactly afterwards.
         return la < lb;
     }
 };
-__global__ void k_tie_flags(const u8* T, const u32* S, const u32* KL, const u32* __restrict__ srt, u32 d,
+__global__ void k_tie_flags(const u8* T, run_tab R, const u32* S, const u32* KL, const u32* __restrict__ srt, u32 d,
                             u8* __restrict__ tie) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= d) return;
     if (r == 0) { tie[0] = 0; return; }
     const u32 a = srt[r - 1], b = srt[r];
     const u64 la = min<u64>(KL[a], CMP_BOUND), lb = min<u64>(KL[b], CMP_BOUND);
-    tie[r] = (la == lb && dev_naive_lce(T, S[a], S[b], la) == la) ? 1 : 0;
+    tie[r] = (la == lb && dev_lce_fwd(T, R, S[a], S[b], la) == la) ? 1 : 0;
 }
 // Tie segments (keys equal within CMP_BOUND) are finished by a merge sort in
 // which every comparison is done by a whole wave (64 lanes x 8 bytes per step):
 // items are (segment << 32 | key); segments stay contiguous and ordered.
-__device__ __forceinline__ bool wave_less(const u8* T, const u32* S, const u32* KL, u64 x, u64 y, u32 lane) {
+__device__ __forceinline__ bool wave_less(const u8* T, const run_tab& R, const u32* S, const u32* KL, u64 x, u64 y,
+                                          u32 lane) {
     const u32 sx = (u32)(x >> 32), sy = (u32)(y >> 32);
     if (sx != sy) return sx < sy;
-    return wave_key_cmp(T, S, KL, (u32)x, (u32)y, lane) < 0;
+    return wave_key_cmp(T, R, S, KL, (u32)x, (u32)y, lane) < 0;
 }
-__global__ __launch_bounds__(256) void k_wmerge(const u8* T, const u32* S, const u32* KL, const u64* __restrict__ in,
+__global__ __launch_bounds__(256) void k_wmerge(const u8* T, run_tab R, const u32* S, const u32* KL, const u64* __restrict__ in,
                                                 u64* __restrict__ out, u32 m, u32 w, u32 opw) {
     // each wave produces opw = min(64, 2w) outputs, so they never span two merges
     const u64 wave = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -233,7 +219,7 @@ __global__ __launch_bounds__(256) void k_wmerge(const u8* T, const u32* S, const
     u64 lo = diag > lb ? diag - lb : 0, hi = min(diag, la);
     while (lo < hi) {
         const u64 mid = (lo + hi) >> 1;
-        if (!wave_less(T, S, KL, in[b0 + diag - 1 - mid], in[a0 + mid], lane)) lo = mid + 1; else hi = mid;
+        if (!wave_less(T, R, S, KL, in[b0 + diag - 1 - mid], in[a0 + mid], lane)) lo = mid + 1; else hi = mid;
     }
     u64 i = lo, j = diag - lo;
     const u64 pend = min<u64>(p0 + opw, b1);
@@ -241,7 +227,7 @@ __global__ __launch_bounds__(256) void k_wmerge(const u8* T, const u32* S, const
         bool takeA;
         if (i >= la) takeA = false;
         else if (j >= lb) takeA = true;
-        else takeA = !wave_less(T, S, KL, in[b0 + j], in[a0 + i], lane);
+        else takeA = !wave_less(T, R, S, KL, in[b0 + j], in[a0 + i], lane);
         const u64 v = takeA ? in[a0 + i++] : in[b0 + j++];
         if (lane == 0) out[p] = v;
     }
@@ -377,7 +363,7 @@ void engine::build_sa_s(const u8* T) {
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, H, Hs, idx_in, idx, (int)s, 0, 64, st));
         u32* ctr = counters.get(16);
         LZ_HIP(hipMemsetAsync(ctr + 2, 0, 4, st));
-        k_group_verify<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, dS, KL, Hs, idx, s, flag, ctr + 2);
+        k_group_verify<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, Hs, idx, s, flag, ctr + 2);
         scan_incl(flag, rank, s, scan_tmp, st);  // rank[t] = group id + 1
         const u32 collide = rd1(ctr + 2, st);
         if (debug_enabled()) fprintf(stderr, "[sa_s] s=%u collide=%u\n", s, collide);
@@ -388,10 +374,10 @@ void engine::build_sa_s(const u8* T) {
             // 2. sort distinct keys: bounded comparison, then exact wave sort of bounded ties
             u32* srt = rep;
             SA_DBG("reps");
-            merge_sort_u32(srt, sa_tmp2.get(d), d, rep_less_bounded{T, dS, KL}, st);
+            merge_sort_u32(srt, sa_tmp2.get(d), d, rep_less_bounded{T, dS, KL, runs()}, st);
             SA_DBG("bounded sort");
             u8* tie = tmp_bytes.get(d);
-            k_tie_flags<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, tie);
+            k_tie_flags<<<cdiv(d, 256), 256, 0, st>>>(T, runs(), dS, KL, srt, d, tie);
             if (debug_enabled()) fprintf(stderr, "[sa_s] distinct=%u sorted\n", d);
             std::vector<u8> htie(d);
             LZ_HIP(hipMemcpyAsync(htie.data(), tie, d, hipMemcpyDeviceToHost, st));
@@ -420,7 +406,7 @@ void engine::build_sa_s(const u8* T) {
                 SA_DBG("tie items");
                 for (u64 w = 1; w < mt; w *= 2) {
                     const u32 opw = (u32)std::min<u64>(64, 2 * w);
-                    k_wmerge<<<cdiv((u64)cdiv(mt, opw) * 64, 256), 256, 0, st>>>(T, dS, KL, it_a, it_b, mt, (u32)w, opw);
+                    k_wmerge<<<cdiv((u64)cdiv(mt, opw) * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, it_a, it_b, mt, (u32)w, opw);
                     std::swap(it_a, it_b);
                     SA_DBG("wmerge");
                 }

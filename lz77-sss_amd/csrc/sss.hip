@@ -7,15 +7,16 @@
 //   Q       = { j : T[j..j+tau) has a period <= floor(tau/3) }
 //   S       = { i <= n-2tau : min Phi'[i..i+tau] < inf at i or at i+tau }
 //
-// Three launches:
+// Launches:
 //   k_q_anchors  -- per anchor a (every 128 positions) the smallest period <= 170
-//                   of T[a..a+340) and the Q interval it induces on (a-128, a]
-//   k_sss_main   -- lanes stream contiguous 4 KiB segments; text is staged
-//                   through LDS in coalesced 128-B rows; per lane a rolling
-//                   61-bit Karp-Rabin hash feeds a monotone deque (LDS) that
-//                   decides "forward-window minimum" (A) and "backward-window
-//                   minimum" (B); i in S <=> A(i) or B(i+tau)
-//   k_sss_compact-- per-lane outputs -> sorted S
+//                   of T[a..a+340), the Q interval it induces on (a-128, a], and
+//                   the local extent of the periodic run (run table, lce_dev.h)
+//   k_run_elems + 2 scans + k_run_finish -- exact run ends/starts along chains
+//   k_sss_tile   -- one workgroup per tile of 7168 decisions: bytes staged once
+//                   in LDS, prefix-hash scan + rolls give Phi', van Herk minima
+//                   over 512-blocks in registers, ordered per-tile output
+//   k_sss_fallback -- exact slow path for tiles with more than TCAP outputs
+//   k_sss_compact-- per-tile outputs -> sorted S
 #include "../include/engine.h"
 
 #include <hipcub/hipcub.hpp>
@@ -34,16 +35,24 @@ __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64
                                                    u16* __restrict__ qinfo, u32* __restrict__ any_q,
                                                    u8* __restrict__ run_p, u32* __restrict__ run_hi,
                                                    u32* __restrict__ run_lo, u8* __restrict__ run_cap) {
-    __shared__ __attribute__((aligned(16))) u8 buf[QT_LDS];
+    // LDS text with one pad word per 128 bytes: the anchors of a wave sit 128 bytes
+    // apart, so unpadded their accesses would all hit the same bank
+    __shared__ __attribute__((aligned(16))) u32 b32[QT_LDS / 4 + QT_LDS / 128 + 2];
     const u64 A0 = (u64)blockIdx.x * QT_SPAN;
     const int64_t base = (int64_t)A0 - 256;
     for (int x = threadIdx.x * 16; x < QT_LDS; x += 128 * 16) {
         int64_t g = base + x;
         uint4 v = {0, 0, 0, 0};
         if (g >= 0 && (u64)g + 16 <= n + TEXT_PAD) v = *(const uint4*)(T + g);
-        *(uint4*)&buf[x] = v;
+        const int w = (x >> 2) + (x >> 7);
+        b32[w] = v.x;
+        b32[w + 1] = v.y;
+        b32[w + 2] = v.z;
+        b32[w + 3] = v.w;
     }
     __syncthreads();
+    auto word = [&](int64_t w) -> u32 { return b32[w + (w >> 5)]; };
+    auto byte = [&](int64_t x) -> u32 { return (word(x >> 2) >> (8 * (x & 3))) & 255u; };
     const u64 t = (u64)blockIdx.x * QT_ANCH + threadIdx.x;
     if (t >= nanch) return;
     const u64 a = t * QA;
@@ -52,34 +61,50 @@ __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64
     u8 rcap = 0;
     if (a + QM <= n) {
         const int la = (int)(a - base);  // multiple of 4
-        const u32* b32 = (const u32*)buf;
-        const u32 w0 = b32[la >> 2];
+        // 4 bytes at any LDS offset
+        auto w32 = [&](int64_t o) -> u32 {
+            const int64_t q = o >> 2;
+            return __builtin_amdgcn_alignbyte(word(q + 1), word(q), (u32)(o & 3));
+        };
+        // first q in [h, cap) with T[q] != T[q+p] (cap if none)
+        auto ext_fwd = [&](u64 h, u64 cap, u32 p) -> u64 {
+            while (h < cap) {
+                u32 d = w32((int64_t)h - base) ^ w32((int64_t)(h + p) - base);
+                const u64 rem = cap - h;
+                if (rem < 4) d &= (1u << (8 * rem)) - 1;
+                if (d) return h + (__builtin_ctz(d) >> 3);
+                h += rem < 4 ? rem : 4;
+            }
+            return cap;
+        };
+        // smallest l in [cap, l0] with T[q] == T[q+p] for all q in [l, l0)
+        auto ext_bwd = [&](u64 l, u64 cap, u32 p) -> u64 {
+            while (l >= cap + 4) {
+                const u32 d = w32((int64_t)l - 4 - base) ^ w32((int64_t)(l - 4 + p) - base);
+                if (d) return l - 4 + ((31 - __builtin_clz(d)) >> 3) + 1;
+                l -= 4;
+            }
+            while (l > cap && byte((int64_t)l - 1 - base) == byte((int64_t)(l - 1 + p) - base)) l--;
+            return l;
+        };
+        const u32 w0 = word(la >> 2);
         u32 p = 0;
         u32 dprev = w0;
         for (int k = 0; k <= (int)(QL / 4) && !p; k++) {
-            u32 dnext = b32[(la >> 2) + k + 1];
+            u32 dnext = word((la >> 2) + k + 1);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 u32 pp = 4 * k + r;
                 if (!p && pp >= 1 && pp <= QL) {
                     u32 w = __builtin_amdgcn_alignbyte(dnext, dprev, r);
-                    if (w == w0) {
-                        bool ok = true;
-                        for (u32 x = 4; x < QM - pp; x++)
-                            if (buf[la + x] != buf[la + pp + x]) { ok = false; break; }
-                        if (ok) p = pp;
-                    }
+                    if (w == w0 && ext_fwd(a + 4, a + QM - pp, pp) == a + QM - pp) p = pp;
                 }
             }
             dprev = dnext;
         }
         if (p) {
-            u64 hi = a + QM - p;
-            const u64 hi_cap = min(a + TAU - p, n - p);
-            while (hi < hi_cap && buf[hi - base] == buf[hi + p - base]) hi++;
-            const u64 lo_cap = a >= 127 ? a - 127 : 0;
-            u64 lo = a;
-            while (lo > lo_cap && buf[lo - 1 - base] == buf[lo - 1 + p - base]) lo--;
+            const u64 hi = ext_fwd(a + QM - p, min(a + TAU - p, n - p), p);
+            const u64 lo = ext_bwd(a, a >= 127 ? a - 127 : 0, p);
             // Q on (a-128, a]: j >= lo, j + tau - p <= hi, j <= n - tau
             int64_t jlo = (int64_t)lo;
             int64_t jhi = min((int64_t)a, (int64_t)hi + (int64_t)p - (int64_t)TAU);
@@ -90,12 +115,9 @@ __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64
                 atomicOr(any_q, 1u);
             }
             // local extent of the p-periodic run around the window (for run-skipping LCE)
-            u64 h2 = hi;
             const u64 h2_cap = min(a + RUN_HCAP - p, n - p);
-            while (h2 < h2_cap && buf[h2 - base] == buf[h2 + p - base]) h2++;
-            u64 l2 = lo;
-            const u64 l2_cap = a >= RUN_LCAP ? a - RUN_LCAP : 0;
-            while (l2 > l2_cap && buf[l2 - 1 - base] == buf[l2 - 1 + p - base]) l2--;
+            const u64 h2 = hi < min(a + TAU - p, n - p) ? hi : ext_fwd(hi, h2_cap, p);
+            const u64 l2 = (lo > (a >= 127 ? a - 127 : 0)) ? lo : ext_bwd(lo, a >= RUN_LCAP ? a - RUN_LCAP : 0, p);
             rp = p;
             rhi = (u32)(h2 + p);
             rlo = (u32)l2;
@@ -140,179 +162,216 @@ __global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restr
 }
 
 // ---------------------------------------------------------------------------
-// main pass
-constexpr int SL = 4096;     // sync candidates per lane
-constexpr int NLW = 256;     // lanes per workgroup
-constexpr int CH = 128;      // staging chunk (bytes per lane row)
-constexpr int RSB = CH + 16; // LDS row stride (conflict-free ds_read_b128)
-constexpr int DQ = 32;       // deque capacity per lane
-constexpr int LCAP = 128;    // per-lane output capacity
-constexpr int NCH = (SL + 2 * TAU) / CH;
+// main pass: one workgroup per tile of TL decisions i in [t0, t0+TL)
+//
+//   bytes   T[t0 .. t0+8192)             staged once in LDS (coalesced uint4)
+//   hashes  Phi(j), j in [t0, t0+7680)   prefix-hash scan over 512 threads x 16
+//                                        bytes, then 15 rolls per thread
+//   minima  m_i = min Phi'[i..i+512]     van Herk / Gil-Werman with 512-blocks:
+//                                        m_i = min(suffix_c[o], prefix_c+1[o]),
+//                                        both from wave scans held in registers
+//   output  i in S  <=>  m_i < inf and (Phi'(i) == m_i or Phi'(i+512) == m_i)
+constexpr int TL = 7168;            // decisions per tile (14 blocks of 512)
+constexpr int TB = TL + 2 * TAU;    // staged bytes = 8192 = 512 threads x 16
+constexpr int TP = TL + TAU;        // Phi' values per tile = 7680 (15 blocks)
+constexpr int TWG = 512;            // threads per tile
+constexpr int TCAP = 256;           // sync positions per tile before the exact fallback
+static_assert(TB == TWG * 16, "tile bytes must be 16 per thread");
 
-struct lane_state {
-    u64 fp;
-    u64 front_val, back_val;
-    u32 front_pos, cnt, h;
-    u64 last_emit;
-    u32 nout, flag;
+struct sss_pow {
+    u32 scan[6];   // b^(16 * 2^d)
+    u32 pw16[64];  // b^(16 k)
+    u32 b1024;     // b^1024 (one wave of bytes)
+    u32 b512;      // b^512 = b^tau
+    u32 bn;        // P - b^tau
 };
 
-__global__ __launch_bounds__(256, 1) void k_sss_main(const u8* __restrict__ T, u64 n, u64 last_i,
-                                                     const u16* __restrict__ qinfo, u32* __restrict__ lane_out,
-                                                     u32* __restrict__ lane_cnt, u32* __restrict__ lane_flag,
-                                                     u32* __restrict__ any_flag, u32 b, u64 bn) {
-    __shared__ __attribute__((aligned(16))) u8 s_in[NLW * RSB];
-    __shared__ __attribute__((aligned(16))) u8 s_out[NLW * RSB];
-    __shared__ u64 s_dqv[DQ * NLW];
-    __shared__ u16 s_dqp[DQ * NLW];
-    const int tid = threadIdx.x;
-    const u64 lane = (u64)blockIdx.x * NLW + tid;
-    const u64 wg_i0 = (u64)blockIdx.x * NLW * SL;
-    const u64 i0 = lane * SL;
-    const bool active = i0 <= last_i;
-    const u64 i_end = active ? min(i0 + SL, last_i + 1) : i0;
-    const u64 j_end = active ? min(i0 + SL + TAU - 1, n - TAU) : 0;
-    const u64 kend = active ? j_end - i0 + TAU : 0;
-    const u32 bn_lo = (u32)bn, bn_hi = (u32)(bn >> 32);
+// canonical x mod (2^31 - 1) for x < 2^63
+__device__ __forceinline__ u32 red31(u64 x) {
+    u64 r = (x & P31) + (x >> 31);
+    r = (r & P31) + (r >> 31);
+    return (u32)(r >= P31 ? r - P31 : r);
+}
+__device__ __forceinline__ u32 mulmod31(u32 a, u32 c) { return red31((u64)a * c); }
+__device__ __forceinline__ u32 shfl_up32(u32 v, u32 d) { return __shfl_up(v, d, 64); }
+__device__ __forceinline__ u32 shfl_down32(u32 v, u32 d) { return __shfl_down(v, d, 64); }
 
-    u64 fp = 0, front_val = 0, back_val = 0, last_emit = INF64;
-    u32 front_pos = 0, cnt = 0, h = 0, nout = 0, flag = 0;
-    u64 cur_anchor = INF64;
-    u32 qs = 255, qe = 0;
-    u32* myout = lane_out + lane * LCAP;
+__global__ __launch_bounds__(TWG, 3) void k_sss_tile(const u8* __restrict__ T, u64 n, u64 last_i,
+                                                     const u16* __restrict__ qinfo, u32* __restrict__ tile_out,
+                                                     u32* __restrict__ tile_cnt, u32* __restrict__ tile_flag,
+                                                     u32* __restrict__ any_flag, u32 b, sss_pow PW) {
+    __shared__ __attribute__((aligned(16))) u8 s_t[TB + 16];
+    __shared__ u32 s_h[TWG + 1];
+    __shared__ u32 s_phi[TP + TP / 16];  // padded: index u + u/16 (bank spread)
+    __shared__ u32 s_wt[TWG / 64];
+    __shared__ u32 s_bc[TL / 512];
+    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const u64 t0 = (u64)blockIdx.x * TL;
 
-    auto emit = [&](u64 i) {
-        if (last_emit == INF64 || i > last_emit) {
-            if (nout < LCAP) myout[nout] = (u32)i; else flag = 1;
-            nout++;
-            last_emit = i;
-        }
-    };
-
-    for (int c = 0; c < NCH; c++) {
-        __syncthreads();
+    // 1. stage the tile's bytes (zero padded past n + TEXT_PAD)
+    {
+        const u64 g = t0 + 16ull * tid;
+        uint4 v = {0, 0, 0, 0};
+        if (g + 16 <= n + TEXT_PAD) v = *(const uint4*)(T + g);
+        *(uint4*)&s_t[16 * tid] = v;
+        if (tid == 0) *(uint4*)&s_t[TB] = uint4{0, 0, 0, 0};
+    }
+    __syncthreads();
+    // 2. prefix hashes at every 16-byte boundary
+    const uint4 mine = *(const uint4*)&s_t[16 * tid];
+    const u32 mw[4] = {mine.x, mine.y, mine.z, mine.w};
+    u32 h = 0;
 #pragma unroll
-        for (int r = 0; r < (NLW * CH / 16) / NLW; r++) {
-            const int piece = r * NLW + tid;
-            const int row = piece >> 3, col = (piece & 7) * 16;
-            const u64 rowi0 = wg_i0 + (u64)row * SL;
-            const u64 g = rowi0 + (u64)c * CH + col;
-            uint4 vin = {0, 0, 0, 0}, vout = {0, 0, 0, 0};
-            if (rowi0 <= last_i) {
-                vin = *(const uint4*)(T + g);
-                if (c * CH >= (int)TAU) vout = *(const uint4*)(T + g - TAU);
+    for (int k = 0; k < 16; k++) h = red31((u64)h * b + ((mw[k >> 2] >> (8 * (k & 3))) & 255u));
+    u32 inc = h;
+#pragma unroll
+    for (int d = 0; d < 6; d++) {
+        const u32 left = shfl_up32(inc, 1u << d);
+        if (lane >= (1u << d)) inc = red31((u64)left * PW.scan[d] + inc);
+    }
+    u32 exc = shfl_up32(inc, 1);
+    if (lane == 0) exc = 0;
+    if (lane == 63) s_wt[wv] = inc;
+    __syncthreads();
+    u32 hw = 0;  // prefix hash of the bytes before this wave
+    for (u32 v = 0; v < wv; v++) hw = red31((u64)hw * PW.b1024 + s_wt[v]);
+    const u32 hl = red31((u64)hw * PW.pw16[lane] + exc);
+    s_h[tid] = hl;
+    if (tid == TWG - 1) s_h[TWG] = red31((u64)hl * PW.scan[0] + h);
+    __syncthreads();
+    // 3. Phi'(u) for u in [16 tid, 16 tid + 16), u < TP
+    if (16 * tid < (u32)TP) {
+        // Phi(u0) = H(u0 + 512) - H(u0) * b^512
+        u32 fp = red31((u64)s_h[tid + 32] + (P31 - mulmod31(hl, PW.b512)));
+        const u64 j0 = t0 + 16ull * tid;
+        const u64 jmax = n >= TAU ? n - TAU : 0;  // last position with a full window
+        const u64 ta = (j0 + 127) >> 7;
+        u16 q0 = 0xFF00, q1 = 0xFF00;
+        if (j0 <= jmax) {
+            q0 = qinfo[ta];
+            if (((j0 + 15 + 127) >> 7) != ta && j0 + 15 <= jmax) q1 = qinfo[ta + 1];
+        }
+        const uint4 ahead = *(const uint4*)&s_t[16 * tid + TAU];
+        const u32 aw[4] = {ahead.x, ahead.y, ahead.z, ahead.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const u32 u = 16 * tid + k;
+            const u64 j = j0 + k;
+            u32 v = fp;
+            if (j > jmax) {
+                v = INF32;
+            } else {
+                const u64 t = (j + 127) >> 7;
+                const u16 qi = t == ta ? q0 : q1;
+                const u32 rel = (u32)(j + 127 - (t << 7));
+                if (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) v = INF32;
             }
-            *(uint4*)&s_in[row * RSB + col] = vin;
-            *(uint4*)&s_out[row * RSB + col] = vout;
-        }
-        __syncthreads();
-        if (!active) continue;
-        for (int qd = 0; qd < CH / 16; qd++) {
-            const uint4 vi = *(const uint4*)&s_in[tid * RSB + qd * 16];
-            const uint4 vo = *(const uint4*)&s_out[tid * RSB + qd * 16];
-            const u32 wi4[4] = {vi.x, vi.y, vi.z, vi.w}, wo4[4] = {vo.x, vo.y, vo.z, vo.w};
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                    const u32 k = c * CH + qd * 16 + w * 4 + kk;
-                    const u32 in = (wi4[w] >> (8 * kk)) & 255u, out = (wo4[w] >> (8 * kk)) & 255u;
-                    // fp <- fp*b + in - out*b^tau  (lazy mod 2^61-1, fp < 2^62)
-                    const u32 lo = (u32)fp, hi = (u32)(fp >> 32);
-                    u64 a0 = (u64)lo * b + in;
-                    a0 += (u64)bn_lo * out;
-                    u64 a1 = (u64)hi * b + (a0 >> 32);
-                    a1 += (u64)bn_hi * out;
-                    fp = ((((a1 << 32) | (u32)a0)) & P61) + (a1 >> 29);
-                    if (k + 1 < TAU || k >= kend) continue;
-                    const u64 j = i0 + k - TAU + 1;
-                    const u32 jo = (u32)(j - i0);
-                    const u64 t = (j + 127) >> 7;
-                    if (t != cur_anchor) {
-                        cur_anchor = t;
-                        const u16 qi = qinfo[t];
-                        qs = qi >> 8;
-                        qe = qi & 255;
-                    }
-                    const u32 rel = (u32)(j + 127 - (t << 7));
-                    const u64 v = (rel >= qs && rel <= qe) ? INF64 : mod61_canon(fp);
-                    // 1. expiry of the front: it survived (f, f+tau] -> A(f)
-                    if (cnt && front_pos + TAU + 1 == jo) {
-                        const u64 f = i0 + front_pos;
-                        if (f < i_end) emit(f);
-                        h = (h + 1) & (DQ - 1);
-                        cnt--;
-                        if (cnt) {
-                            front_val = s_dqv[h * NLW + tid];
-                            front_pos = s_dqp[h * NLW + tid];
-                        }
-                    }
-                    // 2. B(j): v <= min of the previous tau values -> i = j - tau
-                    if (v != INF64 && jo >= TAU && (cnt == 0 || v <= front_val)) {
-                        const u64 i = j - TAU;
-                        if (i < i_end) emit(i);
-                    }
-                    // 3. pop larger values from the back
-                    while (cnt && back_val > v) {
-                        cnt--;
-                        if (cnt) back_val = s_dqv[((h + cnt - 1) & (DQ - 1)) * NLW + tid];
-                    }
-                    // 4. push
-                    if (v != INF64) {
-                        if (cnt == DQ) {
-                            flag = 1;
-                        } else {
-                            const u32 e = (h + cnt) & (DQ - 1);
-                            s_dqv[e * NLW + tid] = v;
-                            s_dqp[e * NLW + tid] = (u16)jo;
-                            cnt++;
-                            back_val = v;
-                            if (cnt == 1) { front_val = v; front_pos = jo; }
-                        }
-                    }
-                }
+            s_phi[u + (u >> 4)] = v;
+            if (k < 15) {
+                const u32 in = (aw[k >> 2] >> (8 * (k & 3))) & 255u, out = (mw[k >> 2] >> (8 * (k & 3))) & 255u;
+                fp = red31((u64)fp * b + in + (u64)out * PW.bn);
             }
         }
     }
-    if (active) {
-        for (u32 x = 0; x < cnt; x++) {
-            const u64 f = i0 + s_dqp[((h + x) & (DQ - 1)) * NLW + tid];
-            if (f < i_end) emit(f);
+    __syncthreads();
+    // 4. window minima: wave w handles block pairs (c, c+1) for c = w, w + 8 (c < 14)
+    u32 masks[2] = {0, 0};
+    for (int r = 0; r < 2; r++) {
+        const u32 c = wv + 8 * r;
+        if (c >= (u32)(TL / 512)) break;
+        u32 x[8], y[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const u32 ux = c * 512 + 8 * lane + e, uy = ux + 512;
+            x[e] = s_phi[ux + (ux >> 4)];
+            y[e] = s_phi[uy + (uy >> 4)];
         }
-        lane_cnt[lane] = nout;
-        lane_flag[lane] = flag;
-        if (flag) atomicOr(any_flag, 1u);
-    } else if (lane < (u64)gridDim.x * NLW) {
-        lane_cnt[lane] = 0;
-        lane_flag[lane] = 0;
+        // suffix minima of block c, prefix minima of block c+1
+        u32 sx[8], py[8];
+        sx[7] = x[7];
+#pragma unroll
+        for (int e = 6; e >= 0; e--) sx[e] = min(x[e], sx[e + 1]);
+        py[0] = y[0];
+#pragma unroll
+        for (int e = 1; e < 8; e++) py[e] = min(py[e - 1], y[e]);
+        // lanes after this one (suffix) / before it (prefix)
+        u32 sufL = sx[0], preL = py[7];
+#pragma unroll
+        for (int d = 0; d < 6; d++) {
+            const u32 dn = shfl_down32(sufL, 1u << d);
+            if (lane + (1u << d) < 64) sufL = min(sufL, dn);
+            const u32 up = shfl_up32(preL, 1u << d);
+            if (lane >= (1u << d)) preL = min(preL, up);
+        }
+        u32 suf_after = shfl_down32(sufL, 1), pre_before = shfl_up32(preL, 1);
+        if (lane == 63) suf_after = INF32;
+        if (lane == 0) pre_before = INF32;
+        u32 mk = 0;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const u32 m = min(min(sx[e], suf_after), min(pre_before, py[e]));
+            const u64 i = t0 + c * 512 + 8 * lane + e;
+            if (m != INF32 && (x[e] == m || y[e] == m) && i <= last_i) mk |= 1u << e;
+        }
+        masks[r] = mk;
+        u32 cnt = __popc(mk);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+        if (lane == 0) s_bc[c] = cnt;
+    }
+    __syncthreads();
+    // 5. ordered output: block offsets, then lane offsets inside the block
+    u32 tot = 0;
+    for (int c = 0; c < TL / 512; c++) tot += s_bc[c];
+    for (int r = 0; r < 2; r++) {
+        const u32 c = wv + 8 * r;
+        if (c >= (u32)(TL / 512)) break;
+        u32 boff = 0;
+        for (u32 cc = 0; cc < c; cc++) boff += s_bc[cc];
+        const u32 mk = masks[r];
+        const u32 pc = __popc(mk);
+        u32 incl = pc;
+#pragma unroll
+        for (int d = 0; d < 6; d++) {
+            const u32 up = __shfl_up(incl, 1u << d, 64);
+            if (lane >= (1u << d)) incl += up;
+        }
+        u32 o = boff + incl - pc;
+        for (int e = 0; e < 8; e++)
+            if (mk & (1u << e)) {
+                if (o < (u32)TCAP) tile_out[(u64)blockIdx.x * TCAP + o] = (u32)(t0 + c * 512 + 8 * lane + e);
+                o++;
+            }
+    }
+    if (tid == 0) {
+        tile_cnt[blockIdx.x] = tot;
+        tile_flag[blockIdx.x] = tot > (u32)TCAP;
+        if (tot > (u32)TCAP) atomicOr(any_flag, 1u);
     }
 }
 
-// Exact slow path for lanes whose deque or output buffer overflowed: one
-// workgroup recomputes the lane's Phi' values and the window minima directly.
+// Exact slow path for tiles whose output buffer overflowed: one workgroup
+// recomputes the tile's Phi' values and the window minima directly.
 __global__ __launch_bounds__(256) void k_sss_fallback(const u8* __restrict__ T, u64 n, u64 last_i,
                                                       const u16* __restrict__ qinfo, const u32* __restrict__ lanes,
                                                       u64* __restrict__ scratch, u8* __restrict__ member,
                                                       u32* __restrict__ ovf_out, u32* __restrict__ lane_cnt, u32 b,
                                                       u64 bpow) {
     const u64 lane = lanes[blockIdx.x];
-    const u64 i0 = lane * SL;
-    const u64 i_end = min(i0 + SL, last_i + 1);
-    const u64 j_end = min(i0 + SL + TAU - 1, n - TAU);
-    u64* v = scratch + (u64)blockIdx.x * (SL + TAU);
-    u8* mem = member + (u64)blockIdx.x * SL;
+    const u64 i0 = lane * TL;
+    const u64 i_end = min(i0 + TL, last_i + 1);
+    const u64 j_end = min(i0 + TL + TAU - 1, n - TAU);
+    u64* v = scratch + (u64)blockIdx.x * (TL + TAU);
+    u8* mem = member + (u64)blockIdx.x * TL;
     if (threadIdx.x == 0) {
         u64 fp = 0;
-        for (u64 k = 0; k < TAU; k++) fp = mod61_canon(((u64)((u128)fp * b % P61)) + T[i0 + k]);
+        for (u64 k = 0; k < TAU; k++) fp = (fp * b + T[i0 + k]) % P31;
         for (u64 j = i0; j <= j_end; j++) {
             const u64 t = (j + 127) >> 7;
             const u16 qi = qinfo[t];
             const u32 rel = (u32)(j + 127 - (t << 7));
             v[j - i0] = (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) ? INF64 : fp;
-            if (j < j_end) {
-                u128 x = (u128)fp * b + T[j + TAU] + (u128)(P61 - bpow) * T[j];
-                fp = (u64)(x % P61);
-            }
+            if (j < j_end) fp = (fp * b + T[j + TAU] + (P31 - bpow) * T[j]) % P31;
         }
     }
     __syncthreads();
@@ -325,7 +384,7 @@ __global__ __launch_bounds__(256) void k_sss_fallback(const u8* __restrict__ T, 
     if (threadIdx.x == 0) {
         u32 c = 0;
         for (u64 i = i0; i < i_end; i++)
-            if (mem[i - i0]) ovf_out[(u64)blockIdx.x * SL + c++] = (u32)i;
+            if (mem[i - i0]) ovf_out[(u64)blockIdx.x * TL + c++] = (u32)i;
         lane_cnt[lane] = c;
     }
 }
@@ -337,15 +396,15 @@ __global__ void k_sss_compact(const u32* __restrict__ lane_out, const u32* __res
     const u64 lane = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= nlanes) return;
     const u32 c = lane_cnt[lane], o = lane_off[lane];
-    const u32* src = lane_flag[lane] ? ovf_out + (u64)ovf_slot[lane] * SL : lane_out + lane * LCAP;
+    const u32* src = lane_flag[lane] ? ovf_out + (u64)ovf_slot[lane] * TL : lane_out + lane * TCAP;
     for (u32 x = 0; x < c; x++) S[o + x] = src[x];
 }
 
-static u64 pow61_host(u64 b, u64 e) {
+static u64 pow31_host(u64 b, u64 e) {
     u64 r = 1;
     while (e) {
-        if (e & 1) r = (u64)((u128)r * b % P61);
-        b = (u64)((u128)b * b % P61);
+        if (e & 1) r = r * b % P31;
+        b = b * b % P31;
         e >>= 1;
     }
     return r;
@@ -382,19 +441,28 @@ void engine::build_sss(const u8* T) {
         runs_valid = true;
     }
 
-    const u64 nlanes_need = last_i / SL + 1;
-    const unsigned nwg = cdiv(nlanes_need, NLW);
-    const u64 nlanes = (u64)nwg * NLW;
-    u32* lo = lane_out.get(nlanes * LCAP);
+    const u64 nlanes = last_i / TL + 1;  // tiles
+    u32* lo = lane_out.get(nlanes * TCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
-    const u64 bpow = pow61_host(SSS_BASE, TAU);
-    const u64 bn = (P61 - bpow) % P61;
+    sss_pow PW;
+    {
+        auto mm = [](u64 x, u64 y) { return x * y % P31; };
+        u64 b16 = pow31_host(SSS_BASE, 16);
+        for (int d = 0; d < 6; d++) { PW.scan[d] = (u32)b16; b16 = mm(b16, b16); }
+        PW.pw16[0] = 1;
+        const u64 p16 = pow31_host(SSS_BASE, 16);
+        for (int k = 1; k < 64; k++) PW.pw16[k] = (u32)mm(PW.pw16[k - 1], p16);
+        PW.b1024 = (u32)pow31_host(SSS_BASE, 1024);
+        PW.b512 = (u32)pow31_host(SSS_BASE, TAU);
+        PW.bn = (u32)((P31 - PW.b512) % P31);
+    }
+    const u64 bpow = PW.b512;
     hipEvent_t e0, e1;
     LZ_HIP(hipEventCreate(&e0));
     LZ_HIP(hipEventCreate(&e1));
     LZ_HIP(hipEventRecord(e0, st));
-    k_sss_main<<<nwg, NLW, 0, st>>>(T, n, last_i, qi, lo, lc, lf, ctr + 1, (u32)SSS_BASE, bn);
+    k_sss_tile<<<(unsigned)nlanes, TWG, 0, st>>>(T, n, last_i, qi, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW);
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipEventRecord(e1, st));
 
@@ -408,7 +476,7 @@ void engine::build_sss(const u8* T) {
     (void)hipEventDestroy(e1);
     has_runs = h_ctr[0] != 0;
 
-    // overflow lanes -> exact slow path
+    // overflowing tiles -> exact slow path
     u32* ovf_slot = u32c.get(nlanes);
     u32* ovf_out = nullptr;
     if (h_ctr[1]) {
@@ -420,9 +488,9 @@ void engine::build_sss(const u8* T) {
         u32* d_lanes = u32d.get(lanes.size());
         LZ_HIP(hipMemcpy(d_lanes, lanes.data(), lanes.size() * 4, hipMemcpyHostToDevice));
         LZ_HIP(hipMemcpy(ovf_slot, slot.data(), nlanes * 4, hipMemcpyHostToDevice));
-        u64* scratch = u64a.get(lanes.size() * (SL + TAU));
-        u8* member = tmp_bytes.get(lanes.size() * SL);
-        ovf_out = u32b.get(lanes.size() * SL);
+        u64* scratch = u64a.get(lanes.size() * (TL + TAU));
+        u8* member = tmp_bytes.get(lanes.size() * TL);
+        ovf_out = u32b.get(lanes.size() * TL);
         k_sss_fallback<<<(unsigned)lanes.size(), 256, 0, st>>>(T, n, last_i, qi, d_lanes, scratch, member, ovf_out,
                                                                lc, (u32)SSS_BASE, bpow);
         LZ_HIP(hipGetLastError());

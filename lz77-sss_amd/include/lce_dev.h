@@ -47,6 +47,41 @@ __device__ inline u64 dev_lce_fwd(const u8* T, const run_tab& R, u64 i, u64 j, u
     }
     return lim;
 }
+// wave-cooperative dev_lce_fwd: all 64 lanes call it with the same arguments and
+// get the same result; 512 bytes are compared per step (8 per lane)
+__device__ inline u64 wave_lce_fwd(const u8* T, const run_tab& R, u64 i, u64 j, u64 lim, u32 lane) {
+    u64 k = 0;
+    while (k < lim) {
+        const u64 step = min<u64>(lim - k, 512);
+        const u64 off = 8 * lane;
+        bool diff = false;
+        if (off < step) {
+            u64 x = ldu64(T + i + k + off), y = ldu64(T + j + k + off);
+            const u64 r = step - off;
+            if (r < 8) { const u64 msk = (1ull << (8 * r)) - 1; x &= msk; y &= msk; }
+            diff = x != y;
+        }
+        const u64 bal = __ballot(diff);
+        if (bal) {
+            const u64 fo = k + 8 * (u64)__builtin_ctzll(bal);
+            const u64 x = ldu64(T + i + fo), y = ldu64(T + j + fo);
+            return fo + (__builtin_ctzll(x ^ y) >> 3);
+        }
+        k += step;
+        if (k >= lim || !R.p || k < 512) return min(k, lim);
+        const u64 xi = i + k, yj = j + k;
+        const u64 ax = (xi - 340) >> 7, by = (yj - 340) >> 7;
+        const u32 pp = R.p[ax];
+        if (pp == 0 || R.p[by] != pp) continue;
+        const u64 hx = R.hi[ax], hy = R.hi[by];
+        if (hx < xi || hy < yj) continue;
+        const u64 dx = hx - xi, dy = hy - yj, d = min(dx, dy);
+        if (k + d >= lim) return lim;
+        k += d;
+        if (dx != dy) return k;
+    }
+    return lim;
+}
 // #equal chars going left from i and j (T[i-t] == T[j-t]), at most lim <= min(i,j)+1
 __device__ __forceinline__ u64 dev_naive_lce_left(const u8* T, u64 i, u64 j, u64 lim) {
     u64 k = 0;

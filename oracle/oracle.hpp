@@ -88,7 +88,7 @@ static inline u32 lce_left(const u8* T, u32 i, u32 j, u32 cap = 0xFFFFFFFFu) {
 //  SSS  (definition pinned here; upstream lce::rolling_hash::sss is absent,
 //        called at lce_sss.hpp:53)
 //
-//  Phi(j)  = sum_{k<tau} T[j+k] * b^(tau-1-k)  mod (2^61-1),  b = SSS_BASE,
+//  Phi(j)  = sum_{k<tau} T[j+k] * b^(tau-1-k)  mod (2^31-1),  b = SSS_BASE,
 //            for j in [0, n-tau]                       (Karp-Rabin, canonical)
 //  Q       = { j in [0,n-tau] : T[j..j+tau) has a period p <= floor(tau/3) }
 //  Phi'(j) = Phi(j) if j not in Q, else +inf
@@ -96,21 +96,17 @@ static inline u32 lce_left(const u8* T, u32 i, u32 j, u32 cap = 0xFFFFFFFFu) {
 //                                (Phi'(i) == m_i or Phi'(i+tau) == m_i) }
 //  has_runs = (Q is non-empty)
 // ===========================================================================
-static constexpr u64 P61 = (1ull << 61) - 1;
+static constexpr u64 P31 = (1ull << 31) - 1;  // Mersenne prime of the SSS fingerprint
 static constexpr u64 SSS_BASE = 296819;
 static constexpr u64 SSS_INF = ~0ull;
 static constexpr u32 QL = TAU / 3;      // period bound floor(tau/3) = 170
 static constexpr u32 QM = 2 * QL;       // probe length 340
 static constexpr u32 QA = 128;          // anchor stride (<= tau - 2L + 1)
 
-static inline u64 mod61(u128 x) {
-    u64 r = (u64)(x & P61) + (u64)(x >> 61);
-    r = (r & P61) + (r >> 61);
-    return r >= P61 ? r - P61 : r;
-}
-static inline u64 pow61(u64 b, u64 e) {
+static inline u64 mod31(u64 x) { return x % P31; }
+static inline u64 pow31(u64 b, u64 e) {
     u64 r = 1;
-    while (e) { if (e & 1) r = mod61((u128)r * b); b = mod61((u128)b * b); e >>= 1; }
+    while (e) { if (e & 1) r = mod31(r * b); b = mod31(b * b); e >>= 1; }
     return r;
 }
 
@@ -150,11 +146,10 @@ static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
     has_runs = false;
     if (n < 2 * TAU) return S;
     const u64 last_i = n - 2 * TAU;          // sync candidates i in [0, last_i]
-    const u64 last_j = n - TAU;              // fingerprints j in [0, last_j]
     const u64 BLK = 1 << 20;
     const u64 nblk = last_i / BLK + 1;
-    const u64 bpow = pow61(SSS_BASE, TAU);
-    const u64 negpow = (P61 - bpow) % P61;
+    const u64 bpow = pow31(SSS_BASE, TAU);
+    const u64 negpow = (P31 - bpow) % P31;
     std::vector<std::vector<u32>> part(nblk);
     std::vector<u8> runs_flag(nblk, 0);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -174,11 +169,11 @@ static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
         }
         std::vector<u64> phi(m);
         u64 fp = 0;
-        for (u64 k = 0; k < TAU; k++) fp = mod61((u128)fp * SSS_BASE + T[b + k]);
+        for (u64 k = 0; k < TAU; k++) fp = mod31(fp * SSS_BASE + T[b + k]);
         for (u64 j = b; j <= je; j++) {
             phi[j - b] = q[j - b] ? SSS_INF : fp;
             if (q[j - b]) runs_flag[bi] = 1;
-            if (j < je) fp = mod61((u128)fp * SSS_BASE + T[j + TAU] + (u128)negpow * T[j]);
+            if (j < je) fp = mod31(fp * SSS_BASE + T[j + TAU] + negpow * T[j]);
         }
         // sliding-window minimum over [i, i+tau] (monotone deque of indices)
         std::vector<u64> dq(m);

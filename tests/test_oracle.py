@@ -14,24 +14,24 @@ import pytest
 from conftest import golden_names, load_golden
 
 TAU = 512
-P61 = (1 << 61) - 1
+P31 = (1 << 31) - 1
 BASE = 296819
 
 
 def phi_py(T):
-    """Φ(j) = Σ_k T[j+k]·b^(τ−1−k) mod 2^61−1 by a Python-int rolling hash."""
+    """Φ(j) = Σ_k T[j+k]·b^(τ−1−k) mod 2^31−1 by a Python-int rolling hash."""
     n = len(T)
     if n < TAU:
         return np.zeros(0, np.uint64)
-    bp = pow(BASE, TAU, P61)
+    bp = pow(BASE, TAU, P31)
     out = np.zeros(n - TAU + 1, np.uint64)
     h = 0
     t = [int(x) for x in T]
     for k in range(TAU):
-        h = (h * BASE + t[k]) % P61
+        h = (h * BASE + t[k]) % P31
     out[0] = h
     for j in range(1, n - TAU + 1):
-        h = (h * BASE + t[j + TAU - 1] - t[j - 1] * bp) % P61
+        h = (h * BASE + t[j + TAU - 1] - t[j - 1] * bp) % P31
         out[j] = h
     return out
 
