@@ -1,0 +1,105 @@
+// lz77_sss.hpp -- drop-in C++ host mirror of the reference's static template API
+// (include/lz77_sss/lz77_sss.hpp:48-203 of LukasNalbach/lz77-sss) over the
+// C-ABI of liblz77sss_hip.so (include/lz77sss.h).
+//
+// A caller of
+//     lz77_sss<uint32_t>::factorize_approximate<greedy, lpf_opt, 512>(T, n, out, {.num_threads = p});
+//     lz77_sss<uint32_t>::decode(fact_it, out_it, n);
+// keeps its code and links against the HIP library instead.  Differences:
+//   * the factorization runs on an MI355X (device `parameters::device`) with the
+//     p = 1 output stream of the reference (num_threads is accepted and ignored);
+//   * errors surface as lz77_sss_error (the reference only asserts); no CPU fallback;
+//   * pos_t = uint32_t only (n < 2^32); the factor layout is the reference's
+//     `factor{pos_t src, len}` (8 bytes, literal <=> len == 0, src = the byte);
+//   * the input is not modified (the reference's LPF/LNF modes reverse it in place
+//     and restore it, lz77_sss.hpp:385-393).
+#pragma once
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/lz77sss.h"
+
+enum phrase_mode { lpf_naive, lpf_lnf_naive, lpf_opt, lpf_lnf_opt };   // lz77_sss.hpp:48-53
+enum factorize_mode { greedy_naive, greedy, skip_phrases };            // lz77_sss.hpp:55-59
+
+// lz77_sss.hpp:67-70, plus the device-side knobs of this implementation
+struct parameters {
+    uint16_t num_threads = 0;  // accepted for source compatibility (p = 1 semantics)
+    bool log = false;          // phase timings on stderr
+    int device = 0;            // HIP device ordinal
+    uint32_t rk_seed = 42;     // seed of the gap-index Karp-Rabin bases (rolling_hash.hpp:127-130)
+};
+
+struct lz77_sss_error : std::runtime_error {
+    int code;
+    lz77_sss_error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+template <typename pos_t = uint32_t>
+class lz77_sss {
+    static_assert(std::is_same_v<pos_t, uint32_t>, "this implementation provides pos_t = uint32_t");
+
+    static void check(int rc) {
+        if (rc != LZ77SSS_OK) {
+            const char* m = lz77sss_last_error();
+            throw lz77_sss_error(rc, std::string("lz77sss: ") + (m ? m : "error"));
+        }
+    }
+
+  public:
+    static constexpr phrase_mode default_phr_mode = lpf_opt;
+    static constexpr factorize_mode default_fact_mode = greedy;
+    static constexpr uint64_t default_tau = 512;
+
+    struct factor {  // lz77_sss.hpp:129-147 (same 8-byte layout as lz77sss_factor32)
+        pos_t src;
+        pos_t len;
+        pos_t length() const { return len > 1 ? len : 1; }
+    };
+    static_assert(sizeof(factor) == sizeof(lz77sss_factor32));
+
+    // lz77_sss.hpp:176-186: factors are handed to `output` by value, in text order,
+    // on the calling thread.
+    template <factorize_mode fact_mode = default_fact_mode, phrase_mode phr_mode = default_phr_mode,
+              uint64_t tau = default_tau, typename char_t, typename output_fnc_t>
+    static void factorize_approximate(char_t* input, pos_t input_size, output_fnc_t output, parameters params = {}) {
+        static_assert(sizeof(char_t) == 1, "byte alphabet only (lz77_sss.hpp:287)");
+        lz77sss_params p;
+        lz77sss_default_params(&p);
+        p.phr_mode = static_cast<int32_t>(phr_mode);
+        p.fact_mode = static_cast<int32_t>(fact_mode);
+        p.tau = static_cast<uint32_t>(tau);
+        p.rk_seed = params.rk_seed;
+        p.device = params.device;
+        p.log = params.log ? 1 : 0;
+        p.num_threads = params.num_threads;
+        struct ctx_t {
+            output_fnc_t* out;
+        } ctx{&output};
+        auto emit = [](const lz77sss_factor32* batch, uint64_t count, void* user) -> int {
+            auto* c = static_cast<ctx_t*>(user);
+            for (uint64_t k = 0; k < count; k++) (*c->out)(factor{batch[k].src, batch[k].len});
+            return 0;
+        };
+        check(lz77sss_factorize_approx_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p, emit, &ctx));
+    }
+
+    // lz77_sss.hpp:202-203 (algorithms/common.cpp:31-54): sequential host decode
+    template <typename fact_it_t, typename out_it_t>
+    static void decode(fact_it_t fact_it, out_it_t out_it, pos_t output_size) {
+        std::vector<uint8_t> buf(output_size);
+        std::vector<lz77sss_factor32> fs;
+        for (uint64_t pos = 0; pos < output_size;) {
+            const factor f = *fact_it;
+            ++fact_it;
+            fs.push_back({f.src, f.len});
+            pos += f.length();
+        }
+        check(lz77sss_decode_u32(fs.data(), fs.size(), buf.data(), output_size));
+        for (uint64_t i = 0; i < output_size; i++) *out_it++ = static_cast<char>(buf[i]);
+    }
+};

@@ -1,0 +1,36 @@
+// Uses the C++ mirror of the reference API exactly as the reference's own test
+// does (tests/test_lz77_sss.cpp:73-82: decode(factorize(T)) == T), on
+// random_repetitive_string(10^4, 2*10^5) texts with seeds 1..N.
+// Exit status: 0 = all round trips equal, 2 = no device (error surfaced, no fallback), 1 = mismatch.
+#include "../../lz77-sss_amd/host/lz77_sss.hpp"
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+int main(int argc, char** argv) {
+    const int nseeds = argc > 1 ? std::atoi(argv[1]) : 4;
+    using lz = lz77_sss<uint32_t>;
+    for (int seed = 1; seed <= nseeds; seed++) {
+        std::vector<uint8_t> buf(200000 + 16);
+        const int64_t n = lz77sss_gen_random_repetitive(10000, 200000, seed, -1.0, -1.0, buf.data(), 200000);
+        if (n < 0) return 1;
+        std::string T(reinterpret_cast<char*>(buf.data()), (size_t)n);
+        std::vector<lz::factor> F;
+        try {
+            lz::factorize_approximate<greedy, lpf_opt>(T.data(), (uint32_t)n, [&](lz::factor f) { F.push_back(f); });
+        } catch (const lz77_sss_error& e) {
+            std::printf("error %d: %s\n", e.code, e.what());
+            return e.code == LZ77SSS_ENODEV ? 2 : 1;
+        }
+        std::string D;
+        lz::decode(F.begin(), std::back_inserter(D), (uint32_t)n);
+        if (D != T) {
+            std::printf("seed %d: round trip FAILED\n", seed);
+            return 1;
+        }
+        std::printf("seed %d: n=%lld z=%zu ok\n", seed, (long long)n, F.size());
+    }
+    return 0;
+}

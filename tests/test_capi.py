@@ -70,3 +70,26 @@ def test_no_cpu_fallback_without_device(lz):
         lz.factorize_approximate(T)
     with pytest.raises(lz.Lz77SssError):
         lz.Session(1 << 20)
+
+
+def build_cpp_client(tmp_path):
+    import subprocess
+
+    exe = tmp_path / "api_roundtrip"
+    src = ROOT / "tests" / "cpp" / "api_roundtrip.cpp"
+    libdir = ROOT / "lz77-sss_amd" / "lib"
+    subprocess.run(["g++", "-O1", "-std=c++20", str(src), "-o", str(exe), f"-L{libdir}", "-llz77sss_hip",
+                    f"-Wl,-rpath,{libdir}"], check=True)
+    return exe
+
+
+def test_cpp_mirror_compiles_and_fails_loudly_without_device(lz, tmp_path):
+    """The C++ template mirror (lz77-sss_amd/host/lz77_sss.hpp) builds against the C-ABI; without a
+    device the factorization raises lz77_sss_error(ENODEV) instead of falling back to the CPU."""
+    import subprocess
+
+    exe = build_cpp_client(tmp_path)
+    if lz.load_library().lz77sss_device_count() > 0:
+        pytest.skip("a device is present (the GPU test runs the binary)")
+    r = subprocess.run([str(exe), "1"], capture_output=True, text=True)
+    assert r.returncode == 2, r.stdout + r.stderr

@@ -154,3 +154,15 @@ def test_one_gib_properties(session, orc, lz, kind):
     if kind == "rr":  # the oracle finishes this one in seconds
         F_ref, _ = orc.factorize(T)
         assert np.array_equal(F, F_ref)
+
+
+def test_cpp_mirror_roundtrip(tmp_path):
+    """The reference's own test shape through the C++ template mirror on the GPU."""
+    import subprocess
+
+    from test_capi import build_cpp_client
+
+    exe = build_cpp_client(tmp_path)
+    r = subprocess.run([str(exe), "8"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(" ok") == 8
