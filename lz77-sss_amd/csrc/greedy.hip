@@ -343,20 +343,6 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
     out.nbnd = nb;
 }
 
-template <bool WRITE>
-__global__ void k_walk(walk_ctx W, const seg_in* __restrict__ segs, u32 nseg, seg_out* __restrict__ outs,
-                       const u64* __restrict__ offs, u32* __restrict__ fact) {
-    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nseg) return;
-    seg_out o;
-    o.flags = 0;
-    o.e = segs[t].start;
-    o.nfact = 0;
-    o.nsingle = 0;
-    walk_segment<WRITE>(W, segs[t], o, WRITE ? fact + 2 * offs[t] : nullptr);
-    if (!WRITE) outs[t] = o;
-}
-
 // successor insert (next position of the same slot after y) in the current set:
 // the only query whose lookup can change when y joins or leaves I
 __global__ void k_dirty(walk_ctx W, const u32* __restrict__ ys, u64 m, u32* __restrict__ out) {
@@ -402,33 +388,6 @@ __global__ void k_flip(walk_ctx W, const u32* __restrict__ ys, const u8* __restr
     in_base[k] = rk != NONE;
     if (rk != NONE) rem[rk] = joined[k] ? 0 : 1;
 }
-// rem[r] = (base position r is not in I); I given as sorted disjoint intervals
-__global__ void k_rem_from_set(const u32* __restrict__ ipos, u64 nb, const u32* __restrict__ ia,
-                               const u32* __restrict__ ib, u32 ni, u8* __restrict__ rem) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nb) return;
-    const u32 q = ipos[r];
-    u32 lo = 0, hi = ni;
-    while (lo < hi) {
-        const u32 mid = (lo + hi) >> 1;
-        if (ia[mid] <= q) lo = mid + 1; else hi = mid;
-    }
-    rem[r] = (lo == 0 || q >= ib[lo - 1]) ? 1 : 0;
-}
-// a walked segment is stale iff a dirty position lies in its covered range
-__global__ void k_stale(const u32* __restrict__ lo, const u32* __restrict__ hi, u64 nseg,
-                        const u32* __restrict__ dirty, u64 nd, u8* __restrict__ stale) {
-    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= nseg) return;
-    const u32 a = lo[g], b = hi[g];
-    u64 l = 0, h = nd;
-    while (l < h) {
-        const u64 mid = (l + h) >> 1;
-        if (dirty[mid] < a) l = mid + 1; else h = mid;
-    }
-    stale[g] = (l < nd && dirty[l] <= b) ? 1 : 0;
-}
-
 // ---------------------------------------------------------------------------
 // exact single-thread walk from a segment start to the end of the text, with
 // a local model of the inserts in the tail region (last 64 positions)
@@ -611,48 +570,386 @@ static gap_params_h choose_gap_params(u32 n, u32 num_lpf, u32 len_lpf_phr, u32 n
     return g;
 }
 
-struct interval { u32 a, b; };  // [a, b)
-using ivec = std::vector<interval>;
+// ---------------------------------------------------------------------------
+// device-resident segment table and orchestration (engine::factorize_greedy)
+constexpr u32 PENDING = 0xFFFFFFFEu;  // seg_at entry being created in this pass
 
-static void normalize(ivec& v) {
-    std::sort(v.begin(), v.end(), [](const interval& x, const interval& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); });
-    ivec out;
-    out.reserve(v.size());
-    for (auto& x : v) {
-        if (x.b <= x.a) continue;
-        if (!out.empty() && x.a <= out.back().b) out.back().b = std::max(out.back().b, x.b);
-        else out.push_back(x);
+struct seg_tab {
+    seg_in* sin;
+    seg_out* sout;
+    u8* valid;       // output exact for the current lookup state
+    u32* succ;       // id of the segment starting at sout.next (NONE = unknown)
+    u32* seg_at;     // text position -> segment id (NONE / PENDING)
+    u32* nseg;       // device counter
+    u32 cap;
+    const u32* cbv;  // chunk boundaries (sorted)
+    u32 ncb;
+    const u32* P;    // phrases (beg, end, src) + sentinel
+    u32 m;
+    u32 N, zmask0;
+    u32* err;        // bit 1: table full, 2: too many LPF-start queries, 4: walk guard
+};
+
+__device__ __forceinline__ u32 first_phrase_after(const u32* P, u32 m, u32 a) {  // smallest k: end_k > a
+    u32 lo = 0, hi = m;
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (P[3 * mid + 1] <= a) lo = mid + 1; else hi = mid;
     }
-    v.swap(out);
+    return lo;
 }
-static void clip(ivec& v, u32 nt) {
-    for (auto& x : v) { x.a = std::min(x.a, nt); x.b = std::min(x.b, nt); }
-    normalize(v);
+__device__ __forceinline__ u32 upper_cb(const seg_tab& S, u32 a) {  // first chunk boundary > a (N if none)
+    u32 lo = 0, hi = S.ncb;
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (S.cbv[mid] <= a) lo = mid + 1; else hi = mid;
+    }
+    return lo < S.ncb ? S.cbv[lo] : S.N;
 }
-// a \ b for normalized interval lists
-static ivec subtract(const ivec& a, const ivec& b) {
-    ivec out;
-    size_t j = 0;
-    for (auto x : a) {
-        u32 cur = x.a;
-        while (j < b.size() && b[j].b <= cur) j++;
-        for (size_t k = j; k < b.size() && b[k].a < x.b; k++) {
-            if (b[k].a > cur) out.push_back({cur, b[k].a});
-            cur = std::max(cur, b[k].b);
-            if (cur >= x.b) break;
+__device__ __forceinline__ seg_in make_seg_in(const seg_tab& S, u32 a) {
+    return seg_in{a, first_phrase_after(S.P, S.m, a), a, S.zmask0, upper_cb(S, a)};
+}
+
+// default segments: one per gap (phrase k's gap [end_{k-1}, beg_k)) + chunk
+// boundaries inside long gaps; also the initial speculation I_0 and the base
+// superset (gaps + the LPF-start query position, + interiors of short phrases)
+__device__ __forceinline__ void gap_of(const u32* P, u32 k, u32& a, u32& b) {
+    a = k ? P[3 * (k - 1) + 1] : 0;
+    b = P[3 * k];
+}
+__device__ __forceinline__ u32 gap_chunks(u32 a, u32 b, u32 CH) {
+    return (b > a && b - a > 2 * CH) ? (b - a - CH / 2 - 1) / CH : 0;
+}
+__global__ void k_gap_counts(const u32* __restrict__ P, u32 m, u32 CH, u32* __restrict__ nsegs, u32* __restrict__ ncbs) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > m) return;
+    u32 a, b;
+    gap_of(P, (u32)k, a, b);
+    const u32 K = gap_chunks(a, b, CH);
+    nsegs[k] = (a < b) ? 1 + K : 0;
+    ncbs[k] = K;
+}
+__global__ void k_gap_cbv(const u32* __restrict__ P, u32 m, u32 CH, const u32* __restrict__ cb_off, u32* __restrict__ cbv) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > m) return;
+    u32 a, b;
+    gap_of(P, (u32)k, a, b);
+    const u32 K = gap_chunks(a, b, CH);
+    for (u32 t = 1; t <= K; t++) cbv[cb_off[k] + t - 1] = a + t * CH;
+}
+__global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > S.m) return;
+    u32 a, b;
+    gap_of(S.P, (u32)k, a, b);
+    if (a >= b) return;
+    const u32 K = gap_chunks(a, b, CH);
+    for (u32 t = 0; t <= K; t++) {
+        const u32 x = a + t * CH, id = seg_off[k] + t;
+        S.sin[id] = seg_in{x, (u32)k, x, S.zmask0, upper_cb(S, x)};
+        S.valid[id] = 0;
+        S.succ[id] = NONE;
+        S.seg_at[x] = id;
+    }
+}
+// bitmaps over text positions (bit q of word q >> 5)
+__device__ __forceinline__ void bm_set_range(u32* bm, u32 a, u32 b) {  // [a, b)
+    while (a < b) {
+        const u32 w = a >> 5, lo = a & 31, hi = min(32u, lo + (b - a));
+        const u32 mask = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & ~((1u << lo) - 1);
+        atomicOr(&bm[w], mask);
+        a += hi - lo;
+    }
+}
+__global__ void k_gap_bitmaps(const u32* __restrict__ P, u32 m, u32 N, u32 nt, u32* __restrict__ bmI,
+                              u32* __restrict__ bmSup) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > m) return;
+    u32 a, b;
+    gap_of(P, (u32)k, a, b);
+    if (a < b) {
+        const u32 e = min(min(b + 1, N), nt);
+        if (a < e) {
+            bm_set_range(bmI, a, e);
+            bm_set_range(bmSup, a, e);
         }
-        if (cur < x.b) out.push_back({cur, x.b});
     }
-    return out;
+    if (k < m) {
+        const u32 pb = P[3 * k], pe = P[3 * k + 1];
+        if (pe - pb <= 48 && pb < nt) bm_set_range(bmSup, pb, min(pe, nt));
+    }
 }
-static u64 total_len(const ivec& v) {
-    u64 t = 0;
-    for (auto& x : v) t += x.b - x.a;
-    return t;
+// maximal runs of ones -> intervals [st, en): count starts/ends per word, then write
+__global__ void k_bm_count(const u32* __restrict__ bm, u64 nw, u32* __restrict__ ns, u32* __restrict__ ne) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const u32 b = bm[w], prev = w ? (bm[w - 1] >> 31) : 0u;
+    const u32 sh = (b << 1) | prev;
+    ns[w] = __popc(b & ~sh);
+    ne[w] = __popc(~b & sh);
+}
+__global__ void k_bm_write_runs(const u32* __restrict__ bm, u64 nw, const u32* __restrict__ os,
+                                const u32* __restrict__ oe, u32* __restrict__ st, u32* __restrict__ en) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const u32 b = bm[w], prev = w ? (bm[w - 1] >> 31) : 0u;
+    const u32 sh = (b << 1) | prev;
+    u32 sm = b & ~sh, em = ~b & sh;
+    u32 o = os[w];
+    while (sm) { st[o++] = (u32)(32 * w + __builtin_ctz(sm)); sm &= sm - 1; }
+    o = oe[w];
+    while (em) { en[o++] = (u32)(32 * w + __builtin_ctz(em)); em &= em - 1; }
+}
+// positions of set bits (ascending) with a flag bit from a second bitmap
+__global__ void k_bm_count1(const u32* __restrict__ bm, u64 nw, u32* __restrict__ c) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < nw) c[w] = __popc(bm[w]);
+}
+__global__ void k_bm_xor(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < nw) x[w] = a[w] ^ b[w];
+}
+__global__ void k_bm_andnot(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < nw) x[w] = a[w] & ~b[w];
+}
+__global__ void k_bm_or(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < nw) x[w] = a[w] | b[w];
+}
+__global__ void k_bm_list(const u32* __restrict__ bm, const u32* __restrict__ flagbm, u64 nw, const u32* __restrict__ off,
+                          u32* __restrict__ pos, u8* __restrict__ flag) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    u32 b = bm[w], o = off[w];
+    const u32 f = flagbm ? flagbm[w] : 0u;
+    while (b) {
+        const u32 t = __builtin_ctz(b);
+        pos[o] = (u32)(32 * w + t);
+        if (flag) flag[o] = (f >> t) & 1;
+        o++;
+        b &= b - 1;
+    }
+}
+// intervals -> <= 1024-position chunks with ranks (rank0 = exclusive scan of lengths)
+__global__ void k_iv_chunk_counts(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, u32* __restrict__ nch,
+                                  u32* __restrict__ len) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ni) return;
+    const u32 l = en[k] - st[k];
+    len[k] = l;
+    nch[k] = (l + 1023) / 1024;
+}
+__global__ void k_iv_chunks(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, const u32* __restrict__ choff,
+                            const u32* __restrict__ rank, ichunk* __restrict__ ch) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ni) return;
+    u32 o = choff[k];
+    for (u32 q = st[k]; q < en[k]; q += 1024) ch[o++] = ichunk{q, min(en[k], q + 1024), rank[k] + (q - st[k])};
+}
+// rem[r] = base position r not in I
+__global__ void k_rem_from_bm(const u32* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, u8* __restrict__ rem) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nb) return;
+    const u32 q = ipos[r];
+    rem[r] = ((bmI[q >> 5] >> (q & 31)) & 1) ? 0 : 1;
+}
+
+// walks over a list of segment ids (outputs in the table; WRITE: factors at offs)
+template <bool WRITE>
+__global__ void k_walk(walk_ctx W, seg_tab S, const u32* __restrict__ ids, u32 cnt, const u64* __restrict__ offs,
+                       u32* __restrict__ fact) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const u32 g = ids[t];
+    seg_out o;
+    o.flags = 0;
+    o.e = S.sin[g].start;
+    o.nfact = 0;
+    o.nsingle = 0;
+    walk_segment<WRITE>(W, S.sin[g], o, WRITE ? fact + 2 * offs[t] : nullptr);
+    if (o.flags & 2) atomicOr(S.err, 2u);
+    if (o.flags & 4) atomicOr(S.err, 4u);
+    if (!WRITE) {
+        S.sout[g] = o;
+        S.valid[g] = 1;
+        S.succ[g] = NONE;
+    }
+}
+__global__ void k_todo(seg_tab S, u32 nseg, u32* __restrict__ ids, u32* __restrict__ cnt) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg || S.valid[g]) return;
+    ids[atomicAdd(cnt, 1u)] = (u32)g;
+}
+// claim the segment starting at x (created by this thread iff *mine)
+__device__ u32 seg_claim(const seg_tab& S, u32 x, bool& mine) {
+    mine = false;
+    const u32 old = atomicCAS(&S.seg_at[x], NONE, PENDING);
+    if (old != NONE) return old;
+    const u32 id = atomicAdd(S.nseg, 1u);
+    if (id >= S.cap) {
+        atomicOr(S.err, 1u);
+        atomicExch(&S.seg_at[x], NONE);
+        return NONE;
+    }
+    mine = true;
+    return id;
+}
+// link every valid segment to the segment starting at its next state; unknown
+// next states become alias segments (the real chain enters a valid chunk walk
+// at one of its recorded factor starts) or fresh segments to walk
+__global__ void k_link(seg_tab S, u32 nseg) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg || !S.valid[g] || S.succ[g] != NONE) return;
+    const seg_out& o = S.sout[g];
+    if ((o.flags & 1) || o.next >= S.N) return;
+    const u32 x = o.next;
+    const u32 s = S.seg_at[x];
+    if (s == PENDING) return;
+    if (s != NONE) { S.succ[g] = s; return; }
+    // alias into the chunk walk that covers x?
+    u32 src = NONE, k_at = 0;
+    {
+        u32 lo = 0, hi = S.ncb;  // last boundary <= x
+        while (lo < hi) {
+            const u32 mid = (lo + hi) >> 1;
+            if (S.cbv[mid] <= x) lo = mid + 1; else hi = mid;
+        }
+        if (lo > 0 && S.cbv[lo - 1] < x) {
+            const u32 gc = S.seg_at[S.cbv[lo - 1]];
+            if (gc < S.cap) {
+                if (!S.valid[gc]) return;  // the chunk walk is stale: walked next round, link again
+                const seg_out& oc = S.sout[gc];
+                for (u32 k = 1; k < oc.nbnd; k++)
+                    if (oc.bnd[k] == x) { src = gc; k_at = k; break; }
+            }
+        }
+    }
+    bool mine;
+    const u32 id = seg_claim(S, x, mine);
+    if (!mine) return;  // another thread creates it; resolved by the next link pass
+    S.sin[id] = make_seg_in(S, x);
+    S.succ[id] = NONE;
+    if (src != NONE) {
+        seg_out oa = S.sout[src];
+        oa.nfact -= k_at;
+        oa.nbnd = 0;
+        S.sout[id] = oa;
+        S.valid[id] = 1;
+    } else {
+        S.valid[id] = 0;
+    }
+    __threadfence();
+    atomicExch(&S.seg_at[x], id);
+    S.succ[g] = id;
+}
+// pointer doubling along succ: J = terminal-or-successor, D = hops
+__global__ void k_jump0(seg_tab S, u32 nseg, u32* __restrict__ J, u32* __restrict__ D) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg) return;
+    bool term = !S.valid[g] || S.succ[g] >= S.cap;
+    if (!term) {
+        const seg_out& o = S.sout[g];
+        term = (o.flags & 1) || o.next >= S.N;
+    }
+    J[g] = term ? (u32)g : S.succ[g];
+    D[g] = term ? 0 : 1;
+}
+__global__ void k_jumpk(const u32* __restrict__ J, const u32* __restrict__ D, u32 nseg, u32* __restrict__ J2,
+                        u32* __restrict__ D2) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg) return;
+    const u32 j = J[g];
+    J2[g] = J[j];
+    D2[g] = D[g] + D[j];
+}
+struct chain_status { u32 term, hops, valid, flags, next, err, nseg, pad; };
+__global__ void k_chain_status(seg_tab S, const u32* __restrict__ J, const u32* __restrict__ D, chain_status* out) {
+    const u32 t = J[0];
+    chain_status c{};
+    c.term = t;
+    c.hops = D[0];
+    c.valid = S.valid[t];
+    c.flags = S.sout[t].flags;
+    c.next = S.sout[t].next;
+    c.err = *S.err;
+    c.nseg = *S.nseg;
+    *out = c;
+}
+// chain[k] = k-th successor of segment 0 (binary lifting over the stored levels)
+struct jump_levels { const u32* J[MAX_LV]; u32 nlv; };
+__global__ void k_chain_expand(jump_levels JL, u32 len, u32* __restrict__ chain) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= len) return;
+    u32 g = 0;
+    for (u32 l = 0; l < JL.nlv; l++)
+        if ((k >> l) & 1) g = JL.J[l][g];
+    chain[k] = g;
+}
+// I' bitmap: what the chain inserted below nt ([start, e) + LPF-start queries)
+__global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, u32 nt, u32* __restrict__ bm) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= cnt) return;
+    const u32 g = chain[k];
+    const seg_out& o = S.sout[g];
+    const u32 a = S.sin[g].start, b = min(o.e, nt);
+    if (a < b) bm_set_range(bm, a, b);
+    for (u32 t = 0; t < o.nsingle && t < 4; t++)
+        if (o.single[t] < nt) atomicOr(&bm[o.single[t] >> 5], 1u << (o.single[t] & 31));
+}
+__global__ void k_set_pairs(const u32* __restrict__ pairs, u32 np, u32* __restrict__ bm) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < np) bm_set_range(bm, pairs[2 * k], pairs[2 * k + 1]);
+}
+__global__ void k_chain_nfact(seg_tab S, const u32* __restrict__ chain, u32 cnt, u64* __restrict__ nf) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < cnt) nf[k] = S.sout[chain[k]].nfact;
+}
+// a walked segment is stale iff a dirty position lies in its covered range
+__global__ void k_stale(seg_tab S, u32 nseg, const u32* __restrict__ dirty, u64 nd) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg || !S.valid[g]) return;
+    const seg_out& o = S.sout[g];
+    const u32 a = S.sin[g].start, b = (o.flags & 1) ? S.N : max(o.next, o.e + 1);
+    u64 l = 0, h = nd;
+    while (l < h) {
+        const u64 mid = (l + h) >> 1;
+        if (dirty[mid] < a) l = mid + 1; else h = mid;
+    }
+    if (l < nd && dirty[l] <= b) {
+        S.valid[g] = 0;
+        S.succ[g] = NONE;
+    }
+}
+// segments whose cached successor became invalid keep the id (the table entry is re-walked in place)
+__global__ void k_invalidate_all(seg_tab S, u32 nseg) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg) return;
+    S.valid[g] = 0;
+    S.succ[g] = NONE;
 }
 
 static double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+__global__ void k_put3(u32* p, u32 a, u32 b, u32 c) {
+    p[0] = a;
+    p[1] = b;
+    p[2] = c;
+}
+__global__ void k_sum_u8(const u8* __restrict__ f, u64 m, u32* __restrict__ acc) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m && !f[k]) atomicAdd(acc, 1u);
+}
+// exclusive scan of cnt[0..m) into off[0..m] (off[m] = total); cnt needs m+1 entries
+template <class T>
+static T excl_scan(T* cnt, T* off, u64 m, dbuf<u8>& tmp, hipStream_t st) {
+    LZ_HIP(hipMemsetAsync(cnt + m, 0, sizeof(T), st));
+    size_t tb = 0;
+    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)(m + 1), st));
+    u8* t = tmp.get(tb);
+    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, cnt, off, (int)(m + 1), st));
+    return rd1(off + m, st);
 }
 
 u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
@@ -668,21 +965,15 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     const u32 N = (u32)n;
     const u32 m = num_phr;  // phrases; P[m] = sentinel
     u32* P = lpf.get((u64)(m + 1) * 3);
-    {
-        const u32 sent[3] = {N, N + 1, 0};
-        LZ_HIP(hipMemcpyAsync(P + 3 * (u64)m, sent, 12, hipMemcpyHostToDevice, st));
-    }
+    k_put3<<<1, 1, 0, st>>>(P + 3 * (u64)m, N, N + 1, 0);
     // ---- phrase statistics -> parameters (lz77_sss.hpp:420-461)
     u32 num_lpf = m, len_lpf_phr = 0, num_gaps = 1;
     if (m > 0) {
         u32* acc = counters.get(16);
         LZ_HIP(hipMemsetAsync(acc, 0, 8, st));
         k_phrase_info<<<cdiv(m, 256), 256, 0, st>>>(P, m, N, acc);
-        u32 h[2];
-        LZ_HIP(hipMemcpyAsync(h, acc, 8, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
-        len_lpf_phr = h[0];
-        num_gaps = h[1];
+        len_lpf_phr = rd1(acc, st);
+        num_gaps = rd1(acc + 1, st);
     }
     gap_params_h gp = choose_gap_params(N, num_lpf, len_lpf_phr, num_gaps);
     if (log2_override > 0) gp.log2_size_h = (u32)log2_override;
@@ -701,6 +992,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     }
     u128* d_negpow = (u128*)tmp_greedy.get(5 * 256 * sizeof(u128));
     LZ_HIP(hipMemcpyAsync(d_negpow, negpow.data(), 5 * 256 * sizeof(u128), hipMemcpyHostToDevice, st));
+    LZ_HIP(hipStreamSynchronize(st));
 
     stats.assign(24, 0);
     stats[0] = s; stats[1] = has_runs; stats[2] = num_lpf; stats[3] = len_lpf_phr; stats[4] = num_gaps;
@@ -714,183 +1006,124 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     G.thr = gp.roll_threshold;
     G.mask = (u32)((1ull << gp.log2_size_h) - 1);
     G.negpow = d_negpow;
-
-    std::vector<u32> hP((u64)(m + 1) * 3);
-    LZ_HIP(hipMemcpyAsync(hP.data(), P, hP.size() * 4, hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipStreamSynchronize(st));
-    auto first_phrase_after = [&](u32 i) -> u32 {  // smallest k with P[k].end > i
-        u32 lo = 0, hi = m;
-        while (lo < hi) {
-            const u32 mid = (lo + hi) >> 1;
-            if (hP[3 * mid + 1] <= i) lo = mid + 1; else hi = mid;
-        }
-        return lo;
-    };
     u32 zmask0 = 0;
     for (int x = 0; x < 5; x++) zmask0 |= (G.lens[x] >= N) ? (1u << x) : 0u;  // reinit(0) at construction
+    const u64 nw = (u64)N / 32 + 2;  // bitmap words (a zero word past the end)
+    const unsigned gw = cdiv(nw, 256);
 
-    // ---- segments (flat arrays; ids in creation order)
-    // Long gaps are cut into chunks of GAP_CHUNK positions: a segment's gap walk
-    // stops at the first factor start at or after the next chunk boundary.  Every
-    // gap position is inserted whatever the factor boundaries are, so a chunk
-    // walk started at its boundary is exact from the first factor start it
-    // shares with the real chain (the chain enters through an alias segment).
-    const u32 GAP_CHUNK = std::getenv("LZ77SSS_NO_CHUNK") ? 0xFFFFFFF : 512;
-    std::vector<u32> cbv;  // chunk boundaries (sorted)
-    std::vector<seg_in> hsegs;
-    std::vector<seg_out> houts;
-    std::vector<u8> valid;       // output exact for the current lookup state
-    std::vector<u32> seg_next;   // cached id of the segment starting at houts.next (NONE = unknown)
-    std::unordered_map<u32, u32> seg_at;  // start -> id
-    auto add_segment = [&](u32 a) {
-        auto it = std::upper_bound(cbv.begin(), cbv.end(), a);
-        const u32 lim = it == cbv.end() ? N : *it;
-        seg_at[a] = (u32)hsegs.size();
-        hsegs.push_back({a, first_phrase_after(a), a, zmask0, lim});
-        houts.push_back(seg_out{});
-        valid.push_back(0);
-        seg_next.push_back(NONE);
+    // ---- default segments: gaps + chunk boundaries of long gaps
+    const u32 CH = std::getenv("LZ77SSS_NO_CHUNK") ? 0x0FFFFFFFu : 512u;
+    u32* cnt_seg = g_tmp1.get(m + 2);
+    u32* cnt_cb = g_tmp2.get(m + 2);
+    u32* off_seg = g_tmp3.get(m + 2);
+    u32* off_cb = g_tmp4.get(m + 2);
+    k_gap_counts<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, cnt_seg, cnt_cb);
+    const u32 nseg0 = excl_scan(cnt_seg, off_seg, m + 1, scan_tmp, st);
+    const u32 ncb = excl_scan(cnt_cb, off_cb, m + 1, scan_tmp, st);
+    u32* cbv = g_cbv.get(ncb + 1);
+    k_gap_cbv<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, off_cb, cbv);
+    u32 cap = nseg0 + nseg0 / 2 + (1u << 16);
+    seg_tab S{};
+    auto bind_tab = [&]() {
+        S.sin = g_sin.p; S.sout = g_sout.p; S.valid = g_valid.p; S.succ = g_succ.p; S.cap = cap;
     };
-    auto find_seg = [&](u32 a) -> u32 {
-        auto it = seg_at.find(a);
-        return it == seg_at.end() ? NONE : it->second;
-    };
-    u64 n_alias = 0;
-    // segment starting at x: existing, or an alias entering a valid chunk walk at one
-    // of its recorded factor starts; NONE otherwise (*blocked: the chunk walk is stale)
-    auto resolve = [&](u32 x, bool* blocked) -> u32 {
-        u32 g = find_seg(x);
-        if (g != NONE) return g;
-        auto it = std::upper_bound(cbv.begin(), cbv.end(), x);
-        if (it == cbv.begin()) return NONE;
-        const u32 c = *(it - 1);
-        const u32 gc = find_seg(c);
-        if (gc == NONE) return NONE;
-        if (!valid[gc]) {
-            if (blocked) *blocked = true;
-            return NONE;
-        }
-        const seg_out& oc = houts[gc];
-        for (u32 k = 1; k < oc.nbnd; k++) {
-            if (oc.bnd[k] != x) continue;
-            seg_out oa = oc;
-            oa.nfact -= k;
-            oa.nbnd = 0;
-            add_segment(x);
-            g = (u32)hsegs.size() - 1;
-            houts[g] = oa;
-            valid[g] = 1;
-            n_alias++;
-            return g;
-        }
-        return NONE;
-    };
-    // default segments and I_0 (every gap + the LPF-start query that follows it)
-    ivec I;
-    {
-        u32 prev_end = 0;
-        std::vector<u32> starts;
-        for (u32 k = 0; k <= m; k++) {
-            const u32 b = hP[3 * k], e = hP[3 * k + 1];
-            if (prev_end < b) {
-                starts.push_back(prev_end);
-                if (b - prev_end > 2 * (u64)GAP_CHUNK)
-                    for (u32 c = prev_end + GAP_CHUNK; c + GAP_CHUNK / 2 < b; c += GAP_CHUNK) cbv.push_back(c);
-                I.push_back({prev_end, std::min(b + 1, N)});
-            }
-            prev_end = std::max(prev_end, e);
-        }
-        if (starts.empty() || starts[0] != 0) starts.insert(starts.begin(), 0);  // phrases begin at >= 1
-        for (u32 a : starts) add_segment(a);
-        for (u32 c : cbv) add_segment(c);
-    }
-    clip(I, G.nt);
-    // base superset: the speculated gaps plus the interiors of short phrases,
-    // where walk overruns insert (greedy.cpp:69-78); those start "removed"
-    ivec Isup = I;
-    for (u32 k = 0; k < m; k++) {
-        const u32 b = hP[3 * k], e = hP[3 * k + 1];
-        if (e - b <= 48) Isup.push_back({b, e});
-    }
-    clip(Isup, G.nt);
+    g_sin.get(cap); g_sout.get(cap); g_valid.get(cap); g_succ.get(cap);
+    bind_tab();
+    S.seg_at = g_seg_at.get((u64)N + 1);
+    LZ_HIP(hipMemsetAsync(S.seg_at, 0xFF, ((u64)N + 1) * 4, st));
+    S.nseg = (u32*)counters64.get(4);
+    S.err = S.nseg + 1;
+    LZ_HIP(hipMemsetAsync(S.nseg, 0, 8, st));
+    LZ_HIP(hipMemcpyAsync(S.nseg, &nseg0, 4, hipMemcpyHostToDevice, st));
+    S.cbv = cbv; S.ncb = ncb; S.P = P; S.m = m; S.N = N; S.zmask0 = zmask0;
+    k_gap_segs<<<cdiv(m + 1, 256), 256, 0, st>>>(S, CH, off_seg);
+    // bitmaps: I (current speculation), I' (what the chain inserted), Ib (base set), scratch
+    u32* bmI = g_bmI.get(nw);
+    u32* bmI2 = g_bmI2.get(nw);
+    u32* bmIb = g_bmIb.get(nw);
+    u32* bmT = g_bmT.get(nw);
+    LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
+    LZ_HIP(hipMemsetAsync(bmT, 0, nw * 4, st));
+    k_gap_bitmaps<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, bmI, bmT);
+    LZ_HIP(hipStreamSynchronize(st));
     lap("greedy setup");
 
-    // ---- base build
-    ivec Ib;
-    std::vector<u32> h_is, h_ie, h_ir;
-    u64 nb = 0, ne = 0;
+    // ---- base set (entries sorted by slot) and delta
     walk_ctx W{};
     W.T = T;
     W.G = G;
     W.P = P;
     W.L = view(T);
-    auto build_base = [&](const ivec& Inew) {
-        Ib = Inew;
-        h_is.clear(); h_ie.clear(); h_ir.clear();
-        std::vector<ichunk> chunks;
-        nb = 0;
-        for (auto& iv : Ib) {
-            h_is.push_back(iv.a); h_ie.push_back(iv.b); h_ir.push_back((u32)nb);
-            for (u32 q = iv.a; q < iv.b; q += 1024)
-                chunks.push_back({q, std::min<u32>(iv.b, q + 1024), (u32)(nb + (q - iv.a))});
-            nb += iv.b - iv.a;
+    u64 nb = 0;
+    u32* ns = g_tmp1.get(nw + 1);
+    u32* ne = g_tmp2.get(nw + 1);
+    u32* os = g_tmp3.get(nw + 1);
+    u32* oe = g_tmp4.get(nw + 1);
+    // runs of a bitmap -> intervals (st, en), ranks, <= 1024-position chunks
+    auto runs_to_chunks = [&](const u32* bm, dbuf<u32>& dst, dbuf<u32>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
+                              u64& npos, u32& nch) -> ichunk* {
+        k_bm_count<<<gw, 256, 0, st>>>(bm, nw, ns, ne);
+        ni = excl_scan(ns, os, nw, scan_tmp, st);
+        excl_scan(ne, oe, nw, scan_tmp, st);
+        u32* a = dst.get(ni + 1);
+        u32* b = den.get(ni + 1);
+        k_bm_write_runs<<<gw, 256, 0, st>>>(bm, nw, os, oe, a, b);
+        u32* len = g_tmp5.get(ni + 1);
+        u32* nc = g_tmp6.get(ni + 1);
+        u32* rk = drk.get(ni + 1);
+        u32* choff = g_tmp7.get(ni + 1);
+        npos = 0;
+        nch = 0;
+        if (ni) {
+            k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(a, b, ni, nc, len);
+            npos = excl_scan(len, rk, ni, scan_tmp, st);
+            nch = excl_scan(nc, choff, ni, scan_tmp, st);
         }
+        ichunk* ch = (ichunk*)dch.get(std::max<u64>(1, nch) * sizeof(ichunk));
+        if (ni) k_iv_chunks<<<cdiv(ni, 256), 256, 0, st>>>(a, b, ni, choff, rk, ch);
+        return ch;
+    };
+    auto build_base = [&](const u32* bm) {
+        if (bm != bmIb) LZ_HIP(hipMemcpyAsync(bmIb, bm, nw * 4, hipMemcpyDeviceToDevice, st));
+        u32 ni, nch;
+        ichunk* ch = runs_to_chunks(bmIb, ist, iend, irank, chunk_buf, ni, nb, nch);
         if (5 * nb >= (1ull << 32)) throw error(-1, "gap region too large for 32-bit entry ids");
-        ne = 5 * nb;
-        u32* d_is = ist.get(h_is.size() + 1);
-        u32* d_ie = iend.get(h_ie.size() + 1);
-        u32* d_ir = irank.get(h_ir.size() + 1);
-        if (!h_is.empty()) {
-            LZ_HIP(hipMemcpyAsync(d_is, h_is.data(), h_is.size() * 4, hipMemcpyHostToDevice, st));
-            LZ_HIP(hipMemcpyAsync(d_ie, h_ie.data(), h_ie.size() * 4, hipMemcpyHostToDevice, st));
-            LZ_HIP(hipMemcpyAsync(d_ir, h_ir.data(), h_ir.size() * 4, hipMemcpyHostToDevice, st));
-        }
-        ichunk* d_ch = (ichunk*)chunk_buf.get(std::max<size_t>(1, chunks.size()) * sizeof(ichunk));
-        if (!chunks.empty())
-            LZ_HIP(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(ichunk), hipMemcpyHostToDevice, st));
-        u32* keys = ekeys.get(ne + 1);
-        u32* vals = evals.get(ne + 1);
-        u32* skeys = ekeys2.get(ne + 1);
-        u32* svals = evals2.get(ne + 1);
+        const u64 ne5 = 5 * nb;
+        u32* keys = ekeys.get(ne5 + 1);
+        u32* vals = evals.get(ne5 + 1);
+        u32* skeys = ekeys2.get(ne5 + 1);
+        u32* svals = evals2.get(ne5 + 1);
         u32* ipos = ipos_buf.get(nb + 1);
-        u32* pred5 = occ_buf.get(ne + 1);
+        u32* pred5 = occ_buf.get(ne5 + 1);
         u8* rem = rem_buf.get(nb + 1);
         LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
-        if (!chunks.empty()) {
-            k_slots<<<cdiv(chunks.size(), 64), 64, 0, st>>>(T, G, d_ch, (u32)chunks.size(), keys, vals, ipos);
+        if (nch) {
+            k_slots<<<cdiv(nch, 64), 64, 0, st>>>(T, G, ch, nch, keys, vals, ipos);
             size_t tb = 0;
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, skeys, vals, svals, (int)ne, 0,
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, skeys, vals, svals, (int)ne5, 0,
                                                       (int)gp.log2_size_h, st));
             u8* t = scan_tmp.get(tb);
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, skeys, vals, svals, (int)ne, 0,
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, skeys, vals, svals, (int)ne5, 0,
                                                       (int)gp.log2_size_h, st));
-            k_pred<<<cdiv(ne, 256), 256, 0, st>>>(skeys, svals, ne, pred5);
+            k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
         }
-        W.istart = d_is; W.iend = d_ie; W.irank = d_ir; W.nint = (u32)h_is.size();
-        W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne;
+        W.istart = ist.p; W.iend = iend.p; W.irank = irank.p; W.nint = ni;
+        W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne5;
         W.rem = rem; W.akeys = nullptr; W.nadd = 0;
         lap("base build (slots+sort+pred)");
     };
-    std::vector<u32> A_pos;  // sorted positions of I outside the base set
-    // rebuild the added-entry list from A_pos
+    // added entries: positions of I outside the base set
     auto rebuild_added = [&]() {
+        k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmT);
+        u32 ni, nch;
+        u64 na;
+        ichunk* ch = runs_to_chunks(bmT, g_ast, g_aen, g_ark, chunk_buf2, ni, na, nch);
         W.nadd = 0;
         W.akeys = nullptr;
-        if (A_pos.empty()) return;
-        std::vector<ichunk> chunks;
-        u64 na = 0;
-        for (size_t k = 0; k < A_pos.size();) {
-            size_t j = k + 1;
-            while (j < A_pos.size() && A_pos[j] == A_pos[j - 1] + 1 && j - k < 1024) j++;
-            chunks.push_back({A_pos[k], A_pos[j - 1] + 1, (u32)na});
-            na += j - k;
-            k = j;
-        }
-        ichunk* d_ch = (ichunk*)chunk_buf2.get(chunks.size() * sizeof(ichunk));
-        LZ_HIP(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(ichunk), hipMemcpyHostToDevice, st));
+        if (!na) return;
         u32* akey32 = add_keys32.get(5 * na);
         u32* apos = add_pos.get(na);
-        k_slots<<<cdiv(chunks.size(), 64), 64, 0, st>>>(T, G, d_ch, (u32)chunks.size(), akey32, nullptr, apos);
+        k_slots<<<cdiv(nch, 64), 64, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
         u64* ak = add_keys.get(5 * na);
         u64* ak2 = add_keys2.get(5 * na);
         k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
@@ -901,232 +1134,172 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         W.akeys = ak2;
         W.nadd = 5 * na;
     };
-    // full state for I (I must be a subset of the base set here)
-    auto set_state = [&](const ivec& Iset) {
-        std::vector<u32> ia(Iset.size()), ib(Iset.size());
-        for (size_t k = 0; k < Iset.size(); k++) { ia[k] = Iset[k].a; ib[k] = Iset[k].b; }
-        u32* d_a = dirty_in.get(ia.size() + 1);
-        u32* d_b = dirty_out.get(ib.size() + 1);
-        if (!ia.empty()) {
-            LZ_HIP(hipMemcpyAsync(d_a, ia.data(), ia.size() * 4, hipMemcpyHostToDevice, st));
-            LZ_HIP(hipMemcpyAsync(d_b, ib.data(), ib.size() * 4, hipMemcpyHostToDevice, st));
-        }
-        if (nb) k_rem_from_set<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, d_a, d_b, (u32)ia.size(), (u8*)W.rem);
-        A_pos.clear();
+    auto set_state = [&]() {  // rem + added for the current I
+        if (nb) k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, (u8*)W.rem);
         rebuild_added();
-        LZ_HIP(hipStreamSynchronize(st));
     };
+    build_base(bmT);  // superset: gaps + short phrase interiors
+    set_state();
 
-    build_base(Isup);
-    set_state(I);
-    std::vector<seg_in> tin;
-    std::vector<seg_out> tout;
-    auto walk_ids = [&](const std::vector<u32>& ids) {
-        if (ids.empty()) return;
-        tin.resize(ids.size());
-        for (size_t t = 0; t < ids.size(); t++) tin[t] = hsegs[ids[t]];
-        seg_in* ds = seg_in_buf.get(ids.size());
-        seg_out* dout = seg_out_buf.get(ids.size());
-        LZ_HIP(hipMemcpyAsync(ds, tin.data(), tin.size() * sizeof(seg_in), hipMemcpyHostToDevice, st));
-        k_walk<false><<<cdiv(ids.size(), 64), 64, 0, st>>>(W, ds, (u32)ids.size(), dout, nullptr, nullptr);
-        LZ_HIP(hipGetLastError());
-        tout.resize(ids.size());
-        LZ_HIP(hipMemcpyAsync(tout.data(), dout, tout.size() * sizeof(seg_out), hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
-        for (size_t t = 0; t < ids.size(); t++) {
-            const u32 g = ids[t];
-            houts[g] = tout[t];
-            valid[g] = 1;
-            seg_next[g] = NONE;
-            if (houts[g].flags & 2) throw error(-6, "greedy: too many LPF-start queries in one segment");
-            if (houts[g].flags & 4) throw error(-6, "greedy: walk guard tripped (internal error)");
-        }
-    };
-
-    std::vector<u32> chain;
-    bool tail_reached = false;
-    std::vector<u32> todo;
-    for (u32 g = 0; g < hsegs.size(); g++) todo.push_back(g);
-    u64 total_fact = 0;
+    // ---- walk + link until the chain from position 0 is complete, then check I
+    u32 nseg = nseg0;
+    u32* ids = g_ids.get(cap);
+    u32* d_cnt = counters.get(16);
+    chain_status cs{};
+    chain_status* d_cs = (chain_status*)g_cs.get(sizeof(chain_status));
+    jump_levels JL{};
+    u64 total_fact = 0, walked_total = 0;
     int outer = 0, rounds_total = 0;
-    u64 walked_total = 0;
     for (;; outer++) {
         if (outer > 500) throw error(-6, "greedy speculation did not converge");
-        // ---- walk + link until the chain from position 0 is complete and exact
         for (int round = 0;; round++) {
             rounds_total++;
             if (round > 100000) throw error(-6, "greedy segment linking did not converge");
-            walk_ids(todo);
-            walked_total += todo.size();
+            LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
+            k_todo<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, ids, d_cnt);
+            const u32 ntodo = rd1(d_cnt, st);
+            if (ntodo) {
+                k_walk<false><<<cdiv(ntodo, 64), 64, 0, st>>>(W, S, ids, ntodo, nullptr, nullptr);
+                LZ_HIP(hipGetLastError());
+                walked_total += ntodo;
+            }
             lap("walk");
-            todo.clear();
-            chain.clear();
-            tail_reached = false;
-            u32 g = find_seg(0);
-            u32 idxp = 0, zm = zmask0;
-            bool complete = true;
-            for (;;) {
-                if (chain.size() > hsegs.size()) throw error(-6, "greedy: segment chain has a cycle");
-                if (!valid[g]) { todo.push_back(g); complete = false; break; }
-                chain.push_back(g);
-                hsegs[g].idxpos = idxp;  // exact inputs of chain segments (used by the tail walk)
-                hsegs[g].zmask = zm;
-                const seg_out& o = houts[g];
-                if (o.flags & 1) { tail_reached = true; break; }
-                if (o.next >= N) break;
-                idxp = o.idxpos;
-                zm = o.zmask;
-                u32 nx = seg_next[g];
-                if (nx == NONE) {
-                    bool blocked = false;
-                    nx = resolve(o.next, &blocked);
-                    seg_next[g] = nx;
-                    if (blocked) todo.push_back(g);  // a stale chunk walk: re-walk the invalid ones
-                }
-                if (nx == NONE) { complete = false; break; }
-                g = nx;
+            for (;;) {  // link; grow the table when full
+                k_link<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
+                u32 h2[2];
+                LZ_HIP(hipMemcpyAsync(h2, S.nseg, 8, hipMemcpyDeviceToHost, st));
+                LZ_HIP(hipStreamSynchronize(st));
+                if (!(h2[1] & 1)) { nseg = h2[0]; break; }
+                const u32 ncap = cap * 2;
+                g_sin.grow_keep(ncap, cap, st); g_sout.grow_keep(ncap, cap, st);
+                g_valid.grow_keep(ncap, cap, st); g_succ.grow_keep(ncap, cap, st);
+                g_ids.get(ncap);
+                ids = g_ids.p;
+                cap = ncap;
+                bind_tab();
+                const u32 fix[2] = {cap < h2[0] ? cap : h2[0], h2[1] & ~1u};
+                LZ_HIP(hipMemcpyAsync(S.nseg, fix, 8, hipMemcpyHostToDevice, st));
+                LZ_HIP(hipStreamSynchronize(st));
             }
+            // pointer doubling along succ from every segment
+            u32* D0 = g_dist[0].get(nseg);
+            u32* D1 = g_dist[1].get(nseg);
+            k_jump0<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, jump[0].get(nseg), D0);
+            u32 nlv = 1;
+            while ((1ull << (nlv - 1)) < nseg) {
+                if (nlv >= (u32)MAX_LV) throw error(-6, "greedy: too many jump levels");
+                k_jumpk<<<cdiv(nseg, 256), 256, 0, st>>>(jump[nlv - 1].p, D0, nseg, jump[nlv].get(nseg), D1);
+                std::swap(D0, D1);
+                nlv++;
+            }
+            JL.nlv = nlv;
+            for (u32 l = 0; l < nlv; l++) JL.J[l] = jump[l].p;
+            k_chain_status<<<1, 1, 0, st>>>(S, jump[nlv - 1].p, D0, d_cs);
+            LZ_HIP(hipMemcpyAsync(&cs, d_cs, sizeof(cs), hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));
             lap("link");
+            if (cs.err & 2) throw error(-6, "greedy: too many LPF-start queries in one segment");
+            if (cs.err & 4) throw error(-6, "greedy: walk guard tripped (internal error)");
             if (dbg)
-                std::fprintf(stderr,
-                             "[lz77sss-debug] greedy outer=%d round=%d segs=%zu chain=%zu complete=%d tail=%d |I|=%llu "
-                             "adds=%llu rems=%zu\n",
-                             outer, round, hsegs.size(), chain.size(), (int)complete, (int)tail_reached,
-                             (unsigned long long)total_len(I), (unsigned long long)(W.nadd / 5), A_pos.size());
-            if (complete) break;
-            if (!todo.empty()) {
-                // batch: re-walk every stale segment, not only the one the link stopped at
-                todo.clear();
-                for (u32 h = 0; h < hsegs.size(); h++)
-                    if (!valid[h]) todo.push_back(h);
-                continue;
-            }
-            // speculatively create every unknown next state of current segments
-            std::vector<u32> fresh;
-            for (u32 h = 0; h < houts.size(); h++) {
-                if (!valid[h]) continue;
-                const seg_out& o = houts[h];
-                if ((o.flags & 1) || o.next >= N || seg_next[h] != NONE) continue;
-                bool blocked = false;
-                if (resolve(o.next, &blocked) != NONE || blocked) continue;
-                fresh.push_back(o.next);
-            }
-            std::sort(fresh.begin(), fresh.end());
-            fresh.erase(std::unique(fresh.begin(), fresh.end()), fresh.end());
-            if (fresh.empty()) throw error(-6, "greedy: chain broken without new states");
-            for (u32 a : fresh) {
-                todo.push_back((u32)hsegs.size());
-                add_segment(a);
-            }
+                std::fprintf(stderr, "[lz77sss-debug] greedy outer=%d round=%d segs=%u walked=%u chain=%u valid=%u flags=%u\n",
+                             outer, round, nseg, ntodo, cs.hops + 1, cs.valid, cs.flags);
+            if (cs.valid && ((cs.flags & 1) || cs.next >= N)) break;
         }
-        // ---- tail: exact single-thread walk from the chain segment that enters the tail region
-        u64 tail_count = 0;
-        ivec tail_ins;
+        // ---- the chain, its factor offsets, the tail
+        const bool tail = cs.flags & 1;
+        const u32 nall = cs.hops + 1, nchain = nall - (tail ? 1u : 0u);
+        u32* chain = g_chain.get(nall + 1);
+        k_chain_expand<<<cdiv(nall, 256), 256, 0, st>>>(JL, nall, chain);
+        u64* nf = seg_offs.get(nall + 2);
+        u64* offs = g_offs.get(nall + 2);
         u64 chain_fact = 0;
-        const size_t nchain = chain.size() - (tail_reached ? 1 : 0);
-        for (size_t c = 0; c < nchain; c++) chain_fact += houts[chain[c]].nfact;
-        const u64 tail_bound = tail_reached ? (u64)N - hsegs[chain.back()].start + 1 : 0;
-        u32* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
-        if (tail_reached) {
-            u64* d_cnt = counters64.get(4);
+        if (nchain) {
+            k_chain_nfact<<<cdiv(nchain, 256), 256, 0, st>>>(S, chain, nchain, nf);
+            chain_fact = excl_scan(nf, offs, nchain, scan_tmp, st);
+        }
+        u64 tail_count = 0, tail_bound = 0;
+        u32 tail_pairs[16];
+        u64 hc[3] = {0, 0, 0};
+        if (tail) {
+            seg_in tin;
+            LZ_HIP(hipMemcpyAsync(&tin, g_sin.p + cs.term, sizeof(seg_in), hipMemcpyDeviceToHost, st));
+            seg_out prev{};
+            if (nall >= 2) {
+                u32 pg;
+                LZ_HIP(hipMemcpyAsync(&pg, chain + nall - 2, 4, hipMemcpyDeviceToHost, st));
+                LZ_HIP(hipStreamSynchronize(st));
+                LZ_HIP(hipMemcpyAsync(&prev, g_sout.p + pg, sizeof(seg_out), hipMemcpyDeviceToHost, st));
+            }
+            LZ_HIP(hipStreamSynchronize(st));
+            tin.idxpos = nall >= 2 ? prev.idxpos : 0;  // exact chain state entering the tail walk
+            tin.zmask = nall >= 2 ? prev.zmask : zmask0;
+            tail_bound = (u64)N - tin.start + 1;
+            u32* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
+            u64* d_tc = (u64*)g_tailc.get(4 * sizeof(u64));
             u32* d_tins = tail_ins_buf.get(16);
-            k_tail<<<1, 64, 0, st>>>(W, hsegs[chain.back()], fo, chain_fact, d_cnt, d_tins);
+            k_tail<<<1, 64, 0, st>>>(W, tin, fo, chain_fact, d_tc, d_tins);
             LZ_HIP(hipGetLastError());
-            u64 hc[3];
-            u32 hti[16];
-            LZ_HIP(hipMemcpyAsync(hc, d_cnt, 24, hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipMemcpyAsync(hti, d_tins, 64, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipMemcpyAsync(hc, d_tc, 24, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipMemcpyAsync(tail_pairs, d_tins, 64, hipMemcpyDeviceToHost, st));
             LZ_HIP(hipStreamSynchronize(st));
             if (hc[2]) throw error(-6, "greedy tail: insert overflow or guard tripped");
             tail_count = hc[0];
-            for (u64 k = 0; k < hc[1]; k++) tail_ins.push_back({hti[2 * k], hti[2 * k + 1]});
             lap("tail");
+        } else {
+            fact.get(2 * chain_fact + 2);
         }
-        // ---- the insert set the chain actually produced
-        ivec I2 = tail_ins;
-        I2.reserve(tail_ins.size() + 2 * nchain);
-        for (size_t c = 0; c < nchain; c++) {
-            const seg_in& si = hsegs[chain[c]];
-            const seg_out& o = houts[chain[c]];
-            I2.push_back({si.start, o.e});
-            for (u32 k = 0; k < o.nsingle && k < 4; k++) I2.push_back({o.single[k], o.single[k] + 1});
+        // ---- the insert set the chain actually produced vs the speculation
+        LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
+        if (nchain) k_chain_inserts<<<cdiv(nchain, 256), 256, 0, st>>>(S, chain, nchain, G.nt, bmI2);
+        if (tail && hc[1]) {
+            u32* d_tins = tail_ins_buf.p;
+            k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], bmI2);
         }
-        clip(I2, G.nt);
-        bool same = I2.size() == I.size();
-        for (size_t k = 0; same && k < I.size(); k++) same = I2[k].a == I[k].a && I2[k].b == I[k].b;
+        k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
+        k_bm_count1<<<gw, 256, 0, st>>>(bmT, nw, ns);
+        const u64 ny = excl_scan(ns, os, nw, scan_tmp, st);
         lap("insert set");
-        if (same) {
-            // ---- every lookup of the chain was exact: emit the factors
+        if (ny == 0) {
+            // every lookup of the chain was exact: emit the factors
             if (nchain) {
-                std::vector<u64> offs(nchain);
-                std::vector<seg_in> cin(nchain);
-                u64 o = 0;
-                for (size_t c = 0; c < nchain; c++) { offs[c] = o; o += houts[chain[c]].nfact; cin[c] = hsegs[chain[c]]; }
-                u64* doffs = seg_offs.get(nchain);
-                seg_in* ds = seg_in_buf.get(nchain);
-                LZ_HIP(hipMemcpyAsync(ds, cin.data(), nchain * sizeof(seg_in), hipMemcpyHostToDevice, st));
-                LZ_HIP(hipMemcpyAsync(doffs, offs.data(), nchain * 8, hipMemcpyHostToDevice, st));
-                k_walk<true><<<cdiv(nchain, 64), 64, 0, st>>>(W, ds, (u32)nchain, nullptr, doffs, fo);
+                k_walk<true><<<cdiv(nchain, 64), 64, 0, st>>>(W, S, chain, nchain, offs, fact.p);
                 LZ_HIP(hipGetLastError());
                 lap("write");
             }
             total_fact = chain_fact + tail_count;
             break;
         }
-        // ---- I changed: the positions that joined (1) or left (0) it
-        const ivec joined_iv = subtract(I2, I), left_iv = subtract(I, I2);
-        std::vector<u32> ys;
-        std::vector<u8> yj;
-        for (auto& iv : joined_iv)
-            for (u32 q = iv.a; q < iv.b; q++) { ys.push_back(q); yj.push_back(1); }
-        for (auto& iv : left_iv)
-            for (u32 q = iv.a; q < iv.b; q++) { ys.push_back(q); yj.push_back(0); }
-        I.swap(I2);
-        const u64 outside = total_len(subtract(I, Ib));
+        // positions that joined (flag 1) or left (0) I
+        u32* d_y = dirty_in.get(ny + 1);
+        u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
+        k_bm_list<<<gw, 256, 0, st>>>(bmT, bmI2, nw, os, d_y, d_j);
+        // many positions outside the base set: rebuild it as I' u I_b, re-walk everything
+        k_bm_andnot<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
+        k_bm_count1<<<gw, 256, 0, st>>>(bmT, nw, ne);
+        const u64 outside = excl_scan(ne, oe, nw, scan_tmp, st);
         if (outside * 50 > nb) {
-            // many positions outside the base set: rebuild it as I u I_b, re-walk everything
-            ivec Inew = I;
-            Inew.insert(Inew.end(), Ib.begin(), Ib.end());
-            normalize(Inew);
-            build_base(Inew);
-            set_state(I);
-            std::fill(valid.begin(), valid.end(), 0);
-            todo.clear();
-            for (u32 g = 0; g < hsegs.size(); g++) todo.push_back(g);
+            k_bm_or<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
+            std::swap(g_bmI.p, g_bmI2.p);
+            bmI = g_bmI.p;
+            bmI2 = g_bmI2.p;
+            build_base(bmT);
+            set_state();
+            k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
             if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy rebuild: outside=%llu\n", (unsigned long long)outside);
             continue;
         }
         // dirty = changed positions + their same-slot successors before and after the update
-        const u64 ny = ys.size();
-        u32* d_y = dirty_in.get(ny + 1);
-        u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
         u32* d_d = dirty_out.get(11 * ny + 1);
-        LZ_HIP(hipMemcpyAsync(d_y, ys.data(), ny * 4, hipMemcpyHostToDevice, st));
-        LZ_HIP(hipMemcpyAsync(d_j, yj.data(), ny, hipMemcpyHostToDevice, st));
         LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * 4, hipMemcpyDeviceToDevice, st));
         k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + ny);
         k_flip<<<cdiv(ny, 256), 256, 0, st>>>(W, d_y, d_j, ny, (u8*)W.rem, d_j + ny);
-        std::vector<u8> inb(ny);
-        LZ_HIP(hipMemcpyAsync(inb.data(), d_j + ny, ny, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
-        bool a_changed = false;
-        {
-            std::vector<u32> add, del;
-            for (u64 k = 0; k < ny; k++)
-                if (!inb[k]) (yj[k] ? add : del).push_back(ys[k]);
-            if (!add.empty() || !del.empty()) {
-                a_changed = true;
-                std::sort(add.begin(), add.end());
-                std::sort(del.begin(), del.end());
-                std::vector<u32> tmp;
-                std::set_difference(A_pos.begin(), A_pos.end(), del.begin(), del.end(), std::back_inserter(tmp));
-                A_pos.clear();
-                std::merge(tmp.begin(), tmp.end(), add.begin(), add.end(), std::back_inserter(A_pos));
-            }
-        }
-        if (a_changed) rebuild_added();
+        std::swap(g_bmI.p, g_bmI2.p);
+        bmI = g_bmI.p;
+        bmI2 = g_bmI2.p;
+        LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
+        k_sum_u8<<<cdiv(ny, 256), 256, 0, st>>>(d_j + ny, ny, d_cnt);
+        if (rd1(d_cnt, st)) rebuild_added();
         k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + 6 * ny);
-        // sort dirty positions (NONE entries sort last and are ignored)
         u32* d_ds = dirty_sorted.get(11 * ny + 1);
         {
             size_t tb = 0;
@@ -1134,38 +1307,17 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             u8* t = scan_tmp.get(tb);
             LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, d_d, d_ds, (int)(11 * ny), 0, 32, st));
         }
-        // staleness of every walked segment
-        const u64 ns = hsegs.size();
-        std::vector<u32> lo(ns), hi(ns);
-        for (u64 g = 0; g < ns; g++) {
-            lo[g] = hsegs[g].start;
-            hi[g] = (houts[g].flags & 1) ? N : std::max(houts[g].next, houts[g].e + 1);
-        }
-        u32* d_lo = seg_lo.get(ns);
-        u32* d_hi = seg_hi.get(ns);
-        u8* d_st = (u8*)tmp_greedy3.get(ns);
-        LZ_HIP(hipMemcpyAsync(d_lo, lo.data(), ns * 4, hipMemcpyHostToDevice, st));
-        LZ_HIP(hipMemcpyAsync(d_hi, hi.data(), ns * 4, hipMemcpyHostToDevice, st));
-        k_stale<<<cdiv(ns, 256), 256, 0, st>>>(d_lo, d_hi, ns, d_ds, 11 * ny, d_st);
-        std::vector<u8> stale(ns);
-        LZ_HIP(hipMemcpyAsync(stale.data(), d_st, ns, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
-        todo.clear();
-        for (u64 g = 0; g < ns; g++) {
-            if (stale[g]) valid[g] = 0;
-            if (!valid[g]) todo.push_back((u32)g);
-        }
+        k_stale<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, d_ds, 11 * ny);
         lap("delta + dirty");
-        if (dbg)
-            std::fprintf(stderr, "[lz77sss-debug] greedy delta: changed=%llu outside=%zu rewalk=%zu\n",
-                         (unsigned long long)ny, A_pos.size(), todo.size());
+        if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy delta: changed=%llu outside=%llu\n",
+                              (unsigned long long)ny, (unsigned long long)outside);
     }
     stats[12] = outer + 1;
     stats[13] = rounds_total;
     stats[14] = stats_fallback_lanes;
     stats[15] = walked_total;
-    stats[16] = n_alias;
-    stats[17] = cbv.size();
+    stats[16] = nseg;
+    stats[17] = nseg0;
     return total_fact;
 }
 

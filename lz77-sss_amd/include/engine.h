@@ -121,6 +121,14 @@ struct engine {
     dbuf<seg_out> seg_out_buf;
     dbuf<u32> seg_ids, ist, iend, irank, ekeys, evals, ekeys2, evals2, ipos_buf, occ_buf, tail_ins_buf;
     dbuf<u64> seg_offs, counters64;
+    // device-resident greedy orchestration (csrc/greedy.hip)
+    dbuf<seg_in> g_sin;
+    dbuf<seg_out> g_sout;
+    dbuf<u8> g_valid, g_cs, g_tailc;
+    dbuf<u32> g_succ, g_seg_at, g_cbv, g_ids, g_chain, g_dist[2];
+    dbuf<u32> g_bmI, g_bmI2, g_bmIb, g_bmT;
+    dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_ast, g_aen, g_ark;
+    dbuf<u64> g_offs;
     u64 num_fact = 0;
     std::vector<u64> stats;
 

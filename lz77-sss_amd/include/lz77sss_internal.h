@@ -74,6 +74,21 @@ struct dbuf {
         }
         return p;
     }
+    // grow keeping the first `keep` elements (stream-ordered copy on st)
+    T* grow_keep(size_t n, size_t keep, hipStream_t st) {
+        if (n <= cap) return p;
+        T* q = nullptr;
+        const size_t c = std::max<size_t>(n, cap + cap / 2);
+        LZ_HIP(hipMalloc(&q, c * sizeof(T)));
+        if (p && keep) LZ_HIP(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
+        if (p) {
+            LZ_HIP(hipStreamSynchronize(st));
+            LZ_HIP(hipFree(p));
+        }
+        p = q;
+        cap = c;
+        return p;
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
