@@ -123,6 +123,29 @@ __global__ void k_pred(const u32* __restrict__ skeys, const u32* __restrict__ sv
     if (t >= m) return;
     pred5[svals[t]] = (t > 0 && skeys[t - 1] == skeys[t]) ? svals[t - 1] : NONE;
 }
+// bucket tables over slots: bucket[s] = first sorted index with slot >= s (bucket[nslots] = m)
+struct key_u32 { const u32* k; __device__ u32 operator()(u64 t) const { return k[t]; } };
+struct key_u64 { const u64* k; __device__ u32 operator()(u64 t) const { return (u32)(k[t] >> 35); } };
+template <class K>
+__global__ void k_bucket_dense(K key, u64 m, u32 nslots, u32* __restrict__ bucket) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > m) return;
+    const u32 cur = t == m ? nslots : key(t);
+    const int64_t prev = t == 0 ? -1 : (int64_t)key(t - 1);
+    if ((int64_t)cur == prev) return;
+    for (int64_t x = prev + 1; x <= (int64_t)cur; x++) bucket[x] = (u32)t;
+}
+template <class K>
+__global__ void k_bucket_search(K key, u64 m, u32 nslots, u32* __restrict__ bucket) {
+    const u64 sl = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sl > nslots) return;
+    u64 lo = 0, hi = m;
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (key(mid) < sl) lo = mid + 1; else hi = mid;
+    }
+    bucket[sl] = (u32)lo;
+}
 // added entries -> 64-bit keys (slot << 35 | pos << 3 | order)
 __global__ void k_pack_added(const u32* __restrict__ keys, const u32* __restrict__ ipos, u64 m, u64* __restrict__ out) {
     const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -150,10 +173,17 @@ struct walk_ctx {
     const u32* pred5;    // predecessor entry in the same slot
     const u32* ipos;     // rank -> position
     u64 nentries;
+    const u32* bstart;   // slot -> first sorted base entry (nslots + 1)
     // delta
     const u8* rem;       // removed base ranks
-    const u64* akeys;    // sorted added keys
+    const u64* akeys;    // sorted added keys (main list)
     u64 nadd;
+    const u32* abeg;     // slot -> first added key (nslots + 1)
+    const u64* akeys2;   // sorted added keys (extra list, positions joined after the main build)
+    u64 nadd2;
+    const u32* abeg2;
+    const u32* bmI;      // current insert set (membership of added positions)
+    int use_pred;        // base lookups via pred5 (else bucket search)
     lce_view L;
 };
 
@@ -182,22 +212,9 @@ __device__ __forceinline__ u32 occ_min(u32 a, u32 b) {
 }
 // last base entry strictly before (slot, q, ord) in processing order, skipping removed
 __device__ u32 base_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
-    u64 lo = 0, hi = W.nentries;  // first index with key > slot
-    while (lo < hi) {
-        const u64 mid = (lo + hi) >> 1;
-        if (W.skeys[mid] <= slot) lo = mid + 1; else hi = mid;
-    }
-    const u64 end = lo;
-    lo = 0;
-    hi = end;  // first index with key >= slot
-    while (lo < hi) {
-        const u64 mid = (lo + hi) >> 1;
-        if (W.skeys[mid] < slot) lo = mid + 1; else hi = mid;
-    }
-    const u64 beg = lo;
+    const u64 beg = W.bstart[slot], end = W.bstart[slot + 1];
     // within [beg, end) entries are in (position, order) order: first >= (q, ord)
-    lo = beg;
-    hi = end;
+    u64 lo = beg, hi = end;
     while (lo < hi) {
         const u64 mid = (lo + hi) >> 1;
         const u32 e = W.svals[mid];
@@ -210,18 +227,26 @@ __device__ u32 base_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
     }
     return NONE;
 }
-__device__ u32 added_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
-    if (!W.nadd) return NONE;
+__device__ __forceinline__ bool in_I(const walk_ctx& W, u32 q) { return (W.bmI[q >> 5] >> (q & 31)) & 1; }
+__device__ u32 added_last_before_1(const walk_ctx& W, const u64* ak, const u32* ab, u32 slot, u32 q, u32 ord) {
     const u64 key = ((u64)slot << 35) | ((u64)q << 3) | ord;
-    u64 lo = 0, hi = W.nadd;  // first >= key
+    u64 lo = ab[slot], hi = ab[slot + 1];  // first >= key
+    const u64 beg = lo;
     while (lo < hi) {
         const u64 mid = (lo + hi) >> 1;
-        if (W.akeys[mid] < key) lo = mid + 1; else hi = mid;
+        if (ak[mid] < key) lo = mid + 1; else hi = mid;
     }
-    if (lo == 0) return NONE;
-    const u64 k = W.akeys[lo - 1];
-    if ((k >> 35) != slot) return NONE;
-    return (u32)((k >> 3) & 0xFFFFFFFFull);
+    for (u64 t = lo; t > beg; t--) {
+        const u32 pq = (u32)((ak[t - 1] >> 3) & 0xFFFFFFFFull);
+        if (pq == q || in_I(W, pq)) return pq;
+    }
+    return NONE;
+}
+__device__ u32 added_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
+    u32 r = NONE;
+    if (W.nadd) r = added_last_before_1(W, W.akeys, W.abeg, slot, q, ord);
+    if (W.nadd2) r = occ_max(r, added_last_before_1(W, W.akeys2, W.abeg2, slot, q, ord));
+    return r;
 }
 // H[slot of (q,x)] just before longest_prev_occ's advance_and_get_occ<x> at q
 __device__ u32 lookup(const walk_ctx& W, u32 q, int x, int& hint) {
@@ -231,9 +256,24 @@ __device__ u32 lookup(const walk_ctx& W, u32 q, int x, int& hint) {
     if (rk != NONE) {
         const u32 e = 5 * rk + ord;
         slot = W.keys[e];
-        u32 p = W.pred5[e];
-        while (p != NONE && W.rem[p / 5] && W.ipos[p / 5] != q) p = W.pred5[p];
-        cb = p == NONE ? NONE : W.ipos[p / 5];
+        if (W.use_pred) {
+            u32 p = W.pred5[e];
+            while (p != NONE && W.rem[p / 5] && W.ipos[p / 5] != q) p = W.pred5[p];
+            cb = p == NONE ? NONE : W.ipos[p / 5];
+        } else {
+            // entries of a bucket are in ascending entry order: locate e, then walk back
+            const u64 beg = W.bstart[slot];
+            u64 lo = beg, hi = W.bstart[slot + 1];
+            while (lo < hi) {
+                const u64 mid = (lo + hi) >> 1;
+                if (W.svals[mid] < e) lo = mid + 1; else hi = mid;
+            }
+            cb = NONE;
+            for (u64 t = lo; t > beg; t--) {
+                const u32 r2 = W.svals[t - 1] / 5;
+                if (!W.rem[r2] || W.ipos[r2] == q) { cb = W.ipos[r2]; break; }
+            }
+        }
     } else {
         slot = (u32)((u64)kr_direct(W.T, q, W.G.lens[x], W.G.base[x]) & W.G.mask);
         cb = base_last_before(W, slot, q, ord);
@@ -353,25 +393,31 @@ __global__ void k_dirty(walk_ctx W, const u32* __restrict__ ys, u64 m, u32* __re
     for (int x = 0; x < 5; x++) {
         const u32 slot = (u32)((u64)kr_direct(W.T, y, W.G.lens[x], W.G.base[x]) & W.G.mask);
         u32 best = NONE;
-        u64 lo = 0, hi = W.nentries;  // first entry after (slot, y)
+        const u64 bend = W.bstart[slot + 1];
+        u64 lo = W.bstart[slot], hi = bend;  // first entry after (slot, y)
         while (lo < hi) {
             const u64 mid = (lo + hi) >> 1;
-            const u32 key = W.skeys[mid];
-            const u32 pq = W.ipos[W.svals[mid] / 5];
-            if (key < slot || (key == slot && pq <= y)) lo = mid + 1; else hi = mid;
+            if (W.ipos[W.svals[mid] / 5] <= y) lo = mid + 1; else hi = mid;
         }
-        for (u64 t = lo; t < W.nentries && W.skeys[t] == slot; t++) {
+        for (u64 t = lo; t < bend; t++) {
             const u32 rk = W.svals[t] / 5;
             if (!W.rem[rk]) { best = W.ipos[rk]; break; }
         }
-        if (W.nadd) {
+        for (int li = 0; li < 2; li++) {
+            const u64* ak = li ? W.akeys2 : W.akeys;
+            const u32* ab = li ? W.abeg2 : W.abeg;
+            if (!(li ? W.nadd2 : W.nadd)) continue;
             const u64 key = ((u64)slot << 35) | ((u64)(y + 1) << 3);
-            u64 a = 0, b = W.nadd;
+            u64 a = ab[slot], b = ab[slot + 1];
+            const u64 aend = b;
             while (a < b) {
                 const u64 mid = (a + b) >> 1;
-                if (W.akeys[mid] < key) a = mid + 1; else b = mid;
+                if (ak[mid] < key) a = mid + 1; else b = mid;
             }
-            if (a < W.nadd && (W.akeys[a] >> 35) == slot) best = occ_min(best, (u32)((W.akeys[a] >> 3) & 0xFFFFFFFFull));
+            for (; a < aend; a++) {
+                const u32 pq = (u32)((ak[a] >> 3) & 0xFFFFFFFFull);
+                if (in_I(W, pq)) { best = occ_min(best, pq); break; }
+            }
         }
         out[5 * k + x] = best;
     }
@@ -638,13 +684,14 @@ __global__ void k_gap_cbv(const u32* __restrict__ P, u32 m, u32 CH, const u32* _
     for (u32 t = 1; t <= K; t++) cbv[cb_off[k] + t - 1] = a + t * CH;
 }
 __global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per gap
+    const u32 lane = threadIdx.x & 63;
     if (k > S.m) return;
     u32 a, b;
     gap_of(S.P, (u32)k, a, b);
     if (a >= b) return;
     const u32 K = gap_chunks(a, b, CH);
-    for (u32 t = 0; t <= K; t++) {
+    for (u32 t = lane; t <= K; t += 64) {
         const u32 x = a + t * CH, id = seg_off[k] + t;
         S.sin[id] = seg_in{x, (u32)k, x, S.zmask0, upper_cb(S, x)};
         S.valid[id] = 0;
@@ -661,22 +708,32 @@ __device__ __forceinline__ void bm_set_range(u32* bm, u32 a, u32 b) {  // [a, b)
         a += hi - lo;
     }
 }
+// one wave sets [a, b): lanes stride over the 32-bit words
+__device__ __forceinline__ void bm_set_range_wave(u32* bm, u32 a, u32 b, u32 lane) {
+    if (a >= b) return;
+    const u32 w0 = a >> 5, w1 = (b - 1) >> 5;
+    for (u32 w = w0 + lane; w <= w1; w += 64) {
+        u32 mask = 0xFFFFFFFFu;
+        if (w == w0) mask &= ~((1u << (a & 31)) - 1);
+        if (w == w1 && (b & 31)) mask &= (1u << (b & 31)) - 1;
+        atomicOr(&bm[w], mask);
+    }
+}
 __global__ void k_gap_bitmaps(const u32* __restrict__ P, u32 m, u32 N, u32 nt, u32* __restrict__ bmI,
                               u32* __restrict__ bmSup) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per phrase
+    const u32 lane = threadIdx.x & 63;
     if (k > m) return;
     u32 a, b;
     gap_of(P, (u32)k, a, b);
     if (a < b) {
         const u32 e = min(min(b + 1, N), nt);
-        if (a < e) {
-            bm_set_range(bmI, a, e);
-            bm_set_range(bmSup, a, e);
-        }
+        bm_set_range_wave(bmI, a, e, lane);
+        bm_set_range_wave(bmSup, a, e, lane);
     }
     if (k < m) {
         const u32 pb = P[3 * k], pe = P[3 * k + 1];
-        if (pe - pb <= 48 && pb < nt) bm_set_range(bmSup, pb, min(pe, nt));
+        if (pe - pb <= 48 && pb < nt) bm_set_range_wave(bmSup, pb, min(pe, nt), lane);
     }
 }
 // maximal runs of ones -> intervals [st, en): count starts/ends per word, then write
@@ -888,14 +945,14 @@ __global__ void k_chain_expand(jump_levels JL, u32 len, u32* __restrict__ chain)
 }
 // I' bitmap: what the chain inserted below nt ([start, e) + LPF-start queries)
 __global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, u32 nt, u32* __restrict__ bm) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per chain node
+    const u32 lane = threadIdx.x & 63;
     if (k >= cnt) return;
     const u32 g = chain[k];
     const seg_out& o = S.sout[g];
     const u32 a = S.sin[g].start, b = min(o.e, nt);
-    if (a < b) bm_set_range(bm, a, b);
-    for (u32 t = 0; t < o.nsingle && t < 4; t++)
-        if (o.single[t] < nt) atomicOr(&bm[o.single[t] >> 5], 1u << (o.single[t] & 31));
+    bm_set_range_wave(bm, a, b, lane);
+    if (lane < o.nsingle && lane < 4 && o.single[lane] < nt) atomicOr(&bm[o.single[lane] >> 5], 1u << (o.single[lane] & 31));
 }
 __global__ void k_set_pairs(const u32* __restrict__ pairs, u32 np, u32* __restrict__ bm) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1036,7 +1093,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     LZ_HIP(hipMemsetAsync(S.nseg, 0, 8, st));
     LZ_HIP(hipMemcpyAsync(S.nseg, &nseg0, 4, hipMemcpyHostToDevice, st));
     S.cbv = cbv; S.ncb = ncb; S.P = P; S.m = m; S.N = N; S.zmask0 = zmask0;
-    k_gap_segs<<<cdiv(m + 1, 256), 256, 0, st>>>(S, CH, off_seg);
+    k_gap_segs<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(S, CH, off_seg);
     // bitmaps: I (current speculation), I' (what the chain inserted), Ib (base set), scratch
     u32* bmI = g_bmI.get(nw);
     u32* bmI2 = g_bmI2.get(nw);
@@ -1044,7 +1101,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     u32* bmT = g_bmT.get(nw);
     LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
     LZ_HIP(hipMemsetAsync(bmT, 0, nw * 4, st));
-    k_gap_bitmaps<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, bmI, bmT);
+    k_gap_bitmaps<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(P, m, N, G.nt, bmI, bmT);
     LZ_HIP(hipStreamSynchronize(st));
     lap("greedy setup");
 
@@ -1059,6 +1116,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     u32* ne = g_tmp2.get(nw + 1);
     u32* os = g_tmp3.get(nw + 1);
     u32* oe = g_tmp4.get(nw + 1);
+    const u32 nslots = G.mask + 1;
+    auto build_buckets = [&](auto key, u64 mk, dbuf<u32>& bk) {
+        u32* b = bk.get((u64)nslots + 1);
+        if (mk * 16 >= nslots) k_bucket_dense<<<cdiv(mk + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
+        else k_bucket_search<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
+    };
     // runs of a bitmap -> intervals (st, en), ranks, <= 1024-position chunks
     auto runs_to_chunks = [&](const u32* bm, dbuf<u32>& dst, dbuf<u32>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
                               u64& npos, u32& nch) -> ichunk* {
@@ -1105,39 +1168,63 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             u8* t = scan_tmp.get(tb);
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, skeys, vals, svals, (int)ne5, 0,
                                                       (int)gp.log2_size_h, st));
-            k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
+            if (W.use_pred) k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
         }
+        build_buckets(key_u32{skeys}, ne5, g_bstart);
         W.istart = ist.p; W.iend = iend.p; W.irank = irank.p; W.nint = ni;
         W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne5;
-        W.rem = rem; W.akeys = nullptr; W.nadd = 0;
+        W.bstart = g_bstart.p;
+        W.rem = rem; W.akeys = nullptr; W.nadd = 0; W.akeys2 = nullptr; W.nadd2 = 0;
         lap("base build (slots+sort+pred)");
     };
-    // added entries: positions of I outside the base set
-    auto rebuild_added = [&]() {
-        k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmT);
+    // added entries: positions of I outside the base set.  The main list is
+    // rebuilt rarely (membership of its positions is read from the I bitmap);
+    // positions that join later and are missing from it go to the small extra list.
+    u32* bmA = g_bmA.get(nw);
+    u64 na_main = 0;
+    auto build_list = [&](const u32* bm, dbuf<u32>& k32, dbuf<u32>& kpos, dbuf<u64>& ka, dbuf<u64>& kb,
+                          dbuf<u32>& bucket, const u64*& keys_out, u64& nkeys, const u32*& bk_out) -> u64 {
         u32 ni, nch;
         u64 na;
-        ichunk* ch = runs_to_chunks(bmT, g_ast, g_aen, g_ark, chunk_buf2, ni, na, nch);
-        W.nadd = 0;
-        W.akeys = nullptr;
-        if (!na) return;
-        u32* akey32 = add_keys32.get(5 * na);
-        u32* apos = add_pos.get(na);
+        ichunk* ch = runs_to_chunks(bm, g_ast, g_aen, g_ark, chunk_buf2, ni, na, nch);
+        nkeys = 0;
+        keys_out = nullptr;
+        if (!na) return 0;
+        u32* akey32 = k32.get(5 * na);
+        u32* apos = kpos.get(na);
         k_slots<<<cdiv(nch, 64), 64, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
-        u64* ak = add_keys.get(5 * na);
-        u64* ak2 = add_keys2.get(5 * na);
+        u64* ak = ka.get(5 * na);
+        u64* ak2 = kb.get(5 * na);
         k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
         size_t tb = 0;
         LZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, ak, ak2, (int)(5 * na), 0, 63, st));
         u8* t = scan_tmp.get(tb);
         LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, ak, ak2, (int)(5 * na), 0, 63, st));
-        W.akeys = ak2;
-        W.nadd = 5 * na;
+        keys_out = ak2;
+        nkeys = 5 * na;
+        build_buckets(key_u64{ak2}, 5 * na, bucket);
+        bk_out = bucket.p;
+        return na;
+    };
+    auto rebuild_main = [&]() {
+        k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmA);
+        na_main = build_list(bmA, add_keys32, add_pos, add_keys, add_keys2, g_abeg, W.akeys, W.nadd, W.abeg);
+        W.nadd2 = 0;
+        W.akeys2 = nullptr;
+    };
+    auto rebuild_added = [&](bool main_list) {
+        if (main_list) return rebuild_main();
+        k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmT);
+        k_bm_andnot<<<gw, 256, 0, st>>>(bmT, bmA, nw, bmT);
+        const u64 nx = build_list(bmT, g_x32, g_xpos, g_xk, g_xk2, g_abeg2, W.akeys2, W.nadd2, W.abeg2);
+        if (nx * 4 > na_main + (1u << 16)) rebuild_main();
     };
     auto set_state = [&]() {  // rem + added for the current I
+        W.bmI = bmI;
         if (nb) k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, (u8*)W.rem);
-        rebuild_added();
+        rebuild_added(true);
     };
+    W.use_pred = std::getenv("LZ77SSS_NO_PRED") ? 0 : 1;
     build_base(bmT);  // superset: gaps + short phrase interiors
     set_state();
 
@@ -1250,7 +1337,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         }
         // ---- the insert set the chain actually produced vs the speculation
         LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
-        if (nchain) k_chain_inserts<<<cdiv(nchain, 256), 256, 0, st>>>(S, chain, nchain, G.nt, bmI2);
+        if (nchain) k_chain_inserts<<<cdiv((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, G.nt, bmI2);
         if (tail && hc[1]) {
             u32* d_tins = tail_ins_buf.p;
             k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], bmI2);
@@ -1277,7 +1364,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         k_bm_andnot<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
         k_bm_count1<<<gw, 256, 0, st>>>(bmT, nw, ne);
         const u64 outside = excl_scan(ne, oe, nw, scan_tmp, st);
-        if (outside * 50 > nb) {
+        if (outside * 8 > nb) {
             k_bm_or<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
             std::swap(g_bmI.p, g_bmI2.p);
             bmI = g_bmI.p;
@@ -1286,6 +1373,18 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             set_state();
             k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
             if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy rebuild: outside=%llu\n", (unsigned long long)outside);
+            continue;
+        }
+        if (ny > nseg) {
+            // too many changes for dirty tracking to pay off: new state, re-walk everything
+            std::swap(g_bmI.p, g_bmI2.p);
+            bmI = g_bmI.p;
+            bmI2 = g_bmI2.p;
+            set_state();
+            k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
+            lap("delta (full)");
+            if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy delta (full): changed=%llu outside=%llu\n",
+                                  (unsigned long long)ny, (unsigned long long)outside);
             continue;
         }
         // dirty = changed positions + their same-slot successors before and after the update
@@ -1298,7 +1397,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         bmI2 = g_bmI2.p;
         LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
         k_sum_u8<<<cdiv(ny, 256), 256, 0, st>>>(d_j + ny, ny, d_cnt);
-        if (rd1(d_cnt, st)) rebuild_added();
+        W.bmI = bmI;
+        if (rd1(d_cnt, st)) rebuild_added(false);
         k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + 6 * ny);
         u32* d_ds = dirty_sorted.get(11 * ny + 1);
         {

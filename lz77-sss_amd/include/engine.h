@@ -129,6 +129,8 @@ struct engine {
     dbuf<u32> g_bmI, g_bmI2, g_bmIb, g_bmT;
     dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_ast, g_aen, g_ark;
     dbuf<u64> g_offs;
+    dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
+    dbuf<u64> g_xk, g_xk2;
     u64 num_fact = 0;
     std::vector<u64> stats;
 
