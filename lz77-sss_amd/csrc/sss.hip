@@ -31,7 +31,8 @@ constexpr int QT_LDS = QT_SPAN + 256 + 1024; // [A0-256, A0+16384+1024)
 constexpr u32 RUN_HCAP = 640;                // local run extension: [a-256, a+640)
 constexpr u32 RUN_LCAP = 256;
 
-__global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64 n, u64 nanch,
+constexpr int QT_THREADS = QT_ANCH + 64;     // + one wave for the neighbour anchors
+__global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__ T, u64 n, u64 nanch,
                                                    u16* __restrict__ qinfo, u32* __restrict__ any_q,
                                                    u8* __restrict__ run_p, u32* __restrict__ run_hi,
                                                    u32* __restrict__ run_lo, u8* __restrict__ run_cap) {
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64
     __shared__ __attribute__((aligned(16))) u32 b32[QT_LDS / 4 + QT_LDS / 128 + 2];
     const u64 A0 = (u64)blockIdx.x * QT_SPAN;
     const int64_t base = (int64_t)A0 - 256;
-    for (int x = threadIdx.x * 16; x < QT_LDS; x += 128 * 16) {
+    for (int x = threadIdx.x * 16; x < QT_LDS; x += QT_THREADS * 16) {
         int64_t g = base + x;
         uint4 v = {0, 0, 0, 0};
         if (g >= 0 && (u64)g + 16 <= n + TEXT_PAD) v = *(const uint4*)(T + g);
@@ -53,75 +54,115 @@ __global__ __launch_bounds__(128) void k_q_anchors(const u8* __restrict__ T, u64
     __syncthreads();
     auto word = [&](int64_t w) -> u32 { return b32[w + (w >> 5)]; };
     auto byte = [&](int64_t x) -> u32 { return (word(x >> 2) >> (8 * (x & 3))) & 255u; };
-    const u64 t = (u64)blockIdx.x * QT_ANCH + threadIdx.x;
-    if (t >= nanch) return;
+    __shared__ u8 s_p[QT_ANCH + 3];  // s_p[i]: period of anchor blockIdx*QT_ANCH - 1 + i
+    // 4 bytes at any LDS offset
+    auto w32 = [&](int64_t o) -> u32 {
+        const int64_t q = o >> 2;
+        return __builtin_amdgcn_alignbyte(word(q + 1), word(q), (u32)(o & 3));
+    };
+    // first q in [h, cap) with T[q] != T[q+p] (cap if none)
+    auto ext_fwd = [&](u64 h, u64 cap, u32 p) -> u64 {
+        while (h < cap) {
+            u32 d = w32((int64_t)h - base) ^ w32((int64_t)(h + p) - base);
+            const u64 rem = cap - h;
+            if (rem < 4) d &= (1u << (8 * rem)) - 1;
+            if (d) return h + (__builtin_ctz(d) >> 3);
+            h += rem < 4 ? rem : 4;
+        }
+        return cap;
+    };
+    // smallest l in [cap, l0] with T[q] == T[q+p] for all q in [l, l0)
+    auto ext_bwd = [&](u64 l, u64 cap, u32 p) -> u64 {
+        while (l >= cap + 4) {
+            const u32 d = w32((int64_t)l - 4 - base) ^ w32((int64_t)(l - 4 + p) - base);
+            if (d) return l - 4 + ((31 - __builtin_clz(d)) >> 3) + 1;
+            l -= 4;
+        }
+        while (l > cap && byte((int64_t)l - 1 - base) == byte((int64_t)(l - 1 + p) - base)) l--;
+        return l;
+    };
+    // smallest period p <= 170 of T[a..a+340) (0 if none): a 4-byte filter marks the
+    // candidates (uniform loop), then every lane verifies its own lowest pending
+    // candidate, so lanes with different periods verify concurrently
+    auto period_of = [&](u64 a) -> u32 {
+        if (a + QM > n) return 0;
+        const int la = (int)((int64_t)a - base);  // multiple of 4
+        const u32 w0 = word(la >> 2);
+        u32 cm[6] = {0, 0, 0, 0, 0, 0};  // bit pp-1
+        u32 dprev = w0;
+#pragma unroll 4
+        for (int k = 0; k <= (int)(QL / 4); k++) {
+            const u32 dnext = word((la >> 2) + k + 1);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const u32 pp = 4 * k + r;
+                if (pp >= 1 && pp <= QL && __builtin_amdgcn_alignbyte(dnext, dprev, r) == w0)
+                    cm[(pp - 1) >> 5] |= 1u << ((pp - 1) & 31);
+            }
+            dprev = dnext;
+        }
+        for (int wi = 0; wi < 6;) {
+            if (!cm[wi]) { wi++; continue; }
+            const u32 pp = 32 * wi + __builtin_ctz(cm[wi]) + 1;
+            if (ext_fwd(a + 4, a + QM - pp, pp) == a + QM - pp) return pp;
+            cm[wi] &= cm[wi] - 1;
+        }
+        return 0;
+    };
+    const u64 t0 = (u64)blockIdx.x * QT_ANCH;
+    if (threadIdx.x < QT_ANCH) {
+        const u64 tt = t0 + threadIdx.x;
+        s_p[threadIdx.x + 1] = tt < nanch ? (u8)period_of(tt * QA) : 0;
+    } else if (threadIdx.x < QT_ANCH + 3) {  // the anchor before the block and the two after it
+        const u32 x = threadIdx.x - QT_ANCH;
+        const u64 tn = x == 0 ? t0 - 1 : t0 + QT_ANCH + x - 1;
+        const u32 slot = x == 0 ? 0 : QT_ANCH + x;
+        s_p[slot] = (x == 0 && t0 == 0) || tn >= nanch ? 0 : (u8)period_of(tn * QA);
+    }
+    __syncthreads();
+    const u64 t = t0 + threadIdx.x;
+    if (threadIdx.x >= QT_ANCH || t >= nanch) return;
     const u64 a = t * QA;
     u16 res = 0xFF00;  // empty interval
     u32 rp = 0, rhi = 0, rlo = 0;
     u8 rcap = 0;
-    if (a + QM <= n) {
-        const int la = (int)(a - base);  // multiple of 4
-        // 4 bytes at any LDS offset
-        auto w32 = [&](int64_t o) -> u32 {
-            const int64_t q = o >> 2;
-            return __builtin_amdgcn_alignbyte(word(q + 1), word(q), (u32)(o & 3));
-        };
-        // first q in [h, cap) with T[q] != T[q+p] (cap if none)
-        auto ext_fwd = [&](u64 h, u64 cap, u32 p) -> u64 {
-            while (h < cap) {
-                u32 d = w32((int64_t)h - base) ^ w32((int64_t)(h + p) - base);
-                const u64 rem = cap - h;
-                if (rem < 4) d &= (1u << (8 * rem)) - 1;
-                if (d) return h + (__builtin_ctz(d) >> 3);
-                h += rem < 4 ? rem : 4;
-            }
-            return cap;
-        };
-        // smallest l in [cap, l0] with T[q] == T[q+p] for all q in [l, l0)
-        auto ext_bwd = [&](u64 l, u64 cap, u32 p) -> u64 {
-            while (l >= cap + 4) {
-                const u32 d = w32((int64_t)l - 4 - base) ^ w32((int64_t)(l - 4 + p) - base);
-                if (d) return l - 4 + ((31 - __builtin_clz(d)) >> 3) + 1;
-                l -= 4;
-            }
-            while (l > cap && byte((int64_t)l - 1 - base) == byte((int64_t)(l - 1 + p) - base)) l--;
-            return l;
-        };
-        const u32 w0 = word(la >> 2);
-        u32 p = 0;
-        u32 dprev = w0;
-        for (int k = 0; k <= (int)(QL / 4) && !p; k++) {
-            u32 dnext = word((la >> 2) + k + 1);
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                u32 pp = 4 * k + r;
-                if (!p && pp >= 1 && pp <= QL) {
-                    u32 w = __builtin_amdgcn_alignbyte(dnext, dprev, r);
-                    if (w == w0 && ext_fwd(a + 4, a + QM - pp, pp) == a + QM - pp) p = pp;
-                }
-            }
-            dprev = dnext;
+    const u32 p = s_p[threadIdx.x + 1];
+    if (p) {
+        // neighbours with the same period: their windows overlap this one by >= 212 >= p
+        // bytes, so the union is p-periodic and the extensions are known without scanning
+        const bool contb = s_p[threadIdx.x] == p, contf = s_p[threadIdx.x + 2] == p;
+        const bool contf2 = contf && s_p[threadIdx.x + 3] == p;
+        const u64 hi_cap = min(a + TAU - p, n - p), lo_cap = a >= 127 ? a - 127 : 0;
+        const u64 hi = contf2 ? hi_cap : ext_fwd(a + QM - p, hi_cap, p);
+        const u64 lo = contb ? lo_cap : ext_bwd(a, lo_cap, p);
+        // Q on (a-128, a]: j >= lo, j + tau - p <= hi, j <= n - tau
+        int64_t jlo = (int64_t)lo;
+        int64_t jhi = min((int64_t)a, (int64_t)hi + (int64_t)p - (int64_t)TAU);
+        jhi = min(jhi, (int64_t)n - (int64_t)TAU);
+        if (jlo <= jhi) {
+            int64_t r0 = (int64_t)a - 127;  // rel(j) = j - r0 in [0,127]
+            res = (u16)(((jlo - r0) << 8) | (jhi - r0));
+            atomicOr(any_q, 1u);
         }
-        if (p) {
-            const u64 hi = ext_fwd(a + QM - p, min(a + TAU - p, n - p), p);
-            const u64 lo = ext_bwd(a, a >= 127 ? a - 127 : 0, p);
-            // Q on (a-128, a]: j >= lo, j + tau - p <= hi, j <= n - tau
-            int64_t jlo = (int64_t)lo;
-            int64_t jhi = min((int64_t)a, (int64_t)hi + (int64_t)p - (int64_t)TAU);
-            jhi = min(jhi, (int64_t)n - (int64_t)TAU);
-            if (jlo <= jhi) {
-                int64_t r0 = (int64_t)a - 127;  // rel(j) = j - r0 in [0,127]
-                res = (u16)(((jlo - r0) << 8) | (jhi - r0));
-                atomicOr(any_q, 1u);
-            }
-            // local extent of the p-periodic run around the window (for run-skipping LCE)
+        // local extent of the p-periodic run around the window (for run-skipping LCE);
+        // inside a chain of same-period anchors the values only need to mark the chain
+        rp = p;
+        if (contf) {
+            rhi = (u32)(a + RUN_HCAP);
+            rcap |= 1;
+        } else {
             const u64 h2_cap = min(a + RUN_HCAP - p, n - p);
-            const u64 h2 = hi < min(a + TAU - p, n - p) ? hi : ext_fwd(hi, h2_cap, p);
-            const u64 l2 = (lo > (a >= 127 ? a - 127 : 0)) ? lo : ext_bwd(lo, a >= RUN_LCAP ? a - RUN_LCAP : 0, p);
-            rp = p;
+            const u64 h2 = hi < hi_cap ? hi : ext_fwd(hi, h2_cap, p);
             rhi = (u32)(h2 + p);
+            rcap |= h2 == a + RUN_HCAP - p ? 1 : 0;
+        }
+        if (contb) {
+            rlo = (u32)(a >= RUN_LCAP ? a - RUN_LCAP : a - QA);
+            rcap |= 2;
+        } else {
+            const u64 l2 = (lo > lo_cap) ? lo : ext_bwd(lo, a >= RUN_LCAP ? a - RUN_LCAP : 0, p);
             rlo = (u32)l2;
-            rcap = (h2 == a + RUN_HCAP - p ? 1 : 0) | (l2 == a - RUN_LCAP && a >= RUN_LCAP ? 2 : 0);
+            rcap |= (l2 == a - RUN_LCAP && a >= RUN_LCAP) ? 2 : 0;
         }
     }
     qinfo[t] = res;
@@ -425,7 +466,7 @@ void engine::build_sss(const u8* T) {
     u32* rhi = run_hi.get(nanch);
     u32* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
-    k_q_anchors<<<cdiv(nanch, QT_ANCH), QT_ANCH, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap);
+    k_q_anchors<<<cdiv(nanch, QT_ANCH), QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap);
     LZ_HIP(hipGetLastError());
     {
         u64* ea = run_scan_a.get(2 * nanch);
