@@ -48,7 +48,8 @@ void engine::destroy() {
 
 u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log) {
     LZ_HIP(hipSetDevice(device));
-    if (phr_mode != LZ77SSS_LPF_OPT) throw error(LZ77SSS_EINVAL, "unsupported phrase mode (lpf_opt only)");
+    if (phr_mode != LZ77SSS_LPF_OPT && phr_mode != LZ77SSS_LPF_LNF_OPT && phr_mode != LZ77SSS_LPF_LNF_NAIVE)
+        throw error(LZ77SSS_EINVAL, "unsupported phrase mode (lpf_opt, lpf_lnf_opt, lpf_lnf_naive)");
     if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
     num_fact = 0;
     stats.assign(24, 0);
@@ -60,18 +61,23 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log) {
         LZ_HIP(hipStreamSynchronize(st));
         std::fprintf(stderr, "[lz77sss-debug] done %s (|S|=%u phrases=%u)\n", what, s, num_phr);
     };
-    build_sss(d_text);
-    timer.mark("sss");
-    trace("sss");
-    build_sa_s(d_text);
-    timer.mark("sa_s");
-    trace("sa_s");
-    build_lcp_rmq(d_text);
-    timer.mark("lcp_rmq");
-    trace("lcp_rmq");
-    build_lpf_opt(d_text);
-    timer.mark("lpf");
-    trace("lpf");
+    if (phr_mode == LZ77SSS_LPF_OPT) {
+        build_sss(d_text);
+        timer.mark("sss");
+        trace("sss");
+        build_sa_s(d_text);
+        timer.mark("sa_s");
+        trace("sa_s");
+        build_lcp_rmq(d_text);
+        timer.mark("lcp_rmq");
+        trace("lcp_rmq");
+        build_lpf_opt(d_text);
+        timer.mark("lpf");
+        trace("lpf");
+    } else {
+        build_lpf_lnf(phr_mode == LZ77SSS_LPF_LNF_OPT ? 1 : 0);
+        trace("lpf_lnf");
+    }
     num_fact = factorize_greedy(d_text, rk_seed, log2_override);
     timer.mark("greedy");
     trace("greedy");
@@ -140,7 +146,9 @@ static void check_params(const lz77sss_params* prm) {
     if (!prm) throw lz::error(LZ77SSS_EINVAL, "params is NULL");
     if (prm->tau != 512) throw lz::error(LZ77SSS_EINVAL, "only tau = 512 is supported");
     if (prm->fact_mode != LZ77SSS_GREEDY) throw lz::error(LZ77SSS_EINVAL, "only fact_mode = greedy is supported");
-    if (prm->phr_mode != LZ77SSS_LPF_OPT) throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
+    if (prm->phr_mode != LZ77SSS_LPF_OPT && prm->phr_mode != LZ77SSS_LPF_LNF_OPT &&
+        prm->phr_mode != LZ77SSS_LPF_LNF_NAIVE)
+        throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
     if (prm->index_log2_size < 0 || prm->index_log2_size > 30) throw lz::error(LZ77SSS_EINVAL, "bad index_log2_size");
 }
 

@@ -129,6 +129,9 @@ struct engine {
     dbuf<u32> g_bmI, g_bmI2, g_bmIb, g_bmT;
     dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_ast, g_aen, g_ark;
     dbuf<u64> g_offs;
+    // LPF/LNF mode (csrc/lnf.hip)
+    dbuf<u32> l_V, l_b, l_d, l_e, l_r, l_sflag_lnf, l_slots_lnf, l_sflag, l_slots, l_off, l_P, l_Q;
+    dbuf<u64> l_tmp64;
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
     dbuf<u64> g_xk, g_xk2;
     u64 num_fact = 0;
@@ -145,6 +148,9 @@ struct engine {
     void build_sa_s(const u8* T);
     void build_lcp_rmq(const u8* T);
     void build_lpf_opt(const u8* T);
+    void build_lpf_lnf(int opt);  // csrc/lnf.hip
+    void all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slots, u32* sflag);
+    void path_marks(u32 m, u32* nxt0, u32* marks);
     u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override);
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log);
     lce_view view(const u8* T) const;

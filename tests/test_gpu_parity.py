@@ -125,6 +125,8 @@ def test_invalid_parameters_fail_loudly(session, lz):
         s.factorize(tau=256)
     with pytest.raises(lz.Lz77SssError):
         s.factorize(fact_mode=lz.SKIP_PHRASES)
+    with pytest.raises(lz.Lz77SssError):
+        s.factorize(phr_mode=lz.LPF_NAIVE)
     small = lz.Session(1 << 10)
     with pytest.raises(lz.Lz77SssError):
         small.load(T)
@@ -166,3 +168,31 @@ def test_cpp_mirror_roundtrip(tmp_path):
     r = subprocess.run([str(exe), "8"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count(" ok") == 8
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_lpf_lnf_stream(session, name):
+    """Config 3: factorize_approximate<greedy, lpf_lnf_opt> (reversed-text LNF phrases + selection)."""
+    g = load_golden(name)
+    s, F = run(session, g["text"], phr_mode=3)
+    assert np.array_equal(F, g["factors_lnf"])
+    assert s.stats()[:12] == [int(x) for x in g["stats_lnf"][:12]]
+
+
+@pytest.mark.parametrize("seed", range(1, 9))
+@pytest.mark.parametrize("mode", [3, 1])
+def test_c1_lpf_lnf_vs_oracle(session, orc, lz, seed, mode):
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    _, F = run(session, T, phr_mode=mode)
+    F_ref, _ = orc.factorize(T, phr_mode=mode)
+    assert np.array_equal(F, F_ref)
+    assert np.array_equal(lz.decode(F, T.size), T)
+
+
+@pytest.mark.parametrize("kind,mib", [("genome", 8), ("rr", 32)])
+def test_medium_lpf_lnf_vs_oracle(session, orc, lz, kind, mib):
+    n = mib << 20
+    T = lz.gen_genome(n, 1 << 20, 0.001, 3) if kind == "genome" else lz.gen_random_repetitive(n, n, 9, 0.5, 0.05)
+    _, F = run(session, T, phr_mode=3)
+    F_ref, _ = orc.factorize(T, phr_mode=3)
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
