@@ -75,16 +75,20 @@ def pmc_traffic(workload: str, n: int):
     return None if best is None else best.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(lz, workload: str, sample_mib: int):
+PHR = {"lpf_opt": 2, "lpf_lnf_opt": 3}
+
+
+def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2):
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # the CPU port (test/bench infrastructure only)
 
     n = sample_mib << 20
     T = make_text(lz, workload, n, 0)
-    z, sec, _ = oracle.factorize_timed(T)
+    z, sec, _ = oracle.factorize_timed(T, phr_mode=phr_mode)
     desc = ("full 1 GiB workload text" if n == GIB else f"first {sample_mib} MiB-sized instance of the same generator")
     return {"value": round(n / sec / 1e6, 2), "unit": "MB/s", "cores": oracle.num_threads(), "kind": "port",
-            "sample": f"{workload}: {desc} (n={n}, z={z}), oracle factorize_approximate<greedy,lpf_opt> p=1 "
+            "sample": f"{workload}: {desc} (n={n}, z={z}), oracle factorize_approximate<greedy,"
+                      f"{'lpf_opt' if phr_mode == 2 else 'lpf_lnf_opt'}> p=1 "
                       f"restatement with OpenMP stages, {sec:.2f} s"}
 
 
@@ -95,6 +99,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="rr", choices=["rr", "genome"])
     ap.add_argument("--size-mib", type=int, default=1024)
+    ap.add_argument("--phr-mode", default="lpf_opt", choices=["lpf_opt", "lpf_lnf_opt"],
+                    help="lpf_opt = configs[1]; lpf_lnf_opt = configs[2] (LPF/LNF phrases)")
     ap.add_argument("--cpu-sample-mib", type=int, default=-1,
                     help="oracle sample size (default: full text for rr, 128 MiB for genome)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -123,7 +129,7 @@ def main():
     t_load = time.perf_counter() - t_load0
 
     for _ in range(args.warmup):
-        sess.factorize(device=local_rank)
+        sess.factorize(device=local_rank, phr_mode=PHR[args.phr_mode])
 
     def barrier():
         if dist is not None:
@@ -135,7 +141,7 @@ def main():
     t0 = time.perf_counter()
     z = 0
     for _ in range(args.steps):
-        z = sess.factorize(device=local_rank)
+        z = sess.factorize(device=local_rank, phr_mode=PHR[args.phr_mode])
         ms, b = sess.sss_kernel_time()
         kern_ms.append(ms)
         kern_bytes.append(b)
@@ -157,7 +163,7 @@ def main():
         bytes_launch = kern_bytes[-1]
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
         out = {
-            "metric": "factorization MB/s (3-aprx LZ77, greedy + lpf_opt, tau=512)",
+            "metric": f"factorization MB/s (3-aprx LZ77, greedy + {args.phr_mode}, tau=512)",
             "value": round(value, 2),
             "unit": "MB/s",
             "n_gpus": world,
@@ -172,7 +178,7 @@ def main():
             if args.workload == "rr" else "synthetic (genome-like: 64 MiB ACGT base block, 0.1% mutations)",
             "config": {
                 "workload": f"{args.workload} n={n} ({args.size_mib} MiB) per GPU, pos_t=uint32",
-                "n": n, "tau": 512, "phr_mode": "lpf_opt", "fact_mode": "greedy", "virtual_p": 1,
+                "n": n, "tau": 512, "phr_mode": args.phr_mode, "fact_mode": "greedy", "virtual_p": 1,
                 "parallelism": f"independent-texts x{world}" if world > 1 else "single GPU",
                 "factors": int(z), "comp_ratio": round(n / max(z, 1), 2),
                 "sss_size": int(st[0]) if st else None, "has_runs": bool(st[1]) if st else None,
@@ -196,7 +202,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else (
                 args.size_mib if args.workload == "rr" else min(128, args.size_mib))
-            out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample)
+            out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample, PHR[args.phr_mode])
         print(json.dumps(out), flush=True)
     sess.close()
     if dist is not None:
