@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--phr-mode", default="lpf_opt", choices=["lpf_opt", "lpf_lnf_opt"],
                     help="lpf_opt = configs[1]; lpf_lnf_opt = configs[2] (LPF/LNF phrases)")
     ap.add_argument("--cpu-sample-mib", type=int, default=-1,
-                    help="oracle sample size (default: full text for rr, 128 MiB for genome)")
+                    help="oracle sample size in MiB (default: the full workload text, 2-30 s of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -200,8 +200,7 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else (
-                args.size_mib if args.workload == "rr" else min(128, args.size_mib))
+            sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else args.size_mib
             out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample, PHR[args.phr_mode])
         print(json.dumps(out), flush=True)
     sess.close()
