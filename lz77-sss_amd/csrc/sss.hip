@@ -234,6 +234,12 @@ __device__ __forceinline__ u32 red31(u64 x) {
     return (u32)(r >= P31 ? r - P31 : r);
 }
 __device__ __forceinline__ u32 mulmod31(u32 a, u32 c) { return red31((u64)a * c); }
+// canonical x mod (2^31 - 1) for x < 2^51 (one fold: the high part fits 20 bits)
+__device__ __forceinline__ u32 red31s(u64 x) {
+    const u32 lo = (u32)x, hi = (u32)(x >> 32);
+    const u32 r = (lo & (u32)P31) + __builtin_amdgcn_alignbit(hi, lo, 31);
+    return r >= (u32)P31 ? r - (u32)P31 : r;
+}
 __device__ __forceinline__ u32 shfl_up32(u32 v, u32 d) { return __shfl_up(v, d, 64); }
 __device__ __forceinline__ u32 shfl_down32(u32 v, u32 d) { return __shfl_down(v, d, 64); }
 
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(TWG, 3) void k_sss_tile(const u8* __restrict__ T, u
     const u32 mw[4] = {mine.x, mine.y, mine.z, mine.w};
     u32 h = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) h = red31((u64)h * b + ((mw[k >> 2] >> (8 * (k & 3))) & 255u));
+    for (int k = 0; k < 16; k++) h = red31s((u64)h * b + ((mw[k >> 2] >> (8 * (k & 3))) & 255u));
     u32 inc = h;
 #pragma unroll
     for (int d = 0; d < 6; d++) {
@@ -294,28 +300,33 @@ __global__ __launch_bounds__(TWG, 3) void k_sss_tile(const u8* __restrict__ T, u
         }
         const uint4 ahead = *(const uint4*)&s_t[16 * tid + TAU];
         const u32 aw[4] = {ahead.x, ahead.y, ahead.z, ahead.w};
+        const bool noq = q0 == 0xFF00 && q1 == 0xFF00 && j0 + 15 <= jmax;  // common case: no Q, no end
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const u32 u = 16 * tid + k;
             const u64 j = j0 + k;
             u32 v = fp;
-            if (j > jmax) {
-                v = INF32;
-            } else {
-                const u64 t = (j + 127) >> 7;
-                const u16 qi = t == ta ? q0 : q1;
-                const u32 rel = (u32)(j + 127 - (t << 7));
-                if (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) v = INF32;
+            if (!noq) {
+                if (j > jmax) {
+                    v = INF32;
+                } else {
+                    const u64 t = (j + 127) >> 7;
+                    const u16 qi = t == ta ? q0 : q1;
+                    const u32 rel = (u32)(j + 127 - (t << 7));
+                    if (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) v = INF32;
+                }
             }
             s_phi[u + (u >> 4)] = v;
             if (k < 15) {
                 const u32 in = (aw[k >> 2] >> (8 * (k & 3))) & 255u, out = (mw[k >> 2] >> (8 * (k & 3))) & 255u;
-                fp = red31((u64)fp * b + in + (u64)out * PW.bn);
+                fp = red31s((u64)fp * b + in + (u64)out * PW.bn);
             }
         }
     }
     __syncthreads();
     // 4. window minima: wave w handles block pairs (c, c+1) for c = w, w + 8 (c < 14)
+    const u32 ilim = last_i >= t0 ? (u32)min<u64>(last_i - t0, (u64)TL) : 0u;  // decisions u <= ilim
+    const bool any_i = last_i >= t0;
     u32 masks[2] = {0, 0};
     for (int r = 0; r < 2; r++) {
         const u32 c = wv + 8 * r;
@@ -351,8 +362,7 @@ __global__ __launch_bounds__(TWG, 3) void k_sss_tile(const u8* __restrict__ T, u
 #pragma unroll
         for (int e = 0; e < 8; e++) {
             const u32 m = min(min(sx[e], suf_after), min(pre_before, py[e]));
-            const u64 i = t0 + c * 512 + 8 * lane + e;
-            if (m != INF32 && (x[e] == m || y[e] == m) && i <= last_i) mk |= 1u << e;
+            if (m != INF32 && (x[e] == m || y[e] == m) && any_i && c * 512 + 8 * lane + e <= ilim) mk |= 1u << e;
         }
         masks[r] = mk;
         u32 cnt = __popc(mk);
