@@ -146,6 +146,11 @@ __global__ void k_bucket_search(K key, u64 m, u32 nslots, u32* __restrict__ buck
     }
     bucket[sl] = (u32)lo;
 }
+// predecessor in sorted order (NONE at a slot boundary), to be sorted back by entry id
+__global__ void k_pred_sorted(const u32* __restrict__ skeys, const u32* __restrict__ svals, u64 m, u32* __restrict__ pv) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < m) pv[t] = (t > 0 && skeys[t - 1] == skeys[t]) ? svals[t - 1] : NONE;
+}
 // added entries -> 64-bit keys (slot << 35 | pos << 3 | order)
 __global__ void k_pack_added(const u32* __restrict__ keys, const u32* __restrict__ ipos, u64 m, u64* __restrict__ out) {
     const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1168,7 +1173,21 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             u8* t = scan_tmp.get(tb);
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, skeys, vals, svals, (int)ne5, 0,
                                                       (int)gp.log2_size_h, st));
-            if (W.use_pred) k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
+            if (W.use_pred && ne5 < (1ull << 27)) {
+                k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
+            } else if (W.use_pred) {
+                // pred5[e] = predecessor of entry e in its slot: a radix sort by entry id of the
+                // sorted-order predecessors (a random scatter of 4-byte writes is ~3x slower)
+                u32* pv = vals;  // the unsorted values are no longer needed
+                u32* kdump = g_predk.get(ne5 + 1);
+                k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
+                int eb = 1;
+                while (eb < 32 && (1ull << eb) < ne5) eb++;
+                size_t tb2 = 0;
+                LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
+                u8* t2 = scan_tmp.get(tb2);
+                LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
+            }
         }
         build_buckets(key_u32{skeys}, ne5, g_bstart);
         W.istart = ist.p; W.iend = iend.p; W.irank = irank.p; W.nint = ni;
