@@ -289,18 +289,29 @@ __device__ u32 lookup(const walk_ctx& W, u32 q, int x, int& hint) {
 // ---------------------------------------------------------------------------
 // walks
 template <bool WRITE>
-__device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fout) {
+__device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__ og, u32* fout) {
+    // outputs go straight to the table entry og (the bnd/single lists are indexed
+    // dynamically: a local copy of seg_out would live in scratch memory)
     const u8* T = W.T;
     const u32 n = W.G.n, nt = W.G.nt;
     const u32* P = W.P;
     u32 i = in.start, p = in.p, idx = in.idxpos, zm = in.zmask;
-    u32 nf = 0, ns = 0, flags = 0, e = in.start, nb = 0;
+    u32 nf = 0, ns = 0, flags = 0, e = in.start, nb = 0, next = n;
     bool first_gap = true;
     int hint = -1;
-    out.next = n;
-    out.nbnd = 0;
     u64 guard = 0;
     const u64 guard_max = 4ull * n + 1024;
+    auto finish = [&]() {
+        if (WRITE) return;
+        og->next = next;
+        og->e = e;
+        og->nfact = nf;
+        og->idxpos = idx;
+        og->zmask = zm;
+        og->nsingle = ns;
+        og->flags = flags;
+        og->nbnd = nb;
+    };
     auto emit = [&](u32 src, u32 len) {
         if (WRITE) { fout[2 * nf] = src; fout[2 * nf + 1] = len; }
         nf++;
@@ -329,19 +340,14 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
             }
             do {
                 if (i >= in.lim) {  // chunk boundary reached: stop at the next factor start
-                    out.next = i;
-                    out.e = i;
-                    out.nfact = nf;
-                    out.idxpos = idx;
-                    out.zmask = zm;
-                    out.nsingle = ns;
-                    out.flags = flags;
-                    out.nbnd = nb;
+                    next = i;
+                    e = i;
+                    finish();
                     return;
                 }
-                if (i >= nt) { out.flags = flags | 1; out.nbnd = nb; return; }
-                if (++guard > guard_max || i > n) { out.flags = flags | 4; return; }
-                if (first_gap && nb < SEG_NBND) out.bnd[nb++] = i;
+                if (i >= nt) { flags |= 1; finish(); return; }
+                if (++guard > guard_max || i > n) { flags |= 4; finish(); return; }
+                if (!WRITE && first_gap && nb < SEG_NBND) og->bnd[nb++] = i;
                 u32 fsrc, flen;
                 query(i, fsrc, flen);
                 idx = i + 1;
@@ -365,27 +371,21 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out& out, u32* fo
         const u32 exc = i - gap_end;
         u32 lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
         if (idx == i) {
-            if (i >= nt) { out.flags = flags | 1; return; }
+            if (i >= nt) { flags |= 1; finish(); return; }
             u32 fsrc, flen;
             query(i, fsrc, flen);
             idx = i + 1;
-            if (ns < 4) out.single[ns] = i; else flags |= 2;
+            if (ns < 4) { if (!WRITE) og->single[ns] = i; } else flags |= 2;
             ns++;
             if (flen > llen) { lsrc = fsrc; llen = flen; }
         }
         emit(lsrc, llen);
         i += llen;
-        if (++guard > guard_max || i > n || llen == 0) { out.flags = flags | 4; return; }
+        if (++guard > guard_max || i > n || llen == 0) { flags |= 4; finish(); return; }
         while (P[3 * p + 1] <= i) p++;
-        if (i < P[3 * p]) { out.next = i; break; }
+        if (i < P[3 * p]) { next = i; break; }
     }
-    out.e = e;
-    out.nfact = nf;
-    out.idxpos = idx;
-    out.zmask = zm;
-    out.nsingle = ns;
-    out.flags = flags;
-    out.nbnd = nb;
+    finish();
 }
 
 // successor insert (next position of the same slot after y) in the current set:
@@ -824,19 +824,23 @@ __global__ void k_walk(walk_ctx W, seg_tab S, const u32* __restrict__ ids, u32 c
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const u32 g = ids[t];
-    seg_out o;
-    o.flags = 0;
-    o.e = S.sin[g].start;
-    o.nfact = 0;
-    o.nsingle = 0;
-    walk_segment<WRITE>(W, S.sin[g], o, WRITE ? fact + 2 * offs[t] : nullptr);
-    if (o.flags & 2) atomicOr(S.err, 2u);
-    if (o.flags & 4) atomicOr(S.err, 4u);
+    seg_out* og = WRITE ? nullptr : S.sout + g;
+    walk_segment<WRITE>(W, S.sin[g], og, WRITE ? fact + 2 * offs[t] : nullptr);
     if (!WRITE) {
-        S.sout[g] = o;
+        const u32 fl = og->flags;
+        if (fl & 2) atomicOr(S.err, 2u);
+        if (fl & 4) atomicOr(S.err, 4u);
         S.valid[g] = 1;
         S.succ[g] = NONE;
     }
+}
+// expected walk length of a segment (its first gap stretch), to group similar walks in a wave
+__global__ void k_walk_keys(seg_tab S, const u32* __restrict__ ids, u32 cnt, u32* __restrict__ keys) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const seg_in si = S.sin[ids[t]];
+    const u32 ge = min(S.P[3 * si.p], si.lim);
+    keys[t] = ge > si.start ? ge - si.start : 0u;
 }
 __global__ void k_todo(seg_tab S, u32 nseg, u32* __restrict__ ids, u32* __restrict__ cnt) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1264,8 +1268,19 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
             k_todo<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, ids, d_cnt);
             const u32 ntodo = rd1(d_cnt, st);
+            const u32* wids = ids;
+            if (ntodo >= (1u << 16)) {  // sort the walks by expected length: less divergence per wave
+                u32* wk = g_wk.get(2ull * ntodo);
+                u32* ids2 = g_ids2.get(ntodo);
+                k_walk_keys<<<cdiv(ntodo, 256), 256, 0, st>>>(S, ids, ntodo, wk);
+                size_t tb = 0;
+                LZ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, wk, wk + ntodo, ids, ids2, (int)ntodo, 0, 32, st));
+                u8* t = scan_tmp.get(tb);
+                LZ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(t, tb, wk, wk + ntodo, ids, ids2, (int)ntodo, 0, 32, st));
+                wids = ids2;
+            }
             if (ntodo) {
-                k_walk<false><<<cdiv(ntodo, 64), 64, 0, st>>>(W, S, ids, ntodo, nullptr, nullptr);
+                k_walk<false><<<cdiv(ntodo, 64), 64, 0, st>>>(W, S, wids, ntodo, nullptr, nullptr);
                 LZ_HIP(hipGetLastError());
                 walked_total += ntodo;
             }
