@@ -157,6 +157,10 @@ def main():
     F = sess.factors(z)
     t_out = time.perf_counter() - t_out0
     del F
+    # device decode of the same factors, compared in HBM with the input (outside the timed region)
+    _, mism = sess.decode(out=False)
+    dec_ms = sess.phase_times().get("decode", float("nan"))
+    dec_rounds = sess.stats()[18]
 
     if rank == 0:
         avg_ms = sum(kern_ms) / len(kern_ms)
@@ -185,6 +189,8 @@ def main():
                 "lpf_phrases": int(st[2]) if st else None,
                 "phase_ms": {k: round(v, 3) for k, v in phases.items()},
                 "pcie_inclusive_mbps": round(n / (dt + t_load + t_out) / 1e6, 2),
+                "device_decode": {"mismatches": int(mism), "ms": round(dec_ms, 3), "jump_rounds": int(dec_rounds),
+                                  "mbps": round(n / (dec_ms * 1e-3) / 1e6, 1)},
             },
             "roofline": {
                 "kernel": "k_sss_tile",

@@ -85,6 +85,11 @@ int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_
 /* Decode nf factors into out[0..n) (host memory), algorithms/common.cpp:31-54. */
 int lz77sss_decode_u32(const lz77sss_factor32* factors, uint64_t nf, uint8_t* out, uint64_t n);
 
+/* Same, decoded on `device` (csrc/decode.hip: pointer jumping over source
+ * references, O(n log depth) work).  Stricter than the host decode: the factor
+ * lengths must sum to exactly n. */
+int lz77sss_decode_u32_device(const lz77sss_factor32* factors, uint64_t nf, uint8_t* out, uint64_t n, int device);
+
 /* ---- device-resident session (text stays in HBM across calls) ---- */
 typedef struct lz77sss_session lz77sss_session;
 
@@ -96,6 +101,11 @@ int lz77sss_session_load(lz77sss_session* s, const uint8_t* text, uint64_t n);
 int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_params* prm, uint64_t* num_factors);
 /* Copies the factors HBM -> host (cap >= num_factors). */
 int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32* out, uint64_t cap);
+/* Decodes the factors of the last factorize call on the device.  out (host,
+ * cap >= n) may be NULL; when mismatches is given it receives the number of
+ * positions where the decoded text differs from the loaded one (0 = round trip
+ * holds), without leaving HBM.  Timed as phase "decode". */
+int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* mismatches);
 /* Runs only the string-synchronizing-set pass (kernel 1) on the loaded text. */
 int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs);
 /* Copies the sync set of the last sss/factorize call HBM -> host. */

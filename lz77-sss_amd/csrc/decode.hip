@@ -1,0 +1,135 @@
+// decode.hip -- LZ77 decode on the device (the host
+// decode is lz77_sss<>::decode, algorithms/common.cpp:31-54).
+//
+// Position p of the output is covered by factor fid[p] (starts scattered, then
+// a max-scan).  A literal position resolves to itself; a copied position points
+// at its source src + (p - start) < p.  Pointer jumping on these references
+// reaches a literal in ceil(log2(chain depth)) rounds; the byte is that
+// literal's factor source.  Runs of self-overlapping copies (dist 1) give the
+// deepest chains: 30 rounds for a 1 GiB run.
+#include "../../include/lz77sss.h"
+#include "../include/engine.h"
+
+#include <hipcub/hipcub.hpp>
+
+namespace lz {
+
+__global__ void k_dec_lens(const u32* __restrict__ F, u64 nf, u32* __restrict__ len) {
+    const u64 f = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < nf) len[f] = F[2 * f + 1] ? F[2 * f + 1] : 1u;
+}
+__global__ void k_dec_heads(const u32* __restrict__ start, u64 nf, u64 n, u32* __restrict__ head) {
+    const u64 f = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < nf && start[f] < n) head[start[f]] = (u32)f;
+}
+struct max_u32 {
+    __device__ __forceinline__ u32 operator()(const u32& a, const u32& b) const { return a > b ? a : b; }
+};
+// ref[p]: p for literals, the source position for copies; err on a forward reference
+__global__ void k_dec_refs(const u32* __restrict__ F, const u32* __restrict__ start, const u32* __restrict__ fid, u64 n,
+                           u32* __restrict__ ref, u32* __restrict__ err) {
+    const u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const u32 f = fid[p];
+    const u32 len = F[2 * (u64)f + 1];
+    if (len == 0) { ref[p] = (u32)p; return; }
+    const u64 r = (u64)F[2 * (u64)f] + (p - start[f]);
+    if (r >= p) { atomicOr(err, 1u); ref[p] = (u32)p; return; }
+    ref[p] = (u32)r;
+}
+// one pointer-jumping round.  Grid-stride over a fixed grid so that the change
+// flag costs one atomic per block: millions of same-address atomics (even one
+// per wave) serialize at ~10 ns each.
+constexpr unsigned DEC_GRID = 4096;
+__global__ void __launch_bounds__(256) k_dec_jump(const u32* __restrict__ ref, u64 n, u32* __restrict__ out,
+                                                  u32* __restrict__ changed) {
+    __shared__ u32 any;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    bool ch = false;
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+    u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; p + 3 * stride < n; p += 4 * stride) {  // 4 independent gathers in flight per lane
+        u32 r[4], rr[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) r[k] = ref[p + k * stride];
+#pragma unroll
+        for (int k = 0; k < 4; k++) rr[k] = ref[r[k]];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            out[p + k * stride] = rr[k];
+            ch |= rr[k] != r[k];
+        }
+    }
+    for (; p < n; p += stride) {
+        const u32 r = ref[p];
+        const u32 rr = ref[r];
+        out[p] = rr;
+        ch |= rr != r;
+    }
+    if (ch) any = 1;
+    __syncthreads();
+    if (threadIdx.x == 0 && any) atomicOr(changed, 1u);
+}
+__global__ void k_dec_bytes(const u32* __restrict__ F, const u32* __restrict__ fid, const u32* __restrict__ ref, u64 n,
+                            const u8* __restrict__ cmp, u8* __restrict__ out, u32* __restrict__ mism) {
+    const u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const u8 c = (u8)F[2 * (u64)fid[ref[p]]];
+    if (out) out[p] = c;
+    if (cmp && cmp[p] != c) atomicAdd(mism, 1u);  // only on a failed round trip
+}
+
+// decodes nf factors (device array, 2 x u32 each) of a text of length n; writes
+// the text to out (device, may be null) and, when cmp is given, counts the
+// positions where it differs from cmp.  Returns the mismatch count, or throws
+// on an invalid stream (lengths not summing to n, forward references).
+u64 engine::decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cmp) {
+    if (n_out == 0) {
+        if (nf) throw error(LZ77SSS_EINVAL, "factors for an empty text");
+        return 0;
+    }
+    if (nf == 0 || nf > n_out) throw error(LZ77SSS_EINVAL, "factor count does not fit the text length");
+    if (n_out > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
+    u32* len = dec_len.get(nf + 1);
+    u32* start = dec_start.get(nf + 1);
+    k_dec_lens<<<cdiv(nf, 256), 256, 0, st>>>(F, nf, len);
+    LZ_HIP(hipMemsetAsync(len + nf, 0, 4, st));
+    {
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len, start, (int)(nf + 1), st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, len, start, (int)(nf + 1), st));
+    }
+    if (rd1(start + nf, st) != n_out) throw error(LZ77SSS_EINVAL, "factor lengths do not sum to n");
+    u32* head = dec_fid.get(n_out);
+    u32* fid = dec_ref2.get(n_out);
+    LZ_HIP(hipMemsetAsync(head, 0, n_out * 4, st));
+    k_dec_heads<<<cdiv(nf, 256), 256, 0, st>>>(start, nf, n_out, head);
+    {
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, head, fid, max_u32{}, (int)n_out, st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, head, fid, max_u32{}, (int)n_out, st));
+    }
+    u32* ref = dec_ref.get(n_out);
+    u32* ref2 = head;  // free after the scan
+    u32* flags = counters.get(16);
+    LZ_HIP(hipMemsetAsync(flags, 0, 8, st));
+    k_dec_refs<<<cdiv(n_out, 256), 256, 0, st>>>(F, start, fid, n_out, ref, flags);
+    if (rd1(flags, st)) throw error(LZ77SSS_EINVAL, "factor source not before its position");
+    dec_rounds = 0;
+    for (int round = 0; round < 40; round++) {
+        dec_rounds++;
+        LZ_HIP(hipMemsetAsync(flags + 1, 0, 4, st));
+        k_dec_jump<<<std::min<u64>(cdiv(n_out, 256), DEC_GRID), 256, 0, st>>>(ref, n_out, ref2, flags + 1);
+        std::swap(ref, ref2);
+        if (!rd1(flags + 1, st)) break;
+    }
+    LZ_HIP(hipMemsetAsync(flags + 2, 0, 4, st));
+    k_dec_bytes<<<cdiv(n_out, 256), 256, 0, st>>>(F, fid, ref, n_out, cmp, out, flags + 2);
+    LZ_HIP(hipGetLastError());
+    return cmp ? rd1(flags + 2, st) : 0;
+}
+
+}  // namespace lz

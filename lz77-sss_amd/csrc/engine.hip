@@ -190,6 +190,24 @@ LZ77SSS_API int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32
     });
 }
 
+// decode on the device: the factors of the last factorize call (already in HBM)
+LZ77SSS_API int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* mismatches) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        lz::engine& E = s->E;
+        LZ_HIP(hipSetDevice(E.device));
+        if (out && cap < E.n) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        lz::u8* d_out = out && E.n ? E.dec_out.get(E.n) : nullptr;
+        E.timer.begin(E.st);
+        const uint64_t bad = E.decode_device(E.fact.p, E.num_fact, E.n, d_out, mismatches ? E.d_text : nullptr);
+        E.timer.mark("decode");
+        if (E.stats.size() > 18) E.stats[18] = E.dec_rounds;
+        if (mismatches) *mismatches = bad;
+        if (d_out) LZ_HIP(hipMemcpyAsync(out, d_out, E.n, hipMemcpyDeviceToHost, E.st));
+        LZ_HIP(hipStreamSynchronize(E.st));
+    });
+}
+
 LZ77SSS_API int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
@@ -292,6 +310,26 @@ LZ77SSS_API int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, co
             }
         }
     }
+    lz77sss_session_destroy(s);
+    return rc;
+}
+
+// decode on a device: upload, pointer-jumping decode (csrc/decode.hip), download
+LZ77SSS_API int lz77sss_decode_u32_device(const lz77sss_factor32* f, uint64_t nf, uint8_t* out, uint64_t n,
+                                          int device) {
+    if ((!f && nf) || (!out && n)) return LZ77SSS_EINVAL;
+    lz77sss_session* s = nullptr;
+    int rc = lz77sss_session_create(device, n, &s);
+    if (rc) return rc;
+    rc = guarded([&] {
+        lz::engine& E = s->E;
+        lz::u32* F = E.fact.get(2 * nf + 2);
+        if (nf) LZ_HIP(hipMemcpyAsync(F, f, nf * sizeof(lz77sss_factor32), hipMemcpyHostToDevice, E.st));
+        lz::u8* d_out = n ? E.dec_out.get(n) : nullptr;
+        E.decode_device(F, nf, n, d_out, nullptr);
+        if (n) LZ_HIP(hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, E.st));
+        LZ_HIP(hipStreamSynchronize(E.st));
+    });
     lz77sss_session_destroy(s);
     return rc;
 }

@@ -575,13 +575,15 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
 // phrase statistics (approximate/common.cpp:98-157, p = 1)
 __global__ void k_phrase_info(const u32* __restrict__ P, u32 m, u32 n, u32* __restrict__ acc) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m) return;
-    const u32 b = P[3 * k], e = P[3 * k + 1];
-    atomicAdd(&acc[0], e - b);
-    u32 gaps = 0;
-    if (k == 0 ? b > 0 : b > P[3 * (k - 1) + 1]) gaps++;
-    if (k == m - 1 && e < n) gaps++;
-    if (gaps) atomicAdd(&acc[1], gaps);
+    u32 len = 0, gaps = 0;
+    if (k < m) {
+        const u32 b = P[3 * k], e = P[3 * k + 1];
+        len = e - b;
+        if (k == 0 ? b > 0 : b > P[3 * (k - 1) + 1]) gaps++;
+        if (k == m - 1 && e < n) gaps++;
+    }
+    block_add(&acc[0], len);
+    block_add(&acc[1], gaps);
 }
 
 // ---------------------------------------------------------------------------
@@ -844,8 +846,9 @@ __global__ void k_walk_keys(seg_tab S, const u32* __restrict__ ids, u32 cnt, u32
 }
 __global__ void k_todo(seg_tab S, u32 nseg, u32* __restrict__ ids, u32* __restrict__ cnt) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= nseg || S.valid[g]) return;
-    ids[atomicAdd(cnt, 1u)] = (u32)g;
+    const bool todo = g < nseg && !S.valid[g];
+    const u32 slot = block_count_claim(cnt, todo);
+    if (todo) ids[slot] = (u32)g;
 }
 // claim the segment starting at x (created by this thread iff *mine)
 __device__ u32 seg_claim(const seg_tab& S, u32 x, bool& mine) {
@@ -1005,7 +1008,7 @@ __global__ void k_put3(u32* p, u32 a, u32 b, u32 c) {
 }
 __global__ void k_sum_u8(const u8* __restrict__ f, u64 m, u32* __restrict__ acc) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < m && !f[k]) atomicAdd(acc, 1u);
+    block_add(acc, k < m && !f[k] ? 1u : 0u);
 }
 // exclusive scan of cnt[0..m) into off[0..m] (off[m] = total); cnt needs m+1 entries
 template <class T>

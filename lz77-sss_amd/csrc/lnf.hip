@@ -219,7 +219,7 @@ __global__ void k_window_terms(const u32* __restrict__ chain, const u32* __restr
 }
 __global__ void k_first_ge_end0(const u32* __restrict__ Q, u32 p, u32* __restrict__ out) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 1 && t < p && Q[3 * t + 1] >= Q[1]) atomicMin(out, (u32)t);
+    block_min(out, t >= 1 && t < p && Q[3 * t + 1] >= Q[1] ? (u32)t : 0xFFFFFFFFu);
 }
 // trimmed output phrases along the selection chain
 __global__ void k_select_emit(const u32* __restrict__ Q, const u32* __restrict__ chain, u32 len,

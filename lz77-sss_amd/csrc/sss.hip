@@ -120,56 +120,66 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
         s_p[slot] = (x == 0 && t0 == 0) || tn >= nanch ? 0 : (u8)period_of(tn * QA);
     }
     __syncthreads();
-    const u64 t = t0 + threadIdx.x;
-    if (threadIdx.x >= QT_ANCH || t >= nanch) return;
-    const u64 a = t * QA;
-    u16 res = 0xFF00;  // empty interval
-    u32 rp = 0, rhi = 0, rlo = 0;
-    u8 rcap = 0;
-    const u32 p = s_p[threadIdx.x + 1];
-    if (p) {
-        // neighbours with the same period: their windows overlap this one by >= 212 >= p
-        // bytes, so the union is p-periodic and the extensions are known without scanning
-        const bool contb = s_p[threadIdx.x] == p, contf = s_p[threadIdx.x + 2] == p;
-        const bool contf2 = contf && s_p[threadIdx.x + 3] == p;
-        const u64 hi_cap = min(a + TAU - p, n - p), lo_cap = a >= 127 ? a - 127 : 0;
-        const u64 hi = contf2 ? hi_cap : ext_fwd(a + QM - p, hi_cap, p);
-        const u64 lo = contb ? lo_cap : ext_bwd(a, lo_cap, p);
-        // Q on (a-128, a]: j >= lo, j + tau - p <= hi, j <= n - tau
-        int64_t jlo = (int64_t)lo;
-        int64_t jhi = min((int64_t)a, (int64_t)hi + (int64_t)p - (int64_t)TAU);
-        jhi = min(jhi, (int64_t)n - (int64_t)TAU);
-        if (jlo <= jhi) {
-            int64_t r0 = (int64_t)a - 127;  // rel(j) = j - r0 in [0,127]
-            res = (u16)(((jlo - r0) << 8) | (jhi - r0));
-            atomicOr(any_q, 1u);
+    __shared__ u32 s_anyq;
+    auto q_anchor_body = [&](const u64 t) {
+        const u64 a = t * QA;
+        u16 res = 0xFF00;  // empty interval
+        u32 rp = 0, rhi = 0, rlo = 0;
+        u8 rcap = 0;
+        const u32 p = s_p[threadIdx.x + 1];
+        if (p) {
+            // neighbours with the same period: their windows overlap this one by >= 212 >= p
+            // bytes, so the union is p-periodic and the extensions are known without scanning
+            const bool contb = s_p[threadIdx.x] == p, contf = s_p[threadIdx.x + 2] == p;
+            const bool contf2 = contf && s_p[threadIdx.x + 3] == p;
+            const u64 hi_cap = min(a + TAU - p, n - p), lo_cap = a >= 127 ? a - 127 : 0;
+            const u64 hi = contf2 ? hi_cap : ext_fwd(a + QM - p, hi_cap, p);
+            const u64 lo = contb ? lo_cap : ext_bwd(a, lo_cap, p);
+            // Q on (a-128, a]: j >= lo, j + tau - p <= hi, j <= n - tau
+            int64_t jlo = (int64_t)lo;
+            int64_t jhi = min((int64_t)a, (int64_t)hi + (int64_t)p - (int64_t)TAU);
+            jhi = min(jhi, (int64_t)n - (int64_t)TAU);
+            if (jlo <= jhi) {
+                int64_t r0 = (int64_t)a - 127;  // rel(j) = j - r0 in [0,127]
+                res = (u16)(((jlo - r0) << 8) | (jhi - r0));
+                s_anyq = 1;
+            }
+            // local extent of the p-periodic run around the window (for run-skipping LCE);
+            // inside a chain of same-period anchors the values only need to mark the chain
+            rp = p;
+            if (contf) {
+                rhi = (u32)(a + RUN_HCAP);
+                rcap |= 1;
+            } else {
+                const u64 h2_cap = min(a + RUN_HCAP - p, n - p);
+                const u64 h2 = hi < hi_cap ? hi : ext_fwd(hi, h2_cap, p);
+                rhi = (u32)(h2 + p);
+                rcap |= h2 == a + RUN_HCAP - p ? 1 : 0;
+            }
+            if (contb) {
+                rlo = (u32)(a >= RUN_LCAP ? a - RUN_LCAP : a - QA);
+                rcap |= 2;
+            } else {
+                const u64 l2 = (lo > lo_cap) ? lo : ext_bwd(lo, a >= RUN_LCAP ? a - RUN_LCAP : 0, p);
+                rlo = (u32)l2;
+                rcap |= (l2 == a - RUN_LCAP && a >= RUN_LCAP) ? 2 : 0;
+            }
         }
-        // local extent of the p-periodic run around the window (for run-skipping LCE);
-        // inside a chain of same-period anchors the values only need to mark the chain
-        rp = p;
-        if (contf) {
-            rhi = (u32)(a + RUN_HCAP);
-            rcap |= 1;
-        } else {
-            const u64 h2_cap = min(a + RUN_HCAP - p, n - p);
-            const u64 h2 = hi < hi_cap ? hi : ext_fwd(hi, h2_cap, p);
-            rhi = (u32)(h2 + p);
-            rcap |= h2 == a + RUN_HCAP - p ? 1 : 0;
-        }
-        if (contb) {
-            rlo = (u32)(a >= RUN_LCAP ? a - RUN_LCAP : a - QA);
-            rcap |= 2;
-        } else {
-            const u64 l2 = (lo > lo_cap) ? lo : ext_bwd(lo, a >= RUN_LCAP ? a - RUN_LCAP : 0, p);
-            rlo = (u32)l2;
-            rcap |= (l2 == a - RUN_LCAP && a >= RUN_LCAP) ? 2 : 0;
-        }
+        qinfo[t] = res;
+        run_p[t] = (u8)rp;
+        run_hi[t] = rhi;
+        run_lo[t] = rlo;
+        run_cap[t] = rcap;
+    };
+    if (threadIdx.x == 0) s_anyq = 0;
+    __syncthreads();
+    {
+        const u64 t = t0 + threadIdx.x;
+        if (threadIdx.x < QT_ANCH && t < nanch) q_anchor_body(t);
     }
-    qinfo[t] = res;
-    run_p[t] = (u8)rp;
-    run_hi[t] = rhi;
-    run_lo[t] = rlo;
-    run_cap[t] = rcap;
+    __syncthreads();
+    // one atomic per block: same-address atomics from every anchor serialize
+    if (threadIdx.x == 0 && s_anyq) atomicOr(any_q, 1u);
 }
 
 // run chains: anchor t continues into t+1 (same run) when both have period p

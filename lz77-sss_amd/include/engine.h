@@ -135,6 +135,10 @@ struct engine {
     dbuf<u32> g_predk, g_wk, g_ids2;
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
     dbuf<u64> g_xk, g_xk2;
+    // device decode (csrc/decode.hip)
+    dbuf<u32> dec_len, dec_start, dec_fid, dec_ref, dec_ref2;
+    dbuf<u8> dec_out;
+    u32 dec_rounds = 0;
     u64 num_fact = 0;
     std::vector<u64> stats;
 
@@ -154,6 +158,7 @@ struct engine {
     void path_marks(u32 m, u32* nxt0, u32* marks);
     u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override);
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log);
+    u64 decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
     lce_view view(const u8* T) const;
 };
 

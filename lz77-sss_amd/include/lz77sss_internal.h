@@ -43,6 +43,56 @@ inline bool debug_enabled() {
     return v == 1;
 }
 
+// Block-aggregated counters.  The compiler already folds a uniform-address
+// atomic into one per wave, but a device-scope atomic still costs ~10 ns and
+// same-address ones serialize: a kernel with millions of waves pays seconds
+// (the first decode: 16M wave atomics, 190 ms per round).  These helpers issue
+// one atomic per workgroup; every thread of the block must call them.
+// Needs blockDim.x <= 1024.
+__device__ inline u32 block_count_claim(u32* ctr, bool pred) {
+    __shared__ u32 s_wc[16], s_base;
+    const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    const u64 m = __ballot(pred);
+    if (lane == 0) s_wc[wv] = (u32)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u32 tot = 0;
+        for (u32 w = 0; w < nw; w++) {
+            const u32 c = s_wc[w];
+            s_wc[w] = tot;
+            tot += c;
+        }
+        s_base = tot ? atomicAdd(ctr, tot) : 0;
+    }
+    __syncthreads();
+    const u32 r = s_base + s_wc[wv] + (u32)__popcll(m & ((1ull << lane) - 1));
+    __syncthreads();  // s_wc / s_base reusable by a following call
+    return r;
+}
+// adds v (per thread) to *acc with one atomic per workgroup
+__device__ inline void block_add(u32* acc, u32 v) {
+    __shared__ u32 s_sum;
+    if (threadIdx.x == 0) s_sum = 0;
+    __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&s_sum, v);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_sum) atomicAdd(acc, s_sum);
+    __syncthreads();
+}
+
+// *acc = min(*acc, v over the block) with one atomic per workgroup
+__device__ inline void block_min(u32* acc, u32 v) {
+    __shared__ u32 s_min;
+    if (threadIdx.x == 0) s_min = 0xFFFFFFFFu;
+    __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (u32)__shfl_down(v, o, 64));
+    if ((threadIdx.x & 63) == 0 && v != 0xFFFFFFFFu) atomicMin(&s_min, v);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_min != 0xFFFFFFFFu) atomicMin(acc, s_min);
+    __syncthreads();
+}
+
 struct error : std::runtime_error {
     int code;
     error(int c, const std::string& m) : std::runtime_error(m), code(c) {}

@@ -45,6 +45,8 @@ _SYMBOLS = {
     "lz77sss_default_params": (None, [ctypes.POINTER(Params)]),
     "lz77sss_factorize_approx_u32": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), _P, _P]),
     "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
+    "lz77sss_decode_u32_device": (ctypes.c_int, [_P, _U64, _P, _U64, ctypes.c_int]),
+    "lz77sss_session_decode": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_create": (ctypes.c_int, [ctypes.c_int, _U64, ctypes.POINTER(_P)]),
     "lz77sss_session_load": (ctypes.c_int, [_P, _P, _U64]),
     "lz77sss_session_factorize": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.POINTER(_U64)]),
@@ -152,6 +154,15 @@ class Session:
         _check(load_library().lz77sss_session_get_factors(self._h, out.ctypes.data_as(_P), z))
         return out[:z]
 
+    def decode(self, out: bool = True, verify: bool = True):
+        """Decodes the last factorization on the device (csrc/decode.hip).
+        Returns (text or None, mismatches vs the loaded text or None)."""
+        buf = np.empty(max(self.n, 1), np.uint8) if out else None
+        m = _U64()
+        _check(load_library().lz77sss_session_decode(self._h, buf.ctypes.data_as(_P) if out else None,
+                                                     self.n if out else 0, ctypes.byref(m) if verify else None))
+        return (buf[:self.n] if out else None), (m.value if verify else None)
+
     def sss(self):
         s, r = _U64(), ctypes.c_int()
         _check(load_library().lz77sss_session_sss(self._h, ctypes.byref(s), ctypes.byref(r)))
@@ -210,6 +221,15 @@ def decode(factors: np.ndarray, n: int) -> np.ndarray:
     f = np.ascontiguousarray(factors, dtype=np.uint32)
     out = np.empty(max(n, 1), np.uint8)
     _check(load_library().lz77sss_decode_u32(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P), n))
+    return out[:n]
+
+
+def decode_device(factors: np.ndarray, n: int, device: int = 0) -> np.ndarray:
+    """Same as decode, on the device (pointer jumping, csrc/decode.hip)."""
+    f = np.ascontiguousarray(factors, dtype=np.uint32).reshape(-1, 2)
+    out = np.empty(max(n, 1), np.uint8)
+    _check(load_library().lz77sss_decode_u32_device(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P), n,
+                                                     device))
     return out[:n]
 
 

@@ -151,6 +151,8 @@ def test_one_gib_properties(session, orc, lz, kind):
     s, F = run(session, T)
     _check_valid(T, F)
     assert np.array_equal(lz.decode(F, n), T)
+    _, mism = s.decode(out=False)  # device decode compared in HBM with the loaded text
+    assert mism == 0
     st = s.stats()
     assert st[0] <= 2 * n // 512 + 1024
     if kind == "rr":  # the oracle finishes this one in seconds
@@ -196,3 +198,61 @@ def test_medium_lpf_lnf_vs_oracle(session, orc, lz, kind, mib):
     _, F = run(session, T, phr_mode=3)
     F_ref, _ = orc.factorize(T, phr_mode=3)
     assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
+# ---- device decode (csrc/decode.hip) vs the reference's sequential decode (algorithms/common.cpp:31-54)
+
+@pytest.mark.parametrize("name", golden_names())
+def test_device_decode_golden(lz, name):
+    g = load_golden(name)
+    T, F = g["text"], g["factors"]
+    assert np.array_equal(lz.decode_device(F, T.size), T)
+
+
+def _deep_chain_stream(n):
+    """'a' then one self-overlapping copy (src 0): every position's chain has depth p."""
+    return np.array([[ord("a"), 0], [0, n - 1]], np.uint32)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 1 << 20, (1 << 24) + 7])
+def test_device_decode_deep_chains(lz, n):
+    F = _deep_chain_stream(n) if n > 1 else np.array([[ord("a"), 0]], np.uint32)
+    assert np.array_equal(lz.decode_device(F, n), np.full(n, ord("a"), np.uint8))
+    # period-3 run: literals x y z then a copy of distance 3
+    if n > 3:
+        F3 = np.array([[120, 0], [121, 0], [122, 0], [0, n - 3]], np.uint32)
+        assert np.array_equal(lz.decode_device(F3, n), np.resize(np.array([120, 121, 122], np.uint8), n))
+
+
+@pytest.mark.parametrize("seed", range(1, 9))
+def test_device_decode_session_roundtrip(session, lz, seed):
+    T = lz.gen_random_repetitive(50000, 400000, seed)
+    s, F = run(session, T)
+    D, mism = s.decode()
+    assert mism == 0 and np.array_equal(D, T)
+    assert np.array_equal(lz.decode_device(F, T.size), lz.decode(F, T.size))
+
+
+def test_device_decode_random_streams(lz):
+    """Arbitrary valid streams (not LZ77-greedy): random sources and lengths."""
+    rng = np.random.default_rng(3)
+    for n in [10, 1000, 100000]:
+        F, pos = [], 0
+        while pos < n:
+            if pos == 0 or rng.random() < 0.3:
+                F.append((int(rng.integers(0, 256)), 0)); pos += 1
+            else:
+                ln = int(min(n - pos, rng.integers(1, 2 * pos + 2)))
+                F.append((int(rng.integers(0, pos)), ln)); pos += ln
+        F = np.array(F, np.uint32)
+        assert np.array_equal(lz.decode_device(F, n), lz.decode(F, n))
+
+
+def test_device_decode_rejects_invalid(lz):
+    with pytest.raises(lz.Lz77SssError):  # forward reference
+        lz.decode_device(np.array([[97, 0], [1, 2]], np.uint32), 3)
+    with pytest.raises(lz.Lz77SssError):  # lengths do not sum to n
+        lz.decode_device(np.array([[97, 0], [0, 2]], np.uint32), 5)
+    with pytest.raises(lz.Lz77SssError):
+        lz.decode_device(np.array([[97, 0]], np.uint32), 0)
+    assert lz.decode_device(np.zeros((0, 2), np.uint32), 0).size == 0
