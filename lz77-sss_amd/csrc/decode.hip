@@ -5,8 +5,9 @@
 // a max-scan).  A literal position resolves to itself; a copied position points
 // at its source src + (p - start) < p.  Pointer jumping on these references
 // reaches a literal in ceil(log2(chain depth)) rounds; the byte is that
-// literal's factor source.  Runs of self-overlapping copies (dist 1) give the
-// deepest chains: 30 rounds for a 1 GiB run.
+// literal's factor source.  Self-overlapping copies are folded into their first
+// period, so every reference leaves its factor and the depth is counted in
+// factors, not positions.
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
 
@@ -33,9 +34,14 @@ __global__ void k_dec_refs(const u32* __restrict__ F, const u32* __restrict__ st
     const u32 f = fid[p];
     const u32 len = F[2 * (u64)f + 1];
     if (len == 0) { ref[p] = (u32)p; return; }
-    const u64 r = (u64)F[2 * (u64)f] + (p - start[f]);
-    if (r >= p) { atomicOr(err, 1u); ref[p] = (u32)p; return; }
-    ref[p] = (u32)r;
+    const u32 src = F[2 * (u64)f], st = start[f];
+    if (src >= st) { atomicOr(err, 1u); ref[p] = (u32)p; return; }  // only on an invalid stream
+    // a self-overlapping copy (distance d < len) is d-periodic: fold the offset
+    // into the first period so the reference lands before the factor start
+    const u32 d = st - src;
+    u32 off = (u32)(p - st);
+    if (off >= d) off %= d;
+    ref[p] = src + off;
 }
 // one pointer-jumping round.  Grid-stride over a fixed grid so that the change
 // flag costs one atomic per block: millions of same-address atomics (even one

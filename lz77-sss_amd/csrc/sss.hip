@@ -24,75 +24,112 @@
 namespace lz {
 
 // ---------------------------------------------------------------------------
-// Q anchors
-constexpr int QT_ANCH = 128;                 // anchors per workgroup
-constexpr int QT_SPAN = QT_ANCH * QA;        // 16384 positions
-constexpr int QT_LDS = QT_SPAN + 256 + 1024; // [A0-256, A0+16384+1024)
-constexpr u32 RUN_HCAP = 640;                // local run extension: [a-256, a+640)
+// Q anchors.  A workgroup of 256 lanes covers anchors tb-1 .. tb+254 (lane i ->
+// anchor tb-1+i) and owns tb .. tb+252; the three halo anchors give the owned
+// ones their neighbours' periods.  Text [a(tb-1) - 256, a(tb+254) + 1024) is
+// staged in LDS.
+constexpr int QT_THREADS = 256;
+constexpr int QT_OWN = QT_THREADS - 3;                  // owned anchors per workgroup
+constexpr int QT_LDS = QT_THREADS * (int)QA + 256 + 1024;
+constexpr u32 RUN_HCAP = 640;                           // local run extension: [a-256, a+640)
 constexpr u32 RUN_LCAP = 256;
 
-constexpr int QT_THREADS = QT_ANCH + 64;     // + one wave for the neighbour anchors
 __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__ T, u64 n, u64 nanch,
-                                                   u16* __restrict__ qinfo, u32* __restrict__ any_q,
-                                                   u8* __restrict__ run_p, u32* __restrict__ run_hi,
-                                                   u32* __restrict__ run_lo, u8* __restrict__ run_cap) {
+                                                          u16* __restrict__ qinfo, u32* __restrict__ any_q,
+                                                          u8* __restrict__ run_p, u32* __restrict__ run_hi,
+                                                          u32* __restrict__ run_lo, u8* __restrict__ run_cap) {
     // LDS text with one pad word per 128 bytes: the anchors of a wave sit 128 bytes
     // apart, so unpadded their accesses would all hit the same bank
     __shared__ __attribute__((aligned(16))) u32 b32[QT_LDS / 4 + QT_LDS / 128 + 2];
-    const u64 A0 = (u64)blockIdx.x * QT_SPAN;
-    const int64_t base = (int64_t)A0 - 256;
-    for (int x = threadIdx.x * 16; x < QT_LDS; x += QT_THREADS * 16) {
-        int64_t g = base + x;
-        uint4 v = {0, 0, 0, 0};
-        if (g >= 0 && (u64)g + 16 <= n + TEXT_PAD) v = *(const uint4*)(T + g);
-        const int w = (x >> 2) + (x >> 7);
-        b32[w] = v.x;
-        b32[w + 1] = v.y;
-        b32[w + 2] = v.z;
-        b32[w + 3] = v.w;
+    __shared__ u8 s_p1[QT_THREADS], s_c[QT_THREADS], s_p[QT_THREADS];
+    __shared__ u32 s_anyq;
+    const int i = (int)threadIdx.x;
+    const int64_t tb = (int64_t)blockIdx.x * QT_OWN;
+    const int64_t base = (tb - 1) * (int64_t)QA - 256;  // LDS offset 0
+    {
+        // all global loads first (one round trip), then the LDS writes.  Loads are
+        // unconditional: out-of-range lanes read the zero padding at T + n (a guarded
+        // or zeroed load becomes a branch with its own s_waitcnt)
+        constexpr int NL = (QT_THREADS * (int)QA) / (QT_THREADS * 16);  // 8 full rounds
+        constexpr int TAIL = QT_LDS - NL * QT_THREADS * 16;              // 1280 bytes
+        static_assert(TAIL > 0 && TAIL <= QT_THREADS * 16, "one tail round");
+        auto src = [&](int x) -> const uint4* {
+            const int64_t g = base + x;
+            const bool okr = g >= 0 && (u64)g + 16 <= n + TEXT_PAD;
+            return (const uint4*)(T + (okr ? (u64)g : n));
+        };
+        uint4 v[NL + 1];
+#pragma unroll
+        for (int r = 0; r < NL; r++) v[r] = *src(i * 16 + r * QT_THREADS * 16);
+        v[NL] = *src(i * 16 < TAIL ? NL * QT_THREADS * 16 + i * 16 : -(1 << 20));
+        auto put = [&](int x, uint4 q) {
+            const int w = (x >> 2) + (x >> 7);
+            b32[w] = q.x;
+            b32[w + 1] = q.y;
+            b32[w + 2] = q.z;
+            b32[w + 3] = q.w;
+        };
+#pragma unroll
+        for (int r = 0; r < NL; r++) put(i * 16 + r * QT_THREADS * 16, v[r]);
+        if (i * 16 < TAIL) put(NL * QT_THREADS * 16 + i * 16, v[NL]);
     }
+    if (i == 0) s_anyq = 0;
     __syncthreads();
-    auto word = [&](int64_t w) -> u32 { return b32[w + (w >> 5)]; };
-    auto byte = [&](int64_t x) -> u32 { return (word(x >> 2) >> (8 * (x & 3))) & 255u; };
-    __shared__ u8 s_p[QT_ANCH + 3];  // s_p[i]: period of anchor blockIdx*QT_ANCH - 1 + i
-    // 4 bytes at any LDS offset
-    auto w32 = [&](int64_t o) -> u32 {
-        const int64_t q = o >> 2;
-        return __builtin_amdgcn_alignbyte(word(q + 1), word(q), (u32)(o & 3));
-    };
-    // first q in [h, cap) with T[q] != T[q+p] (cap if none)
-    auto ext_fwd = [&](u64 h, u64 cap, u32 p) -> u64 {
-        while (h < cap) {
-            u32 d = w32((int64_t)h - base) ^ w32((int64_t)(h + p) - base);
-            const u64 rem = cap - h;
+    // LDS accessors on offsets o = position - base
+    auto word = [&](int w) -> u32 { return b32[w + (w >> 5)]; };
+    auto byte = [&](int o) -> u32 { return (word(o >> 2) >> (8 * (o & 3))) & 255u; };
+    // first o in [h, cap) with T[o] != T[o+p] (cap if none)
+    auto ext_fwd = [&](int h, int cap, int p) -> int {
+        for (; h < cap && (h & 3); h++)
+            if (byte(h) != byte(h + p)) return h;
+        int q = (h + p) >> 2;
+        const u32 sh = (u32)((h + p) & 3);
+        u32 lo = word(q);
+        for (; h < cap; h += 4) {
+            const u32 hi = word(q + 1);
+            u32 d = word(h >> 2) ^ __builtin_amdgcn_alignbyte(hi, lo, sh);
+            const int rem = cap - h;
             if (rem < 4) d &= (1u << (8 * rem)) - 1;
             if (d) return h + (__builtin_ctz(d) >> 3);
-            h += rem < 4 ? rem : 4;
+            lo = hi;
+            q++;
         }
         return cap;
     };
-    // smallest l in [cap, l0] with T[q] == T[q+p] for all q in [l, l0)
-    auto ext_bwd = [&](u64 l, u64 cap, u32 p) -> u64 {
-        while (l >= cap + 4) {
-            const u32 d = w32((int64_t)l - 4 - base) ^ w32((int64_t)(l - 4 + p) - base);
-            if (d) return l - 4 + ((31 - __builtin_clz(d)) >> 3) + 1;
-            l -= 4;
+    // smallest l' in [cap, l] with T[o] == T[o+p] for all o in [l', l)
+    auto ext_bwd = [&](int l, int cap, int p) -> int {
+        for (; l > cap && (l & 3); l--)
+            if (byte(l - 1) != byte(l - 1 + p)) return l;
+        if (l >= cap + 4) {
+            int q = (l - 4 + p) >> 2;
+            const u32 sh = (u32)((l + p) & 3);
+            u32 hi = word(q + 1);
+            for (; l >= cap + 4; l -= 4) {
+                const u32 lo = word(q);
+                const u32 d = word((l - 4) >> 2) ^ __builtin_amdgcn_alignbyte(hi, lo, sh);
+                if (d) return l - 4 + ((31 - __builtin_clz(d)) >> 3) + 1;
+                hi = lo;
+                q--;
+            }
         }
-        while (l > cap && byte((int64_t)l - 1 - base) == byte((int64_t)(l - 1 + p) - base)) l--;
+        for (; l > cap && byte(l - 1) == byte(l - 1 + p); l--) {
+        }
         return l;
     };
-    // smallest period p <= 170 of T[a..a+340) (0 if none): a 4-byte filter marks the
-    // candidates (uniform loop), then every lane verifies its own lowest pending
-    // candidate, so lanes with different periods verify concurrently
-    auto period_of = [&](u64 a) -> u32 {
-        if (a + QM > n) return 0;
-        const int la = (int)((int64_t)a - base);  // multiple of 4
-        const u32 w0 = word(la >> 2);
-        u32 cm[6] = {0, 0, 0, 0, 0, 0};  // bit pp-1
+
+    // ---- 1. candidate periods of the probe T[a..a+340): a 4-byte filter (fully
+    // unrolled: mask word and bit of each candidate are compile-time constants)
+    const int64_t t = tb - 1 + i;
+    const int oa = i * (int)QA + 256;  // LDS offset of the anchor
+    const u64 a = (u64)t * QA;
+    const bool probe_ok = t >= 0 && (u64)t < nanch && a + QM <= n;
+    u32 cm[6] = {0, 0, 0, 0, 0, 0};  // bit pp-1
+    if (probe_ok) {
+        const u32 w0 = word(oa >> 2);
         u32 dprev = w0;
-#pragma unroll 4
+#pragma unroll
         for (int k = 0; k <= (int)(QL / 4); k++) {
-            const u32 dnext = word((la >> 2) + k + 1);
+            const u32 dnext = word((oa >> 2) + k + 1);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const u32 pp = 4 * k + r;
@@ -101,46 +138,84 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
             }
             dprev = dnext;
         }
-        for (int wi = 0; wi < 6;) {
-            if (!cm[wi]) { wi++; continue; }
-            const u32 pp = 32 * wi + __builtin_ctz(cm[wi]) + 1;
-            if (ext_fwd(a + 4, a + QM - pp, pp) == a + QM - pp) return pp;
-            cm[wi] &= cm[wi] - 1;
-        }
-        return 0;
-    };
-    const u64 t0 = (u64)blockIdx.x * QT_ANCH;
-    if (threadIdx.x < QT_ANCH) {
-        const u64 tt = t0 + threadIdx.x;
-        s_p[threadIdx.x + 1] = tt < nanch ? (u8)period_of(tt * QA) : 0;
-    } else if (threadIdx.x < QT_ANCH + 3) {  // the anchor before the block and the two after it
-        const u32 x = threadIdx.x - QT_ANCH;
-        const u64 tn = x == 0 ? t0 - 1 : t0 + QT_ANCH + x - 1;
-        const u32 slot = x == 0 ? 0 : QT_ANCH + x;
-        s_p[slot] = (x == 0 && t0 == 0) || tn >= nanch ? 0 : (u8)period_of(tn * QA);
     }
+    u32 p1 = 0;
+    for (int wi = 0; wi < 6 && !p1; wi++)
+        if (cm[wi]) p1 = 32 * wi + __builtin_ctz(cm[wi]) + 1;
+    // ---- 2. shift-p1 agreement over the anchor's own 128 bytes; a probe that
+    // agrees over its whole chunk is verified from its two successors' chunks
+    // when they test the same shift (inside a run: every anchor), so each byte
+    // of a run is compared about once instead of 340/128 times
+    const int c = p1 ? ext_fwd(oa, oa + (int)QA, (int)p1) - oa : 0;
+    s_p1[i] = (u8)p1;
+    s_c[i] = (u8)c;
     __syncthreads();
-    __shared__ u32 s_anyq;
-    auto q_anchor_body = [&](const u64 t) {
-        const u64 a = t * QA;
+    u32 per = 0;
+    if (p1) {
+        const int need = (int)(QM - p1);  // bytes of the probe that must agree with shift p1
+        int f = -1;                       // first disagreement of shift p1 (offset from a), -1: none
+        if (c < min(need, (int)QA)) {
+            f = c;
+        } else {
+            const bool s1 = i + 1 < QT_THREADS && s_p1[i + 1] == p1;
+            const bool s2 = need <= 2 * (int)QA || (i + 2 < QT_THREADS && s_p1[i + 2] == p1);
+            if (s1 && s2) {
+                if (s_c[i + 1] < min(need - (int)QA, (int)QA)) f = (int)QA + s_c[i + 1];
+                else if (need > 2 * (int)QA && s_c[i + 2] < need - 2 * (int)QA) f = 2 * (int)QA + s_c[i + 2];
+            } else {
+                const int e = ext_fwd(oa + (int)QA, oa + need, (int)p1);
+                if (e < oa + need) f = e - oa;
+            }
+        }
+        if (f < 0) {
+            per = p1;
+        } else {
+            // p1 is the smallest candidate and T[a..a+f+p1) has period p1, so by
+            // Fine-Wilf a period pp <= f of the probe would share gcd(p1, pp) = p1
+            // with it, and every multiple of p1 up to f disagrees at f - pp + p1:
+            // only candidates pp > f remain (at run ends this skips ~85 full checks)
+            cm[(p1 - 1) >> 5] &= ~(1u << ((p1 - 1) & 31));
+            for (int wi = 0; wi < 6; wi++) {
+                const int lo = 32 * wi + 1;  // candidate of bit 0
+                if (f + 1 >= lo + 32) cm[wi] = 0;
+                else if (f + 1 > lo) cm[wi] &= ~0u << (f + 1 - lo);
+            }
+            for (int wi = 0; wi < 6 && !per;) {
+                if (!cm[wi]) {
+                    wi++;
+                    continue;
+                }
+                const u32 pp = 32 * wi + __builtin_ctz(cm[wi]) + 1;
+                if (ext_fwd(oa + 4, oa + (int)(QM - pp), (int)pp) == oa + (int)(QM - pp)) per = pp;
+                cm[wi] &= cm[wi] - 1;
+            }
+        }
+    }
+    s_p[i] = (u8)per;
+    __syncthreads();
+
+    // ---- 3. owned anchors: Q interval on (a-128, a] and the local run extent
+    if (i >= 1 && i <= QT_OWN && (u64)t < nanch) {
         u16 res = 0xFF00;  // empty interval
         u32 rp = 0, rhi = 0, rlo = 0;
         u8 rcap = 0;
-        const u32 p = s_p[threadIdx.x + 1];
+        const u32 p = per;
         if (p) {
             // neighbours with the same period: their windows overlap this one by >= 212 >= p
             // bytes, so the union is p-periodic and the extensions are known without scanning
-            const bool contb = s_p[threadIdx.x] == p, contf = s_p[threadIdx.x + 2] == p;
-            const bool contf2 = contf && s_p[threadIdx.x + 3] == p;
+            const bool contb = s_p[i - 1] == p, contf = s_p[i + 1] == p;
+            const bool contf2 = contf && s_p[i + 2] == p;
             const u64 hi_cap = min(a + TAU - p, n - p), lo_cap = a >= 127 ? a - 127 : 0;
-            const u64 hi = contf2 ? hi_cap : ext_fwd(a + QM - p, hi_cap, p);
-            const u64 lo = contb ? lo_cap : ext_bwd(a, lo_cap, p);
+            const int o_hicap = (int)((int64_t)hi_cap - base), o_locap = (int)((int64_t)lo_cap - base);
+            const int o_hi = contf2 ? o_hicap : ext_fwd(oa + (int)(QM - p), o_hicap, (int)p);
+            const int o_lo = contb ? o_locap : ext_bwd(oa, o_locap, (int)p);
+            const u64 hi = (u64)(base + o_hi), lo = (u64)(base + o_lo);
             // Q on (a-128, a]: j >= lo, j + tau - p <= hi, j <= n - tau
-            int64_t jlo = (int64_t)lo;
+            const int64_t jlo = (int64_t)lo;
             int64_t jhi = min((int64_t)a, (int64_t)hi + (int64_t)p - (int64_t)TAU);
             jhi = min(jhi, (int64_t)n - (int64_t)TAU);
             if (jlo <= jhi) {
-                int64_t r0 = (int64_t)a - 127;  // rel(j) = j - r0 in [0,127]
+                const int64_t r0 = (int64_t)a - 127;  // rel(j) = j - r0 in [0,127]
                 res = (u16)(((jlo - r0) << 8) | (jhi - r0));
                 s_anyq = 1;
             }
@@ -152,7 +227,7 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
                 rcap |= 1;
             } else {
                 const u64 h2_cap = min(a + RUN_HCAP - p, n - p);
-                const u64 h2 = hi < hi_cap ? hi : ext_fwd(hi, h2_cap, p);
+                const u64 h2 = hi < hi_cap ? hi : (u64)(base + ext_fwd(o_hi, (int)((int64_t)h2_cap - base), (int)p));
                 rhi = (u32)(h2 + p);
                 rcap |= h2 == a + RUN_HCAP - p ? 1 : 0;
             }
@@ -160,7 +235,8 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
                 rlo = (u32)(a >= RUN_LCAP ? a - RUN_LCAP : a - QA);
                 rcap |= 2;
             } else {
-                const u64 l2 = (lo > lo_cap) ? lo : ext_bwd(lo, a >= RUN_LCAP ? a - RUN_LCAP : 0, p);
+                const u64 l2_cap = a >= RUN_LCAP ? a - RUN_LCAP : 0;
+                const u64 l2 = (lo > lo_cap) ? lo : (u64)(base + ext_bwd(o_lo, (int)((int64_t)l2_cap - base), (int)p));
                 rlo = (u32)l2;
                 rcap |= (l2 == a - RUN_LCAP && a >= RUN_LCAP) ? 2 : 0;
             }
@@ -170,16 +246,10 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
         run_hi[t] = rhi;
         run_lo[t] = rlo;
         run_cap[t] = rcap;
-    };
-    if (threadIdx.x == 0) s_anyq = 0;
-    __syncthreads();
-    {
-        const u64 t = t0 + threadIdx.x;
-        if (threadIdx.x < QT_ANCH && t < nanch) q_anchor_body(t);
     }
     __syncthreads();
     // one atomic per block: same-address atomics from every anchor serialize
-    if (threadIdx.x == 0 && s_anyq) atomicOr(any_q, 1u);
+    if (i == 0 && s_anyq) atomicOr(any_q, 1u);
 }
 
 // run chains: anchor t continues into t+1 (same run) when both have period p
@@ -486,7 +556,7 @@ void engine::build_sss(const u8* T) {
     u32* rhi = run_hi.get(nanch);
     u32* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
-    k_q_anchors<<<cdiv(nanch, QT_ANCH), QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap);
+    k_q_anchors<<<cdiv(nanch, QT_OWN), QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap);
     LZ_HIP(hipGetLastError());
     {
         u64* ea = run_scan_a.get(2 * nanch);

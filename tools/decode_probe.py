@@ -1,8 +1,9 @@
 """Times the device decode (csrc/decode.hip) on a 1 GiB workload; run under rocprofv3 for per-kernel times."""
+import os
 import sys
 import time
 
-sys.path.insert(0, "lz77-sss_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lz77-sss_amd"))
 import lz77sss as lz  # noqa: E402
 
 kind = sys.argv[1] if len(sys.argv) > 1 else "rr"
