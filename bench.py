@@ -18,7 +18,7 @@ independent objects, one 1 GiB text per rank (seed 42 + rank); no data-path
 collective, the barrier/max-over-ranks timing only (weak scaling).
 
 Also reported:
-  roofline      the SSS kernel (k_sss_tile), algorithmic bytes n + 4|S| per
+  roofline      the SSS kernel (k_sss_stream), algorithmic bytes n + 4|S| per
                 launch over its HIP-event time on the library's own stream,
                 against the 8 TB/s HBM3E peak; ``traffic`` from the committed
                 rocprofv3 PMC summary (profiles/) when one exists for this
@@ -63,7 +63,7 @@ def aggregate(dt_local: float, n_per_rank: int, world: int, dist=None, device="c
 
 
 def pmc_traffic(workload: str, n: int):
-    """Per-launch HBM bytes of k_sss_tile from profiles/*_pmc_sss.json (rocprofv3 --pmc passes)."""
+    """Per-launch HBM bytes of k_sss_stream from profiles/*_pmc_sss.json (rocprofv3 --pmc passes)."""
     best = None
     for p in sorted((ROOT / "profiles").glob("*_pmc_sss.json")):
         try:
@@ -193,7 +193,7 @@ def main():
                                   "mbps": round(n / (dec_ms * 1e-3) / 1e6, 1)},
             },
             "roofline": {
-                "kernel": "k_sss_tile",
+                "kernel": "k_sss_stream",
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,

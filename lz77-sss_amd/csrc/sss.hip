@@ -3,7 +3,7 @@
 // patched-files/external/lce/include/ds/lce_sss.hpp:53; its source is absent
 // upstream, the definition pinned here is DESIGN.md section 4.1):
 //
-//   Phi(j)  = KR fingerprint of T[j..j+tau) mod 2^61-1 (base SSS_BASE)
+//   Phi(j)  = KR fingerprint of T[j..j+tau) mod 2^31-1 (base SSS_BASE)
 //   Q       = { j : T[j..j+tau) has a period <= floor(tau/3) }
 //   S       = { i <= n-2tau : min Phi'[i..i+tau] < inf at i or at i+tau }
 //
@@ -12,14 +12,16 @@
 //                   of T[a..a+340), the Q interval it induces on (a-128, a], and
 //                   the local extent of the periodic run (run table, lce_dev.h)
 //   k_run_elems + 2 scans + k_run_finish -- exact run ends/starts along chains
-//   k_sss_tile   -- one workgroup per tile of 7168 decisions: bytes staged once
-//                   in LDS, prefix-hash scan + rolls give Phi', van Herk minima
-//                   over 512-blocks in registers, ordered per-tile output
-//   k_sss_fallback -- exact slow path for tiles with more than TCAP outputs
-//   k_sss_compact-- per-tile outputs -> sorted S
+//   k_sss_stream -- one wave per stripe of 16384 decisions, walked in 512-blocks
+//                   with bytes, prefix hashes and Phi' in registers: lane Horner +
+//                   wave scan, 7 rolls per lane, van Herk minima by lane-local
+//                   and wave scans, ordered per-stripe output
+//   k_sss_fallback -- exact slow path for stripes with more than SCAP outputs
+//   k_sss_compact-- per-stripe outputs -> sorted S
 #include "../include/engine.h"
 
 #include <hipcub/hipcub.hpp>
+
 
 namespace lz {
 
@@ -282,31 +284,6 @@ __global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restr
     rlo[t] = (u32)slo[t];
 }
 
-// ---------------------------------------------------------------------------
-// main pass: one workgroup per tile of TL decisions i in [t0, t0+TL)
-//
-//   bytes   T[t0 .. t0+8192)             staged once in LDS (coalesced uint4)
-//   hashes  Phi(j), j in [t0, t0+7680)   prefix-hash scan over 512 threads x 16
-//                                        bytes, then 15 rolls per thread
-//   minima  m_i = min Phi'[i..i+512]     van Herk / Gil-Werman with 512-blocks:
-//                                        m_i = min(suffix_c[o], prefix_c+1[o]),
-//                                        both from wave scans held in registers
-//   output  i in S  <=>  m_i < inf and (Phi'(i) == m_i or Phi'(i+512) == m_i)
-constexpr int TL = 7168;            // decisions per tile (14 blocks of 512)
-constexpr int TB = TL + 2 * TAU;    // staged bytes = 8192 = 512 threads x 16
-constexpr int TP = TL + TAU;        // Phi' values per tile = 7680 (15 blocks)
-constexpr int TWG = 512;            // threads per tile
-constexpr int TCAP = 256;           // sync positions per tile before the exact fallback
-static_assert(TB == TWG * 16, "tile bytes must be 16 per thread");
-
-struct sss_pow {
-    u32 scan[6];   // b^(16 * 2^d)
-    u32 pw16[64];  // b^(16 k)
-    u32 b1024;     // b^1024 (one wave of bytes)
-    u32 b512;      // b^512 = b^tau
-    u32 bn;        // P - b^tau
-};
-
 // canonical x mod (2^31 - 1) for x < 2^63
 __device__ __forceinline__ u32 red31(u64 x) {
     u64 r = (x & P31) + (x >> 31);
@@ -320,105 +297,185 @@ __device__ __forceinline__ u32 red31s(u64 x) {
     const u32 r = (lo & (u32)P31) + __builtin_amdgcn_alignbit(hi, lo, 31);
     return r >= (u32)P31 ? r - (u32)P31 : r;
 }
-__device__ __forceinline__ u32 shfl_up32(u32 v, u32 d) { return __shfl_up(v, d, 64); }
-__device__ __forceinline__ u32 shfl_down32(u32 v, u32 d) { return __shfl_down(v, d, 64); }
 
-__global__ __launch_bounds__(TWG, 3) void k_sss_tile(const u8* __restrict__ T, u64 n, u64 last_i,
-                                                     const u16* __restrict__ qinfo, u32* __restrict__ tile_out,
-                                                     u32* __restrict__ tile_cnt, u32* __restrict__ tile_flag,
-                                                     u32* __restrict__ any_flag, u32 b, sss_pow PW) {
-    __shared__ __attribute__((aligned(16))) u8 s_t[TB + 16];
-    __shared__ u32 s_h[TWG + 1];
-    __shared__ u32 s_phi[TP + TP / 16];  // padded: index u + u/16 (bank spread)
-    __shared__ u32 s_wt[TWG / 64];
-    __shared__ u32 s_bc[TL / 512];
-    const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const u64 t0 = (u64)blockIdx.x * TL;
+// ---------------------------------------------------------------------------
+// main pass, streaming form: one wave per stripe of SD = 32 x 512 decisions,
+// walked block by block with everything in registers (no LDS, no barriers).
+// Lane L owns positions s_k + 8L .. s_k + 8L + 7 of every 512-block k.
+//
+//   bytes   8 per lane and block (one coalesced 512-byte load per wave),
+//           prefetched two blocks ahead
+//   hashes  H(s_k + 8L) (prefix hash relative to the stripe start) from a
+//           lane Horner over 8 bytes + a 6-step wave scan of affine maps;
+//           Phi(s_k + 8L) = H(s_k+1 + 8L) - H(s_k + 8L) * b^512, then 7 rolls
+//   minima  van Herk / Gil-Werman with 512-blocks: for decision block c the
+//           wave holds Phi'(block c) and Phi'(block c+1) in registers;
+//           m_i = min(suffix_c, prefix_c+1) from lane-local scans + wave scans
+//   output  i in S  <=>  m_i < inf and (Phi'(i) == m_i or Phi'(i+512) == m_i),
+//           ordered per stripe (capacity SCAP, exact fallback beyond)
+constexpr int SNB = 32;                       // decision blocks per stripe
+constexpr int SD = SNB * (int)TAU;            // decisions per stripe (16384)
+constexpr int SCAP = 512;                     // sync positions per stripe before the fallback
+constexpr int SWAVES = 4;                     // independent waves per workgroup
 
-    // 1. stage the tile's bytes (zero padded past n + TEXT_PAD)
+struct sss_pow2 {
+    u32 pw8[8];    // b^(7 - e)
+    u32 b8, ib8;   // b^8 and its inverse mod P31
+    u32 b512;      // b^512 = b^tau
+    u32 bn;        // P - b^tau
+};
+
+// canonical x mod (2^31 - 1) for x < 2^32
+__device__ __forceinline__ u32 canon31(u32 r) { return min(r, r - (u32)P31); }
+// < 2^32 and congruent to x mod P31, for x < 2^62; canon31 of it is canonical
+// (a fold of a product of two canonical values never reaches 2 P31)
+__device__ __forceinline__ u32 fold31(u64 x) {
+    return ((u32)x & (u32)P31) + __builtin_amdgcn_alignbit((u32)(x >> 32), (u32)x, 31);
+}
+__device__ __forceinline__ u32 mm31(u32 a, u32 c) { return canon31(fold31((u64)a * c)); }
+__device__ __forceinline__ u32 addm31(u32 a, u32 c) { return canon31(a + c); }
+__device__ __forceinline__ u32 subm31(u32 a, u32 c) { return canon31(a + (u32)P31 - c); }
+
+// wave scans by DPP (gfx9 row shifts + row broadcasts; no LDS round trips)
+template <int CTRL, int ROWM = 0xF>
+__device__ __forceinline__ u32 dpp(u32 old, u32 v) {
+    return (u32)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWM, 0xF, false);
+}
+__device__ __forceinline__ u32 wave_prefix_min(u32 v) {  // inclusive, over lanes <= L
+    v = min(v, dpp<0x111>(INF32, v));
+    v = min(v, dpp<0x112>(INF32, v));
+    v = min(v, dpp<0x114>(INF32, v));
+    v = min(v, dpp<0x118>(INF32, v));
+    v = min(v, dpp<0x142, 0xA>(INF32, v));
+    v = min(v, dpp<0x143, 0xC>(INF32, v));
+    return v;
+}
+__device__ __forceinline__ u32 wave_prefix_addm31(u32 v) {  // inclusive sums mod P31
+    v = addm31(v, dpp<0x111>(0, v));
+    v = addm31(v, dpp<0x112>(0, v));
+    v = addm31(v, dpp<0x114>(0, v));
+    v = addm31(v, dpp<0x118>(0, v));
+    v = addm31(v, dpp<0x142, 0xA>(0, v));
+    v = addm31(v, dpp<0x143, 0xC>(0, v));
+    return v;
+}
+__device__ __forceinline__ u32 wave_suffix_min(u32 v, u32 lane) {  // inclusive, over lanes >= L
+    v = min(v, dpp<0x101>(INF32, v));
+    v = min(v, dpp<0x102>(INF32, v));
+    v = min(v, dpp<0x104>(INF32, v));
+    v = min(v, dpp<0x108>(INF32, v));
+    const u32 r1 = (u32)__builtin_amdgcn_readlane((int)v, 16), r2 = (u32)__builtin_amdgcn_readlane((int)v, 32),
+              r3 = (u32)__builtin_amdgcn_readlane((int)v, 48);
+    const u32 a1 = min(r2, r3), a0 = min(r1, a1);
+    return min(v, lane < 16 ? a0 : lane < 32 ? a1 : lane < 48 ? r3 : INF32);
+}
+
+__global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict__ T, u64 n, u64 last_i,
+                                                           const u16* __restrict__ qinfo, u64 nstripes,
+                                                           u32* __restrict__ s_out, u32* __restrict__ s_cnt,
+                                                           u32* __restrict__ s_flag, u32* __restrict__ any_flag,
+                                                           u32 b, sss_pow2 PW) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 w = (u64)blockIdx.x * SWAVES + (threadIdx.x >> 6);
+    if (w >= nstripes) return;  // whole wave
+    const u64 i0 = w * (u64)SD;
+    const u64 jmax = n - TAU;                  // last position with a full window (n >= 2 tau here)
+    const u64 ilim = min<u64>(last_i - i0, (u64)SD - 1);  // decisions i0 + u, u <= ilim
+    // per-lane powers: pwl = b^(8 lane), ipw = b^(-8 (lane + 1))
+    u32 pwl = 1, ipw = PW.ib8;
     {
-        const u64 g = t0 + 16ull * tid;
-        uint4 v = {0, 0, 0, 0};
-        if (g + 16 <= n + TEXT_PAD) v = *(const uint4*)(T + g);
-        *(uint4*)&s_t[16 * tid] = v;
-        if (tid == 0) *(uint4*)&s_t[TB] = uint4{0, 0, 0, 0};
-    }
-    __syncthreads();
-    // 2. prefix hashes at every 16-byte boundary
-    const uint4 mine = *(const uint4*)&s_t[16 * tid];
-    const u32 mw[4] = {mine.x, mine.y, mine.z, mine.w};
-    u32 h = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) h = red31s((u64)h * b + ((mw[k >> 2] >> (8 * (k & 3))) & 255u));
-    u32 inc = h;
-#pragma unroll
-    for (int d = 0; d < 6; d++) {
-        const u32 left = shfl_up32(inc, 1u << d);
-        if (lane >= (1u << d)) inc = red31((u64)left * PW.scan[d] + inc);
-    }
-    u32 exc = shfl_up32(inc, 1);
-    if (lane == 0) exc = 0;
-    if (lane == 63) s_wt[wv] = inc;
-    __syncthreads();
-    u32 hw = 0;  // prefix hash of the bytes before this wave
-    for (u32 v = 0; v < wv; v++) hw = red31((u64)hw * PW.b1024 + s_wt[v]);
-    const u32 hl = red31((u64)hw * PW.pw16[lane] + exc);
-    s_h[tid] = hl;
-    if (tid == TWG - 1) s_h[TWG] = red31((u64)hl * PW.scan[0] + h);
-    __syncthreads();
-    // 3. Phi'(u) for u in [16 tid, 16 tid + 16), u < TP
-    if (16 * tid < (u32)TP) {
-        // Phi(u0) = H(u0 + 512) - H(u0) * b^512
-        u32 fp = red31((u64)s_h[tid + 32] + (P31 - mulmod31(hl, PW.b512)));
-        const u64 j0 = t0 + 16ull * tid;
-        const u64 jmax = n >= TAU ? n - TAU : 0;  // last position with a full window
-        const u64 ta = (j0 + 127) >> 7;
-        u16 q0 = 0xFF00, q1 = 0xFF00;
-        if (j0 <= jmax) {
-            q0 = qinfo[ta];
-            if (((j0 + 15 + 127) >> 7) != ta && j0 + 15 <= jmax) q1 = qinfo[ta + 1];
+        u32 f = PW.b8, g = PW.ib8;
+        for (int d = 0; d < 6; d++) {
+            if (lane & (1u << d)) {
+                pwl = mm31(pwl, f);
+                ipw = mm31(ipw, g);
+            }
+            f = mm31(f, f);
+            g = mm31(g, g);
         }
-        const uint4 ahead = *(const uint4*)&s_t[16 * tid + TAU];
-        const u32 aw[4] = {ahead.x, ahead.y, ahead.z, ahead.w};
-        const bool noq = q0 == 0xFF00 && q1 == 0xFF00 && j0 + 15 <= jmax;  // common case: no Q, no end
+    }
+    auto load8 = [&](u64 k) -> u64 { return *(const u64*)(T + i0 + k * TAU + 8 * lane); };
+    // A_k(lane) = H(s_k + 8 lane) b^(-8 lane) for block k from its bytes, where H
+    // is the prefix hash from the stripe start: with g = h8(lane) b^(-8(lane+1)),
+    // A = carry + (exclusive prefix sum of g), a plain DPP sum scan mod P31.
+    // carry = H(s_k) in, H(s_k+1) = b^512 (carry + sum of all g) out
+    auto block_hash = [&](u64 bytes, u32& carry) -> u32 {
+        const u32 lo = (u32)bytes, hi = (u32)(bytes >> 32);
+        u64 acc = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const u32 u = 16 * tid + k;
-            const u64 j = j0 + k;
-            u32 v = fp;
-            if (!noq) {
+        for (int e = 0; e < 8; e++) {
+            const u32 c = ((e < 4 ? lo : hi) >> (8 * (e & 3))) & 255u;
+            acc += (u64)c * PW.pw8[e];
+        }
+        const u32 g = mm31(canon31(fold31(acc)), ipw);
+        const u32 G = wave_prefix_addm31(g);
+        const u32 A = addm31(carry, subm31(G, g));
+        carry = mm31(addm31(carry, (u32)__builtin_amdgcn_readlane((int)G, 63)), PW.b512);
+        return A;
+    };
+    // Phi'(s_k + 8 lane + e), e < 8, into v
+    auto phi_block = [&](u64 k, u32 h0, u32 h1, u64 bo, u64 bi, u16 q0, u16 q1, u32* v) {
+        // Phi(s_k + 8 lane) = H(s_k+1 + 8 lane) - H(s_k + 8 lane) b^512 = b^(8 lane) (A_k+1 - A_k b^512)
+        u32 fp = mm31(subm31(h1, mm31(h0, PW.b512)), pwl);
+        const u32 olo = (u32)bo, ohi = (u32)(bo >> 32), ilo = (u32)bi, ihi = (u32)(bi >> 32);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            v[e] = fp;
+            if (e < 7) {
+                const u32 in = ((e < 4 ? ilo : ihi) >> (8 * (e & 3))) & 255u;
+                const u32 out = ((e < 4 ? olo : ohi) >> (8 * (e & 3))) & 255u;
+                fp = canon31(fold31((u64)fp * b + in + (u64)out * PW.bn));
+            }
+        }
+        const u64 j0 = i0 + k * TAU + 8 * lane;
+        const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
+        if (__builtin_expect(__ballot(q0 != 0xFF00 || q1 != 0xFF00) != 0 || endblk, 0)) {
+            const u64 ta = (j0 + 127) >> 7;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const u64 j = j0 + e;
                 if (j > jmax) {
-                    v = INF32;
+                    v[e] = INF32;
                 } else {
                     const u64 t = (j + 127) >> 7;
                     const u16 qi = t == ta ? q0 : q1;
                     const u32 rel = (u32)(j + 127 - (t << 7));
-                    if (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) v = INF32;
+                    if (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) v[e] = INF32;
                 }
             }
-            s_phi[u + (u >> 4)] = v;
-            if (k < 15) {
-                const u32 in = (aw[k >> 2] >> (8 * (k & 3))) & 255u, out = (mw[k >> 2] >> (8 * (k & 3))) & 255u;
-                fp = red31s((u64)fp * b + in + (u64)out * PW.bn);
-            }
         }
-    }
-    __syncthreads();
-    // 4. window minima: wave w handles block pairs (c, c+1) for c = w, w + 8 (c < 14)
-    const u32 ilim = last_i >= t0 ? (u32)min<u64>(last_i - t0, (u64)TL) : 0u;  // decisions u <= ilim
-    const bool any_i = last_i >= t0;
-    u32 masks[2] = {0, 0};
-    for (int r = 0; r < 2; r++) {
-        const u32 c = wv + 8 * r;
-        if (c >= (u32)(TL / 512)) break;
-        u32 x[8], y[8];
-#pragma unroll
-        for (int e = 0; e < 8; e++) {
-            const u32 ux = c * 512 + 8 * lane + e, uy = ux + 512;
-            x[e] = s_phi[ux + (ux >> 4)];
-            y[e] = s_phi[uy + (uy >> 4)];
+    };
+    auto loadq = [&](u64 k, u16& q0, u16& q1) {
+        const u64 j0 = i0 + k * TAU + 8 * lane;
+        const u64 ta = (j0 + 127) >> 7;
+        q0 = q1 = 0xFF00;
+        if (j0 <= jmax) {
+            q0 = qinfo[ta];
+            if ((j0 & 127) == 0 && j0 + 1 <= jmax) q1 = qinfo[ta + 1];
         }
-        // suffix minima of block c, prefix minima of block c+1
+    };
+
+    // prologue: H for blocks 0 and 1, Phi'(block 0)
+    u32 carry = 0;
+    u64 B0 = load8(0), B1 = load8(1), B2 = load8(2);
+    u16 qa0, qa1, qb0, qb1;
+    loadq(0, qa0, qa1);
+    loadq(1, qb0, qb1);
+    const u32 H0 = block_hash(B0, carry);
+    u32 H1 = block_hash(B1, carry);
+    u32 x[8], y[8];
+    phi_block(0, H0, H1, B0, B1, qa0, qa1, x);
+    u32 nout = 0;       // outputs of this stripe so far (uniform)
+    u32* out = s_out + w * SCAP;
+    const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
+    for (u32 c = 0; c < nblk; c++) {
+        // block c+2: bytes (prefetched), hash; block c+1: Phi'
+        const u64 B3 = load8(c + 3);  // prefetch (the text pad covers the stripe's end)
+        u16 qc0, qc1;
+        loadq(c + 2, qc0, qc1);
+        const u32 H2 = block_hash(B2, carry);
+        phi_block(c + 1, H1, H2, B1, B2, qb0, qb1, y);
+        // window minima for decisions of block c
         u32 sx[8], py[8];
         sx[7] = x[7];
 #pragma unroll
@@ -426,74 +483,67 @@ __global__ __launch_bounds__(TWG, 3) void k_sss_tile(const u8* __restrict__ T, u
         py[0] = y[0];
 #pragma unroll
         for (int e = 1; e < 8; e++) py[e] = min(py[e - 1], y[e]);
-        // lanes after this one (suffix) / before it (prefix)
-        u32 sufL = sx[0], preL = py[7];
-#pragma unroll
-        for (int d = 0; d < 6; d++) {
-            const u32 dn = shfl_down32(sufL, 1u << d);
-            if (lane + (1u << d) < 64) sufL = min(sufL, dn);
-            const u32 up = shfl_up32(preL, 1u << d);
-            if (lane >= (1u << d)) preL = min(preL, up);
-        }
-        u32 suf_after = shfl_down32(sufL, 1), pre_before = shfl_up32(preL, 1);
-        if (lane == 63) suf_after = INF32;
-        if (lane == 0) pre_before = INF32;
+        const u32 sufL = wave_suffix_min(sx[0], lane), preL = wave_prefix_min(py[7]);
+        const u32 suf_after = dpp<0x130>(INF32, sufL);   // wave_shl:1 -> lane + 1 (63: inf)
+        const u32 pre_before = dpp<0x138>(INF32, preL);  // wave_shr:1 -> lane - 1 (0: inf)
+        const u32 g = min(suf_after, pre_before);
         u32 mk = 0;
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-            const u32 m = min(min(sx[e], suf_after), min(pre_before, py[e]));
-            if (m != INF32 && (x[e] == m || y[e] == m) && any_i && c * 512 + 8 * lane + e <= ilim) mk |= 1u << e;
+            const u32 m = min(min(sx[e], g), py[e]);
+            if (m != INF32 && (x[e] == m || y[e] == m)) mk |= 1u << e;
         }
-        masks[r] = mk;
-        u32 cnt = __popc(mk);
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
-        if (lane == 0) s_bc[c] = cnt;
-    }
-    __syncthreads();
-    // 5. ordered output: block offsets, then lane offsets inside the block
-    u32 tot = 0;
-    for (int c = 0; c < TL / 512; c++) tot += s_bc[c];
-    for (int r = 0; r < 2; r++) {
-        const u32 c = wv + 8 * r;
-        if (c >= (u32)(TL / 512)) break;
-        u32 boff = 0;
-        for (u32 cc = 0; cc < c; cc++) boff += s_bc[cc];
-        const u32 mk = masks[r];
-        const u32 pc = __popc(mk);
-        u32 incl = pc;
-#pragma unroll
-        for (int d = 0; d < 6; d++) {
-            const u32 up = __shfl_up(incl, 1u << d, 64);
-            if (lane >= (1u << d)) incl += up;
+        if (c * TAU + TAU - 1 > ilim) {  // last block of the last stripe
+            const int64_t keep = (int64_t)ilim - (int64_t)(c * TAU + 8 * lane) + 1;  // decisions of this lane kept
+            mk &= keep <= 0 ? 0u : keep >= 8 ? 0xFFu : (1u << keep) - 1;
         }
-        u32 o = boff + incl - pc;
-        for (int e = 0; e < 8; e++)
-            if (mk & (1u << e)) {
-                if (o < (u32)TCAP) tile_out[(u64)blockIdx.x * TCAP + o] = (u32)(t0 + c * 512 + 8 * lane + e);
+        // ordered output: rank = sum of popc over lower lanes (4 ballots on the bits of popc)
+        const u64 anyb = __ballot(mk != 0);
+        if (anyb) {
+            const u32 pc = __popc(mk);
+            u32 rank = 0, tot = 0;
+#pragma unroll
+            for (int bit = 0; bit < 4; bit++) {
+                const u64 bb = __ballot((pc >> bit) & 1);
+                rank += (u32)__popcll(bb & ((1ull << lane) - 1)) << bit;
+                tot += (u32)__popcll(bb) << bit;
+            }
+            u32 o = nout + rank;
+            for (u32 mm = mk; mm; mm &= mm - 1) {
+                if (o < (u32)SCAP) out[o] = (u32)(i0 + c * TAU + 8 * lane + __builtin_ctz(mm));
                 o++;
             }
+            nout += tot;
+        }
+        // shift the pipeline
+#pragma unroll
+        for (int e = 0; e < 8; e++) x[e] = y[e];
+        H1 = H2;
+        B1 = B2;
+        B2 = B3;
+        qb0 = qc0;
+        qb1 = qc1;
     }
-    if (tid == 0) {
-        tile_cnt[blockIdx.x] = tot;
-        tile_flag[blockIdx.x] = tot > (u32)TCAP;
-        if (tot > (u32)TCAP) atomicOr(any_flag, 1u);
+    if (lane == 0) {
+        s_cnt[w] = nout;
+        s_flag[w] = nout > (u32)SCAP;
+        if (nout > (u32)SCAP) atomicOr(any_flag, 1u);
     }
 }
 
-// Exact slow path for tiles whose output buffer overflowed: one workgroup
-// recomputes the tile's Phi' values and the window minima directly.
+// Exact slow path for stripes whose output buffer overflowed: one workgroup
+// recomputes the stripe's Phi' values and the window minima directly.
 __global__ __launch_bounds__(256) void k_sss_fallback(const u8* __restrict__ T, u64 n, u64 last_i,
                                                       const u16* __restrict__ qinfo, const u32* __restrict__ lanes,
                                                       u64* __restrict__ scratch, u8* __restrict__ member,
                                                       u32* __restrict__ ovf_out, u32* __restrict__ lane_cnt, u32 b,
                                                       u64 bpow) {
     const u64 lane = lanes[blockIdx.x];
-    const u64 i0 = lane * TL;
-    const u64 i_end = min(i0 + TL, last_i + 1);
-    const u64 j_end = min(i0 + TL + TAU - 1, n - TAU);
-    u64* v = scratch + (u64)blockIdx.x * (TL + TAU);
-    u8* mem = member + (u64)blockIdx.x * TL;
+    const u64 i0 = lane * SD;
+    const u64 i_end = min(i0 + SD, last_i + 1);
+    const u64 j_end = min(i0 + SD + TAU - 1, n - TAU);
+    u64* v = scratch + (u64)blockIdx.x * (SD + TAU);
+    u8* mem = member + (u64)blockIdx.x * SD;
     if (threadIdx.x == 0) {
         u64 fp = 0;
         for (u64 k = 0; k < TAU; k++) fp = (fp * b + T[i0 + k]) % P31;
@@ -515,7 +565,7 @@ __global__ __launch_bounds__(256) void k_sss_fallback(const u8* __restrict__ T, 
     if (threadIdx.x == 0) {
         u32 c = 0;
         for (u64 i = i0; i < i_end; i++)
-            if (mem[i - i0]) ovf_out[(u64)blockIdx.x * TL + c++] = (u32)i;
+            if (mem[i - i0]) ovf_out[(u64)blockIdx.x * SD + c++] = (u32)i;
         lane_cnt[lane] = c;
     }
 }
@@ -527,7 +577,7 @@ __global__ void k_sss_compact(const u32* __restrict__ lane_out, const u32* __res
     const u64 lane = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= nlanes) return;
     const u32 c = lane_cnt[lane], o = lane_off[lane];
-    const u32* src = lane_flag[lane] ? ovf_out + (u64)ovf_slot[lane] * TL : lane_out + lane * TCAP;
+    const u32* src = lane_flag[lane] ? ovf_out + (u64)ovf_slot[lane] * SD : lane_out + lane * SCAP;
     for (u32 x = 0; x < c; x++) S[o + x] = src[x];
 }
 
@@ -572,19 +622,17 @@ void engine::build_sss(const u8* T) {
         runs_valid = true;
     }
 
-    const u64 nlanes = last_i / TL + 1;  // tiles
-    u32* lo = lane_out.get(nlanes * TCAP);
+    const u64 nlanes = last_i / SD + 1;  // stripes
+    u32* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
-    sss_pow PW;
+    sss_pow2 PW;
     {
         auto mm = [](u64 x, u64 y) { return x * y % P31; };
-        u64 b16 = pow31_host(SSS_BASE, 16);
-        for (int d = 0; d < 6; d++) { PW.scan[d] = (u32)b16; b16 = mm(b16, b16); }
-        PW.pw16[0] = 1;
-        const u64 p16 = pow31_host(SSS_BASE, 16);
-        for (int k = 1; k < 64; k++) PW.pw16[k] = (u32)mm(PW.pw16[k - 1], p16);
-        PW.b1024 = (u32)pow31_host(SSS_BASE, 1024);
+        (void)mm;
+        PW.b8 = (u32)pow31_host(SSS_BASE, 8);
+        PW.ib8 = (u32)pow31_host(PW.b8, P31 - 2);  // Fermat inverse
+        for (int e = 0; e < 8; e++) PW.pw8[e] = (u32)pow31_host(SSS_BASE, 7 - e);
         PW.b512 = (u32)pow31_host(SSS_BASE, TAU);
         PW.bn = (u32)((P31 - PW.b512) % P31);
     }
@@ -593,7 +641,8 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipEventCreate(&e0));
     LZ_HIP(hipEventCreate(&e1));
     LZ_HIP(hipEventRecord(e0, st));
-    k_sss_tile<<<(unsigned)nlanes, TWG, 0, st>>>(T, n, last_i, qi, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW);
+    k_sss_stream<<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
+                                                               (u32)SSS_BASE, PW);
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipEventRecord(e1, st));
 
@@ -619,9 +668,9 @@ void engine::build_sss(const u8* T) {
         u32* d_lanes = u32d.get(lanes.size());
         LZ_HIP(hipMemcpy(d_lanes, lanes.data(), lanes.size() * 4, hipMemcpyHostToDevice));
         LZ_HIP(hipMemcpy(ovf_slot, slot.data(), nlanes * 4, hipMemcpyHostToDevice));
-        u64* scratch = u64a.get(lanes.size() * (TL + TAU));
-        u8* member = tmp_bytes.get(lanes.size() * TL);
-        ovf_out = u32b.get(lanes.size() * TL);
+        u64* scratch = u64a.get(lanes.size() * (SD + TAU));
+        u8* member = tmp_bytes.get(lanes.size() * SD);
+        ovf_out = u32b.get(lanes.size() * SD);
         k_sss_fallback<<<(unsigned)lanes.size(), 256, 0, st>>>(T, n, last_i, qi, d_lanes, scratch, member, ovf_out,
                                                                lc, (u32)SSS_BASE, bpow);
         LZ_HIP(hipGetLastError());

@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_${TAG}_${WL}" -o run -- \
     python3 "$REPO/bench.py" --steps 3 --warmup 1 --workload "$WL" --no-cpu-baseline > "$OUT/prof_${TAG}_${WL}.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_sss_tile -f csv -d "$OUT/pmc_${TAG}_${WL}_fetch" -o run -- \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_sss_stream -f csv -d "$OUT/pmc_${TAG}_${WL}_fetch" -o run -- \
     python3 "$REPO/bench.py" --steps 2 --warmup 0 --workload "$WL" --no-cpu-baseline > "$OUT/pmc_${TAG}_${WL}_fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_sss_tile -f csv -d "$OUT/pmc_${TAG}_${WL}_write" -o run -- \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_sss_stream -f csv -d "$OUT/pmc_${TAG}_${WL}_write" -o run -- \
     python3 "$REPO/bench.py" --steps 2 --warmup 0 --workload "$WL" --no-cpu-baseline > "$OUT/pmc_${TAG}_${WL}_write.log" 2>&1

@@ -1,4 +1,4 @@
-"""Runs only the SSS pass (k_q_anchors + k_sss_tile + compaction) a few times on a 1 GiB workload;
+"""Runs only the SSS pass (k_q_anchors + k_sss_stream + compaction) a few times on a 1 GiB workload;
 used under rocprofv3 --pmc to read the instruction mix of the SSS kernels."""
 import os
 import sys

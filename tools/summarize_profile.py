@@ -3,10 +3,10 @@
 
   profiles/<tag>_<wl>_kernel_stats.csv   rocprofv3 --kernel-trace --stats (as produced)
   profiles/<tag>_<wl>_kernels.txt        top kernels, per-bench-step totals
-  profiles/<tag>_<wl>_pmc_sss.json       HBM bytes per launch of k_sss_tile from the two PMC passes
+  profiles/<tag>_<wl>_pmc_sss.json       HBM bytes per launch of k_sss_stream from the two PMC passes
 
 HBM bytes follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read (k_sss_tile
+on gfx950 FETCH_SIZE reports half the bytes of a 16-B-per-lane streaming read (k_sss_stream
 stages its tile with one uint4 load per lane), so it is doubled; WRITE_SIZE is taken as is.
 """
 import csv
@@ -42,9 +42,9 @@ def counter(path, name):
 
 fetch, nf = counter(src / f"pmc_{tag}_{wl}_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
 write, nw = counter(src / f"pmc_{tag}_{wl}_write" / "run_counter_collection.csv", "WRITE_SIZE")
-sss_avg_ns = [float(r["AverageNs"]) for r in rows if r["Name"].startswith("lz::k_sss_tile")][0]
+sss_avg_ns = [float(r["AverageNs"]) for r in rows if r["Name"].startswith("lz::k_sss_stream")][0]
 hbm = 2 * fetch * 1024 + write * 1024
-out = {"kernel": "k_sss_tile", "workload": wl, "n": n, "launches": {"fetch": nf, "write": nw},
+out = {"kernel": "k_sss_stream", "workload": wl, "n": n, "launches": {"fetch": nf, "write": nw},
        "fetch_size_kib": fetch, "write_size_kib": write, "fetch_correction": 2.0,
        "hbm_bytes_per_launch": int(hbm), "avg_launch_ns_kernel_trace": sss_avg_ns}
 (dst / f"{tag}_{wl}_pmc_sss.json").write_text(json.dumps(out, indent=1) + "\n")
