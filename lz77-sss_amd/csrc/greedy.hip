@@ -795,21 +795,30 @@ __global__ void k_bm_list(const u32* __restrict__ bm, const u32* __restrict__ fl
         b &= b - 1;
     }
 }
-// intervals -> <= 1024-position chunks with ranks (rank0 = exclusive scan of lengths)
+// intervals -> <= SLOT_CHUNK-position chunks with ranks (rank0 = exclusive scan of
+// lengths).  Short chunks keep k_slots (one thread per chunk, a direct
+// fingerprint of <= 64 bytes per pattern, then rolls) wide on the device.
+constexpr u32 SLOT_CHUNK = 128;
 __global__ void k_iv_chunk_counts(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, u32* __restrict__ nch,
                                   u32* __restrict__ len) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ni) return;
     const u32 l = en[k] - st[k];
     len[k] = l;
-    nch[k] = (l + 1023) / 1024;
+    nch[k] = (l + SLOT_CHUNK - 1) / SLOT_CHUNK;
 }
+// one thread per chunk; its interval by binary search over the chunk offsets
 __global__ void k_iv_chunks(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, const u32* __restrict__ choff,
-                            const u32* __restrict__ rank, ichunk* __restrict__ ch) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= ni) return;
-    u32 o = choff[k];
-    for (u32 q = st[k]; q < en[k]; q += 1024) ch[o++] = ichunk{q, min(en[k], q + 1024), rank[k] + (q - st[k])};
+                            u32 nch, const u32* __restrict__ rank, ichunk* __restrict__ ch) {
+    const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nch) return;
+    u32 lo = 0, hi = ni;  // last k with choff[k] <= c (every interval has >= 1 chunk)
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (choff[mid] <= c) lo = mid; else hi = mid;
+    }
+    const u32 q = st[lo] + (u32)(c - choff[lo]) * SLOT_CHUNK;
+    ch[c] = ichunk{q, min(en[lo], q + SLOT_CHUNK), rank[lo] + (q - st[lo])};
 }
 // rem[r] = base position r not in I
 __global__ void k_rem_from_bm(const u32* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, u8* __restrict__ rem) {
@@ -911,6 +920,11 @@ __global__ void k_link(seg_tab S, u32 nseg) {
     __threadfence();
     atomicExch(&S.seg_at[x], id);
     S.succ[g] = id;
+}
+// sparse reset of the position -> segment map (every entry set was a segment start)
+__global__ void k_seg_at_clear(seg_tab S, u32 nseg) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < nseg) S.seg_at[S.sin[g].start] = NONE;
 }
 // pointer doubling along succ: J = terminal-or-successor, D = hops
 __global__ void k_jump0(seg_tab S, u32 nseg, u32* __restrict__ J, u32* __restrict__ D) {
@@ -1098,8 +1112,17 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     };
     g_sin.get(cap); g_sout.get(cap); g_valid.get(cap); g_succ.get(cap);
     bind_tab();
-    S.seg_at = g_seg_at.get((u64)N + 1);
-    LZ_HIP(hipMemsetAsync(S.seg_at, 0xFF, ((u64)N + 1) * 4, st));
+    {
+        // the position -> segment map is cleared sparsely after each call (k_seg_at_clear);
+        // a fresh or reallocated map, or one left dirty by a failed call, is cleared densely
+        u32* prev = g_seg_at.p;
+        S.seg_at = g_seg_at.get((u64)N + 1);
+        if (S.seg_at != prev || !seg_at_clean || seg_at_n < (u64)N + 1) {
+            LZ_HIP(hipMemsetAsync(S.seg_at, 0xFF, g_seg_at.cap * 4, st));
+            seg_at_n = g_seg_at.cap;
+        }
+        seg_at_clean = false;
+    }
     S.nseg = (u32*)counters64.get(4);
     S.err = S.nseg + 1;
     LZ_HIP(hipMemsetAsync(S.nseg, 0, 8, st));
@@ -1134,7 +1157,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         if (mk * 16 >= nslots) k_bucket_dense<<<cdiv(mk + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
         else k_bucket_search<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
     };
-    // runs of a bitmap -> intervals (st, en), ranks, <= 1024-position chunks
+    // runs of a bitmap -> intervals (st, en), ranks, <= SLOT_CHUNK-position chunks
     auto runs_to_chunks = [&](const u32* bm, dbuf<u32>& dst, dbuf<u32>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
                               u64& npos, u32& nch) -> ichunk* {
         k_bm_count<<<gw, 256, 0, st>>>(bm, nw, ns, ne);
@@ -1155,13 +1178,16 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             nch = excl_scan(nc, choff, ni, scan_tmp, st);
         }
         ichunk* ch = (ichunk*)dch.get(std::max<u64>(1, nch) * sizeof(ichunk));
-        if (ni) k_iv_chunks<<<cdiv(ni, 256), 256, 0, st>>>(a, b, ni, choff, rk, ch);
+        if (nch) k_iv_chunks<<<cdiv(nch, 256), 256, 0, st>>>(a, b, ni, choff, nch, rk, ch);
         return ch;
     };
     auto build_base = [&](const u32* bm) {
         if (bm != bmIb) LZ_HIP(hipMemcpyAsync(bmIb, bm, nw * 4, hipMemcpyDeviceToDevice, st));
         u32 ni, nch;
         ichunk* ch = runs_to_chunks(bmIb, ist, iend, irank, chunk_buf, ni, nb, nch);
+        if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy base: intervals=%u positions=%llu chunks=%u slots=2^%u\n", ni,
+                              (unsigned long long)nb, nch, gp.log2_size_h);
+        lap("base intervals");
         if (5 * nb >= (1ull << 32)) throw error(-1, "gap region too large for 32-bit entry ids");
         const u64 ne5 = 5 * nb;
         u32* keys = ekeys.get(ne5 + 1);
@@ -1173,7 +1199,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u8* rem = rem_buf.get(nb + 1);
         LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
         if (nch) {
-            k_slots<<<cdiv(nch, 64), 64, 0, st>>>(T, G, ch, nch, keys, vals, ipos);
+            k_slots<<<cdiv(nch, 128), 128, 0, st>>>(T, G, ch, nch, keys, vals, ipos);
+            lap("base slots");
             size_t tb = 0;
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, skeys, vals, svals, (int)ne5, 0,
                                                       (int)gp.log2_size_h, st));
@@ -1196,12 +1223,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
                 LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
             }
         }
+        lap("base sort + pred");
         build_buckets(key_u32{skeys}, ne5, g_bstart);
         W.istart = ist.p; W.iend = iend.p; W.irank = irank.p; W.nint = ni;
         W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne5;
         W.bstart = g_bstart.p;
         W.rem = rem; W.akeys = nullptr; W.nadd = 0; W.akeys2 = nullptr; W.nadd2 = 0;
-        lap("base build (slots+sort+pred)");
+        lap("base buckets");
     };
     // added entries: positions of I outside the base set.  The main list is
     // rebuilt rarely (membership of its positions is read from the I bitmap);
@@ -1218,7 +1246,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         if (!na) return 0;
         u32* akey32 = k32.get(5 * na);
         u32* apos = kpos.get(na);
-        k_slots<<<cdiv(nch, 64), 64, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
+        k_slots<<<cdiv(nch, 128), 128, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
         u64* ak = ka.get(5 * na);
         u64* ak2 = kb.get(5 * na);
         k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
@@ -1449,6 +1477,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy delta: changed=%llu outside=%llu\n",
                               (unsigned long long)ny, (unsigned long long)outside);
     }
+    k_seg_at_clear<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
+    seg_at_clean = true;
     stats[12] = outer + 1;
     stats[13] = rounds_total;
     stats[14] = stats_fallback_lanes;

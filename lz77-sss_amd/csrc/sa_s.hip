@@ -126,22 +126,66 @@ __device__ __forceinline__ u64 mix64(u64 z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
-// one wave per key: h = sum over 8-byte words w of mix(word_w + w*C) + mix(len)
-__global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, const u32* __restrict__ S,
-                                                  const u32* __restrict__ KL, u32 s, u64* __restrict__ H) {
-    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const u32 lane = threadIdx.x & 63;
+// h(key) = mix(len) + sum over its 8-byte words w of mix(word_w + w*C).  The sum is
+// order-free, so a key is cut into KH_CHUNK-byte pieces hashed by different waves
+// and added atomically: long keys (gaps of MBs inside periodic runs) no longer
+// serialize on one wave.  k_key_prep sets H = mix(len) and the piece counts.
+constexpr u32 KH_CHUNK = 16384;
+constexpr u32 KH_WAVES = 16384;
+__global__ void k_key_prep(const u32* __restrict__ KL, u32 s, u64* __restrict__ H, u32* __restrict__ CC) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s) return;
-    const u64 beg = S[k], len = KL[k];
-    u64 h = 0;
-    for (u64 w = lane; 8 * w < len; w += 64) {
-        u64 x = ldu64(T + beg + 8 * w);
-        const u64 rem = len - 8 * w;
-        if (rem < 8) x &= (1ull << (8 * rem)) - 1;
-        h += mix64(x + w * 0x9e3779b97f4a7c15ull);
+    const u64 len = KL[k];
+    H[k] = mix64(len ^ 0xd6e8feb86659fd93ull);
+    CC[k] = (u32)max<u64>(1, (len + KH_CHUNK - 1) / KH_CHUNK);
+}
+// OFF = inclusive scan of the piece counts; wave w hashes pieces [w*per, (w+1)*per)
+__global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, const u32* __restrict__ S,
+                                                  const u32* __restrict__ KL, const u32* __restrict__ OFF, u32 s,
+                                                  u64* __restrict__ H) {
+    const u32 wave = (u32)(((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const u32 lane = threadIdx.x & 63;
+    const u32 total = OFF[s - 1];
+    const u32 per = (total + KH_WAVES - 1) / KH_WAVES;
+    u32 c = wave * per;
+    const u32 cend = min(total, c + per);
+    if (c >= cend) return;
+    // key holding piece c: first k with OFF[k] > c
+    u32 lo = 0, hi = s - 1;
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (OFF[mid] > c) hi = mid; else lo = mid + 1;
     }
-    for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o);
-    if (lane == 0) H[k] = h + mix64(len ^ 0xd6e8feb86659fd93ull);
+    u32 k = lo;
+    for (; c < cend; c++) {
+        while (OFF[k] <= c) k++;
+        const u32 first = k ? OFF[k - 1] : 0;
+        const u64 beg = S[k], len = KL[k];
+        const u64 b0 = (u64)(c - first) * KH_CHUNK, b1 = min<u64>(len, b0 + KH_CHUNK);
+        u64 h = 0;
+        for (u64 w = b0 / 8 + lane; 8 * w < b1; w += 64) {
+            u64 x = ldu64(T + beg + 8 * w);
+            const u64 rem = len - 8 * w;
+            if (rem < 8) x &= (1ull << (8 * rem)) - 1;
+            h += mix64(x + w * 0x9e3779b97f4a7c15ull);
+        }
+        for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o);
+        if (lane == 0 && b0 < b1) atomicAdd((unsigned long long*)&H[k], (unsigned long long)h);
+    }
+}
+// big-endian 8-byte word i of a key (zero past its end): radix keys of the presort
+__device__ __forceinline__ u64 key_word_be(const u8* T, u64 beg, u64 len, u32 i) {
+    const u64 off = 8ull * i;
+    if (off >= len) return 0;
+    u64 x = ldu64(T + beg + off);
+    const u64 r = len - off;
+    if (r < 8) x &= (1ull << (8 * r)) - 1;
+    return __builtin_bswap64(x);
+}
+__global__ void k_word_keys(const u8* __restrict__ T, const u32* __restrict__ S, const u32* __restrict__ KL,
+                            const u32* __restrict__ v, u32 d, u32 i, u64* __restrict__ key) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < d) key[t] = key_word_be(T, S[v[t]], KL[v[t]], i);
 }
 // wave-parallel exact comparison of two keys (all 64 lanes must call it)
 __device__ int wave_key_cmp(const u8* T, const run_tab& R, const u32* S, const u32* KL, u32 a, u32 b, u32 lane) {
@@ -173,72 +217,72 @@ __global__ void k_reps(const u32* __restrict__ flag, const u32* __restrict__ grp
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < s && flag[t]) rep[grp[t] - 1] = idx[t];
 }
-// bounded comparison (first CMP_BOUND bytes of each key)
-constexpr u64 CMP_BOUND = 2048;
-struct rep_less_bounded {
-    const u8* T;
-    const u32* S;
-    const u32* KL;
-    run_tab R;
-    __device__ bool operator()(const u32& a, const u32& b) const {
-        const u64 la = min<u64>(KL[a], CMP_BOUND), lb = min<u64>(KL[b], CMP_BOUND), m = min(la, lb);
-        const u64 c = dev_lce_fwd(T, R, S[a], S[b], m);
-        if (c < m) return T[(u64)S[a] + c] < T[(u64)S[b] + c];
-        // equal within the bound: stays in input order (stable sort), resolved exactly afterwards.
-        return la < lb;
-    }
-};
-__global__ void k_tie_flags(const u8* T, run_tab R, const u32* S, const u32* KL, const u32* __restrict__ srt, u32 d,
-                            u8* __restrict__ tie) {
+// distinct keys are radix-sorted by their first PRESORT_WORDS big-endian words
+// (LSD: one stable 64-bit radix pass per word); keys equal on that prefix form
+// tie segments finished by exact wave comparisons below
+constexpr u32 PRESORT_WORDS = 4;
+__global__ void k_prefix_ties(const u8* __restrict__ T, const u32* __restrict__ S, const u32* __restrict__ KL,
+                              const u32* __restrict__ srt, u32 d, u8* __restrict__ tie) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= d) return;
     if (r == 0) { tie[0] = 0; return; }
     const u32 a = srt[r - 1], b = srt[r];
-    const u64 la = min<u64>(KL[a], CMP_BOUND), lb = min<u64>(KL[b], CMP_BOUND);
-    tie[r] = (la == lb && dev_lce_fwd(T, R, S[a], S[b], la) == la) ? 1 : 0;
+    bool eq = true;
+    for (u32 i = 0; i < PRESORT_WORDS && eq; i++)
+        eq = key_word_be(T, S[a], KL[a], i) == key_word_be(T, S[b], KL[b], i);
+    tie[r] = eq ? 1 : 0;
 }
-// Tie segments (keys equal within CMP_BOUND) are finished by a merge sort in
-// which every comparison is done by a whole wave (64 lanes x 8 bytes per step):
-// items are (segment << 32 | key); segments stay contiguous and ordered.
-__device__ __forceinline__ bool wave_less(const u8* T, const run_tab& R, const u32* S, const u32* KL, u64 x, u64 y,
-                                          u32 lane) {
-    const u32 sx = (u32)(x >> 32), sy = (u32)(y >> 32);
-    if (sx != sy) return sx < sy;
-    return wave_key_cmp(T, R, S, KL, (u32)x, (u32)y, lane) < 0;
+// Tie segments (keys equal on the presort prefix) are finished by a merge sort in
+// which every comparison is done by a whole wave (64 lanes x 8 bytes per step).
+// Items hold key ids, segment k occupies [sbeg[k], sbeg[k+1]).
+// A pass of width w merges, inside every segment, neighbouring sorted blocks of
+// w items (local offsets).  Each wave produces opw = min(64, 2w) outputs of one
+// merge; uoff is the exclusive scan of the per-segment wave counts, so passes
+// cost O(members) and only log2(longest segment) passes run.
+__global__ void k_seg_units(const u32* __restrict__ sbeg, u32 nseg, u32 opw, u32* __restrict__ units) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nseg) units[k] = (sbeg[k + 1] - sbeg[k] + opw - 1) / opw;
 }
-__global__ __launch_bounds__(256) void k_wmerge(const u8* T, run_tab R, const u32* S, const u32* KL, const u64* __restrict__ in,
-                                                u64* __restrict__ out, u32 m, u32 w, u32 opw) {
-    // each wave produces opw = min(64, 2w) outputs, so they never span two merges
-    const u64 wave = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+__global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const u32* S, const u32* KL,
+                                                  const u32* __restrict__ sbeg, const u32* __restrict__ uoff, u32 nseg,
+                                                  u32 nunits, const u32* __restrict__ in, u32* __restrict__ out, u32 w,
+                                                  u32 opw) {
+    const u32 unit = (u32)(((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const u32 lane = threadIdx.x & 63;
-    const u64 p0 = wave * opw;
-    if (p0 >= m) return;
-    const u64 base = p0 / (2ull * w) * (2ull * w);
-    const u64 a0 = base, a1 = min<u64>(base + w, m), b0 = a1, b1 = min<u64>(base + 2ull * w, m);
-    const u64 la = a1 - a0, lb = b1 - b0, diag = p0 - base;
-    u64 lo = diag > lb ? diag - lb : 0, hi = min(diag, la);
-    while (lo < hi) {
-        const u64 mid = (lo + hi) >> 1;
-        if (!wave_less(T, R, S, KL, in[b0 + diag - 1 - mid], in[a0 + mid], lane)) lo = mid + 1; else hi = mid;
+    if (unit >= nunits) return;
+    u32 lo = 0, hi = nseg;  // last k with uoff[k] <= unit
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (uoff[mid] <= unit) lo = mid; else hi = mid;
     }
-    u64 i = lo, j = diag - lo;
-    const u64 pend = min<u64>(p0 + opw, b1);
-    for (u64 p = p0; p < pend; p++) {
+    const u32 k = lo, o = sbeg[k], L = sbeg[k + 1] - o;
+    const u64 p0 = (u64)(unit - uoff[k]) * opw;
+    const u64 base = p0 / (2ull * w) * (2ull * w);
+    const u64 a0 = o + base, a1 = o + min<u64>(base + w, L), b0 = a1, b1 = o + min<u64>(base + 2ull * w, L);
+    const u64 la = a1 - a0, lb = b1 - b0, diag = p0 - base;
+    u64 l2 = diag > lb ? diag - lb : 0, h2 = min(diag, la);
+    while (l2 < h2) {
+        const u64 mid = (l2 + h2) >> 1;
+        if (!(wave_key_cmp(T, R, S, KL, in[b0 + diag - 1 - mid], in[a0 + mid], lane) < 0)) l2 = mid + 1; else h2 = mid;
+    }
+    u64 i = l2, j = diag - l2;
+    const u64 pend = min<u64>(o + p0 + opw, b1);
+    for (u64 p = o + p0; p < pend; p++) {
         bool takeA;
         if (i >= la) takeA = false;
         else if (j >= lb) takeA = true;
-        else takeA = !wave_less(T, R, S, KL, in[b0 + j], in[a0 + i], lane);
-        const u64 v = takeA ? in[a0 + i++] : in[b0 + j++];
+        else takeA = !(wave_key_cmp(T, R, S, KL, in[b0 + j], in[a0 + i], lane) < 0);
+        const u32 v = takeA ? in[a0 + i++] : in[b0 + j++];
         if (lane == 0) out[p] = v;
     }
 }
-__global__ void k_tie_items(const u32* __restrict__ srt, const u32* __restrict__ pos, u32 m, u64* __restrict__ items) {
+__global__ void k_gather_u32(const u32* __restrict__ src, const u32* __restrict__ pos, u32 m, u32* __restrict__ dst) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < m) items[t] |= srt[pos[t]];
+    if (t < m) dst[t] = src[pos[t]];
 }
-__global__ void k_tie_scatter(const u64* __restrict__ items, const u32* __restrict__ pos, u32 m, u32* __restrict__ srt) {
+__global__ void k_scatter_u32(const u32* __restrict__ src, const u32* __restrict__ pos, u32 m, u32* __restrict__ dst) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < m) srt[pos[t]] = (u32)items[t];
+    if (t < m) dst[pos[t]] = src[t];
 }
 __global__ void k_rank_of_group(const u32* __restrict__ srt_grp, u32 d, u32* __restrict__ rank_of) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -337,6 +381,19 @@ static void scan_incl(u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
     LZ_HIP(hipcub::DeviceScan::InclusiveSum(t, tb, in, out, (int)m, st));
 }
 
+// exclusive scan; returns the total (synchronizes)
+static u32 excl_scan32(const u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
+    size_t tb = 0;
+    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)m, st));
+    u8* t = tmp.get(tb);
+    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, (int)m, st));
+    u32 last[2];
+    LZ_HIP(hipMemcpyAsync(&last[0], out + m - 1, 4, hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipMemcpyAsync(&last[1], in + m - 1, 4, hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    return last[0] + last[1];
+}
+
 void engine::build_sa_s(const u8* T) {
     nlev_rank = 0;
     if (s == 0) return;
@@ -355,7 +412,10 @@ void engine::build_sa_s(const u8* T) {
         // 1. group identical keys by a wave-parallel hash, verified exactly
         u64* H = u64a.get(s);
         u64* Hs = u64b.get(s);
-        k_key_hash<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, dS, KL, s, H);
+        u32* CC = u32e.get(s);
+        k_key_prep<<<g, 256, 0, st>>>(KL, s, H, CC);
+        scan_incl(CC, CC, s, scan_tmp, st);
+        k_key_hash<<<KH_WAVES * 64 / 256, 256, 0, st>>>(T, dS, KL, CC, s, H);
         k_iota<<<g, 256, 0, st>>>(idx_in, s);
         size_t tb = 0;
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, H, Hs, idx_in, idx, (int)s, 0, 64, st));
@@ -374,43 +434,62 @@ void engine::build_sa_s(const u8* T) {
             // 2. sort distinct keys: bounded comparison, then exact wave sort of bounded ties
             u32* srt = rep;
             SA_DBG("reps");
-            merge_sort_u32(srt, sa_tmp2.get(d), d, rep_less_bounded{T, dS, KL, runs()}, st);
-            SA_DBG("bounded sort");
+            {
+                u32* v2 = sa_tmp2.get(d);
+                u64* wk = u64b.get(2 * (u64)d);  // sorted hashes no longer needed
+                u64* wk2 = wk + d;
+                size_t tb2 = 0;
+                LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, wk, wk2, srt, v2, (int)d, 0, 64, st));
+                u8* t2 = scan_tmp.get(tb2);
+                for (int i = (int)PRESORT_WORDS - 1; i >= 0; i--) {
+                    k_word_keys<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, (u32)i, wk);
+                    LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, wk, wk2, srt, v2, (int)d, 0, 64, st));
+                    LZ_HIP(hipMemcpyAsync(srt, v2, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+                }
+            }
+            SA_DBG("presort");
             u8* tie = tmp_bytes.get(d);
-            k_tie_flags<<<cdiv(d, 256), 256, 0, st>>>(T, runs(), dS, KL, srt, d, tie);
+            k_prefix_ties<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, tie);
             if (debug_enabled()) fprintf(stderr, "[sa_s] distinct=%u sorted\n", d);
             std::vector<u8> htie(d);
             LZ_HIP(hipMemcpyAsync(htie.data(), tie, d, hipMemcpyDeviceToHost, st));
             LZ_HIP(hipStreamSynchronize(st));
-            // members of tie segments, in order, tagged with their segment
-            std::vector<u64> items;
-            std::vector<u32> ipos;
-            u32 nseg = 0;
+            // members of tie segments, in order, and the segment offsets
+            std::vector<u32> ipos, sbeg;
+            u32 nseg = 0, maxl = 0;
             for (u32 r = 1; r < d;) {
                 if (!htie[r]) { r++; continue; }
                 u32 e = r;
                 while (e < d && htie[e]) e++;
-                for (u32 q = r - 1; q < e; q++) { items.push_back(((u64)nseg << 32)); ipos.push_back(q); }
+                sbeg.push_back((u32)ipos.size());
+                for (u32 q = r - 1; q < e; q++) ipos.push_back(q);
+                maxl = std::max(maxl, e - r + 1);
                 nseg++;
                 r = e;
             }
-            if (debug_enabled()) fprintf(stderr, "[sa_s] tie segments=%u members=%zu\n", nseg, items.size());
-            if (!items.empty()) {
-                const u32 mt = (u32)items.size();
-                u64* it_a = u64a.get(2 * (u64)mt);  // hashes no longer needed
-                u64* it_b = it_a + mt;
+            sbeg.push_back((u32)ipos.size());
+            if (debug_enabled()) fprintf(stderr, "[sa_s] tie segments=%u members=%zu longest=%u\n", nseg, ipos.size(), maxl);
+            if (!ipos.empty()) {
+                const u32 mt = (u32)ipos.size();
+                u32* it_a = (u32*)u64a.get(mt);  // hashes no longer needed
+                u32* it_b = it_a + mt;
                 u32* dpos = sa_tmp3.get(mt);
-                LZ_HIP(hipMemcpyAsync(it_a, items.data(), (size_t)mt * 8, hipMemcpyHostToDevice, st));
+                u32* dsb = u32e.get(2 * (u64)nseg + 2);
+                u32* units = dsb + nseg + 1;
                 LZ_HIP(hipMemcpyAsync(dpos, ipos.data(), (size_t)mt * 4, hipMemcpyHostToDevice, st));
-                k_tie_items<<<cdiv(mt, 256), 256, 0, st>>>(srt, dpos, mt, it_a);
-                SA_DBG("tie items");
-                for (u64 w = 1; w < mt; w *= 2) {
+                LZ_HIP(hipMemcpyAsync(dsb, sbeg.data(), (size_t)(nseg + 1) * 4, hipMemcpyHostToDevice, st));
+                k_gather_u32<<<cdiv(mt, 256), 256, 0, st>>>(srt, dpos, mt, it_a);
+                u32* uoff = sa_tmp1.p == srt ? sa_tmp2.get(nseg + 1) : sa_tmp1.get(nseg + 1);
+                for (u64 w = 1; w < maxl; w *= 2) {
                     const u32 opw = (u32)std::min<u64>(64, 2 * w);
-                    k_wmerge<<<cdiv((u64)cdiv(mt, opw) * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, it_a, it_b, mt, (u32)w, opw);
+                    k_seg_units<<<cdiv(nseg, 256), 256, 0, st>>>(dsb, nseg, opw, units);
+                    const u32 nunits = excl_scan32(units, uoff, nseg, scan_tmp, st);
+                    k_segmerge<<<cdiv((u64)nunits * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, dsb, uoff, nseg, nunits,
+                                                                            it_a, it_b, (u32)w, opw);
                     std::swap(it_a, it_b);
-                    SA_DBG("wmerge");
+                    SA_DBG("segmerge");
                 }
-                k_tie_scatter<<<cdiv(mt, 256), 256, 0, st>>>(it_a, dpos, mt, srt);
+                k_scatter_u32<<<cdiv(mt, 256), 256, 0, st>>>(it_a, dpos, mt, srt);
                 SA_DBG("tie scatter");
                 LZ_HIP(hipGetLastError());
             }

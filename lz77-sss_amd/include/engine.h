@@ -125,6 +125,8 @@ struct engine {
     dbuf<seg_in> g_sin;
     dbuf<seg_out> g_sout;
     dbuf<u8> g_valid, g_cs, g_tailc;
+    bool seg_at_clean = false;  // g_seg_at is all NONE
+    u64 seg_at_n = 0;
     dbuf<u32> g_succ, g_seg_at, g_cbv, g_ids, g_chain, g_dist[2];
     dbuf<u32> g_bmI, g_bmI2, g_bmIb, g_bmT;
     dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_ast, g_aen, g_ark;
