@@ -284,57 +284,33 @@ __global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restr
     rlo[t] = (u32)slo[t];
 }
 
-// canonical x mod (2^31 - 1) for x < 2^63
-__device__ __forceinline__ u32 red31(u64 x) {
-    u64 r = (x & P31) + (x >> 31);
-    r = (r & P31) + (r >> 31);
-    return (u32)(r >= P31 ? r - P31 : r);
-}
-__device__ __forceinline__ u32 mulmod31(u32 a, u32 c) { return red31((u64)a * c); }
-// canonical x mod (2^31 - 1) for x < 2^51 (one fold: the high part fits 20 bits)
-__device__ __forceinline__ u32 red31s(u64 x) {
-    const u32 lo = (u32)x, hi = (u32)(x >> 32);
-    const u32 r = (lo & (u32)P31) + __builtin_amdgcn_alignbit(hi, lo, 31);
-    return r >= (u32)P31 ? r - (u32)P31 : r;
-}
-
 // ---------------------------------------------------------------------------
-// main pass, streaming form: one wave per stripe of SD = 32 x 512 decisions,
+// main pass, streaming form: one wave per stripe of SD = SNB x 512 decisions,
 // walked block by block with everything in registers (no LDS, no barriers).
 // Lane L owns positions s_k + 8L .. s_k + 8L + 7 of every 512-block k.
+// All fingerprint arithmetic is mod 2^32 (plain wrapping u32 multiply-adds).
 //
 //   bytes   8 per lane and block (one coalesced 512-byte load per wave),
 //           prefetched two blocks ahead
-//   hashes  H(s_k + 8L) (prefix hash relative to the stripe start) from a
-//           lane Horner over 8 bytes + a 6-step wave scan of affine maps;
-//           Phi(s_k + 8L) = H(s_k+1 + 8L) - H(s_k + 8L) * b^512, then 7 rolls
+//   hashes  prefix hash Hp(x) from the stripe start: lane Horner over its 8
+//           bytes, lane starts from a DPP sum scan of h8(L) b^(-8(L+1))
+//           (b odd, so b^-1 exists mod 2^32); Phi(j) = Hp(j+512) - b^512 Hp(j)
 //   minima  van Herk / Gil-Werman with 512-blocks: for decision block c the
 //           wave holds Phi'(block c) and Phi'(block c+1) in registers;
 //           m_i = min(suffix_c, prefix_c+1) from lane-local scans + wave scans
-//   output  i in S  <=>  m_i < inf and (Phi'(i) == m_i or Phi'(i+512) == m_i),
-//           ordered per stripe (capacity SCAP, exact fallback beyond)
-constexpr int SNB = 32;                       // decision blocks per stripe
-constexpr int SD = SNB * (int)TAU;            // decisions per stripe (16384)
-constexpr int SCAP = 512;                     // sync positions per stripe before the fallback
+//   output  i in S  <=>  m_i != INF and min(Phi'(i), Phi'(i+512)) == m_i
+//           (m_i <= both, so this is "either equals m_i"); decisions come out
+//           as 8 wave masks, emitted in position order by a scalar loop
+constexpr int SNB = 64;                       // decision blocks per stripe
+constexpr int SD = SNB * (int)TAU;            // decisions per stripe (32768)
+constexpr int SCAP = 1024;                    // sync positions per stripe before the fallback
 constexpr int SWAVES = 4;                     // independent waves per workgroup
 
-struct sss_pow2 {
-    u32 pw8[8];    // b^(7 - e)
-    u32 b8, ib8;   // b^8 and its inverse mod P31
-    u32 b512;      // b^512 = b^tau
-    u32 bn;        // P - b^tau
+struct sss_pow32 {
+    u32 pwb[8];    // b^e, e < 8
+    u32 b8, ib8;   // b^8 and b^-8 (mod 2^32)
+    u32 B;         // b^512 = b^tau
 };
-
-// canonical x mod (2^31 - 1) for x < 2^32
-__device__ __forceinline__ u32 canon31(u32 r) { return min(r, r - (u32)P31); }
-// < 2^32 and congruent to x mod P31, for x < 2^62; canon31 of it is canonical
-// (a fold of a product of two canonical values never reaches 2 P31)
-__device__ __forceinline__ u32 fold31(u64 x) {
-    return ((u32)x & (u32)P31) + __builtin_amdgcn_alignbit((u32)(x >> 32), (u32)x, 31);
-}
-__device__ __forceinline__ u32 mm31(u32 a, u32 c) { return canon31(fold31((u64)a * c)); }
-__device__ __forceinline__ u32 addm31(u32 a, u32 c) { return canon31(a + c); }
-__device__ __forceinline__ u32 subm31(u32 a, u32 c) { return canon31(a + (u32)P31 - c); }
 
 // wave scans by DPP (gfx9 row shifts + row broadcasts; no LDS round trips)
 template <int CTRL, int ROWM = 0xF>
@@ -350,13 +326,13 @@ __device__ __forceinline__ u32 wave_prefix_min(u32 v) {  // inclusive, over lane
     v = min(v, dpp<0x143, 0xC>(INF32, v));
     return v;
 }
-__device__ __forceinline__ u32 wave_prefix_addm31(u32 v) {  // inclusive sums mod P31
-    v = addm31(v, dpp<0x111>(0, v));
-    v = addm31(v, dpp<0x112>(0, v));
-    v = addm31(v, dpp<0x114>(0, v));
-    v = addm31(v, dpp<0x118>(0, v));
-    v = addm31(v, dpp<0x142, 0xA>(0, v));
-    v = addm31(v, dpp<0x143, 0xC>(0, v));
+__device__ __forceinline__ u32 wave_prefix_add(u32 v) {  // inclusive sums mod 2^32
+    v += dpp<0x111>(0, v);
+    v += dpp<0x112>(0, v);
+    v += dpp<0x114>(0, v);
+    v += dpp<0x118>(0, v);
+    v += dpp<0x142, 0xA>(0, v);
+    v += dpp<0x143, 0xC>(0, v);
     return v;
 }
 __device__ __forceinline__ u32 wave_suffix_min(u32 v, u32 lane) {  // inclusive, over lanes >= L
@@ -374,107 +350,104 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
                                                            const u16* __restrict__ qinfo, u64 nstripes,
                                                            u32* __restrict__ s_out, u32* __restrict__ s_cnt,
                                                            u32* __restrict__ s_flag, u32* __restrict__ any_flag,
-                                                           u32 b, sss_pow2 PW) {
+                                                           u32 b, sss_pow32 PW) {
     const u32 lane = threadIdx.x & 63;
     const u64 w = (u64)blockIdx.x * SWAVES + (threadIdx.x >> 6);
     if (w >= nstripes) return;  // whole wave
     const u64 i0 = w * (u64)SD;
     const u64 jmax = n - TAU;                  // last position with a full window (n >= 2 tau here)
     const u64 ilim = min<u64>(last_i - i0, (u64)SD - 1);  // decisions i0 + u, u <= ilim
-    // per-lane powers: pwl = b^(8 lane), ipw = b^(-8 (lane + 1))
-    u32 pwl = 1, ipw = PW.ib8;
+    // per-lane powers: pwl = b^(8 lane), ibl = b^(-8 (lane + 1))
+    u32 pwl = 1, ibl = PW.ib8;
     {
         u32 f = PW.b8, g = PW.ib8;
         for (int d = 0; d < 6; d++) {
             if (lane & (1u << d)) {
-                pwl = mm31(pwl, f);
-                ipw = mm31(ipw, g);
+                pwl *= f;
+                ibl *= g;
             }
-            f = mm31(f, f);
-            g = mm31(g, g);
+            f *= f;
+            g *= g;
         }
     }
+    const u32 nB = 0u - PW.B;
     auto load8 = [&](u64 k) -> u64 { return *(const u64*)(T + i0 + k * TAU + 8 * lane); };
-    // A_k(lane) = H(s_k + 8 lane) b^(-8 lane) for block k from its bytes, where H
-    // is the prefix hash from the stripe start: with g = h8(lane) b^(-8(lane+1)),
-    // A = carry + (exclusive prefix sum of g), a plain DPP sum scan mod P31.
-    // carry = H(s_k) in, H(s_k+1) = b^512 (carry + sum of all g) out
-    auto block_hash = [&](u64 bytes, u32& carry) -> u32 {
+    // Hp(s_k + 8 lane + e), e < 8, into h; carry = Hp(s_k) in, Hp(s_k+1) out (uniform)
+    auto block_prefix = [&](u64 bytes, u32& carry, u32* h) {
         const u32 lo = (u32)bytes, hi = (u32)(bytes >> 32);
-        u64 acc = 0;
+        u32 c[8], loc[8];
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            const u32 c = ((e < 4 ? lo : hi) >> (8 * (e & 3))) & 255u;
-            acc += (u64)c * PW.pw8[e];
-        }
-        const u32 g = mm31(canon31(fold31(acc)), ipw);
-        const u32 G = wave_prefix_addm31(g);
-        const u32 A = addm31(carry, subm31(G, g));
-        carry = mm31(addm31(carry, (u32)__builtin_amdgcn_readlane((int)G, 63)), PW.b512);
-        return A;
+        for (int e = 0; e < 8; e++) c[e] = ((e < 4 ? lo : hi) >> (8 * (e & 3))) & 255u;
+        loc[0] = 0;
+#pragma unroll
+        for (int e = 1; e < 8; e++) loc[e] = loc[e - 1] * b + c[e - 1];
+        const u32 h8 = loc[7] * b + c[7];
+        const u32 g = h8 * ibl;
+        const u32 G = wave_prefix_add(g);
+        const u32 hl = (carry + (G - g)) * pwl;  // Hp(s_k + 8 lane)
+        h[0] = hl;
+#pragma unroll
+        for (int e = 1; e < 8; e++) h[e] = hl * PW.pwb[e] + loc[e];
+        carry = (carry + (u32)__builtin_amdgcn_readlane((int)G, 63)) * PW.B;
     };
-    // Phi'(s_k + 8 lane + e), e < 8, into v
-    auto phi_block = [&](u64 k, u32 h0, u32 h1, u64 bo, u64 bi, u16 q0, u16 q1, u32* v) {
-        // Phi(s_k + 8 lane) = H(s_k+1 + 8 lane) - H(s_k + 8 lane) b^512 = b^(8 lane) (A_k+1 - A_k b^512)
-        u32 fp = mm31(subm31(h1, mm31(h0, PW.b512)), pwl);
-        const u32 olo = (u32)bo, ohi = (u32)(bo >> 32), ilo = (u32)bi, ihi = (u32)(bi >> 32);
+    // Phi'(s_k + 8 lane + e) from the prefix hashes of blocks k and k+1; returns
+    // whether the wave has an INF (Q window or past the last full window) in it.
+    // q holds the Q intervals of the block's 5 anchors (s_k/128 + 0..4), loaded
+    // by the whole wave as one scalar load: the per-lane test runs only when one
+    // of them is non-empty
+    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) -> int {
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            v[e] = fp;
-            if (e < 7) {
-                const u32 in = ((e < 4 ? ilo : ihi) >> (8 * (e & 3))) & 255u;
-                const u32 out = ((e < 4 ? olo : ohi) >> (8 * (e & 3))) & 255u;
-                fp = canon31(fold31((u64)fp * b + in + (u64)out * PW.bn));
-            }
-        }
-        const u64 j0 = i0 + k * TAU + 8 * lane;
+        for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
         const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
-        if (__builtin_expect(__ballot(q0 != 0xFF00 || q1 != 0xFF00) != 0 || endblk, 0)) {
-            const u64 ta = (j0 + 127) >> 7;
+        const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
+        if (__builtin_amdgcn_readfirstlane((int)(anyq || endblk))) {
+            const u64 j0 = i0 + k * TAU + 8 * lane;
+            const u32 qa[5] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu};
+            const u32 ta = (8 * lane + 127) >> 7;  // anchor of the lane's first position (0..4)
+            u32 q0 = 0xFF00, q1 = 0xFF00;
+#pragma unroll
+            for (u32 r = 0; r < 5; r++) {
+                if (ta == r) q0 = qa[r];
+                if (ta + 1 == r) q1 = qa[r];
+            }
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 const u64 j = j0 + e;
                 if (j > jmax) {
                     v[e] = INF32;
                 } else {
-                    const u64 t = (j + 127) >> 7;
-                    const u16 qi = t == ta ? q0 : q1;
-                    const u32 rel = (u32)(j + 127 - (t << 7));
-                    if (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) v[e] = INF32;
+                    const u32 t = (8 * lane + e + 127) >> 7;
+                    const u32 qi = t == ta ? q0 : q1;
+                    const u32 rel = (u32)((8 * lane + e + 127) & 127);
+                    if (rel >= (qi >> 8) && rel <= (qi & 255)) v[e] = INF32;
                 }
             }
+            return 1;
         }
+        return 0;
     };
-    auto loadq = [&](u64 k, u16& q0, u16& q1) {
-        const u64 j0 = i0 + k * TAU + 8 * lane;
-        const u64 ta = (j0 + 127) >> 7;
-        q0 = q1 = 0xFF00;
-        if (j0 <= jmax) {
-            q0 = qinfo[ta];
-            if ((j0 & 127) == 0 && j0 + 1 <= jmax) q1 = qinfo[ta + 1];
-        }
-    };
+    // Q intervals of the anchors of block k (uniform address: a scalar load)
+    auto loadq = [&](u64 k) -> uint4 { return *(const uint4*)(qinfo + ((i0 + k * TAU) >> 7)); };
 
-    // prologue: H for blocks 0 and 1, Phi'(block 0)
+    // prologue: Hp for blocks 0 and 1, Phi'(block 0)
     u32 carry = 0;
-    u64 B0 = load8(0), B1 = load8(1), B2 = load8(2);
-    u16 qa0, qa1, qb0, qb1;
-    loadq(0, qa0, qa1);
-    loadq(1, qb0, qb1);
-    const u32 H0 = block_hash(B0, carry);
-    u32 H1 = block_hash(B1, carry);
-    u32 x[8], y[8];
-    phi_block(0, H0, H1, B0, B1, qa0, qa1, x);
+    u64 Ba = load8(2), Bb = load8(3);
+    const uint4 qa = loadq(0);
+    uint4 qb = loadq(1);
+    u32 hA[8], hB[8], xA[8], xB[8];
+    block_prefix(load8(0), carry, hA);
+    block_prefix(load8(1), carry, hB);
+    int infA = phi_block(0, hA, hB, qa, xA), infB = 0;
     u32 nout = 0;       // outputs of this stripe so far (uniform)
     u32* out = s_out + w * SCAP;
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
-    for (u32 c = 0; c < nblk; c++) {
-        // block c+2: bytes (prefetched), hash; block c+1: Phi'
-        const u64 B3 = load8(c + 3);  // prefetch (the text pad covers the stripe's end)
-        u16 qc0, qc1;
-        loadq(c + 2, qc0, qc1);
-        const u32 H2 = block_hash(B2, carry);
-        phi_block(c + 1, H1, H2, B1, B2, qb0, qb1, y);
+    // one decision block: x = Phi'(block c) (in), y = Phi'(block c+1) (out),
+    // h0 = Hp(block c+1) (in), h1 <- Hp(block c+2); B = bytes of block c+2
+    auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, int infx, int& infy, uint4& qn) {
+        const uint4 qc = loadq(c + 2);
+        block_prefix(B, carry, h1);
+        infy = phi_block(c + 1, h0, h1, qn, y);
+        qn = qc;
         // window minima for decisions of block c
         u32 sx[8], py[8];
         sx[7] = x[7];
@@ -487,42 +460,49 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
         const u32 suf_after = dpp<0x130>(INF32, sufL);   // wave_shl:1 -> lane + 1 (63: inf)
         const u32 pre_before = dpp<0x138>(INF32, preL);  // wave_shr:1 -> lane - 1 (0: inf)
         const u32 g = min(suf_after, pre_before);
-        u32 mk = 0;
+        u64 M[8];
+        u64 U = 0;
 #pragma unroll
         for (int e = 0; e < 8; e++) {
             const u32 m = min(min(sx[e], g), py[e]);
-            if (m != INF32 && (x[e] == m || y[e] == m)) mk |= 1u << e;
+            M[e] = __ballot(min(x[e], y[e]) == m);
+            U |= M[e];
         }
-        if (c * TAU + TAU - 1 > ilim) {  // last block of the last stripe
-            const int64_t keep = (int64_t)ilim - (int64_t)(c * TAU + 8 * lane) + 1;  // decisions of this lane kept
-            mk &= keep <= 0 ? 0u : keep >= 8 ? 0xFFu : (1u << keep) - 1;
-        }
-        // ordered output: rank = sum of popc over lower lanes (4 ballots on the bits of popc)
-        const u64 anyb = __ballot(mk != 0);
-        if (anyb) {
-            const u32 pc = __popc(mk);
-            u32 rank = 0, tot = 0;
+        if (__builtin_amdgcn_readfirstlane(infx | infy)) {  // windows may be all INF
+            U = 0;
 #pragma unroll
-            for (int bit = 0; bit < 4; bit++) {
-                const u64 bb = __ballot((pc >> bit) & 1);
-                rank += (u32)__popcll(bb & ((1ull << lane) - 1)) << bit;
-                tot += (u32)__popcll(bb) << bit;
+            for (int e = 0; e < 8; e++) {
+                const u32 m = min(min(sx[e], g), py[e]);
+                M[e] &= __ballot(m != INF32);
+                U |= M[e];
             }
-            u32 o = nout + rank;
-            for (u32 mm = mk; mm; mm &= mm - 1) {
-                if (o < (u32)SCAP) out[o] = (u32)(i0 + c * TAU + 8 * lane + __builtin_ctz(mm));
-                o++;
-            }
-            nout += tot;
         }
-        // shift the pipeline
+        if (U) {
+            // ordered emission (lanes ascending, then e) by a scalar loop: ~2 outputs per block
+            const u32 base = (u32)(i0 + c * TAU);
+            for (u64 u = U; u; u &= u - 1) {
+                const u32 L = (u32)__builtin_ctzll(u);
+                u32 bits = 0;
 #pragma unroll
-        for (int e = 0; e < 8; e++) x[e] = y[e];
-        H1 = H2;
-        B1 = B2;
-        B2 = B3;
-        qb0 = qc0;
-        qb1 = qc1;
+                for (int e = 0; e < 8; e++) bits |= (u32)((M[e] >> L) & 1) << e;
+                for (; bits; bits &= bits - 1) {
+                    const u32 pos = base + 8 * L + (u32)__builtin_ctz(bits);
+                    if ((u64)pos - i0 <= ilim) {
+                        if (lane == 0 && nout < (u32)SCAP) out[nout] = pos;
+                        nout++;
+                    }
+                }
+            }
+        }
+    };
+    for (u32 c = 0; c < nblk; c += 2) {
+        u64 Bn = load8(c + 4);  // prefetch (the text pad covers the stripe's end)
+        step(c, xA, xB, hB, hA, Ba, infA, infB, qb);
+        Ba = Bn;
+        if (c + 1 >= nblk) break;
+        Bn = load8(c + 5);
+        step(c + 1, xB, xA, hA, hB, Bb, infB, infA, qb);
+        Bb = Bn;
     }
     if (lane == 0) {
         s_cnt[w] = nout;
@@ -535,31 +515,31 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
 // recomputes the stripe's Phi' values and the window minima directly.
 __global__ __launch_bounds__(256) void k_sss_fallback(const u8* __restrict__ T, u64 n, u64 last_i,
                                                       const u16* __restrict__ qinfo, const u32* __restrict__ lanes,
-                                                      u64* __restrict__ scratch, u8* __restrict__ member,
+                                                      u32* __restrict__ scratch, u8* __restrict__ member,
                                                       u32* __restrict__ ovf_out, u32* __restrict__ lane_cnt, u32 b,
-                                                      u64 bpow) {
+                                                      u32 bpow) {
     const u64 lane = lanes[blockIdx.x];
     const u64 i0 = lane * SD;
     const u64 i_end = min(i0 + SD, last_i + 1);
     const u64 j_end = min(i0 + SD + TAU - 1, n - TAU);
-    u64* v = scratch + (u64)blockIdx.x * (SD + TAU);
+    u32* v = scratch + (u64)blockIdx.x * (SD + TAU);
     u8* mem = member + (u64)blockIdx.x * SD;
     if (threadIdx.x == 0) {
-        u64 fp = 0;
-        for (u64 k = 0; k < TAU; k++) fp = (fp * b + T[i0 + k]) % P31;
+        u32 fp = 0;
+        for (u64 k = 0; k < TAU; k++) fp = fp * b + T[i0 + k];
         for (u64 j = i0; j <= j_end; j++) {
             const u64 t = (j + 127) >> 7;
             const u16 qi = qinfo[t];
             const u32 rel = (u32)(j + 127 - (t << 7));
-            v[j - i0] = (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) ? INF64 : fp;
-            if (j < j_end) fp = (fp * b + T[j + TAU] + (P31 - bpow) * T[j]) % P31;
+            v[j - i0] = (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) ? INF32 : fp;
+            if (j < j_end) fp = fp * b + T[j + TAU] - bpow * T[j];
         }
     }
     __syncthreads();
     for (u64 i = i0 + threadIdx.x; i < i_end; i += blockDim.x) {
-        u64 m = INF64;
+        u32 m = INF32;
         for (u64 x = 0; x <= TAU; x++) m = min(m, v[i - i0 + x]);
-        mem[i - i0] = (m != INF64 && (v[i - i0] == m || v[i - i0 + TAU] == m));
+        mem[i - i0] = (m != INF32 && (v[i - i0] == m || v[i - i0 + TAU] == m));
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -581,11 +561,11 @@ __global__ void k_sss_compact(const u32* __restrict__ lane_out, const u32* __res
     for (u32 x = 0; x < c; x++) S[o + x] = src[x];
 }
 
-static u64 pow31_host(u64 b, u64 e) {
-    u64 r = 1;
+static u32 pow32_host(u32 b, u64 e) {
+    u32 r = 1;
     while (e) {
-        if (e & 1) r = r * b % P31;
-        b = b * b % P31;
+        if (e & 1) r *= b;
+        b *= b;
         e >>= 1;
     }
     return r;
@@ -599,7 +579,7 @@ void engine::build_sss(const u8* T) {
     if (n < 2 * (u64)TAU) return;
     const u64 last_i = n - 2 * TAU;
     const u64 nanch = (n - TAU) / QA + 2;
-    u16* qi = q_info.get(nanch);
+    u16* qi = q_info.get(nanch + 64);  // k_sss_stream reads 8 anchors per block, up to 2 blocks past n
     u32* ctr = counters.get(16);
     LZ_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st));
     u8* rp = run_p.get(nanch);
@@ -626,17 +606,12 @@ void engine::build_sss(const u8* T) {
     u32* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
-    sss_pow2 PW;
-    {
-        auto mm = [](u64 x, u64 y) { return x * y % P31; };
-        (void)mm;
-        PW.b8 = (u32)pow31_host(SSS_BASE, 8);
-        PW.ib8 = (u32)pow31_host(PW.b8, P31 - 2);  // Fermat inverse
-        for (int e = 0; e < 8; e++) PW.pw8[e] = (u32)pow31_host(SSS_BASE, 7 - e);
-        PW.b512 = (u32)pow31_host(SSS_BASE, TAU);
-        PW.bn = (u32)((P31 - PW.b512) % P31);
-    }
-    const u64 bpow = PW.b512;
+    sss_pow32 PW;
+    for (int e = 0; e < 8; e++) PW.pwb[e] = pow32_host(SSS_BASE, e);
+    PW.b8 = pow32_host(SSS_BASE, 8);
+    PW.ib8 = pow32_host(PW.b8, (1ull << 31) - 1);  // b8^(2^31 - 1) = b8^-1 (odd units mod 2^32 have order | 2^30)
+    PW.B = pow32_host(SSS_BASE, TAU);
+    const u32 bpow = PW.B;
     hipEvent_t e0, e1;
     LZ_HIP(hipEventCreate(&e0));
     LZ_HIP(hipEventCreate(&e1));
@@ -668,7 +643,7 @@ void engine::build_sss(const u8* T) {
         u32* d_lanes = u32d.get(lanes.size());
         LZ_HIP(hipMemcpy(d_lanes, lanes.data(), lanes.size() * 4, hipMemcpyHostToDevice));
         LZ_HIP(hipMemcpy(ovf_slot, slot.data(), nlanes * 4, hipMemcpyHostToDevice));
-        u64* scratch = u64a.get(lanes.size() * (SD + TAU));
+        u32* scratch = (u32*)u64a.get(lanes.size() * (SD + TAU));
         u8* member = tmp_bytes.get(lanes.size() * SD);
         ovf_out = u32b.get(lanes.size() * SD);
         k_sss_fallback<<<(unsigned)lanes.size(), 256, 0, st>>>(T, n, last_i, qi, d_lanes, scratch, member, ovf_out,

@@ -25,9 +25,8 @@ constexpr u32 QL = TAU / 3;  // period bound of Q (170)
 constexpr u32 QM = 2 * QL;   // anchor probe length (340)
 constexpr u32 QA = 128;      // anchor stride
 constexpr u64 P61 = (1ull << 61) - 1;
-constexpr u64 P31 = (1ull << 31) - 1;  // SSS fingerprint modulus (Mersenne)
-constexpr u32 INF32 = 0xFFFFFFFFu;
-constexpr u64 SSS_BASE = 296819;
+constexpr u32 INF32 = 0xFFFFFFFFu;  // Phi' of Q windows (and of windows hashing to 2^32-1)
+constexpr u32 SSS_BASE = 296819;  // odd: invertible mod 2^32
 constexpr u64 INF64 = ~0ull;
 constexpr u32 NONE = 0xFFFFFFFFu;
 // zero bytes allocated past n in the HBM text buffer: lets vector loads and

@@ -16,7 +16,7 @@
 //     reference sources that DO ship, and pins everything the missing code and
 //     std::random_device left open:
 //       - the tau-synchronizing set (SSS) definition (Kempa-Kociumaka) with
-//         Phi = Karp-Rabin mod 2^61-1, base SSS_BASE (section "SSS" below);
+//         Phi = polynomial hash mod 2^32, base SSS_BASE (section "SSS" below);
 //       - SA_S = true suffix order of the sync positions;
 //       - exact LCE (any exact method gives the same values);
 //       - the 5 gap-index rk_prime<107> bases drawn from mt19937_64(rk_seed)
@@ -88,25 +88,25 @@ static inline u32 lce_left(const u8* T, u32 i, u32 j, u32 cap = 0xFFFFFFFFu) {
 //  SSS  (definition pinned here; upstream lce::rolling_hash::sss is absent,
 //        called at lce_sss.hpp:53)
 //
-//  Phi(j)  = sum_{k<tau} T[j+k] * b^(tau-1-k)  mod (2^31-1),  b = SSS_BASE,
-//            for j in [0, n-tau]                       (Karp-Rabin, canonical)
+//  Phi(j)  = sum_{k<tau} T[j+k] * b^(tau-1-k)  mod 2^32,  b = SSS_BASE (odd),
+//            for j in [0, n-tau]                 (polynomial hash over Z/2^32)
 //  Q       = { j in [0,n-tau] : T[j..j+tau) has a period p <= floor(tau/3) }
-//  Phi'(j) = Phi(j) if j not in Q, else +inf
-//  S       = { i in [0,n-2tau] : m_i = min Phi'[i..i+tau] < inf  and
+//  Phi'(j) = Phi(j) if j not in Q, else INF = 2^32-1  (a window whose Phi is
+//            2^32-1 therefore behaves as a Q window; Phi' stays a function of
+//            the window's content, which is all the SSS consistency needs)
+//  S       = { i in [0,n-2tau] : m_i = min Phi'[i..i+tau] != INF  and
 //                                (Phi'(i) == m_i or Phi'(i+tau) == m_i) }
 //  has_runs = (Q is non-empty)
 // ===========================================================================
-static constexpr u64 P31 = (1ull << 31) - 1;  // Mersenne prime of the SSS fingerprint
 static constexpr u64 SSS_BASE = 296819;
-static constexpr u64 SSS_INF = ~0ull;
+static constexpr u64 SSS_INF = 0xFFFFFFFFull;
 static constexpr u32 QL = TAU / 3;      // period bound floor(tau/3) = 170
 static constexpr u32 QM = 2 * QL;       // probe length 340
 static constexpr u32 QA = 128;          // anchor stride (<= tau - 2L + 1)
 
-static inline u64 mod31(u64 x) { return x % P31; }
-static inline u64 pow31(u64 b, u64 e) {
-    u64 r = 1;
-    while (e) { if (e & 1) r = mod31(r * b); b = mod31(b * b); e >>= 1; }
+static inline u32 pow32(u32 b, u64 e) {
+    u32 r = 1;
+    while (e) { if (e & 1) r *= b; b *= b; e >>= 1; }
     return r;
 }
 
@@ -148,8 +148,7 @@ static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
     const u64 last_i = n - 2 * TAU;          // sync candidates i in [0, last_i]
     const u64 BLK = 1 << 20;
     const u64 nblk = last_i / BLK + 1;
-    const u64 bpow = pow31(SSS_BASE, TAU);
-    const u64 negpow = (P31 - bpow) % P31;
+    const u32 bpow = pow32((u32)SSS_BASE, TAU);
     std::vector<std::vector<u32>> part(nblk);
     std::vector<u8> runs_flag(nblk, 0);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -168,12 +167,12 @@ static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
             if (a + QM <= n) anchor_q(T, n, a, jlo, jhi, q.data(), b);
         }
         std::vector<u64> phi(m);
-        u64 fp = 0;
-        for (u64 k = 0; k < TAU; k++) fp = mod31(fp * SSS_BASE + T[b + k]);
+        u32 fp = 0;
+        for (u64 k = 0; k < TAU; k++) fp = fp * (u32)SSS_BASE + T[b + k];
         for (u64 j = b; j <= je; j++) {
             phi[j - b] = q[j - b] ? SSS_INF : fp;
             if (q[j - b]) runs_flag[bi] = 1;
-            if (j < je) fp = mod31(fp * SSS_BASE + T[j + TAU] + negpow * T[j]);
+            if (j < je) fp = fp * (u32)SSS_BASE + T[j + TAU] - bpow * T[j];
         }
         // sliding-window minimum over [i, i+tau] (monotone deque of indices)
         std::vector<u64> dq(m);

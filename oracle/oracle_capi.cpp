@@ -71,14 +71,15 @@ void oracle_q_bruteforce(const uint8_t* T, uint64_t n, uint8_t* q) {
     if (n < TAU) return;
     for (u64 j = 0; j + TAU <= n; j++) q[j] = q_bruteforce(T, j);
 }
-// Phi' (tests): phi[j] for j in [0, n-tau], SSS_INF for Q
+// Phi' (tests): phi[j] for j in [0, n-tau], SSS_INF = 2^32-1 for Q
 void oracle_phi(const uint8_t* T, uint64_t n, uint64_t* phi) {
     if (n < TAU) return;
-    u64 bp = pow31(SSS_BASE, TAU), neg = (P31 - bp) % P31, fp = 0;
-    for (u64 k = 0; k < TAU; k++) fp = mod31(fp * SSS_BASE + T[k]);
+    const u32 bp = pow32((u32)SSS_BASE, TAU);
+    u32 fp = 0;
+    for (u64 k = 0; k < TAU; k++) fp = fp * (u32)SSS_BASE + T[k];
     for (u64 j = 0; j + TAU <= n; j++) {
         phi[j] = q_bruteforce(T, j) ? SSS_INF : fp;
-        if (j + TAU < n) fp = mod31(fp * SSS_BASE + T[j + TAU] + neg * T[j]);
+        if (j + TAU < n) fp = fp * (u32)SSS_BASE + T[j + TAU] - bp * T[j];
     }
 }
 

@@ -14,24 +14,25 @@ import pytest
 from conftest import golden_names, load_golden
 
 TAU = 512
-P31 = (1 << 31) - 1
+M32 = 1 << 32
 BASE = 296819
+INF32 = M32 - 1
 
 
 def phi_py(T):
-    """Φ(j) = Σ_k T[j+k]·b^(τ−1−k) mod 2^31−1 by a Python-int rolling hash."""
+    """Φ(j) = Σ_k T[j+k]·b^(τ−1−k) mod 2^32 by a Python-int rolling hash."""
     n = len(T)
     if n < TAU:
         return np.zeros(0, np.uint64)
-    bp = pow(BASE, TAU, P31)
+    bp = pow(BASE, TAU, M32)
     out = np.zeros(n - TAU + 1, np.uint64)
     h = 0
     t = [int(x) for x in T]
     for k in range(TAU):
-        h = (h * BASE + t[k]) % P31
+        h = (h * BASE + t[k]) % M32
     out[0] = h
     for j in range(1, n - TAU + 1):
-        h = (h * BASE + t[j + TAU - 1] - t[j - 1] * bp) % P31
+        h = (h * BASE + t[j + TAU - 1] - t[j - 1] * bp) % M32
         out[j] = h
     return out
 
@@ -60,12 +61,11 @@ def sss_numpy(T):
         return np.zeros(0, np.uint32)
     ph = phi_py(T).astype(object)
     q = q_numpy(T)
-    INF = 1 << 62
-    php = np.array([INF if q[j] else int(ph[j]) for j in range(len(ph))], dtype=np.int64)
+    php = np.array([INF32 if q[j] else int(ph[j]) for j in range(len(ph))], dtype=np.int64)
     out = []
     for i in range(n - 2 * TAU + 1):
         m = php[i:i + TAU + 1].min()
-        if m < INF and (php[i] == m or php[i + TAU] == m):
+        if m != INF32 and (php[i] == m or php[i + TAU] == m):
             out.append(i)
     return np.array(out, np.uint32)
 
@@ -84,9 +84,9 @@ def planted_text(seed, n=6000, sigma=4):
 
 @pytest.mark.parametrize("sigma", [256, 4])
 def test_phi_matches_python(orc, sigma):
-    """oracle_phi returns Φ' (Φ outside Q, all-ones on Q)."""
+    """oracle_phi returns Φ' (Φ outside Q, 2^32−1 on Q)."""
     T = planted_text(1, 3000, sigma)
-    want = np.where(q_numpy(T), np.uint64(2**64 - 1), phi_py(T))
+    want = np.where(q_numpy(T), np.uint64(INF32), phi_py(T))
     assert np.array_equal(orc.phi(T), want)
 
 
