@@ -299,8 +299,9 @@ __global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restr
 //           wave holds Phi'(block c) and Phi'(block c+1) in registers;
 //           m_i = min(suffix_c, prefix_c+1) from lane-local scans + wave scans
 //   output  i in S  <=>  m_i != INF and min(Phi'(i), Phi'(i+512)) == m_i
-//           (m_i <= both, so this is "either equals m_i"); decisions come out
-//           as 8 wave masks, emitted in position order by a scalar loop
+//           (m_i <= both, so this is "either equals m_i"; the INF test folds into
+//           a clamp of the cross-lane minimum); decisions come out as 8 wave
+//           masks, emitted in position order by a scalar loop
 constexpr int SNB = 64;                       // decision blocks per stripe
 constexpr int SD = SNB * (int)TAU;            // decisions per stripe (32768)
 constexpr int SCAP = 1024;                    // sync positions per stripe before the fallback
@@ -352,7 +353,8 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
                                                            u32* __restrict__ s_flag, u32* __restrict__ any_flag,
                                                            u32 b, sss_pow32 PW) {
     const u32 lane = threadIdx.x & 63;
-    const u64 w = (u64)blockIdx.x * SWAVES + (threadIdx.x >> 6);
+    // the stripe index is wave-uniform: keep it (and every address derived from it) in SGPRs
+    const u64 w = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (w >= nstripes) return;  // whole wave
     const u64 i0 = w * (u64)SD;
     const u64 jmax = n - TAU;                  // last position with a full window (n >= 2 tau here)
@@ -390,12 +392,11 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
         for (int e = 1; e < 8; e++) h[e] = hl * PW.pwb[e] + loc[e];
         carry = (carry + (u32)__builtin_amdgcn_readlane((int)G, 63)) * PW.B;
     };
-    // Phi'(s_k + 8 lane + e) from the prefix hashes of blocks k and k+1; returns
-    // whether the wave has an INF (Q window or past the last full window) in it.
-    // q holds the Q intervals of the block's 5 anchors (s_k/128 + 0..4), loaded
+    // Phi'(s_k + 8 lane + e) from the prefix hashes of blocks k and k+1 (INF for Q
+    // windows and past the last full window).  q holds the Q intervals of the block's 5 anchors (s_k/128 + 0..4), loaded
     // by the whole wave as one scalar load: the per-lane test runs only when one
     // of them is non-empty
-    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) -> int {
+    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
 #pragma unroll
         for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
         const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
@@ -422,9 +423,7 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
                     if (rel >= (qi >> 8) && rel <= (qi & 255)) v[e] = INF32;
                 }
             }
-            return 1;
         }
-        return 0;
     };
     // Q intervals of the anchors of block k (uniform address: a scalar load)
     auto loadq = [&](u64 k) -> uint4 { return *(const uint4*)(qinfo + ((i0 + k * TAU) >> 7)); };
@@ -437,16 +436,16 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     u32 hA[8], hB[8], xA[8], xB[8];
     block_prefix(load8(0), carry, hA);
     block_prefix(load8(1), carry, hB);
-    int infA = phi_block(0, hA, hB, qa, xA), infB = 0;
+    phi_block(0, hA, hB, qa, xA);
     u32 nout = 0;       // outputs of this stripe so far (uniform)
     u32* out = s_out + w * SCAP;
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
     // one decision block: x = Phi'(block c) (in), y = Phi'(block c+1) (out),
     // h0 = Hp(block c+1) (in), h1 <- Hp(block c+2); B = bytes of block c+2
-    auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, int infx, int& infy, uint4& qn) {
+    auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn) {
         const uint4 qc = loadq(c + 2);
         block_prefix(B, carry, h1);
-        infy = phi_block(c + 1, h0, h1, qn, y);
+        phi_block(c + 1, h0, h1, qn, y);
         qn = qc;
         // window minima for decisions of block c
         u32 sx[8], py[8];
@@ -459,37 +458,30 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
         const u32 sufL = wave_suffix_min(sx[0], lane), preL = wave_prefix_min(py[7]);
         const u32 suf_after = dpp<0x130>(INF32, sufL);   // wave_shl:1 -> lane + 1 (63: inf)
         const u32 pre_before = dpp<0x138>(INF32, preL);  // wave_shr:1 -> lane - 1 (0: inf)
-        const u32 g = min(suf_after, pre_before);
+        // clamped to INF-1: then min(x, y) == m' <=> (min(x, y) == m and m != INF), as m <= min(x, y)
+        const u32 g = min(min(suf_after, pre_before), INF32 - 1);
+        // decisions: M[e] = wave mask of lanes whose position 8 lane + e is in S
         u64 M[8];
         u64 U = 0;
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-            const u32 m = min(min(sx[e], g), py[e]);
-            M[e] = __ballot(min(x[e], y[e]) == m);
+            M[e] = __ballot(min(x[e], y[e]) == min(min(sx[e], g), py[e]));
             U |= M[e];
         }
-        if (__builtin_amdgcn_readfirstlane(infx | infy)) {  // windows may be all INF
-            U = 0;
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const u32 m = min(min(sx[e], g), py[e]);
-                M[e] &= __ballot(m != INF32);
-                U |= M[e];
-            }
-        }
         if (U) {
-            // ordered emission (lanes ascending, then e) by a scalar loop: ~2 outputs per block
+            // ordered emission (lanes ascending, then e) by a scalar loop over the
+            // few emitting lanes (~2 per block)
             const u32 base = (u32)(i0 + c * TAU);
             for (u64 u = U; u; u &= u - 1) {
                 const u32 L = (u32)__builtin_ctzll(u);
-                u32 bits = 0;
 #pragma unroll
-                for (int e = 0; e < 8; e++) bits |= (u32)((M[e] >> L) & 1) << e;
-                for (; bits; bits &= bits - 1) {
-                    const u32 pos = base + 8 * L + (u32)__builtin_ctz(bits);
-                    if ((u64)pos - i0 <= ilim) {
-                        if (lane == 0 && nout < (u32)SCAP) out[nout] = pos;
-                        nout++;
+                for (int e = 0; e < 8; e++) {
+                    if ((M[e] >> L) & 1) {
+                        const u32 pos = base + 8 * L + e;
+                        if ((u64)pos - i0 <= ilim) {
+                            if (lane == 0 && nout < (u32)SCAP) out[nout] = pos;
+                            nout++;
+                        }
                     }
                 }
             }
@@ -497,11 +489,11 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     };
     for (u32 c = 0; c < nblk; c += 2) {
         u64 Bn = load8(c + 4);  // prefetch (the text pad covers the stripe's end)
-        step(c, xA, xB, hB, hA, Ba, infA, infB, qb);
+        step(c, xA, xB, hB, hA, Ba, qb);
         Ba = Bn;
         if (c + 1 >= nblk) break;
         Bn = load8(c + 5);
-        step(c + 1, xB, xA, hA, hB, Bb, infB, infA, qb);
+        step(c + 1, xB, xA, hA, hB, Bb, qb);
         Bb = Bn;
     }
     if (lane == 0) {
