@@ -795,21 +795,23 @@ __global__ void k_bm_list(const u32* __restrict__ bm, const u32* __restrict__ fl
         b &= b - 1;
     }
 }
-// intervals -> <= SLOT_CHUNK-position chunks with ranks (rank0 = exclusive scan of
+// intervals -> chunks of <= ch positions with ranks (rank0 = exclusive scan of
 // lengths).  Short chunks keep k_slots (one thread per chunk, a direct
-// fingerprint of <= 64 bytes per pattern, then rolls) wide on the device.
-constexpr u32 SLOT_CHUNK = 128;
+// fingerprint of <= 64 bytes per pattern, then rolls) wide on the device: the
+// chunk length is 128, or 32 when that leaves fewer than ~2^18 chunks.
+constexpr u32 SLOT_CHUNK_LONG = 128, SLOT_CHUNK_SHORT = 32;
 __global__ void k_iv_chunk_counts(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, u32* __restrict__ nch,
-                                  u32* __restrict__ len) {
+                                  u32* __restrict__ nch_short, u32* __restrict__ len) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ni) return;
     const u32 l = en[k] - st[k];
     len[k] = l;
-    nch[k] = (l + SLOT_CHUNK - 1) / SLOT_CHUNK;
+    nch[k] = (l + SLOT_CHUNK_LONG - 1) / SLOT_CHUNK_LONG;
+    nch_short[k] = (l + SLOT_CHUNK_SHORT - 1) / SLOT_CHUNK_SHORT;
 }
 // one thread per chunk; its interval by binary search over the chunk offsets
 __global__ void k_iv_chunks(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, const u32* __restrict__ choff,
-                            u32 nch, const u32* __restrict__ rank, ichunk* __restrict__ ch) {
+                            u32 nch, u32 chl, const u32* __restrict__ rank, ichunk* __restrict__ ch) {
     const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nch) return;
     u32 lo = 0, hi = ni;  // last k with choff[k] <= c (every interval has >= 1 chunk)
@@ -817,8 +819,8 @@ __global__ void k_iv_chunks(const u32* __restrict__ st, const u32* __restrict__ 
         const u32 mid = (lo + hi) >> 1;
         if (choff[mid] <= c) lo = mid; else hi = mid;
     }
-    const u32 q = st[lo] + (u32)(c - choff[lo]) * SLOT_CHUNK;
-    ch[c] = ichunk{q, min(en[lo], q + SLOT_CHUNK), rank[lo] + (q - st[lo])};
+    const u32 q = st[lo] + (u32)(c - choff[lo]) * chl;
+    ch[c] = ichunk{q, min(en[lo], q + chl), rank[lo] + (q - st[lo])};
 }
 // rem[r] = base position r not in I
 __global__ void k_rem_from_bm(const u32* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, u8* __restrict__ rem) {
@@ -1157,7 +1159,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         if (mk * 16 >= nslots) k_bucket_dense<<<cdiv(mk + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
         else k_bucket_search<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
     };
-    // runs of a bitmap -> intervals (st, en), ranks, <= SLOT_CHUNK-position chunks
+    // runs of a bitmap -> intervals (st, en), ranks, chunks for k_slots
     auto runs_to_chunks = [&](const u32* bm, dbuf<u32>& dst, dbuf<u32>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
                               u64& npos, u32& nch) -> ichunk* {
         k_bm_count<<<gw, 256, 0, st>>>(bm, nw, ns, ne);
@@ -1172,13 +1174,16 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u32* choff = g_tmp7.get(ni + 1);
         npos = 0;
         nch = 0;
+        u32 chl = SLOT_CHUNK_LONG;
         if (ni) {
-            k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(a, b, ni, nc, len);
+            u32* ncs = g_tmp8.get(ni + 1);
+            k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(a, b, ni, nc, ncs, len);
             npos = excl_scan(len, rk, ni, scan_tmp, st);
-            nch = excl_scan(nc, choff, ni, scan_tmp, st);
+            if (npos < (u64)SLOT_CHUNK_LONG << 18) chl = SLOT_CHUNK_SHORT;
+            nch = excl_scan(chl == SLOT_CHUNK_LONG ? nc : ncs, choff, ni, scan_tmp, st);
         }
         ichunk* ch = (ichunk*)dch.get(std::max<u64>(1, nch) * sizeof(ichunk));
-        if (nch) k_iv_chunks<<<cdiv(nch, 256), 256, 0, st>>>(a, b, ni, choff, nch, rk, ch);
+        if (nch) k_iv_chunks<<<cdiv(nch, 256), 256, 0, st>>>(a, b, ni, choff, nch, chl, rk, ch);
         return ch;
     };
     auto build_base = [&](const u32* bm) {

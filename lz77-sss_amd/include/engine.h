@@ -129,7 +129,7 @@ struct engine {
     u64 seg_at_n = 0;
     dbuf<u32> g_succ, g_seg_at, g_cbv, g_ids, g_chain, g_dist[2];
     dbuf<u32> g_bmI, g_bmI2, g_bmIb, g_bmT;
-    dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_ast, g_aen, g_ark;
+    dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_tmp8, g_ast, g_aen, g_ark;
     dbuf<u64> g_offs;
     // LPF/LNF mode (csrc/lnf.hip)
     dbuf<u32> l_V, l_b, l_d, l_e, l_r, l_sflag_lnf, l_slots_lnf, l_sflag, l_slots, l_off, l_P, l_Q;
