@@ -8,6 +8,9 @@
  *   lz77sss_factorize_approx_u32  <- lz77_sss<uint32_t>::factorize_approximate
  *                                    <fact_mode, phr_mode, tau>(input, n, output, params)
  *                                    include/lz77_sss/lz77_sss.hpp:176-186
+ *   lz77sss_factorize_exact_u32   <- lz77_sss<uint32_t>::factorize_exact
+ *                                    <fact_mode, phr_mode, transf_mode, range_ds_t, tau>(input, n, output, params)
+ *                                    include/lz77_sss/lz77_sss.hpp:188-200,333-357
  *   lz77sss_decode_u32            <- lz77_sss<uint32_t>::decode(fact_it, out_it, n)
  *                                    include/lz77_sss/lz77_sss.hpp:202-203,
  *                                    include/lz77_sss/algorithms/common.cpp:31-54
@@ -42,6 +45,9 @@ extern "C" {
 enum { LZ77SSS_LPF_NAIVE = 0, LZ77SSS_LPF_LNF_NAIVE = 1, LZ77SSS_LPF_OPT = 2, LZ77SSS_LPF_LNF_OPT = 3 };
 /* enum factorize_mode, lz77_sss.hpp:55-59 (same numeric values) */
 enum { LZ77SSS_GREEDY_NAIVE = 0, LZ77SSS_GREEDY = 1, LZ77SSS_SKIP_PHRASES = 2 };
+
+/* enum transform_mode, lz77_sss.hpp:60-64 (same numeric values) */
+enum { LZ77SSS_TRANSF_NAIVE = 0, LZ77SSS_TRANSF_WITH_SAMPLES = 1, LZ77SSS_TRANSF_WITHOUT_SAMPLES = 2 };
 
 enum {
     LZ77SSS_OK = 0,
@@ -82,6 +88,19 @@ typedef int (*lz77sss_emit_fn)(const lz77sss_factor32* batch, uint64_t count, vo
 int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
                                  lz77sss_emit_fn emit, void* user);
 
+/* One-shot exact factorization (greedy LZ77: every factor is a longest previous
+ * factor; a copy {src, len >= 1} or the literal {char, 0} when the character is
+ * new).  The factor lengths are the canonical greedy LZ77 ones, as the
+ * reference's exact modes produce at p = 1; the sources follow a fixed rule
+ * (the longer of the PSV/NSV candidates in suffix-array order, the earlier one
+ * on ties) instead of the reference's sample/range-structure visit order.
+ * transf_mode (naive / with_samples / without_samples) and the range structure
+ * of the reference select different ways to the same lengths; all are
+ * accepted and computed by the one device algorithm (csrc/exact.hip).
+ * Requires n < 2^31. */
+int lz77sss_factorize_exact_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm, int transf_mode,
+                                lz77sss_emit_fn emit, void* user);
+
 /* Decode nf factors into out[0..n) (host memory), algorithms/common.cpp:31-54. */
 int lz77sss_decode_u32(const lz77sss_factor32* factors, uint64_t nf, uint8_t* out, uint64_t n);
 
@@ -99,6 +118,9 @@ int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out);
 int lz77sss_session_load(lz77sss_session* s, const uint8_t* text, uint64_t n);
 /* Factorizes the loaded text; factors stay in HBM. */
 int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_params* prm, uint64_t* num_factors);
+/* Exact factorization of the loaded text (see lz77sss_factorize_exact_u32); factors stay in HBM. */
+int lz77sss_session_factorize_exact(lz77sss_session* s, const lz77sss_params* prm, int transf_mode,
+                                    uint64_t* num_factors);
 /* Copies the factors HBM -> host (cap >= num_factors). */
 int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32* out, uint64_t cap);
 /* Decodes the factors of the last factorize call on the device.  out (host,

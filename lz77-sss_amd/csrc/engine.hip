@@ -152,6 +152,17 @@ static void check_params(const lz77sss_params* prm) {
     if (prm->index_log2_size < 0 || prm->index_log2_size > 30) throw lz::error(LZ77SSS_EINVAL, "bad index_log2_size");
 }
 
+// factorize_exact<greedy, lpf_opt, transf_mode, range_ds_t, tau> (lz77_sss.hpp:188-200)
+static void check_exact_params(const lz77sss_params* prm, int transf_mode) {
+    if (!prm) throw lz::error(LZ77SSS_EINVAL, "params is NULL");
+    if (prm->tau != 512) throw lz::error(LZ77SSS_EINVAL, "only tau = 512 is supported");
+    if (prm->fact_mode != LZ77SSS_GREEDY) throw lz::error(LZ77SSS_EINVAL, "exact mode requires fact_mode = greedy");
+    if (prm->phr_mode != LZ77SSS_LPF_OPT && prm->phr_mode != LZ77SSS_LPF_LNF_OPT)
+        throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
+    if (transf_mode < LZ77SSS_TRANSF_NAIVE || transf_mode > LZ77SSS_TRANSF_WITHOUT_SAMPLES)
+        throw lz::error(LZ77SSS_EINVAL, "unsupported transf_mode");
+}
+
 LZ77SSS_API int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out) {
     if (!out) return LZ77SSS_EINVAL;
     *out = nullptr;
@@ -177,6 +188,16 @@ LZ77SSS_API int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_para
     return guarded([&] {
         check_params(prm);
         uint64_t z = s->E.factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0);
+        if (num_factors) *num_factors = z;
+    });
+}
+
+LZ77SSS_API int lz77sss_session_factorize_exact(lz77sss_session* s, const lz77sss_params* prm, int transf_mode,
+                                                uint64_t* num_factors) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        check_exact_params(prm, transf_mode);
+        uint64_t z = s->E.factorize_exact(prm->log != 0);
         if (num_factors) *num_factors = z;
     });
 }
@@ -296,6 +317,35 @@ LZ77SSS_API int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, co
     rc = lz77sss_session_load(s, text, n);
     uint64_t z = 0;
     if (!rc) rc = lz77sss_session_factorize(s, prm, &z);
+    if (!rc && z) {
+        std::vector<lz77sss_factor32> buf;
+        rc = guarded([&] {
+            buf.resize(z);
+            LZ_HIP(hipMemcpy(buf.data(), s->E.fact.p, z * sizeof(lz77sss_factor32), hipMemcpyDeviceToHost));
+        });
+        const uint64_t B = 1 << 16;
+        for (uint64_t o = 0; !rc && o < z; o += B) {
+            if (emit(buf.data() + o, std::min(B, z - o), user) != 0) {
+                g_err = "emit callback aborted";
+                rc = LZ77SSS_ECALLBACK;
+            }
+        }
+    }
+    lz77sss_session_destroy(s);
+    return rc;
+}
+
+LZ77SSS_API int lz77sss_factorize_exact_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
+                                            int transf_mode, lz77sss_emit_fn emit, void* user) {
+    if ((!text && n) || !emit) return LZ77SSS_EINVAL;
+    lz77sss_session* s = nullptr;
+    int rc = guarded([&] { check_exact_params(prm, transf_mode); });
+    if (rc) return rc;
+    rc = lz77sss_session_create(prm->device, n, &s);
+    if (rc) return rc;
+    rc = lz77sss_session_load(s, text, n);
+    uint64_t z = 0;
+    if (!rc) rc = lz77sss_session_factorize_exact(s, prm, transf_mode, &z);
     if (!rc && z) {
         std::vector<lz77sss_factor32> buf;
         rc = guarded([&] {

@@ -137,6 +137,11 @@ struct engine {
     dbuf<u32> g_predk, g_wk, g_ids2;
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
     dbuf<u64> g_xk, g_xk2;
+    // exact mode (csrc/exact.hip)
+    dbuf<u64> x_key, x_key2, x_off, x_wide;
+    dbuf<u32> x_idx, x_idx2, x_rank, x_flag, x_tree, x_lpf, x_src, x_mark, x_chunk;
+    const u32* sa_full = nullptr;    // suffix array of the text (x_idx2) after build_sa_full
+    u32 x_rounds = 0;
     // device decode (csrc/decode.hip)
     dbuf<u32> dec_len, dec_start, dec_fid, dec_ref, dec_ref2;
     dbuf<u8> dec_out;
@@ -160,6 +165,8 @@ struct engine {
     void path_marks(u32 m, u32* nxt0, u32* marks);
     u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override);
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log);
+    void build_sa_full(const u8* T);
+    u64 factorize_exact(bool log);  // csrc/exact.hip
     u64 decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
     lce_view view(const u8* T) const;
 };

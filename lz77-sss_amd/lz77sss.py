@@ -22,6 +22,7 @@ import numpy as np
 
 LPF_NAIVE, LPF_LNF_NAIVE, LPF_OPT, LPF_LNF_OPT = 0, 1, 2, 3   # enum phrase_mode, lz77_sss.hpp:48-53
 GREEDY_NAIVE, GREEDY, SKIP_PHRASES = 0, 1, 2                 # enum factorize_mode, lz77_sss.hpp:55-59
+NAIVE, WITH_SAMPLES, WITHOUT_SAMPLES = 0, 1, 2               # enum transform_mode, lz77_sss.hpp:60-64
 DEFAULT_TAU = 512
 
 _HERE = Path(__file__).resolve().parent
@@ -44,6 +45,9 @@ _SYMBOLS = {
     # name: (restype, argtypes)
     "lz77sss_default_params": (None, [ctypes.POINTER(Params)]),
     "lz77sss_factorize_approx_u32": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), _P, _P]),
+    "lz77sss_factorize_exact_u32": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), ctypes.c_int, _P, _P]),
+    "lz77sss_session_factorize_exact": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.c_int,
+                                                       ctypes.POINTER(_U64)]),
     "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
     "lz77sss_decode_u32_device": (ctypes.c_int, [_P, _U64, _P, _U64, ctypes.c_int]),
     "lz77sss_session_decode": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
@@ -149,6 +153,13 @@ class Session:
         _check(load_library().lz77sss_session_factorize(self._h, ctypes.byref(p), ctypes.byref(z)))
         return z.value
 
+    def factorize_exact(self, transf_mode=WITHOUT_SAMPLES, **kw) -> int:
+        """factorize_exact<greedy, lpf_opt, transf_mode>: canonical greedy LZ77 lengths (csrc/exact.hip)."""
+        p = params(**kw)
+        z = _U64()
+        _check(load_library().lz77sss_session_factorize_exact(self._h, ctypes.byref(p), transf_mode, ctypes.byref(z)))
+        return z.value
+
     def factors(self, z: int) -> np.ndarray:
         out = np.empty((max(z, 1), 2), np.uint32)
         _check(load_library().lz77sss_session_get_factors(self._h, out.ctypes.data_as(_P), z))
@@ -213,6 +224,17 @@ def factorize_approximate(text, fact_mode=GREEDY, phr_mode=LPF_OPT, tau=DEFAULT_
     with Session(max(a.size, 1), device) as s:
         s.load(a)
         z = s.factorize(phr_mode=phr_mode, fact_mode=fact_mode, tau=tau, rk_seed=rk_seed, device=device, log=log)
+        return s.factors(z)
+
+
+def factorize_exact(text, transf_mode=None, fact_mode=GREEDY, phr_mode=LPF_OPT, tau=DEFAULT_TAU, device=0,
+                    log=False) -> np.ndarray:
+    """lz77_sss<>::factorize_exact: returns the (z, 2) uint32 factor array (exact greedy LZ77)."""
+    a = _as_u8(text)
+    with Session(max(a.size, 1), device) as s:
+        s.load(a)
+        z = s.factorize_exact(WITHOUT_SAMPLES if transf_mode is None else transf_mode, phr_mode=phr_mode,
+                              fact_mode=fact_mode, tau=tau, device=device, log=log)
         return s.factors(z)
 
 

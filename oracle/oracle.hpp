@@ -764,6 +764,89 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
     }
 }
 
+// ===========================================================================
+//  Exact greedy LZ77 (factorize_exact, lz77_sss.hpp:188-200,333-357)
+//
+//  The reference's exact modes refine the 3-approximation until every factor
+//  is a longest previous factor, so at p = 1 their factor LENGTHS are the
+//  canonical greedy LZ77 lengths: factor k starts at p_k, has length
+//  max(1, LPF(p_k)) with LPF(p) = max_{j<p} LCE(j, p), and is a literal iff
+//  LPF(p) = 0.  Their SOURCES follow the sample index / range structure's
+//  visit order (transform_to_exact/common.cpp:258-358) and are not restated:
+//  this restatement (and the device path) picks, among the two
+//  Crochemore-Ilie candidates SA[PSV(r)] and SA[NSV(r)] (r = rank of p), the
+//  one with the longer LCE, the smaller position on ties.  Parity of the
+//  lengths is pinned by definition (tests compare with a brute-force LPF on
+//  small inputs); parity of the sources against the reference is unpinned.
+// ===========================================================================
+static constexpr u32 NONE32 = 0xFFFFFFFFu;
+static inline void suffix_array(const u8* T, u64 n, std::vector<u32>& SA) {
+    SA.resize(n);
+    std::vector<u32> R(n), tmp(n);
+    for (u64 i = 0; i < n; i++) { SA[i] = (u32)i; R[i] = T[i] + 1u; }
+    for (u64 h = 1;; h *= 2) {
+        auto key = [&](u32 i) { return std::pair<u32, u32>(R[i], i + h < n ? R[i + h] : 0u); };
+        __gnu_parallel::sort(SA.begin(), SA.end(), [&](u32 a, u32 b) { return key(a) < key(b); });
+        tmp[SA[0]] = 1;
+        for (u64 r = 1; r < n; r++) tmp[SA[r]] = tmp[SA[r - 1]] + (key(SA[r - 1]) < key(SA[r]) ? 1u : 0u);
+        R.swap(tmp);
+        if (R[SA[n - 1]] == n || h > n) break;
+    }
+}
+static inline std::vector<factor> factorize_exact(const u8* T, u64 n) {
+    std::vector<factor> F;
+    if (n == 0) return F;
+    std::vector<u32> SA;
+    suffix_array(T, n, SA);
+    std::vector<u32> ISA(n), LCP(n, 0);
+    for (u64 r = 0; r < n; r++) ISA[SA[r]] = (u32)r;
+    for (u64 i = 0, h = 0; i < n; i++) {  // Kasai
+        if (ISA[i] == 0) { h = 0; continue; }
+        const u64 j = SA[ISA[i] - 1];
+        while (i + h < n && j + h < n && T[i + h] == T[j + h]) h++;
+        LCP[ISA[i]] = (u32)h;
+        if (h) h--;
+    }
+    // sparse table over LCP: min LCP over ranks (a, b]
+    std::vector<std::vector<u32>> sp{LCP};
+    for (u64 k = 1; (1ull << k) <= n; k++) {
+        const auto& pr = sp.back();
+        std::vector<u32> lv(n - (1ull << k) + 1);
+        for (u64 i = 0; i < lv.size(); i++) lv[i] = std::min(pr[i], pr[i + (1ull << (k - 1))]);
+        sp.push_back(std::move(lv));
+    }
+    auto rmq = [&](u64 a, u64 b) {  // min LCP[a+1..b]
+        const u64 l = a + 1, len = b - a, k = 63 - std::countl_zero(len);
+        return std::min(sp[k][l], sp[k][b + 1 - (1ull << k)]);
+    };
+    std::vector<u32> psv(n, NONE32), nsv(n, NONE32), st;
+    for (u64 r = 0; r < n; r++) {
+        while (!st.empty() && SA[st.back()] > SA[r]) st.pop_back();
+        if (!st.empty()) psv[r] = st.back();
+        st.push_back((u32)r);
+    }
+    st.clear();
+    for (u64 r = n; r-- > 0;) {
+        while (!st.empty() && SA[st.back()] > SA[r]) st.pop_back();
+        if (!st.empty()) nsv[r] = st.back();
+        st.push_back((u32)r);
+    }
+    std::vector<u32> lpf(n), src(n);
+    for (u64 r = 0; r < n; r++) {
+        const u32 a = psv[r] != NONE32 ? SA[psv[r]] : NONE32, b = nsv[r] != NONE32 ? SA[nsv[r]] : NONE32;
+        const u64 la = a != NONE32 ? rmq(psv[r], r) : 0, lb = b != NONE32 ? rmq(r, nsv[r]) : 0;
+        const bool pick_a = la > lb || (la == lb && a < b);
+        lpf[SA[r]] = (u32)(pick_a ? la : lb);
+        src[SA[r]] = pick_a ? a : b;
+    }
+    for (u64 p = 0; p < n;) {
+        const u32 l = lpf[p];
+        F.push_back(l ? factor{src[p], l} : factor{T[p], 0});
+        p += std::max<u32>(1, l);
+    }
+    return F;
+}
+
 // decode: restates algorithms/common.cpp:31-54
 static inline void decode(const factor* f, u64 nf, u8* out, u64 n) {
     u64 pos = 0, k = 0;

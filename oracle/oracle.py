@@ -58,6 +58,10 @@ def lib():
         L.oracle_decode.argtypes = [_P, _U64, _P, _U64]
         L.oracle_gap_bases.restype = None
         L.oracle_gap_bases.argtypes = [ctypes.c_uint32, _P]
+        L.oracle_factorize_exact.restype = ctypes.c_int64
+        L.oracle_factorize_exact.argtypes = [_P, _U64, _P, _U64]
+        L.oracle_factorize_exact_timed.restype = ctypes.c_int64
+        L.oracle_factorize_exact_timed.argtypes = [_P, _U64, ctypes.POINTER(ctypes.c_double)]
         L.oracle_num_threads.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         _lib = L
@@ -98,6 +102,26 @@ def factorize_timed(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):
     sec, h = ctypes.c_double(), _U64()
     z = lib().oracle_factorize_timed(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, ctypes.byref(sec), ctypes.byref(h))
     return int(z), sec.value, h.value
+
+
+def factorize_exact(T):
+    """Exact greedy LZ77 restatement (factorize_exact lengths; PSV/NSV source rule) -> (z,2) u32 factors."""
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros((n + 1, 2), np.uint32)
+    z = lib().oracle_factorize_exact(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), n + 1)
+    if z < 0:
+        raise RuntimeError("oracle exact factorization failed")
+    return out[:z].copy()
+
+
+def factorize_exact_timed(T):
+    """Times the exact restatement -> (z, seconds)."""
+    buf = _padded(T)
+    n = _u8(T).size
+    sec = ctypes.c_double()
+    z = lib().oracle_factorize_exact_timed(buf.ctypes.data_as(_P), n, ctypes.byref(sec))
+    return int(z), sec.value
 
 
 def sss(T):

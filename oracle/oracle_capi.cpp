@@ -39,6 +39,21 @@ int64_t oracle_factorize_approx(uint8_t* T, uint64_t n, int phr_mode, uint32_t r
     }
 }
 
+// Exact greedy LZ77 (factorize_exact restatement, oracle.hpp).  Returns z or -1 (cap too small).
+int64_t oracle_factorize_exact(const uint8_t* T, uint64_t n, uint32_t* out, uint64_t cap) {
+    std::vector<factor> F = factorize_exact(T, n);
+    if (F.size() > cap) return -1;
+    for (size_t k = 0; k < F.size(); k++) { out[2 * k] = F[k].src; out[2 * k + 1] = F[k].len; }
+    return (int64_t)F.size();
+}
+// Same, timed (cpu_baseline of the exact mode): factor count, seconds.
+int64_t oracle_factorize_exact_timed(const uint8_t* T, uint64_t n, double* seconds) {
+    const double t0 = omp_get_wtime();
+    std::vector<factor> F = factorize_exact(T, n);
+    *seconds = omp_get_wtime() - t0;
+    return (int64_t)F.size();
+}
+
 // Factor count and wall time only (cpu_baseline); also returns an FNV-1a hash of the stream.
 int64_t oracle_factorize_timed(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed,
                                double* seconds, uint64_t* stream_hash) {

@@ -4,7 +4,8 @@
 The reference ships no golden vectors for this path and cannot
 be built here, so these fixtures pin the oracle restatement itself: every
 fixture holds the input text and the oracle's outputs (S, SA_S, LCP, LPF_opt
-phrases, the factor stream and the approximation statistics).  Texts come
+phrases, the factor stream and the approximation statistics).  The exact-mode stream (factors_exact) follows the oracle's
+PSV/NSV source rule (oracle.hpp, "Exact greedy LZ77").  Texts come
 from numpy's PCG64 or the seeded random_repetitive_string restatement; each
 fixture stores its text, so the fixtures do not depend on any generator.
 
@@ -62,10 +63,12 @@ def main():
         S, has_runs = oracle.sss(T)
         _, SA, LCP = oracle.sa_s(T)
         P = oracle.lpf_opt(T)
+        FX = oracle.factorize_exact(T)
+        assert np.array_equal(oracle.decode(FX, T.size), T)
         np.savez_compressed(HERE / f"{name}.npz", text=T, factors=F, stats=st, factors_lnf=F3, stats_lnf=st3,
-                            sss=S, has_runs=np.array([has_runs]), sa_s=SA, lcp=LCP, lpf=P,
+                            sss=S, has_runs=np.array([has_runs]), sa_s=SA, lcp=LCP, lpf=P, factors_exact=FX,
                             gap_bases_seed42=np.array(oracle.gap_bases(42), np.uint64))
-        print(f"{name}: n={T.size} z={F.shape[0]} z_lnf={F3.shape[0]} |S|={S.size} lpf={P.shape[0]}")
+        print(f"{name}: n={T.size} z={F.shape[0]} z_lnf={F3.shape[0]} z_exact={FX.shape[0]} |S|={S.size} lpf={P.shape[0]}")
 
 
 if __name__ == "__main__":
