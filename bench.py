@@ -92,6 +92,19 @@ def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2):
                       f"restatement with OpenMP stages, {sec:.2f} s"}
 
 
+def cpu_baseline_exact(lz, workload: str, sample_mib: int):
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle  # the CPU port (test/bench infrastructure only)
+
+    n = sample_mib << 20
+    T = make_text(lz, workload, n, 0)
+    z, sec = oracle.factorize_exact_timed(T)
+    return {"value": round(n / sec / 1e6, 2), "unit": "MB/s", "cores": oracle.num_threads(), "kind": "port",
+            "sample": f"{workload}: {sample_mib} MiB instance of the same generator (n={n}, z={z}); the oracle's "
+                      f"exact greedy LZ77 restatement (prefix-doubling SA with a parallel comparison sort, "
+                      f"Kasai LCP, PSV/NSV), not the reference's sample-based transform, {sec:.2f} s"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,6 +114,8 @@ def main():
     ap.add_argument("--size-mib", type=int, default=1024)
     ap.add_argument("--phr-mode", default="lpf_opt", choices=["lpf_opt", "lpf_lnf_opt"],
                     help="lpf_opt = configs[1]; lpf_lnf_opt = configs[2] (LPF/LNF phrases)")
+    ap.add_argument("--mode", default="approx", choices=["approx", "exact"],
+                    help="approx = configs[1]/[2] (3-aprx); exact = configs[4] (exact factorization)")
     ap.add_argument("--cpu-sample-mib", type=int, default=-1,
                     help="oracle sample size in MiB (default: the full workload text, 2-30 s of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -128,8 +143,15 @@ def main():
     sess.load(T)
     t_load = time.perf_counter() - t_load0
 
+    exact = args.mode == "exact"
+
+    def step():
+        if exact:
+            return sess.factorize_exact(device=local_rank)
+        return sess.factorize(device=local_rank, phr_mode=PHR[args.phr_mode])
+
     for _ in range(args.warmup):
-        sess.factorize(device=local_rank, phr_mode=PHR[args.phr_mode])
+        step()
 
     def barrier():
         if dist is not None:
@@ -141,7 +163,7 @@ def main():
     t0 = time.perf_counter()
     z = 0
     for _ in range(args.steps):
-        z = sess.factorize(device=local_rank, phr_mode=PHR[args.phr_mode])
+        z = step()
         ms, b = sess.sss_kernel_time()
         kern_ms.append(ms)
         kern_bytes.append(b)
@@ -167,7 +189,8 @@ def main():
         bytes_launch = kern_bytes[-1]
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
         out = {
-            "metric": f"factorization MB/s (3-aprx LZ77, greedy + {args.phr_mode}, tau=512)",
+            "metric": "factorization MB/s (exact greedy LZ77, factorize_exact, tau=512)" if exact else
+                      f"factorization MB/s (3-aprx LZ77, greedy + {args.phr_mode}, tau=512)",
             "value": round(value, 2),
             "unit": "MB/s",
             "n_gpus": world,
@@ -183,6 +206,7 @@ def main():
             "config": {
                 "workload": f"{args.workload} n={n} ({args.size_mib} MiB) per GPU, pos_t=uint32",
                 "n": n, "tau": 512, "phr_mode": args.phr_mode, "fact_mode": "greedy", "virtual_p": 1,
+                "mode": "exact (configs[4])" if exact else "3-aprx",
                 "parallelism": f"independent-texts x{world}" if world > 1 else "single GPU",
                 "factors": int(z), "comp_ratio": round(n / max(z, 1), 2),
                 "sss_size": int(st[0]) if st else None, "has_runs": bool(st[1]) if st else None,
@@ -207,7 +231,11 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else args.size_mib
-            out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample, PHR[args.phr_mode])
+            if exact:
+                out["cpu_baseline"] = cpu_baseline_exact(lz, args.workload, args.cpu_sample_mib
+                                                         if args.cpu_sample_mib > 0 else 4)
+            else:
+                out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample, PHR[args.phr_mode])
         print(json.dumps(out), flush=True)
     sess.close()
     if dist is not None:

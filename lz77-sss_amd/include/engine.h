@@ -139,8 +139,8 @@ struct engine {
     dbuf<u64> g_xk, g_xk2;
     // exact mode (csrc/exact.hip)
     dbuf<u64> x_key, x_key2, x_off, x_wide;
-    dbuf<u32> x_idx, x_idx2, x_rank, x_flag, x_tree, x_lpf, x_src, x_mark, x_chunk;
-    const u32* sa_full = nullptr;    // suffix array of the text (x_idx2) after build_sa_full
+    dbuf<u32> x_idx, x_idx2, x_sa, x_rank, x_flag, x_tree, x_ltree, x_lcp, x_lpf, x_src, x_mark, x_chunk;
+    const u32* sa_full = nullptr;    // suffix array of the text (x_sa) after build_sa_full
     u32 x_rounds = 0;
     // device decode (csrc/decode.hip)
     dbuf<u32> dec_len, dec_start, dec_fid, dec_ref, dec_ref2;
