@@ -4,6 +4,7 @@
 //
 // A caller of
 //     lz77_sss<uint32_t>::factorize_approximate<greedy, lpf_opt, 512>(T, n, out, {.num_threads = p});
+//     lz77_sss<uint32_t>::factorize_exact<greedy, lpf_opt, with_samples>(T, n, out);
 //     lz77_sss<uint32_t>::decode(fact_it, out_it, n);
 // keeps its code and links against the HIP library instead.  Differences:
 //   * the factorization runs on an MI355X (device `parameters::device`) with the
@@ -25,6 +26,19 @@
 
 enum phrase_mode { lpf_naive, lpf_lnf_naive, lpf_opt, lpf_lnf_opt };   // lz77_sss.hpp:48-53
 enum factorize_mode { greedy_naive, greedy, skip_phrases };            // lz77_sss.hpp:55-59
+enum transform_mode { naive, with_samples, without_samples };          // lz77_sss.hpp:60-64
+
+// Range structures of the reference's exact modes (data_structures/*_range/*.hpp):
+// accepted as template arguments for source compatibility; the device exact
+// path (csrc/exact.hip) does not use them, every choice gives the same lengths.
+template <typename> struct static_weighted_kd_tree {};
+template <typename> struct static_weighted_square_grid {};
+template <typename> struct static_weighted_striped_square {};
+template <typename> struct dynamic_square_grid {};
+template <typename> struct semi_dynamic_square_grid {};
+template <typename> struct decomposed_static_weighted_square_grid {};
+template <typename> struct decomposed_static_weighted_kd_tree {};
+template <typename> struct decomposed_semi_dynamic_square_grid {};
 
 // lz77_sss.hpp:67-70, plus the device-side knobs of this implementation
 struct parameters {
@@ -53,6 +67,8 @@ class lz77_sss {
   public:
     static constexpr phrase_mode default_phr_mode = lpf_opt;
     static constexpr factorize_mode default_fact_mode = greedy;
+    static constexpr transform_mode default_transf_mode = without_samples;
+    template <typename sidx_t> using default_range_ds_t = decomposed_static_weighted_square_grid<sidx_t>;
     static constexpr uint64_t default_tau = 512;
 
     struct factor {  // lz77_sss.hpp:129-147 (same 8-byte layout as lz77sss_factor32)
@@ -86,6 +102,35 @@ class lz77_sss {
             return 0;
         };
         check(lz77sss_factorize_approx_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p, emit, &ctx));
+    }
+
+    // lz77_sss.hpp:188-200: exact factorization (greedy LZ77 lengths; sources by the
+    // device's PSV/NSV rule, see include/lz77sss.h)
+    template <factorize_mode fact_mode = default_fact_mode, phrase_mode phr_mode = default_phr_mode,
+              transform_mode transf_mode = default_transf_mode,
+              template <typename> typename range_ds_t = default_range_ds_t, uint64_t tau = default_tau,
+              typename char_t, typename output_fnc_t>
+    static void factorize_exact(char_t* input, pos_t input_size, output_fnc_t output, parameters params = {}) {
+        static_assert(sizeof(char_t) == 1, "byte alphabet only (lz77_sss.hpp:287)");
+        static_assert(fact_mode != skip_phrases, "lz77_sss.hpp:333");
+        lz77sss_params p;
+        lz77sss_default_params(&p);
+        p.phr_mode = static_cast<int32_t>(phr_mode);
+        p.fact_mode = static_cast<int32_t>(fact_mode);
+        p.tau = static_cast<uint32_t>(tau);
+        p.device = params.device;
+        p.log = params.log ? 1 : 0;
+        p.num_threads = params.num_threads;
+        struct ctx_t {
+            output_fnc_t* out;
+        } ctx{&output};
+        auto emit = [](const lz77sss_factor32* batch, uint64_t count, void* user) -> int {
+            auto* c = static_cast<ctx_t*>(user);
+            for (uint64_t k = 0; k < count; k++) (*c->out)(factor{batch[k].src, batch[k].len});
+            return 0;
+        };
+        check(lz77sss_factorize_exact_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p,
+                                          static_cast<int>(transf_mode), emit, &ctx));
     }
 
     // lz77_sss.hpp:202-203 (algorithms/common.cpp:31-54): sequential host decode

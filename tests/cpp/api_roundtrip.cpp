@@ -30,7 +30,17 @@ int main(int argc, char** argv) {
             std::printf("seed %d: round trip FAILED\n", seed);
             return 1;
         }
-        std::printf("seed %d: n=%lld z=%zu ok\n", seed, (long long)n, F.size());
+        // exact mode, as tests/test_lz77_sss.cpp:95-133 of the reference (round trip only)
+        std::vector<lz::factor> FX;
+        lz::factorize_exact<greedy, lpf_opt, with_samples, decomposed_semi_dynamic_square_grid>(
+            T.data(), (uint32_t)n, [&](lz::factor f) { FX.push_back(f); });
+        std::string DX;
+        lz::decode(FX.begin(), std::back_inserter(DX), (uint32_t)n);
+        if (DX != T || FX.size() > F.size()) {
+            std::printf("seed %d: exact round trip FAILED\n", seed);
+            return 1;
+        }
+        std::printf("seed %d: n=%lld z=%zu z_exact=%zu ok\n", seed, (long long)n, F.size(), FX.size());
     }
     return 0;
 }
