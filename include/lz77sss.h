@@ -63,7 +63,10 @@ typedef struct { uint32_t src; uint32_t len; } lz77sss_factor32;
 
 typedef struct {
     int32_t phr_mode;        /* default LZ77SSS_LPF_OPT, lz77_sss.hpp:77 */
-    int32_t fact_mode;       /* default LZ77SSS_GREEDY, lz77_sss.hpp:78 */
+    int32_t fact_mode;       /* default LZ77SSS_GREEDY, lz77_sss.hpp:78; LZ77SSS_SKIP_PHRASES gives
+                                the gapped stream of factorize_skip_gaps (skip_gaps.cpp:31-61):
+                                {first phrase start, 0}, then {src, len} per LPF phrase, each
+                                followed by {gap length, 0} when the next phrase starts later */
     uint32_t tau;            /* default 512, lz77_sss.hpp:82 (only 512 is supported) */
     uint32_t rk_seed;        /* seeds the 5 gap-index rk_prime<107> bases (replaces the
                                 std::random_device of rolling_hash.hpp:127-130) */

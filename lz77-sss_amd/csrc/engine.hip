@@ -5,6 +5,8 @@
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
 
+#include <hipcub/hipcub.hpp>
+
 #include <chrono>
 #include <cstring>
 #include <mutex>
@@ -46,7 +48,53 @@ void engine::destroy() {
     st = nullptr;
 }
 
-u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log) {
+// fact_mode = skip_phrases: the gapped stream of factorize_skip_gaps
+// (approximate/factorize/skip_gaps.cpp:31-61): {beg of the first phrase, 0}, then
+// per phrase {src, len} followed by {gap length, 0} when the next phrase (or the
+// sentinel {n, n+1, 0}) starts after its end
+__global__ void k_skip_counts(const u32* __restrict__ P, u32 m, u32* __restrict__ cnt) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > m) return;
+    cnt[k] = k == m ? 1u : 1u + (P[3 * (k + 1)] > P[3 * k + 1] ? 1u : 0u);  // slot m: the leading gap record
+}
+__global__ void k_skip_write(const u32* __restrict__ P, u32 m, const u32* __restrict__ off, u32* __restrict__ F) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > m) return;
+    if (k == m) {
+        F[0] = P[0];  // beg of the first phrase (or n: the sentinel)
+        F[1] = 0;
+        return;
+    }
+    const u64 o = 1 + off[k];
+    const u32 beg = P[3 * k], end = P[3 * k + 1], src = P[3 * k + 2], nb = P[3 * (k + 1)];
+    F[2 * o] = src;
+    F[2 * o + 1] = end - beg;
+    if (nb > end) {
+        F[2 * o + 2] = nb - end;
+        F[2 * o + 3] = 0;
+    }
+}
+u64 engine::emit_skip_phrases() {
+    const u32 m = num_phr;
+    u32* P = lpf.get((u64)(m + 1) * 3);
+    const u32 sent[3] = {(u32)n, (u32)n + 1, 0};
+    LZ_HIP(hipMemcpyAsync(P + 3 * (u64)m, sent, 12, hipMemcpyHostToDevice, st));
+    u32* cnt = u32a.get((u64)m + 2);
+    u32* off = u32b.get((u64)m + 2);
+    k_skip_counts<<<cdiv((u64)m + 1, 256), 256, 0, st>>>(P, m, cnt);
+    size_t tb = 0;
+    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)(m + 1), st));
+    u8* t = scan_tmp.get(tb);
+    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, cnt, off, (int)(m + 1), st));
+    const u32 last = rd1(off + m, st);  // records of the m phrases (slot m is the leading record)
+    const u64 z = (u64)last + 1;
+    u32* F = fact.get(2 * z + 2);
+    k_skip_write<<<cdiv((u64)m + 1, 256), 256, 0, st>>>(P, m, off, F);
+    LZ_HIP(hipGetLastError());
+    return z;
+}
+
+u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode) {
     LZ_HIP(hipSetDevice(device));
     if (phr_mode != LZ77SSS_LPF_OPT && phr_mode != LZ77SSS_LPF_LNF_OPT && phr_mode != LZ77SSS_LPF_LNF_NAIVE)
         throw error(LZ77SSS_EINVAL, "unsupported phrase mode (lpf_opt, lpf_lnf_opt, lpf_lnf_naive)");
@@ -78,8 +126,13 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log) {
         build_lpf_lnf(phr_mode == LZ77SSS_LPF_LNF_OPT ? 1 : 0);
         trace("lpf_lnf");
     }
-    num_fact = factorize_greedy(d_text, rk_seed, log2_override);
-    timer.mark("greedy");
+    if (fact_mode == LZ77SSS_SKIP_PHRASES) {
+        num_fact = emit_skip_phrases();
+        timer.mark("skip_phrases");
+    } else {
+        num_fact = factorize_greedy(d_text, rk_seed, log2_override);
+        timer.mark("greedy");
+    }
     trace("greedy");
     LZ_HIP(hipStreamSynchronize(st));
     if (log) {
@@ -145,7 +198,8 @@ LZ77SSS_API void lz77sss_default_params(lz77sss_params* prm) {
 static void check_params(const lz77sss_params* prm) {
     if (!prm) throw lz::error(LZ77SSS_EINVAL, "params is NULL");
     if (prm->tau != 512) throw lz::error(LZ77SSS_EINVAL, "only tau = 512 is supported");
-    if (prm->fact_mode != LZ77SSS_GREEDY) throw lz::error(LZ77SSS_EINVAL, "only fact_mode = greedy is supported");
+    if (prm->fact_mode != LZ77SSS_GREEDY && prm->fact_mode != LZ77SSS_SKIP_PHRASES)
+        throw lz::error(LZ77SSS_EINVAL, "supported fact_modes: greedy, skip_phrases");
     if (prm->phr_mode != LZ77SSS_LPF_OPT && prm->phr_mode != LZ77SSS_LPF_LNF_OPT &&
         prm->phr_mode != LZ77SSS_LPF_LNF_NAIVE)
         throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
@@ -187,7 +241,7 @@ LZ77SSS_API int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_para
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
         check_params(prm);
-        uint64_t z = s->E.factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0);
+        uint64_t z = s->E.factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0, prm->fact_mode);
         if (num_factors) *num_factors = z;
     });
 }

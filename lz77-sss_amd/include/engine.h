@@ -164,7 +164,8 @@ struct engine {
     void all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slots, u32* sflag);
     void path_marks(u32 m, u32* nxt0, u32* marks);
     u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override);
-    u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log);
+    u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode = 1);
+    u64 emit_skip_phrases();  // fact_mode = skip_phrases (csrc/engine.hip)
     void build_sa_full(const u8* T);
     u64 factorize_exact(bool log);  // csrc/exact.hip
     u64 decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cmp);

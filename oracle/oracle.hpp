@@ -672,7 +672,7 @@ struct approx_stats {
 
 template <typename OUT>
 static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed, OUT&& output,
-                                         approx_stats* st = nullptr) {
+                                         approx_stats* st = nullptr, int fact_mode = 1) {
     if (n == 0) return;
     std::vector<lpf> P;
     lce_structure L;
@@ -693,6 +693,22 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
         greedy_phrase_selection(P);  // lz77_sss.hpp:405-409
     } else {
         throw std::runtime_error("phrase mode not supported by the oracle");
+    }
+    if (fact_mode == 2) {
+        // skip_phrases: sentinel (lz77_sss.hpp:417-419), then factorize_skip_gaps
+        // (approximate/factorize/skip_gaps.cpp:31-61) with next_lpf at p = 1
+        P.push_back({n, n + 1, 0});
+        if (st) { st->size_sss = L.s(); st->has_runs = L.has_runs; st->num_lpf = (u32)P.size() - 1; }
+        size_t k = 0;
+        lpf nxt = P[k];
+        output(factor{nxt.beg, 0});
+        while (nxt.beg < n) {
+            const lpf phr = nxt;
+            nxt = P[std::min(++k, P.size() - 1)];
+            output(factor{phr.src, phr.end - phr.beg});
+            if (nxt.beg > phr.end) output(factor{nxt.beg - phr.end, 0});
+        }
+        return;
     }
     phrase_info pi = get_phrase_info(P, n);
     P.push_back({n, n + 1, 0});  // sentinel, lz77_sss.hpp:423

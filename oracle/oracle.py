@@ -58,6 +58,8 @@ def lib():
         L.oracle_decode.argtypes = [_P, _U64, _P, _U64]
         L.oracle_gap_bases.restype = None
         L.oracle_gap_bases.argtypes = [ctypes.c_uint32, _P]
+        L.oracle_factorize_skip.restype = ctypes.c_int64
+        L.oracle_factorize_skip.argtypes = [_P, _U64, ctypes.c_int, _P, _U64]
         L.oracle_factorize_exact.restype = ctypes.c_int64
         L.oracle_factorize_exact.argtypes = [_P, _U64, _P, _U64]
         L.oracle_factorize_exact_timed.restype = ctypes.c_int64
@@ -102,6 +104,17 @@ def factorize_timed(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):
     sec, h = ctypes.c_double(), _U64()
     z = lib().oracle_factorize_timed(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, ctypes.byref(sec), ctypes.byref(h))
     return int(z), sec.value, h.value
+
+
+def factorize_skip(T, phr_mode: int = LPF_OPT):
+    """factorize_approximate<skip_phrases, phr_mode>: the gapped stream ((k,2) u32: {src,len} phrases, {gap,0})."""
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros((2 * n + 4, 2), np.uint32)
+    z = lib().oracle_factorize_skip(buf.ctypes.data_as(_P), n, phr_mode, out.ctypes.data_as(_P), 2 * n + 4)
+    if z < 0:
+        raise RuntimeError("oracle skip_phrases factorization failed")
+    return out[:z].copy()
 
 
 def factorize_exact(T):

@@ -39,6 +39,22 @@ int64_t oracle_factorize_approx(uint8_t* T, uint64_t n, int phr_mode, uint32_t r
     }
 }
 
+// fact_mode = skip_phrases (gapped stream).  Returns the record count or -1.
+int64_t oracle_factorize_skip(uint8_t* T, uint64_t n, int phr_mode, uint32_t* out, uint64_t cap) {
+    try {
+        uint64_t k = 0;
+        bool overflow = false;
+        factorize_approximate(T, (u32)n, phr_mode, 42, [&](factor f) {
+            if (k < cap) { out[2 * k] = f.src; out[2 * k + 1] = f.len; } else overflow = true;
+            k++;
+        }, nullptr, 2);
+        return overflow ? -1 : (int64_t)k;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -1;
+    }
+}
+
 // Exact greedy LZ77 (factorize_exact restatement, oracle.hpp).  Returns z or -1 (cap too small).
 int64_t oracle_factorize_exact(const uint8_t* T, uint64_t n, uint32_t* out, uint64_t cap) {
     std::vector<factor> F = factorize_exact(T, n);

@@ -124,7 +124,7 @@ def test_invalid_parameters_fail_loudly(session, lz):
     with pytest.raises(lz.Lz77SssError):
         s.factorize(tau=256)
     with pytest.raises(lz.Lz77SssError):
-        s.factorize(fact_mode=lz.SKIP_PHRASES)
+        s.factorize(fact_mode=lz.GREEDY_NAIVE)
     with pytest.raises(lz.Lz77SssError):
         s.factorize(phr_mode=lz.LPF_NAIVE)
     small = lz.Session(1 << 10)
