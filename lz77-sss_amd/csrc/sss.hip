@@ -402,27 +402,27 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
         const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
         const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
         if (__builtin_amdgcn_readfirstlane((int)(anyq || endblk))) {
-            const u64 j0 = i0 + k * TAU + 8 * lane;
+            // anchor r (0..4) of the block covers offsets (128r - 128, 128r]; its Q interval
+            // [lo, hi] (rel = offset + 127 - 128r) is an offset interval, uniform per block:
+            // the lane ORs the part that meets its 8 positions into an INF mask
+            const int o = (int)(8 * lane);
             const u32 qa[5] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu};
-            const u32 ta = (8 * lane + 127) >> 7;  // anchor of the lane's first position (0..4)
-            u32 q0 = 0xFF00, q1 = 0xFF00;
+            u32 bits = 0;
 #pragma unroll
-            for (u32 r = 0; r < 5; r++) {
-                if (ta == r) q0 = qa[r];
-                if (ta + 1 == r) q1 = qa[r];
-            }
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const u64 j = j0 + e;
-                if (j > jmax) {
-                    v[e] = INF32;
-                } else {
-                    const u32 t = (8 * lane + e + 127) >> 7;
-                    const u32 qi = t == ta ? q0 : q1;
-                    const u32 rel = (u32)((8 * lane + e + 127) & 127);
-                    if (rel >= (qi >> 8) && rel <= (qi & 255)) v[e] = INF32;
+            for (int r = 0; r < 5; r++) {
+                const int lo = (int)(qa[r] >> 8), hi = min((int)(qa[r] & 255u), 127);
+                if (lo <= hi) {  // uniform
+                    const int l = max(128 * r - 127 + lo - o, 0), h = min(128 * r - 127 + hi - o, 7);
+                    if (l <= h) bits |= ((2u << h) - 1u) & ~((1u << l) - 1u);
                 }
             }
+            if (endblk) {  // positions past the last full window
+                const u64 j0 = i0 + k * TAU + (u64)o;
+                const u64 keep = jmax >= j0 ? min<u64>(jmax - j0 + 1, 8) : 0;
+                bits |= 0xFFu & ~((1u << keep) - 1u);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] |= 0u - ((bits >> e) & 1u);
         }
     };
     // Q intervals of the anchors of block k (uniform address: a scalar load)
