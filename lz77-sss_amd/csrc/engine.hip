@@ -96,8 +96,7 @@ u64 engine::emit_skip_phrases() {
 
 u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode) {
     LZ_HIP(hipSetDevice(device));
-    if (phr_mode != LZ77SSS_LPF_OPT && phr_mode != LZ77SSS_LPF_LNF_OPT && phr_mode != LZ77SSS_LPF_LNF_NAIVE)
-        throw error(LZ77SSS_EINVAL, "unsupported phrase mode (lpf_opt, lpf_lnf_opt, lpf_lnf_naive)");
+    if (phr_mode < LZ77SSS_LPF_NAIVE || phr_mode > LZ77SSS_LPF_LNF_OPT) throw error(LZ77SSS_EINVAL, "unsupported phrase mode");
     if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
     num_fact = 0;
     stats.assign(24, 0);
@@ -109,7 +108,7 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         LZ_HIP(hipStreamSynchronize(st));
         std::fprintf(stderr, "[lz77sss-debug] done %s (|S|=%u phrases=%u)\n", what, s, num_phr);
     };
-    if (phr_mode == LZ77SSS_LPF_OPT) {
+    if (phr_mode == LZ77SSS_LPF_OPT || phr_mode == LZ77SSS_LPF_NAIVE) {
         build_sss(d_text);
         timer.mark("sss");
         trace("sss");
@@ -119,7 +118,8 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         build_lcp_rmq(d_text);
         timer.mark("lcp_rmq");
         trace("lcp_rmq");
-        build_lpf_opt(d_text);
+        if (phr_mode == LZ77SSS_LPF_OPT) build_lpf_opt(d_text);
+        else build_lpf_naive(d_text);
         timer.mark("lpf");
         trace("lpf");
     } else {
@@ -200,8 +200,7 @@ static void check_params(const lz77sss_params* prm) {
     if (prm->tau != 512) throw lz::error(LZ77SSS_EINVAL, "only tau = 512 is supported");
     if (prm->fact_mode != LZ77SSS_GREEDY && prm->fact_mode != LZ77SSS_SKIP_PHRASES)
         throw lz::error(LZ77SSS_EINVAL, "supported fact_modes: greedy, skip_phrases");
-    if (prm->phr_mode != LZ77SSS_LPF_OPT && prm->phr_mode != LZ77SSS_LPF_LNF_OPT &&
-        prm->phr_mode != LZ77SSS_LPF_LNF_NAIVE)
+    if (prm->phr_mode < LZ77SSS_LPF_NAIVE || prm->phr_mode > LZ77SSS_LPF_LNF_OPT)
         throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
     if (prm->index_log2_size < 0 || prm->index_log2_size > 30) throw lz::error(LZ77SSS_EINVAL, "bad index_log2_size");
 }

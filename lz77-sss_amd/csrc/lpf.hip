@@ -178,6 +178,119 @@ struct max_op {
     __device__ u32 operator()(const u32& a, const u32& b) const { return a > b ? a : b; }
 };
 
+// ---------------------------------------------------------------------------
+// build_LPF_naive (lpf_lnf/lpf_naive.cpp:33-110, p = 1): the longer PSV/NSV
+// candidate (strictly longer replaces) at every sync index the previous pushed
+// phrase does not cover; next(i) = first j > i with S[j] >= S[i] + len_i
+// (lpf_naive.cpp:104-108), so the processed indices are again a path from 0.
+// cand2[i] = (src, len)
+__global__ void k_lpf_naive_cand(lce_view L, const u32* __restrict__ SA, const u32* __restrict__ PSV,
+                                 const u32* __restrict__ NSV, u32* __restrict__ cand2) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 s = L.s;
+    if (i >= s) return;
+    const u32 r = L.ISA[i], Si = L.S[i];
+    u32 src = 0, len = 0;
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+        const u32 nb = side == 0 ? PSV[r] : NSV[r];
+        if (nb == s) continue;
+        const u32 sc = L.S[SA[nb]];
+        const u32 lc = (u32)dev_lce(L, sc, Si);
+        if (lc > len) {
+            src = sc;
+            len = lc;
+        }
+    }
+    cand2[2 * i] = src;
+    cand2[2 * i + 1] = len;
+}
+__global__ void k_next_naive(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand2, u32* __restrict__ nxt) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > s) return;
+    if (i == s) { nxt[s] = s; return; }
+    const u64 E = (u64)S[i] + cand2[2 * i + 1];
+    u32 lo = (u32)i + 1, hi = s;  // first k > i with S[k] >= E (s if none)
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if ((u64)S[mid] < E) lo = mid + 1; else hi = mid;
+    }
+    nxt[i] = lo;
+}
+__global__ void k_phrase_naive(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand2,
+                               const u32* __restrict__ mark, u32* __restrict__ ph, u32* __restrict__ push) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= s) return;
+    const u32 len = cand2[2 * i + 1];
+    const bool pu = mark[i] && len > 0;
+    ph[i * 3 + 0] = S[i];
+    ph[i * 3 + 1] = S[i] + len;
+    ph[i * 3 + 2] = cand2[2 * i];
+    push[i] = pu ? 1u : 0u;
+}
+
+// PSV/NSV over SA_S into the engine's PSV / NSV buffers
+void engine::psv_nsv_s() {
+    const unsigned g = cdiv(s, 256);
+    sa_min_levels M{};
+    M.L[0] = SA.p;
+    u32 nl = 1;
+    for (u32 lv = 1; (1ull << lv) <= s; lv++) {
+        const u32 cnt = s - (1u << lv) + 1;
+        u32* out = sa_min[lv].get(cnt);
+        k_sa_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(lv == 1 ? SA.p : sa_min[lv - 1].p, cnt, 1u << (lv - 1), out);
+        M.L[lv] = out;
+        nl = lv + 1;
+    }
+    M.nlev = nl;
+    k_psv_nsv<<<g, 256, 0, st>>>(SA.p, s, M, PSV.get(s), NSV.get(s));
+}
+
+// path of processed indices from 0 along nxt (pointer doubling + top-down expansion) -> mark[i] = 1
+void engine::mark_path(u32* mark) {
+    const u32 m = s + 1;
+    u32 T_lv = 0;
+    while ((1ull << T_lv) < m) T_lv++;
+    for (u32 t = 1; t <= T_lv; t++) k_jump<<<cdiv(m, 256), 256, 0, st>>>(jump[t - 1].p, m, jump[t].get(m));
+    u32* C = u32a.get(2ull << T_lv);
+    u32* C2 = u32b.get(2ull << T_lv);
+    LZ_HIP(hipMemsetAsync(C, 0, 4, st));
+    u32 cnt = 1;
+    for (int t = (int)T_lv - 1; t >= 0; t--) {
+        k_expand<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, jump[t].p, C2);
+        std::swap(C, C2);
+        cnt *= 2;
+    }
+    LZ_HIP(hipMemsetAsync(mark, 0, (size_t)s * 4, st));
+    k_mark<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, s, mark);
+}
+
+void engine::build_lpf_naive(const u8* T) {
+    num_phr = 0;
+    if (s == 0) return;
+    const unsigned g = cdiv(s, 256);
+    psv_nsv_s();
+    u32* cd = cand.get((u64)s * 2);
+    k_lpf_naive_cand<<<g, 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, cd);
+    k_next_naive<<<cdiv(s + 1, 256), 256, 0, st>>>(S.p, s, cd, jump[0].get(s + 1));
+    u32* mark = u32c.get(s);
+    mark_path(mark);
+    u32* ph3 = u32e.get((u64)s * 3);
+    u32* push = u32d.get(s);
+    k_phrase_naive<<<g, 256, 0, st>>>(S.p, s, cd, mark, ph3, push);
+    u32* off = mark;  // mark no longer needed
+    {
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, push, off, (int)s, st));
+        u8* t = scan_tmp.get(tb);
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, push, off, (int)s, st));
+    }
+    num_phr = rd1(off + s - 1, st) + rd1(push + s - 1, st);
+    u32* out = lpf.get((u64)(num_phr + 1) * 3);
+    k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);
+    LZ_HIP(hipGetLastError());
+}
+
 void engine::build_lpf_opt(const u8* T) {
     num_phr = 0;
     if (s == 0) return;

@@ -160,6 +160,9 @@ struct engine {
     void build_sa_s(const u8* T);
     void build_lcp_rmq(const u8* T);
     void build_lpf_opt(const u8* T);
+    void build_lpf_naive(const u8* T);  // lpf_naive mode (csrc/lpf.hip)
+    void psv_nsv_s();
+    void mark_path(u32* mark);
     void build_lpf_lnf(int opt);  // csrc/lnf.hip
     void all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slots, u32* sflag);
     void path_marks(u32 m, u32* nxt0, u32* marks);

@@ -418,6 +418,36 @@ static inline std::vector<lpf> build_lpf_opt(const u8* T, u64 n, const lce_struc
 }
 
 // ===========================================================================
+//  build_LPF_naive for p = 1: restates lpf_lnf/lpf_naive.cpp:33-110 (the
+//  longer of the PSV/NSV candidates -- strictly longer replaces -- at every
+//  sync position not covered by the previous pushed phrase; no left extension;
+//  phrases of length >= 1 are kept)
+// ===========================================================================
+static inline std::vector<lpf> build_lpf_naive(const u8* T, u64 n, const lce_structure& L) {
+    std::vector<u32> PSV, NSV;
+    build_psv_nsv(L, PSV, NSV);
+    std::vector<lpf> out;
+    const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
+    const u32 s = L.s();
+    for (u32 i = 0; i < s;) {
+        u32 src = 0, len = 0;
+        if (PSV[ISA[i]] != s) {
+            const u32 sc = S[SA[PSV[ISA[i]]]], lc = (u32)L.lce(sc, S[i]);
+            if (lc > len) { src = sc; len = lc; }
+        }
+        if (NSV[ISA[i]] != s) {
+            const u32 sc = S[SA[NSV[ISA[i]]]], lc = (u32)L.lce(sc, S[i]);
+            if (lc > len) { src = sc; len = lc; }
+        }
+        if (len > 0) out.push_back({S[i], S[i] + len, src});
+        const u32 pos = S[i];
+        do { i++; } while (i < s && S[i] < pos + len);
+    }
+    (void)T; (void)n;
+    return out;
+}
+
+// ===========================================================================
 //  LPF/LNF (lpf_lnf_opt) for p = 1: restates lpf_lnf.cpp:31-249 and
 //  greedy_phrase_selection (approximate/common.cpp:31-96)
 // ===========================================================================
@@ -679,6 +709,9 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
     if (phr_mode == lpf_opt) {
         L.build(T, n);
         P = build_lpf_opt(T, n, L);
+    } else if (phr_mode == lpf_naive) {
+        L.build(T, n);
+        P = build_lpf_naive(T, n, L);
     } else if (phr_mode == lpf_lnf_opt || phr_mode == lpf_lnf_naive) {
         bool opt = (phr_mode == lpf_lnf_opt);
         std::reverse(T, T + n);  // lz77_sss.hpp:386 (in place on the caller's buffer)

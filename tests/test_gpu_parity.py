@@ -126,7 +126,7 @@ def test_invalid_parameters_fail_loudly(session, lz):
     with pytest.raises(lz.Lz77SssError):
         s.factorize(fact_mode=lz.GREEDY_NAIVE)
     with pytest.raises(lz.Lz77SssError):
-        s.factorize(phr_mode=lz.LPF_NAIVE)
+        s.factorize(phr_mode=7)
     small = lz.Session(1 << 10)
     with pytest.raises(lz.Lz77SssError):
         small.load(T)
@@ -256,3 +256,21 @@ def test_device_decode_rejects_invalid(lz):
     with pytest.raises(lz.Lz77SssError):
         lz.decode_device(np.array([[97, 0]], np.uint32), 0)
     assert lz.decode_device(np.zeros((0, 2), np.uint32), 0).size == 0
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_lpf_naive_vs_oracle(session, orc, name):
+    """phr_mode = lpf_naive (lpf_lnf/lpf_naive.cpp:33-110) with the greedy emitter."""
+    g = load_golden(name)
+    _, F = run(session, g["text"], phr_mode=0)
+    F_ref, _ = orc.factorize(g["text"], phr_mode=0)
+    assert np.array_equal(F, F_ref)
+
+
+@pytest.mark.parametrize("seed", range(1, 9))
+def test_c1_lpf_naive_vs_oracle(session, orc, lz, seed):
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    _, F = run(session, T, phr_mode=lz.LPF_NAIVE)
+    F_ref, _ = orc.factorize(T, phr_mode=0)
+    assert np.array_equal(F, F_ref)
+    assert np.array_equal(lz.decode(F, T.size), T)

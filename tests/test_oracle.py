@@ -240,3 +240,11 @@ def test_gap_bases_pinned(orc):
     assert b == [int(x) for x in g["gap_bases_seed42"]]
     assert all(257 <= x < (1 << 20) for x in b)
     assert orc.gap_bases(43) != b
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_lpf_naive_roundtrip(orc, lz, seed):
+    """lpf_naive phrases feed the same greedy emitter: decode(factorize(T)) == T (test_lz77_sss.cpp:73-82)."""
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    F, st = orc.factorize(T, phr_mode=0)
+    assert np.array_equal(orc.decode(F, T.size), T)
