@@ -126,15 +126,25 @@ __global__ void k_pred(const u32* __restrict__ skeys, const u32* __restrict__ sv
 // bucket tables over slots: bucket[s] = first sorted index with slot >= s (bucket[nslots] = m)
 struct key_u32 { const u32* k; __device__ u32 operator()(u64 t) const { return k[t]; } };
 struct key_u64 { const u64* k; __device__ u32 operator()(u64 t) const { return (u32)(k[t] >> 35); } };
+// dense bucket tables without per-thread fill loops (skewed slot sets leave long
+// empty ranges): every run head t of slot k writes t at reversed index nslots - k,
+// an inclusive min-scan over the reversed array fills the empty slots with the
+// next non-empty slot's start, k_unreverse restores slot order
 template <class K>
-__global__ void k_bucket_dense(K key, u64 m, u32 nslots, u32* __restrict__ bucket) {
+__global__ void k_bucket_heads(K key, u64 m, u32 nslots, u32* __restrict__ rev) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t > m) return;
-    const u32 cur = t == m ? nslots : key(t);
-    const int64_t prev = t == 0 ? -1 : (int64_t)key(t - 1);
-    if ((int64_t)cur == prev) return;
-    for (int64_t x = prev + 1; x <= (int64_t)cur; x++) bucket[x] = (u32)t;
+    if (t == m) { rev[0] = (u32)m; return; }
+    const u32 k = key(t);
+    if (t == 0 || key(t - 1) != k) rev[nslots - k] = (u32)t;
 }
+__global__ void k_unreverse(const u32* __restrict__ rev, u32 nslots, u32* __restrict__ bucket) {
+    const u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x <= nslots) bucket[x] = rev[nslots - x];
+}
+struct min_u32_op {
+    __device__ __forceinline__ u32 operator()(const u32& a, const u32& b) const { return a < b ? a : b; }
+};
 template <class K>
 __global__ void k_bucket_search(K key, u64 m, u32 nslots, u32* __restrict__ bucket) {
     const u64 sl = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1156,8 +1166,19 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     const u32 nslots = G.mask + 1;
     auto build_buckets = [&](auto key, u64 mk, dbuf<u32>& bk) {
         u32* b = bk.get((u64)nslots + 1);
-        if (mk * 16 >= nslots) k_bucket_dense<<<cdiv(mk + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
-        else k_bucket_search<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
+        if (mk * 16 >= nslots) {
+            u32* rev = g_brev.get(2 * ((u64)nslots + 1));
+            u32* scn = rev + nslots + 1;
+            LZ_HIP(hipMemsetAsync(rev, 0xFF, ((u64)nslots + 1) * 4, st));
+            k_bucket_heads<<<cdiv(mk + 1, 256), 256, 0, st>>>(key, mk, nslots, rev);
+            size_t tb = 0;
+            LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, rev, scn, min_u32_op{}, (int)(nslots + 1), st));
+            u8* t = scan_tmp.get(tb);
+            LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, rev, scn, min_u32_op{}, (int)(nslots + 1), st));
+            k_unreverse<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(scn, nslots, b);
+        } else {
+            k_bucket_search<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
+        }
     };
     // runs of a bitmap -> intervals (st, en), ranks, chunks for k_slots
     auto runs_to_chunks = [&](const u32* bm, dbuf<u32>& dst, dbuf<u32>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,

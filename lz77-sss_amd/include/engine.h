@@ -135,6 +135,7 @@ struct engine {
     dbuf<u32> l_V, l_b, l_d, l_e, l_r, l_sflag_lnf, l_slots_lnf, l_sflag, l_slots, l_off, l_P, l_Q;
     dbuf<u64> l_tmp64;
     dbuf<u32> g_predk, g_wk, g_ids2;
+    dbuf<u32> g_brev;
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
     dbuf<u64> g_xk, g_xk2;
     // exact mode (csrc/exact.hip)
