@@ -1024,9 +1024,6 @@ __global__ void k_invalidate_all(seg_tab S, u32 nseg) {
     S.succ[g] = NONE;
 }
 
-static double now_ms() {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 __global__ void k_put3(u32* p, u32 a, u32 b, u32 c) {
     p[0] = a;
     p[1] = b;

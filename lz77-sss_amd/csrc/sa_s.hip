@@ -236,12 +236,13 @@ __global__ void k_prefix_ties(const u8* __restrict__ T, const u32* __restrict__ 
 // which every comparison is done by a whole wave (64 lanes x 8 bytes per step).
 // Items hold key ids, segment k occupies [sbeg[k], sbeg[k+1]).
 // A pass of width w merges, inside every segment, neighbouring sorted blocks of
-// w items (local offsets).  Each wave produces opw = min(64, 2w) outputs of one
+// w items (local offsets).  Each wave produces opw = min(16, 2w) outputs of one
 // merge; uoff is the exclusive scan of the per-segment wave counts, so passes
 // cost O(members) and only log2(longest segment) passes run.
 __global__ void k_seg_units(const u32* __restrict__ sbeg, u32 nseg, u32 opw, u32* __restrict__ units) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < nseg) units[k] = (sbeg[k + 1] - sbeg[k] + opw - 1) / opw;
+    if (k == nseg) units[k] = 0;  // exclusive scan over nseg + 1 -> uoff[nseg] = total
 }
 __global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const u32* S, const u32* KL,
                                                   const u32* __restrict__ sbeg, const u32* __restrict__ uoff, u32 nseg,
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const 
                                                   u32 opw) {
     const u32 unit = (u32)(((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const u32 lane = threadIdx.x & 63;
-    if (unit >= nunits) return;
+    if (unit >= nunits || unit >= uoff[nseg]) return;  // nunits: launch bound, uoff[nseg]: exact count
     u32 lo = 0, hi = nseg;  // last k with uoff[k] <= unit
     while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
@@ -370,7 +371,10 @@ static void merge_sort_u32(u32* a, u32* tmp, u32 d, C cmp, hipStream_t st) {
     do {                                                                              \
         if (debug_enabled()) {                                                        \
             hipError_t se_ = hipStreamSynchronize(st);                                \
-            fprintf(stderr, "[sa_s] %-16s %s\n", what, se_ == hipSuccess ? "ok" : hipGetErrorString(se_)); \
+            const double t_ = now_ms();                                               \
+            fprintf(stderr, "[sa_s] %-16s %s %8.3f ms\n", what, se_ == hipSuccess ? "ok" : hipGetErrorString(se_), \
+                    t_ - sa_dbg_t);                                                   \
+            sa_dbg_t = t_;                                                            \
             LZ_HIP(se_);                                                              \
         }                                                                             \
     } while (0)
@@ -381,20 +385,9 @@ static void scan_incl(u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
     LZ_HIP(hipcub::DeviceScan::InclusiveSum(t, tb, in, out, (int)m, st));
 }
 
-// exclusive scan; returns the total (synchronizes)
-static u32 excl_scan32(const u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
-    size_t tb = 0;
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)m, st));
-    u8* t = tmp.get(tb);
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, in, out, (int)m, st));
-    u32 last[2];
-    LZ_HIP(hipMemcpyAsync(&last[0], out + m - 1, 4, hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipMemcpyAsync(&last[1], in + m - 1, 4, hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipStreamSynchronize(st));
-    return last[0] + last[1];
-}
-
 void engine::build_sa_s(const u8* T) {
+    double sa_dbg_t = now_ms();
+    (void)sa_dbg_t;
     nlev_rank = 0;
     if (s == 0) return;
     const u32* dS = S.p;
@@ -416,6 +409,7 @@ void engine::build_sa_s(const u8* T) {
         k_key_prep<<<g, 256, 0, st>>>(KL, s, H, CC);
         scan_incl(CC, CC, s, scan_tmp, st);
         k_key_hash<<<KH_WAVES * 64 / 256, 256, 0, st>>>(T, dS, KL, CC, s, H);
+        SA_DBG("key hash");
         k_iota<<<g, 256, 0, st>>>(idx_in, s);
         size_t tb = 0;
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, H, Hs, idx_in, idx, (int)s, 0, 64, st));
@@ -423,6 +417,7 @@ void engine::build_sa_s(const u8* T) {
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, H, Hs, idx_in, idx, (int)s, 0, 64, st));
         u32* ctr = counters.get(16);
         LZ_HIP(hipMemsetAsync(ctr + 2, 0, 4, st));
+        SA_DBG("hash sort");
         k_group_verify<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, Hs, idx, s, flag, ctr + 2);
         scan_incl(flag, rank, s, scan_tmp, st);  // rank[t] = group id + 1
         const u32 collide = rd1(ctr + 2, st);
@@ -474,16 +469,23 @@ void engine::build_sa_s(const u8* T) {
                 u32* it_a = (u32*)u64a.get(mt);  // hashes no longer needed
                 u32* it_b = it_a + mt;
                 u32* dpos = sa_tmp3.get(mt);
-                u32* dsb = u32e.get(2 * (u64)nseg + 2);
+                u32* dsb = u32e.get(2 * (u64)nseg + 3);
                 u32* units = dsb + nseg + 1;
                 LZ_HIP(hipMemcpyAsync(dpos, ipos.data(), (size_t)mt * 4, hipMemcpyHostToDevice, st));
                 LZ_HIP(hipMemcpyAsync(dsb, sbeg.data(), (size_t)(nseg + 1) * 4, hipMemcpyHostToDevice, st));
                 k_gather_u32<<<cdiv(mt, 256), 256, 0, st>>>(srt, dpos, mt, it_a);
                 u32* uoff = sa_tmp1.p == srt ? sa_tmp2.get(nseg + 1) : sa_tmp1.get(nseg + 1);
                 for (u64 w = 1; w < maxl; w *= 2) {
-                    const u32 opw = (u32)std::min<u64>(64, 2 * w);
-                    k_seg_units<<<cdiv(nseg, 256), 256, 0, st>>>(dsb, nseg, opw, units);
-                    const u32 nunits = excl_scan32(units, uoff, nseg, scan_tmp, st);
+                    const u32 opw = (u32)std::min<u64>(16, 2 * w);  // short output runs: more waves on long segments
+                    // no host read-back: launch for the upper bound cdiv(members, opw) + segments
+                    k_seg_units<<<cdiv(nseg + 1, 256), 256, 0, st>>>(dsb, nseg, opw, units);
+                    {
+                        size_t tb = 0;
+                        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, units, uoff, (int)(nseg + 1), st));
+                        u8* tq = scan_tmp.get(tb);
+                        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tq, tb, units, uoff, (int)(nseg + 1), st));
+                    }
+                    const u32 nunits = cdiv(mt, opw) + nseg;
                     k_segmerge<<<cdiv((u64)nunits * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, dsb, uoff, nseg, nunits,
                                                                             it_a, it_b, (u32)w, opw);
                     std::swap(it_a, it_b);

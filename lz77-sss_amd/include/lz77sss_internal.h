@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <chrono>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -32,6 +33,11 @@ constexpr u32 NONE = 0xFFFFFFFFu;
 // zero bytes allocated past n in the HBM text buffer: lets vector loads and
 // the SSS lane streams run past the end without bounds checks
 constexpr u64 TEXT_PAD = 64 * 1024;
+
+// wall clock in ms (debug laps)
+inline double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 inline bool debug_enabled() {
     static int v = -1;
