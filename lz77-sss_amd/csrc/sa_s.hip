@@ -277,6 +277,24 @@ __global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const 
         if (lane == 0) out[p] = v;
     }
 }
+// ranks in a tie segment (tie with the previous or the next rank) and segment starts
+__global__ void k_tie_member(const u8* __restrict__ tie, u32 d, u8* __restrict__ member, u8* __restrict__ start) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= d) return;
+    const bool nx = r + 1 < d && tie[r + 1];
+    member[r] = (tie[r] || nx) ? 1 : 0;
+    start[r] = (!tie[r] && nx) ? 1 : 0;
+}
+__global__ void k_gather_u8(const u8* __restrict__ src, const u32* __restrict__ pos, u32 m, u8* __restrict__ dst) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < m) dst[t] = src[pos[t]];
+}
+// sbeg[nseg] = mt; len[k] = sbeg[k+1] - sbeg[k]
+__global__ void k_seg_lens(u32* __restrict__ sbeg, u32 nseg, u32 mt, u32* __restrict__ len) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) sbeg[nseg] = mt;
+    if (k < nseg) len[k] = (k + 1 < nseg ? sbeg[k + 1] : mt) - sbeg[k];
+}
 __global__ void k_gather_u32(const u32* __restrict__ src, const u32* __restrict__ pos, u32 m, u32* __restrict__ dst) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < m) dst[t] = src[pos[t]];
@@ -446,33 +464,45 @@ void engine::build_sa_s(const u8* T) {
             u8* tie = tmp_bytes.get(d);
             k_prefix_ties<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, tie);
             if (debug_enabled()) fprintf(stderr, "[sa_s] distinct=%u sorted\n", d);
-            std::vector<u8> htie(d);
-            LZ_HIP(hipMemcpyAsync(htie.data(), tie, d, hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipStreamSynchronize(st));
-            // members of tie segments, in order, and the segment offsets
-            std::vector<u32> ipos, sbeg;
-            u32 nseg = 0, maxl = 0;
-            for (u32 r = 1; r < d;) {
-                if (!htie[r]) { r++; continue; }
-                u32 e = r;
-                while (e < d && htie[e]) e++;
-                sbeg.push_back((u32)ipos.size());
-                for (u32 q = r - 1; q < e; q++) ipos.push_back(q);
-                maxl = std::max(maxl, e - r + 1);
-                nseg++;
-                r = e;
+            // members of tie segments (ranks r whose key ties with r-1 or r+1, in order) and the
+            // segment offsets, on the device: flags, two flagged selections, a max-reduction
+            u8* mflag = tmp_bytes2.get(2 * (u64)d + 2);
+            u8* sflag = mflag + d + 1;
+            k_tie_member<<<cdiv(d, 256), 256, 0, st>>>(tie, d, mflag, sflag);
+            u32* dpos = sa_tmp3.get(d);
+            u32* cnt4 = counters.get(16) + 8;
+            {
+                size_t tb = 0;
+                hipcub::CountingInputIterator<u32> it0(0);
+                LZ_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, it0, mflag, dpos, cnt4, (int)d, st));
+                u8* tq = scan_tmp.get(tb);
+                LZ_HIP(hipcub::DeviceSelect::Flagged(tq, tb, it0, mflag, dpos, cnt4, (int)d, st));
             }
-            sbeg.push_back((u32)ipos.size());
-            if (debug_enabled()) fprintf(stderr, "[sa_s] tie segments=%u members=%zu longest=%u\n", nseg, ipos.size(), maxl);
-            if (!ipos.empty()) {
-                const u32 mt = (u32)ipos.size();
+            const u32 mt = rd1(cnt4, st);
+            u32 nseg = 0, maxl = 0;
+            u32* dsb = u32e.get(2 * (u64)mt + 4);
+            if (mt) {
+                u8* sf2 = tmp_bytes3.get(mt);
+                k_gather_u8<<<cdiv(mt, 256), 256, 0, st>>>(sflag, dpos, mt, sf2);
+                size_t tb = 0;
+                hipcub::CountingInputIterator<u32> it0(0);
+                LZ_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, it0, sf2, dsb, cnt4 + 1, (int)mt, st));
+                u8* tq = scan_tmp.get(tb);
+                LZ_HIP(hipcub::DeviceSelect::Flagged(tq, tb, it0, sf2, dsb, cnt4 + 1, (int)mt, st));
+                nseg = rd1(cnt4 + 1, st);
+                u32* seglen = dsb + nseg + 1;
+                k_seg_lens<<<cdiv(nseg + 1, 256), 256, 0, st>>>(dsb, nseg, mt, seglen);
+                size_t tb2 = 0;
+                LZ_HIP(hipcub::DeviceReduce::Max(nullptr, tb2, seglen, cnt4 + 2, (int)nseg, st));
+                u8* tq2 = scan_tmp.get(tb2);
+                LZ_HIP(hipcub::DeviceReduce::Max(tq2, tb2, seglen, cnt4 + 2, (int)nseg, st));
+                maxl = rd1(cnt4 + 2, st);
+            }
+            if (debug_enabled()) fprintf(stderr, "[sa_s] tie segments=%u members=%u longest=%u\n", nseg, mt, maxl);
+            if (mt) {
                 u32* it_a = (u32*)u64a.get(mt);  // hashes no longer needed
                 u32* it_b = it_a + mt;
-                u32* dpos = sa_tmp3.get(mt);
-                u32* dsb = u32e.get(2 * (u64)nseg + 3);
                 u32* units = dsb + nseg + 1;
-                LZ_HIP(hipMemcpyAsync(dpos, ipos.data(), (size_t)mt * 4, hipMemcpyHostToDevice, st));
-                LZ_HIP(hipMemcpyAsync(dsb, sbeg.data(), (size_t)(nseg + 1) * 4, hipMemcpyHostToDevice, st));
                 k_gather_u32<<<cdiv(mt, 256), 256, 0, st>>>(srt, dpos, mt, it_a);
                 u32* uoff = sa_tmp1.p == srt ? sa_tmp2.get(nseg + 1) : sa_tmp1.get(nseg + 1);
                 for (u64 w = 1; w < maxl; w *= 2) {

@@ -97,7 +97,7 @@ struct engine {
     dbuf<u32> lcp_rmq[MAX_LV];       // sparse table levels over LCP
     u32 nlev_rank = 0, nlev_rmq = 0;
     dbuf<u32> succ_tab;              // bucket -> first sync index with S >= bucket*512
-    dbuf<u8> tmp_bytes, scan_tmp;
+    dbuf<u8> tmp_bytes, tmp_bytes2, tmp_bytes3, scan_tmp;
     dbuf<u64> u64a, u64b;
     dbuf<u32> sa_tmp1, sa_tmp2, sa_tmp3;
     u64 stats_sa_distinct = 0, stats_sa_ties = 0;
