@@ -52,18 +52,18 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
         // all global loads first (one round trip), then the LDS writes.  Loads are
         // unconditional: out-of-range lanes read the zero padding at T + n (a guarded
         // or zeroed load becomes a branch with its own s_waitcnt)
-        constexpr int NL = (QT_THREADS * (int)QA) / (QT_THREADS * 16);  // 8 full rounds
-        constexpr int TAIL = QT_LDS - NL * QT_THREADS * 16;              // 1280 bytes
-        static_assert(TAIL > 0 && TAIL <= QT_THREADS * 16, "one tail round");
+        constexpr int NR = (QT_LDS + QT_THREADS * 16 - 1) / (QT_THREADS * 16);  // load rounds (last partial)
         auto src = [&](int x) -> const uint4* {
             const int64_t g = base + x;
             const bool okr = g >= 0 && (u64)g + 16 <= n + TEXT_PAD;
             return (const uint4*)(T + (okr ? (u64)g : n));
         };
-        uint4 v[NL + 1];
+        uint4 v[NR];
 #pragma unroll
-        for (int r = 0; r < NL; r++) v[r] = *src(i * 16 + r * QT_THREADS * 16);
-        v[NL] = *src(i * 16 < TAIL ? NL * QT_THREADS * 16 + i * 16 : -(1 << 20));
+        for (int r = 0; r < NR; r++) {
+            const int x = i * 16 + r * QT_THREADS * 16;
+            v[r] = *src(x < QT_LDS ? x : -(1 << 20));
+        }
         auto put = [&](int x, uint4 q) {
             const int w = (x >> 2) + (x >> 7);
             b32[w] = q.x;
@@ -72,8 +72,10 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
             b32[w + 3] = q.w;
         };
 #pragma unroll
-        for (int r = 0; r < NL; r++) put(i * 16 + r * QT_THREADS * 16, v[r]);
-        if (i * 16 < TAIL) put(NL * QT_THREADS * 16 + i * 16, v[NL]);
+        for (int r = 0; r < NR; r++) {
+            const int x = i * 16 + r * QT_THREADS * 16;
+            if (x < QT_LDS) put(x, v[r]);
+        }
     }
     if (i == 0) s_anyq = 0;
     __syncthreads();
