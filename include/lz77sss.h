@@ -135,6 +135,27 @@ int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_t cap, uint6
 int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs);
 /* Copies the sync set of the last sss/factorize call HBM -> host. */
 int lz77sss_session_get_sss(lz77sss_session* s, uint32_t* out, uint64_t cap);
+/* pos_t = uint64_t sync set (lce::rolling_hash::sss<uint64_t, tau>, called at
+ * patched-files/external/lce/include/ds/lce_sss.hpp:53 with the pos_t of
+ * lz77_sss.hpp:72-75): S n [first, end) of the loaded text, any n, computed in
+ * windows of `window` decisions (0 = 2^30, rounded up to a multiple of 4096, at
+ * most 2^31) with a 2*tau-1 byte halo each; end is clamped to n - 2*tau + 1.
+ * Positions are reported + base: a rank of a sharded job loads its block
+ * T[b_r, e_r + 2*tau - 1), passes [0, e_r - b_r) and base = b_r, and the
+ * concatenation over ranks in rank order is the sync set of T.
+ * The result stays in HBM until get_sss64 / copy_sss64_device. */
+int lz77sss_session_sss_range(lz77sss_session* s, uint64_t first, uint64_t end, uint64_t base, uint64_t window,
+                              uint64_t* size_sss, int* has_runs);
+int lz77sss_session_get_sss64(lz77sss_session* s, uint64_t* out, uint64_t cap);
+/* Device-to-device copy of the sss_range result into `dst`, a device buffer on the
+ * session's device (e.g. a collective's send buffer); cap in elements. */
+int lz77sss_session_copy_sss64_device(lz77sss_session* s, void* dst, uint64_t cap);
+/* Fills the session text with n bytes of a chr19-style text generated in HBM: a
+ * random ACGT block of base_len bytes, repeated, each copy byte mutated to another
+ * base with probability mut_rate -- every byte a function of (position, seed), so
+ * any block of it can be generated alone (the C4 input, without a host copy). */
+int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint64_t base_len, double mut_rate, uint32_t seed,
+                               uint64_t offset);
 /* Copies SA_S / LCP_S (suffix order of the sync positions) of the last call. */
 int lz77sss_session_get_sa_s(lz77sss_session* s, uint32_t* sa, uint32_t* lcp, uint64_t cap);
 /* Copies the LPF phrase list (beg,end,src triples) of the last factorize call. */

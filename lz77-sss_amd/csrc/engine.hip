@@ -293,6 +293,80 @@ LZ77SSS_API int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int*
     });
 }
 
+LZ77SSS_API int lz77sss_session_sss_range(lz77sss_session* s, uint64_t first, uint64_t end, uint64_t base,
+                                          uint64_t window, uint64_t* size_sss, int* has_runs) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        LZ_HIP(hipSetDevice(s->E.device));
+        s->E.build_sss_range(first, end, base, window);
+        if (size_sss) *size_sss = s->E.s64;
+        if (has_runs) *has_runs = s->E.has_runs64;
+    });
+}
+
+LZ77SSS_API int lz77sss_session_get_sss64(lz77sss_session* s, uint64_t* out, uint64_t cap) {
+    if (!s || (!out && s->E.s64)) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (cap < s->E.s64) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (s->E.s64) LZ_HIP(hipMemcpy(out, s->E.S64.p, s->E.s64 * 8, hipMemcpyDeviceToHost));
+    });
+}
+
+LZ77SSS_API int lz77sss_session_copy_sss64_device(lz77sss_session* s, void* dst, uint64_t cap) {
+    if (!s || (!dst && s->E.s64)) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (cap < s->E.s64) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        LZ_HIP(hipSetDevice(s->E.device));
+        if (s->E.s64) LZ_HIP(hipMemcpyAsync(dst, s->E.S64.p, s->E.s64 * 8, hipMemcpyDeviceToDevice, s->E.st));
+        LZ_HIP(hipStreamSynchronize(s->E.st));
+    });
+}
+
+// chr19-style text in HBM: byte p of the text is a function of (p, seed) only
+__device__ __forceinline__ lz::u64 gen_mix(lz::u64 x) {  // splitmix64 finalizer
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__global__ void k_gen_genome(lz::u8* __restrict__ out, lz::u64 n, lz::u64 offset, lz::u64 base_len,
+                             lz::u64 mut_thr, lz::u64 seed) {
+    const lz::u64 i0 = ((lz::u64)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i0 >= n) return;
+    lz::u32 w[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 16 && i0 + k < n; k++) {
+        const lz::u64 p = offset + i0 + k;
+        const lz::u64 q = p % base_len;
+        lz::u32 c = (lz::u32)(gen_mix(q ^ (seed << 40)) >> 62);
+        if (p >= base_len) {
+            const lz::u64 h = gen_mix(p ^ (seed * 0xD6E8FEB86659FD93ull) ^ 0x5851F42D4C957F2Dull);
+            if (h < mut_thr) c = (c + 1 + (lz::u32)((h >> 7) % 3)) & 3;
+        }
+        w[k >> 2] |= (lz::u32)"ACGT"[c] << (8 * (k & 3));
+    }
+    if (i0 + 16 <= n) {
+        *(uint4*)(out + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int k = 0; i0 + k < n; k++) out[i0 + k] = (lz::u8)(w[k >> 2] >> (8 * (k & 3)));
+    }
+}
+
+LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint64_t base_len, double mut_rate,
+                                           uint32_t seed, uint64_t offset) {
+    if (!s || base_len == 0 || !(mut_rate >= 0.0 && mut_rate <= 1.0)) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        lz::engine& E = s->E;
+        if (n > E.max_n) throw lz::error(LZ77SSS_EINVAL, "text larger than the session capacity");
+        LZ_HIP(hipSetDevice(E.device));
+        E.n = n;
+        const lz::u64 thr = mut_rate >= 1.0 ? ~0ull : (lz::u64)(mut_rate * 18446744073709551616.0);
+        if (n) k_gen_genome<<<(unsigned)((n + 4095) / 4096), 256, 0, E.st>>>(E.d_text, n, offset, base_len, thr, seed);
+        LZ_HIP(hipGetLastError());
+        LZ_HIP(hipMemsetAsync(E.d_text + n, 0, lz::TEXT_PAD, E.st));
+        LZ_HIP(hipStreamSynchronize(E.st));
+    });
+}
+
 LZ77SSS_API int lz77sss_session_get_sss(lz77sss_session* s, uint32_t* out, uint64_t cap) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
@@ -349,7 +423,7 @@ LZ77SSS_API int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap
 LZ77SSS_API int lz77sss_session_sss_kernel_time(lz77sss_session* s, double* ms, uint64_t* bytes) {
     if (!s) return LZ77SSS_EINVAL;
     if (ms) *ms = s->E.sss_kernel_ms;
-    if (bytes) *bytes = s->E.n + 4ull * s->E.s;
+    if (bytes) *bytes = s->E.sss_kernel_bytes;
     return LZ77SSS_OK;
 }
 

@@ -18,6 +18,7 @@
 //                   and wave scans, ordered per-stripe output
 //   k_sss_fallback -- exact slow path for stripes with more than SCAP outputs
 //   k_sss_compact-- per-stripe outputs -> sorted S
+#include "../../include/lz77sss.h"
 #include "../include/engine.h"
 
 #include <hipcub/hipcub.hpp>
@@ -570,6 +571,7 @@ void engine::build_sss(const u8* T) {
     has_runs = false;
     runs_valid = false;
     sss_kernel_ms = 0;
+    sss_kernel_bytes = 0;
     if (n < 2 * (u64)TAU) return;
     const u64 last_i = n - 2 * TAU;
     const u64 nanch = (n - TAU) / QA + 2;
@@ -657,9 +659,82 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipMemsetAsync(lc + nlanes, 0, sizeof(u32), st));
     LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, lc, off, (int)(nlanes + 1), st));
     s = rd1(off + nlanes, st);
+    sss_kernel_bytes = n + 4ull * s;
     u32* dS = S.get((u64)s + 1);
     k_sss_compact<<<cdiv(nlanes, 256), 256, 0, st>>>(lo, lc, off, lf, ovf_slot, ovf_out, nlanes, dS);
     LZ_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// pos_t = uint64_t sync set of a decision range (lce_sss.hpp:53 instantiated with
+// pos_t = uint64_t, lz77_sss.hpp:72-75).  Phi and Q are functions of window contents
+// only, so S n [b, e) is the sync set of the view T[b, e + 2tau - 1), whose last
+// decision is e - 1: the range is walked in windows of `window` decisions through
+// build_sss on such views (a 2tau-1 byte halo each), and the positions are widened to
+// 64 bits with the view offset plus `base` added.  The same halo is what a rank of a
+// sharded job holds: it loads T[b_r, e_r + 2tau - 1) and passes
+// base = b_r.
+__global__ void k_lower_bound_u32(const u32* __restrict__ S, u32 s, u32 x, u32* __restrict__ out) {
+    u32 lo = 0, hi = s;
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (S[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    *out = lo;
+}
+__global__ void k_sss_widen(const u32* __restrict__ S, u32 s, const u32* __restrict__ skip, u64 add,
+                            u64* __restrict__ out) {
+    const u32 k0 = *skip;
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x + k0;
+    if (k >= s) return;
+    out[k - k0] = (u64)S[k] + add;
+}
+
+void engine::build_sss_range(u64 first, u64 end, u64 base, u64 window) {
+    s64 = 0;
+    has_runs64 = false;
+    stats_sss_windows = 0;
+    if (n < 2 * (u64)TAU) return;
+    end = std::min<u64>(end, n - 2 * TAU + 1);
+    if (first >= end) return;
+    if (window == 0) window = 1ull << 30;
+    window = std::max<u64>(4096, (window + 4095) & ~4095ull);  // view starts stay 256-byte aligned
+    if (window > (1ull << 31)) throw error(LZ77SSS_EINVAL, "window must be at most 2^31 decisions");
+    const u64 n_full = n;
+    u32* ctr = counters.get(16) + 12;  // build_sss clears and uses the first two
+    u64 b = first & ~255ull;  // aligned view start; decisions in [b, first) are dropped
+    double kms = 0;
+    u64 kbytes = 0;
+    try {
+        while (b < end) {
+            const u64 e = std::min(end, b + window);
+            n = e - b + 2 * TAU - 1;  // the view: its last decision is e - 1
+            build_sss(d_text + b);
+            kms += sss_kernel_ms;
+            kbytes += sss_kernel_bytes;
+            has_runs64 |= has_runs;
+            stats_sss_windows++;
+            const u32 x = first > b ? (u32)(first - b) : 0u;
+            k_lower_bound_u32<<<1, 1, 0, st>>>(S.p, s, x, ctr);
+            const u32 skip = x ? rd1(ctr, st) : 0u;
+            const u64 cnt = (u64)s - skip;
+            u64* out = S64.grow_keep(s64 + cnt + 1, s64, st);
+            if (cnt) k_sss_widen<<<cdiv(cnt, 256), 256, 0, st>>>(S.p, s, ctr, b + base, out + s64);
+            LZ_HIP(hipGetLastError());
+            s64 += cnt;
+            b = e;
+        }
+    } catch (...) {
+        n = n_full;
+        throw;
+    }
+    n = n_full;
+    sss_kernel_ms = kms / (double)stats_sss_windows;  // per launch, averaged over the windows
+    sss_kernel_bytes = kbytes / stats_sss_windows;
+    // the u32 structures now describe the last view, not the text
+    s = 0;
+    runs_valid = false;
+    LZ_HIP(hipStreamSynchronize(st));
 }
 
 }  // namespace lz

@@ -80,11 +80,17 @@ struct engine {
     u32 s = 0;
     bool has_runs = false;
     double sss_kernel_ms = 0;  // dominant kernel (SSS main pass) duration
+    u64 sss_kernel_bytes = 0;  // its algorithmic bytes (text + 4|S|) per launch
     u64 stats_fallback_lanes = 0;
     dbuf<u8> run_p;            // periodic-run table per Q anchor (lce_dev.h run_tab)
     dbuf<u32> run_hi, run_lo;
     dbuf<u64> run_scan_a, run_scan_b;
     bool runs_valid = false;
+    // pos_t = uint64_t sync set of a decision range (build_sss_range): any n, windowed
+    dbuf<u64> S64;
+    u64 s64 = 0;
+    bool has_runs64 = false;
+    u64 stats_sss_windows = 0;
     run_tab runs() const {
         run_tab R;
         if (runs_valid) { R.p = run_p.p; R.hi = run_hi.p; R.lo = run_lo.p; }
@@ -158,6 +164,7 @@ struct engine {
 
     // pipeline phases (each enqueues on `st`)
     void build_sss(const u8* T);
+    void build_sss_range(u64 first, u64 end, u64 base, u64 window);  // csrc/sss.hip
     void build_sa_s(const u8* T);
     void build_lcp_rmq(const u8* T);
     void build_lpf_opt(const u8* T);

@@ -57,6 +57,11 @@ _SYMBOLS = {
     "lz77sss_session_get_factors": (ctypes.c_int, [_P, _P, _U64]),
     "lz77sss_session_sss": (ctypes.c_int, [_P, ctypes.POINTER(_U64), ctypes.POINTER(ctypes.c_int)]),
     "lz77sss_session_get_sss": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_sss_range": (ctypes.c_int, [_P, _U64, _U64, _U64, _U64, ctypes.POINTER(_U64),
+                                                 ctypes.POINTER(ctypes.c_int)]),
+    "lz77sss_session_get_sss64": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_copy_sss64_device": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_gen_genome": (ctypes.c_int, [_P, _U64, _U64, ctypes.c_double, ctypes.c_uint32, _U64]),
     "lz77sss_session_get_sa_s": (ctypes.c_int, [_P, _P, _P, _U64]),
     "lz77sss_session_get_lpf": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_phase_times": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
@@ -180,6 +185,28 @@ class Session:
         out = np.empty(max(s.value, 1), np.uint32)
         _check(load_library().lz77sss_session_get_sss(self._h, out.ctypes.data_as(_P), s.value))
         return out[:s.value], bool(r.value)
+
+    def sss_range(self, first: int = 0, end: int = 2**64 - 1, base: int = 0, window: int = 0):
+        """pos_t = uint64_t sync set S n [first, end) of the loaded text, + base (csrc/sss.hip
+        build_sss_range).  Returns (count, has_runs); the positions stay in HBM."""
+        s, r = _U64(), ctypes.c_int()
+        _check(load_library().lz77sss_session_sss_range(self._h, first, end, base, window, ctypes.byref(s),
+                                                        ctypes.byref(r)))
+        return s.value, bool(r.value)
+
+    def sync_set64(self, s: int) -> np.ndarray:
+        out = np.empty(max(s, 1), np.uint64)
+        _check(load_library().lz77sss_session_get_sss64(self._h, out.ctypes.data_as(_P), s))
+        return out[:s]
+
+    def copy_sync_set64(self, dst_ptr: int, cap: int):
+        """Device-to-device copy of the sss_range result to a device address (same device)."""
+        _check(load_library().lz77sss_session_copy_sss64_device(self._h, _P(dst_ptr), cap))
+
+    def gen_genome(self, n: int, base_len: int, mut_rate: float, seed: int, offset: int = 0):
+        """Generates bytes [offset, offset + n) of a chr19-style text directly in HBM."""
+        _check(load_library().lz77sss_session_gen_genome(self._h, n, base_len, mut_rate, seed, offset))
+        self.n = n
 
     def sync_set(self, s: int) -> np.ndarray:
         out = np.empty(max(s, 1), np.uint32)

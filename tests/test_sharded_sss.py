@@ -1,0 +1,213 @@
+"""Sharded / windowed sync set (pos_t = uint64_t, SURVEY.md section 8e collective (1)).
+
+CPU: the block partition, the halo argument checked with the oracle itself (the sync
+set of T[b, e + 2tau - 1) shifted by b is S n [b, e)), and the world_size-2 gloo
+gather driven by the oracle as the block function.  GPU: windowed/ranged
+build_sss_range against the one-shot pass, the sharded path through the C-ABI on
+two ranks sharing the GPU, device text generation by offset, and a text past 2^32.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, str(ROOT / "lz77-sss_amd"))
+import sharded  # noqa: E402
+
+TAU = 512
+
+
+def _texts():
+    import oracle
+
+    rng = np.random.default_rng(5)
+    yield "random", rng.integers(0, 256, 40000).astype(np.uint8)
+    # runs (Q windows) straddling the block boundaries
+    t = rng.integers(0, 4, 50000).astype(np.uint8) + 65
+    t[8000:16000] = np.tile(np.frombuffer(b"ACGTTGCA" * 3, np.uint8), 8000 // 24 + 1)[:8000]
+    t[20000:21500] = 67
+    yield "runs", t
+    yield "genome", _genome(60000)
+
+
+def _genome(n):
+    import lz77sss
+
+    return lz77sss.gen_genome(n, 7000, 0.01, 3)
+
+
+def test_partition_covers_decisions():
+    for n in [0, 1000, 1023, 1024, 5000, 1 << 20, (1 << 20) + 12345]:
+        for world in [1, 2, 3, 8]:
+            parts = sharded.partition(n, world)
+            d = sharded.num_decisions(n)
+            assert len(parts) == world
+            assert parts[0][0] == 0 and parts[-1][1] == d
+            for (b0, e0), (b1, e1) in zip(parts, parts[1:]):
+                assert e0 == b1
+            for b, e in parts:
+                assert b <= e and (b % sharded.ALIGN == 0 or b == d)
+                lo, hi = sharded.block_bytes(n, b, e)
+                if e > b:
+                    assert lo == b and hi == min(n, e + 2 * TAU - 1)
+                    assert hi - lo >= 2 * TAU  # the view has >= 1 decision
+
+
+def _oracle_block(text, b, e, n):
+    import oracle
+
+    lo, hi = sharded.block_bytes(n, b, e)
+    if e <= b:
+        return np.zeros(0, np.uint64), False
+    s, runs = oracle.sss(np.ascontiguousarray(text[lo:hi]))
+    s = s.astype(np.uint64) + np.uint64(b)
+    assert s.size == 0 or int(s[-1]) < e
+    return s, runs
+
+
+@pytest.mark.parametrize("world", [2, 3, 7])
+def test_oracle_halo_blocks(world):
+    import oracle
+
+    for name, T in _texts():
+        full, runs = oracle.sss(T)
+        parts = [_oracle_block(T, b, e, T.size) for b, e in sharded.partition(T.size, world, align=256)]
+        cat = np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, np.uint64)
+        assert np.array_equal(cat, full.astype(np.uint64)), name
+        assert any(p[1] for p in parts) == runs, name
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q, use_gpu, T):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT / "lz77-sss_amd"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import sharded as SH
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if use_gpu:
+            S, runs = SH.sss_sharded(T, T.size, rank, world, device=0)
+        else:
+            S, runs = SH.sss_sharded(T, T.size, rank, world, compute=_oracle_block)
+        q.put((rank, S, runs))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_ranks(world, use_gpu, T):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, use_gpu, T)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_gloo_two_ranks_oracle_blocks():
+    import oracle
+
+    T = dict(_texts())["runs"]
+    full, runs = oracle.sss(T)
+    res = _run_ranks(2, False, T)
+    for _, S, r in res:
+        assert np.array_equal(S, full.astype(np.uint64))
+        assert r == runs
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.mark.gpu
+def test_sss_range_windows_match_one_shot(lz, orc):
+    import lz77sss
+
+    for name, T in _texts():
+        with lz77sss.Session(T.size) as s:
+            s.load(T)
+            full, runs = s.sss()
+            full = full.astype(np.uint64)
+            for window in [4096, 8192, 12288, 0]:
+                c, r = s.sss_range(window=window)
+                assert np.array_equal(s.sync_set64(c), full), (name, window)
+                assert r == runs
+            # sub-ranges with unaligned bounds and a base offset
+            d = sharded.num_decisions(T.size)
+            for first, end in [(1, d), (777, 20001), (4096, 4097), (d - 5, d + 100), (0, 0)]:
+                c, _ = s.sss_range(first, end, base=1 << 40, window=4096)
+                want = full[(full >= first) & (full < min(end, d))] + np.uint64(1 << 40)
+                assert np.array_equal(s.sync_set64(c), want), (name, first, end)
+
+
+@pytest.mark.gpu
+def test_sss_range_large_rr(lz, orc):
+    import lz77sss
+
+    T = lz77sss.gen_random_repetitive(1 << 22, 1 << 22, 9, 0.5, 0.05)
+    with lz77sss.Session(T.size) as s:
+        s.load(T)
+        full, _ = s.sss()
+        c, _ = s.sss_range(window=1 << 20)
+        assert np.array_equal(s.sync_set64(c), full.astype(np.uint64))
+    import oracle
+
+    assert np.array_equal(oracle.sss(T)[0], full)
+
+
+@pytest.mark.gpu
+def test_sharded_two_ranks_on_gpu(lz, orc):
+    import oracle
+
+    T = dict(_texts())["runs"]
+    full, runs = oracle.sss(T)
+    for _, S, r in _run_ranks(2, True, T):
+        assert np.array_equal(S, full.astype(np.uint64))
+        assert r == runs
+
+
+@pytest.mark.gpu
+def test_gen_genome_blocks_and_past_4gib(lz, orc):
+    import lz77sss
+
+    n = (1 << 32) + (3 << 20) + 12345  # positions past 2^32: pos_t = uint64_t
+    with lz77sss.Session(n) as s:
+        s.gen_genome(n, 59 << 20, 0.001, 7)
+        c1, _ = s.sss_range(window=1 << 30)
+        S1 = s.sync_set64(c1)
+        c2, _ = s.sss_range(window=(1 << 28) + 4096)
+        S2 = s.sync_set64(c2)
+        assert np.array_equal(S1, S2)
+        assert S1.size > 0 and int(S1[-1]) > (1 << 32)
+        assert np.all(np.diff(S1.astype(np.int64)) > 0)
+        # |S| near 2n/tau for a random-like text
+        assert 0.5 < S1.size / (2 * n / TAU) < 1.5
+    # a block generated alone by offset equals the same range of the whole text
+    b = (1 << 32) - (1 << 20)
+    e = b + (2 << 20)
+    with lz77sss.Session(e - b + 2 * TAU - 1) as s:
+        s.gen_genome(e - b + 2 * TAU - 1, 59 << 20, 0.001, 7, offset=b)
+        c, _ = s.sss_range(0, e - b, base=b)
+        blk = s.sync_set64(c)
+    want = S1[(S1 >= b) & (S1 < e)]
+    assert np.array_equal(blk, want)
