@@ -185,14 +185,24 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
                 if (f + 1 >= lo + 32) cm[wi] = 0;
                 else if (f + 1 > lo) cm[wi] &= ~0u << (f + 1 - lo);
             }
+            // a period pp must also agree where earlier shifts disagreed: test the
+            // disagreement of p1 (f) and of the last rejected candidate (g) first, so
+            // candidates in a run broken by a single character cost O(1), not a scan
+            int g = f;
             for (int wi = 0; wi < 6 && !per;) {
                 if (!cm[wi]) {
                     wi++;
                     continue;
                 }
                 const u32 pp = 32 * wi + __builtin_ctz(cm[wi]) + 1;
-                if (ext_fwd(oa + 4, oa + (int)(QM - pp), (int)pp) == oa + (int)(QM - pp)) per = pp;
                 cm[wi] &= cm[wi] - 1;
+                const int lim = (int)(QM - pp);  // offsets x < lim are compared (x >= 4 after the filter)
+                if ((f < lim && byte(oa + f) != byte(oa + f + (int)pp)) ||
+                    (g < lim && byte(oa + g) != byte(oa + g + (int)pp)))
+                    continue;
+                const int e = ext_fwd(oa + 4, oa + lim, (int)pp);
+                if (e == oa + lim) per = pp;
+                else g = e - oa;
             }
         }
     }
