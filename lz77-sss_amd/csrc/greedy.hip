@@ -753,32 +753,6 @@ __global__ void k_gap_bitmaps(const u32* __restrict__ P, u32 m, u32 N, u32 nt, u
         if (pe - pb <= 48 && pb < nt) bm_set_range_wave(bmSup, pb, min(pe, nt), lane);
     }
 }
-// maximal runs of ones -> intervals [st, en): count starts/ends per word, then write
-__global__ void k_bm_count(const u32* __restrict__ bm, u64 nw, u32* __restrict__ ns, u32* __restrict__ ne) {
-    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nw) return;
-    const u32 b = bm[w], prev = w ? (bm[w - 1] >> 31) : 0u;
-    const u32 sh = (b << 1) | prev;
-    ns[w] = __popc(b & ~sh);
-    ne[w] = __popc(~b & sh);
-}
-__global__ void k_bm_write_runs(const u32* __restrict__ bm, u64 nw, const u32* __restrict__ os,
-                                const u32* __restrict__ oe, u32* __restrict__ st, u32* __restrict__ en) {
-    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nw) return;
-    const u32 b = bm[w], prev = w ? (bm[w - 1] >> 31) : 0u;
-    const u32 sh = (b << 1) | prev;
-    u32 sm = b & ~sh, em = ~b & sh;
-    u32 o = os[w];
-    while (sm) { st[o++] = (u32)(32 * w + __builtin_ctz(sm)); sm &= sm - 1; }
-    o = oe[w];
-    while (em) { en[o++] = (u32)(32 * w + __builtin_ctz(em)); em &= em - 1; }
-}
-// positions of set bits (ascending) with a flag bit from a second bitmap
-__global__ void k_bm_count1(const u32* __restrict__ bm, u64 nw, u32* __restrict__ c) {
-    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w < nw) c[w] = __popc(bm[w]);
-}
 __global__ void k_bm_xor(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (w < nw) x[w] = a[w] ^ b[w];
@@ -791,19 +765,117 @@ __global__ void k_bm_or(const u32* __restrict__ a, const u32* __restrict__ b, u6
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (w < nw) x[w] = a[w] | b[w];
 }
-__global__ void k_bm_list(const u32* __restrict__ bm, const u32* __restrict__ flagbm, u64 nw, const u32* __restrict__ off,
-                          u32* __restrict__ pos, u8* __restrict__ flag) {
-    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= nw) return;
-    u32 b = bm[w], o = off[w];
-    const u32 f = flagbm ? flagbm[w] : 0u;
-    while (b) {
-        const u32 t = __builtin_ctz(b);
-        pos[o] = (u32)(32 * w + t);
-        if (flag) flag[o] = (f >> t) & 1;
-        o++;
-        b &= b - 1;
+// Bitmap -> positions lists without per-word count arrays: a block of 256 lanes owns
+// BMB = 2048 words (8 per lane); pass 1 writes per-block counts of the marked bits
+// (two masks packed in one u64: hi = mask A, lo = mask B), one scan over the ~nw/2048
+// block counts gives every block its offsets, pass 2 recomputes the lane counts, scans
+// them in LDS and writes the positions in order.  Replaces two full-length (nw) count
+// arrays and their device-wide scans.
+constexpr u32 BMB_T = 256, BMB_W = 8, BMB = BMB_T * BMB_W;
+// masks of word w: runs (A = run starts, B = run ends) or set bits (A = a & ~b, B unused)
+struct bm_runs {
+    const u32* bm;
+    __device__ __forceinline__ void masks(u64 w, u32& a, u32& b) const {
+        const u32 x = bm[w], prev = w ? (bm[w - 1] >> 31) : 0u;
+        const u32 sh = (x << 1) | prev;
+        a = x & ~sh;
+        b = ~x & sh;
     }
+};
+struct bm_bits {
+    const u32* bm;
+    const u32* notbm;  // optional: bits of bm not in notbm
+    __device__ __forceinline__ void masks(u64 w, u32& a, u32& b) const {
+        a = bm[w] & (notbm ? ~notbm[w] : ~0u);
+        b = 0;
+    }
+};
+template <class M>
+__global__ __launch_bounds__(BMB_T) void k_bmb_count(M mk, u64 nw, u64* __restrict__ bsum) {
+    __shared__ u64 red[BMB_T / 64];
+    const u64 w0 = (u64)blockIdx.x * BMB + threadIdx.x;
+    u32 ca = 0, cb = 0;
+#pragma unroll
+    for (u32 r = 0; r < BMB_W; r++) {
+        const u64 w = w0 + (u64)r * BMB_T;
+        if (w < nw) {
+            u32 a, b;
+            mk.masks(w, a, b);
+            ca += __popc(a);
+            cb += __popc(b);
+        }
+    }
+    u64 v = ((u64)ca << 32) | cb;
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+// lane l of a block owns words [w0 + 8l, w0 + 8l + 8) in pass 2 (contiguous, in order)
+template <class M, class OUT>
+__global__ __launch_bounds__(BMB_T) void k_bmb_write(M mk, u64 nw, const u64* __restrict__ bincl, OUT out) {
+    __shared__ u64 part[BMB_T];
+    const u32 l = threadIdx.x;
+    const u64 wb = (u64)blockIdx.x * BMB + (u64)l * BMB_W;
+    u32 ca = 0, cb = 0;
+#pragma unroll
+    for (u32 r = 0; r < BMB_W; r++) {
+        if (wb + r < nw) {
+            u32 a, b;
+            mk.masks(wb + r, a, b);
+            ca += __popc(a);
+            cb += __popc(b);
+        }
+    }
+    const u64 mine = ((u64)ca << 32) | cb;
+    part[l] = mine;
+    __syncthreads();
+    for (u32 d = 1; d < BMB_T; d <<= 1) {
+        const u64 v = l >= d ? part[l - d] : 0ull;
+        __syncthreads();
+        part[l] += v;
+        __syncthreads();
+    }
+    const u64 base = (blockIdx.x ? bincl[blockIdx.x - 1] : 0ull) + part[l] - mine;
+    u32 oa = (u32)(base >> 32), ob = (u32)base;
+#pragma unroll 1
+    for (u32 r = 0; r < BMB_W; r++) {
+        const u64 w = wb + r;
+        if (w >= nw) break;
+        u32 a, b;
+        mk.masks(w, a, b);
+        while (a) { out.a(oa++, (u32)(32 * w + __builtin_ctz(a)), w); a &= a - 1; }
+        while (b) { out.b(ob++, (u32)(32 * w + __builtin_ctz(b))); b &= b - 1; }
+    }
+}
+struct out_runs {
+    u32* st;
+    u32* en;
+    __device__ __forceinline__ void a(u32 o, u32 p, u64) const { st[o] = p; }
+    __device__ __forceinline__ void b(u32 o, u32 p) const { en[o] = p; }
+};
+struct out_list {  // positions + a flag bit from a second bitmap
+    u32* pos;
+    u8* flag;
+    const u32* flagbm;
+    __device__ __forceinline__ void a(u32 o, u32 p, u64 w) const {
+        pos[o] = p;
+        if (flag) flag[o] = (flagbm[w] >> (p & 31)) & 1;
+    }
+    __device__ __forceinline__ void b(u32, u32) const {}
+};
+// totals of the two masks; bincl holds the inclusive block scan afterwards
+template <class M>
+static u64 bmb_scan(M mk, u64 nw, dbuf<u64>& bs, dbuf<u64>& bi, dbuf<u8>& tmp, hipStream_t st) {
+    const u64 nblk = std::max<u64>(1, (nw + BMB - 1) / BMB);
+    u64* s = bs.get(nblk);
+    u64* incl = bi.get(nblk);
+    k_bmb_count<<<(unsigned)nblk, BMB_T, 0, st>>>(mk, nw, s);
+    size_t tb = 0;
+    LZ_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, s, incl, (int)nblk, st));
+    u8* t = tmp.get(tb);
+    LZ_HIP(hipcub::DeviceScan::InclusiveSum(t, tb, s, incl, (int)nblk, st));
+    return rd1(incl + nblk - 1, st);
 }
 // intervals -> chunks of <= ch positions with ranks (rank0 = exclusive scan of
 // lengths).  Short chunks keep k_slots (one thread per chunk, a direct
@@ -1102,6 +1174,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     for (int x = 0; x < 5; x++) zmask0 |= (G.lens[x] >= N) ? (1u << x) : 0u;  // reinit(0) at construction
     const u64 nw = (u64)N / 32 + 2;  // bitmap words (a zero word past the end)
     const unsigned gw = cdiv(nw, 256);
+    const unsigned bmb_blocks = (unsigned)std::max<u64>(1, (nw + BMB - 1) / BMB);
 
     // ---- default segments: gaps + chunk boundaries of long gaps
     const u32 CH = std::getenv("LZ77SSS_NO_CHUNK") ? 0x0FFFFFFFu : 512u;
@@ -1156,10 +1229,6 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     W.P = P;
     W.L = view(T);
     u64 nb = 0;
-    u32* ns = g_tmp1.get(nw + 1);
-    u32* ne = g_tmp2.get(nw + 1);
-    u32* os = g_tmp3.get(nw + 1);
-    u32* oe = g_tmp4.get(nw + 1);
     const u32 nslots = G.mask + 1;
     auto build_buckets = [&](auto key, u64 mk, dbuf<u32>& bk) {
         u32* b = bk.get((u64)nslots + 1);
@@ -1180,12 +1249,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     // runs of a bitmap -> intervals (st, en), ranks, chunks for k_slots
     auto runs_to_chunks = [&](const u32* bm, dbuf<u32>& dst, dbuf<u32>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
                               u64& npos, u32& nch) -> ichunk* {
-        k_bm_count<<<gw, 256, 0, st>>>(bm, nw, ns, ne);
-        ni = excl_scan(ns, os, nw, scan_tmp, st);
-        excl_scan(ne, oe, nw, scan_tmp, st);
+        const u64 tot = bmb_scan(bm_runs{bm}, nw, g_bsum, g_bincl, scan_tmp, st);
+        ni = (u32)(tot >> 32);  // run starts (= run ends)
         u32* a = dst.get(ni + 1);
         u32* b = den.get(ni + 1);
-        k_bm_write_runs<<<gw, 256, 0, st>>>(bm, nw, os, oe, a, b);
+        k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_runs{bm}, nw, g_bincl.p, out_runs{a, b});
         u32* len = g_tmp5.get(ni + 1);
         u32* nc = g_tmp6.get(ni + 1);
         u32* rk = drk.get(ni + 1);
@@ -1431,8 +1499,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], bmI2);
         }
         k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
-        k_bm_count1<<<gw, 256, 0, st>>>(bmT, nw, ns);
-        const u64 ny = excl_scan(ns, os, nw, scan_tmp, st);
+        const u64 ny = bmb_scan(bm_bits{bmT, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
         lap("insert set");
         if (ny == 0) {
             // every lookup of the chain was exact: emit the factors
@@ -1447,11 +1514,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         // positions that joined (flag 1) or left (0) I
         u32* d_y = dirty_in.get(ny + 1);
         u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
-        k_bm_list<<<gw, 256, 0, st>>>(bmT, bmI2, nw, os, d_y, d_j);
+        k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_bits{bmT, nullptr}, nw, g_bincl.p, out_list{d_y, d_j, bmI2});
         // many positions outside the base set: rebuild it as I' u I_b, re-walk everything
-        k_bm_andnot<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
-        k_bm_count1<<<gw, 256, 0, st>>>(bmT, nw, ne);
-        const u64 outside = excl_scan(ne, oe, nw, scan_tmp, st);
+        const u64 outside = bmb_scan(bm_bits{bmI2, bmIb}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
         if (outside * 8 > nb) {
             k_bm_or<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
             std::swap(g_bmI.p, g_bmI2.p);
