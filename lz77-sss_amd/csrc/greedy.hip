@@ -117,6 +117,50 @@ __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __res
         }
     }
 }
+// dense slot ids: a repetitive text hashes its gap positions into few distinct slots
+// (rr 1 GiB: 6 091 of 2^25), so sorting dense ids needs 2 radix passes instead of 4.
+// Presence as one byte per slot written with plain stores (idempotent: hot slots cost
+// no atomics), packed into a bitmap with per-word popcounts; id = rank of the slot.
+__global__ void k_slot_presence(const u32* __restrict__ keys, u64 m, u8* __restrict__ pf) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m) pf[keys[e]] = 1;
+}
+__global__ void k_presence_pack(const u8* __restrict__ pf, u64 nw, u32* __restrict__ pbm, u32* __restrict__ c) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    const uint4* q = (const uint4*)(pf + 32 * w);
+    const uint4 a = q[0], b = q[1];
+    const u32 v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    u32 bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) bits |= ((v[j] >> (8 * k)) & 1u) << (4 * j + k);
+    pbm[w] = bits;
+    c[w] = __popc(bits);
+}
+__device__ __forceinline__ u32 slot_rank(const u32* pbm, const u32* pwp, u32 k) {
+    return pwp[k >> 5] + __popc(pbm[k >> 5] & ((1u << (k & 31)) - 1u));
+}
+__global__ void k_dense_keys(const u32* __restrict__ keys, u64 m, const u32* __restrict__ pbm,
+                             const u32* __restrict__ pwp, u32* __restrict__ dk) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m) dk[e] = slot_rank(pbm, pwp, keys[e]);
+}
+// first sorted index of every dense id (all ids occur), dstart[D] = m
+__global__ void k_dense_heads(const u32* __restrict__ sdk, u64 m, u32 D, u32* __restrict__ dstart) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > m) return;
+    if (t == m) { dstart[D] = (u32)m; return; }
+    if (t == 0 || sdk[t - 1] != sdk[t]) dstart[sdk[t]] = (u32)t;
+}
+// slot -> first sorted index with slot >= s: the start of the next present slot's id
+__global__ void k_bstart_rank(const u32* __restrict__ pbm, const u32* __restrict__ pwp,
+                              const u32* __restrict__ dstart, u32 nslots, u32 D, u32* __restrict__ bstart) {
+    const u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x > nslots) return;
+    bstart[x] = dstart[x < nslots ? slot_rank(pbm, pwp, (u32)x) : D];
+}
 // predecessor entry within the same slot (base set)
 __global__ void k_pred(const u32* __restrict__ skeys, const u32* __restrict__ svals, u64 m, u32* __restrict__ pred5) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1289,15 +1333,43 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u32* pred5 = occ_buf.get(ne5 + 1);
         u8* rem = rem_buf.get(nb + 1);
         LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
+        bool dense = false;
+        u32 D = 0, dense_bits = 0;
+        const u64 npw = ((u64)nslots + 31) / 32;
+        u32* pbm = g_pbm.get(npw + 1);
+        u32* pwp = g_pwp.get(npw + 1);
         if (nch) {
             k_slots<<<cdiv(nch, 128), 128, 0, st>>>(T, G, ch, nch, keys, vals, ipos);
             lap("base slots");
+            // distinct slots -> dense ids when that saves radix passes
+            // (tried below 2^28 entries: a base set that large comes from a non-repetitive
+            // text, whose slots are all in use)
+            if (ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE")) {
+                u32* pcnt = g_pcnt.get(npw + 1);
+                u8* pf = (u8*)g_pflag.get(npw * 8);
+                LZ_HIP(hipMemsetAsync(pf, 0, npw * 32, st));
+                k_slot_presence<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pf);
+                k_presence_pack<<<cdiv(npw, 256), 256, 0, st>>>(pf, npw, pbm, pcnt);
+                D = excl_scan(pcnt, pwp, npw, scan_tmp, st);
+                u32 dbits = 1;
+                while (dbits < 32 && (1ull << dbits) < D) dbits++;
+                dense = (dbits + 7) / 8 < (gp.log2_size_h + 7) / 8;
+                dense_bits = dbits;
+            }
+            u32* sk_in = keys;
+            u32 sbits = gp.log2_size_h;
+            if (dense) {
+                k_dense_keys<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pbm, pwp, skeys);
+                sk_in = skeys;
+                skeys = g_sdk.get(ne5 + 1);
+                sbits = dense_bits;
+            }
+            if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy base: %u distinct slots, %s sort on %u bits\n", D,
+                                  dense ? "dense-id" : "slot", sbits);
             size_t tb = 0;
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, skeys, vals, svals, (int)ne5, 0,
-                                                      (int)gp.log2_size_h, st));
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
             u8* t = scan_tmp.get(tb);
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, skeys, vals, svals, (int)ne5, 0,
-                                                      (int)gp.log2_size_h, st));
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
             if (W.use_pred && ne5 < (1ull << 27)) {
                 k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
             } else if (W.use_pred) {
@@ -1315,7 +1387,14 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             }
         }
         lap("base sort + pred");
-        build_buckets(key_u32{skeys}, ne5, g_bstart);
+        if (dense) {
+            u32* dstart = g_dstart.get((u64)D + 1);
+            k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
+            k_bstart_rank<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
+                                                                      g_bstart.get((u64)nslots + 1));
+        } else {
+            build_buckets(key_u32{skeys}, ne5, g_bstart);
+        }
         W.istart = ist.p; W.iend = iend.p; W.irank = irank.p; W.nint = ni;
         W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne5;
         W.bstart = g_bstart.p;

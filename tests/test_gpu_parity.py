@@ -274,3 +274,14 @@ def test_c1_lpf_naive_vs_oracle(session, orc, lz, seed):
     F_ref, _ = orc.factorize(T, phr_mode=0)
     assert np.array_equal(F, F_ref)
     assert np.array_equal(lz.decode(F, T.size), T)
+
+
+@pytest.mark.parametrize("kind,mib", [("rr", 128), ("rr", 1), ("genome", 8)])
+def test_dense_slot_ids_match_slot_sort(session, lz, kind, mib, monkeypatch):
+    """Greedy base set sorted on dense slot ids (few distinct slots) == sorted on the slots."""
+    n = mib << 20
+    T = lz.gen_genome(n, 1 << 20, 0.001, 13) if kind == "genome" else lz.gen_random_repetitive(n, n, 7, 0.5, 0.05)
+    _, F1 = run(session, T)
+    monkeypatch.setenv("LZ77SSS_NO_DENSE", "1")
+    _, F0 = run(session, T)
+    assert F1.shape == F0.shape and np.array_equal(F1, F0)
