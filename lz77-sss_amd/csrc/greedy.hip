@@ -93,28 +93,27 @@ __device__ __forceinline__ u128 kr_direct(const u8* T, u64 q, u32 len, u64 b) {
 // order of longest_prev_occ (x = 4 .. 0)
 struct ichunk { u32 q0, q1, rank0; };
 
+// one thread per (chunk, x): the 5 fingerprint chains of a chunk run on 5 adjacent
+// lanes (5x the threads of a chunk-per-thread walk for latency hiding, and the 5
+// entries of a position are written by adjacent lanes)
 __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __restrict__ chunks, u32 nch,
                         u32* __restrict__ keys, u32* __restrict__ vals, u32* __restrict__ ipos) {
-    const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nch) return;
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= 5ull * nch) return;
+    const u64 c = g / 5;
+    const int x = 4 - (int)(g - 5 * c);  // lanes of a chunk: x = 4, 3, 2, 1, 0 (entry order)
     const ichunk ch = chunks[c];
-    u128 fp[5];
-#pragma unroll
-    for (int x = 0; x < 5; x++) fp[x] = kr_direct(T, ch.q0, G.lens[x], G.base[x]);
+    const u32 len = G.lens[x];
+    const u64 b = G.base[x];
+    const u128* np = G.negpow + x * 256;
+    u128 fp = kr_direct(T, ch.q0, len, b);
     for (u32 q = ch.q0; q < ch.q1; q++) {
         const u32 rank = ch.rank0 + (q - ch.q0);
-        if (ipos) ipos[rank] = q;
-#pragma unroll
-        for (int x = 4; x >= 0; x--) {
-            const u32 e = 5 * rank + (4 - x);
-            keys[e] = (u32)((u64)fp[x] & G.mask);
-            if (vals) vals[e] = e;
-        }
-        if (q + 1 < ch.q1) {
-#pragma unroll
-            for (int x = 0; x < 5; x++)
-                fp[x] = kr_roll(fp[x], G.base[x], G.negpow[x * 256 + T[q]], T[q + G.lens[x]]);
-        }
+        if (ipos && x == 4) ipos[rank] = q;
+        const u32 e = 5 * rank + (4 - x);
+        keys[e] = (u32)((u64)fp & G.mask);
+        if (vals) vals[e] = e;
+        if (q + 1 < ch.q1) fp = kr_roll(fp, b, np[T[q]], T[q + len]);
     }
 }
 // dense slot ids: a repetitive text hashes its gap positions into few distinct slots
@@ -1339,7 +1338,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u32* pbm = g_pbm.get(npw + 1);
         u32* pwp = g_pwp.get(npw + 1);
         if (nch) {
-            k_slots<<<cdiv(nch, 128), 128, 0, st>>>(T, G, ch, nch, keys, vals, ipos);
+            k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, vals, ipos);
             lap("base slots");
             // distinct slots -> dense ids when that saves radix passes
             // (tried below 2^28 entries: a base set that large comes from a non-repetitive
@@ -1416,7 +1415,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         if (!na) return 0;
         u32* akey32 = k32.get(5 * na);
         u32* apos = kpos.get(na);
-        k_slots<<<cdiv(nch, 128), 128, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
+        k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
         u64* ak = ka.get(5 * na);
         u64* ak2 = kb.get(5 * na);
         k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
