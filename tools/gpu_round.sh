@@ -10,4 +10,5 @@ timeout -k 10 300 python bench.py --workload genome --cpu-sample-mib 128 > gpuru
 timeout -k 10 300 python bench.py --phr-mode lpf_lnf_opt > gpurun_out/bench_rr_lnf.json 2> gpurun_out/bench_rr_lnf.err || exit 1
 timeout -k 10 300 python bench.py --mode exact --steps 3 --warmup 1 > gpurun_out/bench_rr_exact.json 2> gpurun_out/bench_rr_exact.err || exit 1
 timeout -k 10 300 python bench.py --mode exact --workload genome --steps 3 --warmup 1 > gpurun_out/bench_genome_exact.json 2> gpurun_out/bench_genome_exact.err || exit 1
+timeout -k 10 300 python bench.py --mode sss --size-gib 50 --steps 3 --warmup 1 > gpurun_out/bench_sss50.json 2> gpurun_out/bench_sss50.err || exit 1
 cat gpurun_out/bench_*.json
