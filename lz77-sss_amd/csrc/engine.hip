@@ -28,6 +28,8 @@ void engine::init(int dev, u64 maxn) {
     max_n = maxn;
     LZ_HIP(hipMalloc(&d_text, max_n + TEXT_PAD));
     LZ_HIP(hipMemsetAsync(d_text, 0, max_n + TEXT_PAD, st));
+    LZ_HIP(hipHostMalloc(&h_pin, 64, hipHostMallocDefault));
+    for (auto& e : ev_pin) LZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     LZ_HIP(hipStreamSynchronize(st));
 }
 
@@ -44,6 +46,10 @@ void engine::destroy() {
     if (d_text) (void)hipFree(d_text);
     if (d_text_rev) (void)hipFree(d_text_rev);
     d_text = d_text_rev = nullptr;
+    if (h_pin) (void)hipHostFree(h_pin);
+    h_pin = nullptr;
+    for (auto& e : ev_pin)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
     if (st) (void)hipStreamDestroy(st);
     st = nullptr;
 }

@@ -554,6 +554,11 @@ void engine::build_sa_s(const u8* T) {
     while (bits < 32 && (1ull << bits) <= s) bits++;
     u64* kv = u64a.get(s);
     u64* kv2 = u64b.get(s);
+    // every round's max rank goes to pinned memory behind its launches, and is read
+    // only after the NEXT round is enqueued: the device never idles on the host's
+    // convergence test.  The round after convergence is redundant but harmless (all
+    // ranks distinct: the same head ranks again, one more level for the LCP lifting).
+    int pending = -1;  // slot of the last round whose max rank is in flight
     while (maxr < s) {
         if (nlev_rank >= MAX_LV) throw error(-6, "prefix doubling did not converge");
         const u32 h = 1u << (nlev_rank - 1);
@@ -568,9 +573,17 @@ void engine::build_sa_s(const u8* T) {
         u32* Rn = rank_lv[nlev_rank].get(s);
         k_scatter_rank<<<g, 256, 0, st>>>(idx, rank, s, Rn);
         SA_DBG("doubling");
+        const int slot = (int)(nlev_rank & 1);
+        LZ_HIP(hipMemcpyAsync(h_pin + slot, rank + s - 1, 4, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipEventRecord(ev_pin[slot], st));
         nlev_rank++;
-        maxr = rd1(rank + s - 1, st);
+        if (pending >= 0) {
+            LZ_HIP(hipEventSynchronize(ev_pin[pending]));
+            if (h_pin[pending] >= s) break;  // converged one round ago
+        }
+        pending = slot;
     }
+    LZ_HIP(hipGetLastError());
     k_sa_from_rank<<<g, 256, 0, st>>>(rank_lv[nlev_rank - 1].p, s, SA.get(s), ISA.get(s));
     LZ_HIP(hipGetLastError());
 }

@@ -160,6 +160,10 @@ struct engine {
 
     phase_timer timer;
 
+    // pinned read-back slots + events: a host decision overlaps the next launches
+    u32* h_pin = nullptr;
+    hipEvent_t ev_pin[2] = {nullptr, nullptr};
+
     void init(int dev, u64 maxn);
     void load(const u8* h_text, u64 n_);
     void destroy();

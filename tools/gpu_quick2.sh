@@ -1,7 +1,7 @@
 # parity subset + rr/genome bench with phase laps
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "dense or medium or c1_seeds or edge or runs or golden_factor or lpf_lnf" > gpurun_out/pt_q2.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pt_q2.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "dense or medium or c1_seeds or edge or runs or golden or lpf_lnf" > gpurun_out/pt_q2.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pt_q2.log; exit 1; }
 tail -2 gpurun_out/pt_q2.log
 for WL in rr genome; do
 timeout -k 10 300 python bench.py --workload $WL --no-cpu-baseline > gpurun_out/bench_$WL.json 2> gpurun_out/bench_$WL.err || { tail -20 gpurun_out/bench_$WL.err; exit 1; }
