@@ -156,6 +156,11 @@ int lz77sss_session_copy_sss64_device(lz77sss_session* s, void* dst, uint64_t ca
  * any block of it can be generated alone (the C4 input, without a host copy). */
 int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint64_t base_len, double mut_rate, uint32_t seed,
                                uint64_t offset);
+/* ssszip's gapped container of the last factorize call, which must have used
+ * fact_mode = LZ77SSS_SKIP_PHRASES (encode_gapped, cli/ssszip.cpp:119-177, vbyte
+ * codes of misc/vbyte.hpp:62-84, min_lpf_len 64 of cli/ssszip.cpp:37): built in HBM;
+ * *size = its byte length; out (host, cap >= *size) may be NULL to query the size. */
+int lz77sss_session_ssszip_gapped(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size);
 /* Copies SA_S / LCP_S (suffix order of the sync positions) of the last call. */
 int lz77sss_session_get_sa_s(lz77sss_session* s, uint32_t* sa, uint32_t* lcp, uint64_t cap);
 /* Copies the LPF phrase list (beg,end,src triples) of the last factorize call. */

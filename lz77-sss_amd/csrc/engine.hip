@@ -105,6 +105,7 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
     if (phr_mode < LZ77SSS_LPF_NAIVE || phr_mode > LZ77SSS_LPF_LNF_OPT) throw error(LZ77SSS_EINVAL, "unsupported phrase mode");
     if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
     num_fact = 0;
+    last_fact_mode = fact_mode;
     stats.assign(24, 0);
     if (n == 0) return 0;
     timer.begin(st);
@@ -370,6 +371,23 @@ LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint6
         LZ_HIP(hipGetLastError());
         LZ_HIP(hipMemsetAsync(E.d_text + n, 0, lz::TEXT_PAD, E.st));
         LZ_HIP(hipStreamSynchronize(E.st));
+    });
+}
+
+// ssszip's gapped container of the last skip_phrases factorization (csrc/ssszip.hip)
+LZ77SSS_API int lz77sss_session_ssszip_gapped(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        lz::engine& E = s->E;
+        if (E.last_fact_mode != LZ77SSS_SKIP_PHRASES)
+            throw lz::error(LZ77SSS_EINVAL, "ssszip_gapped needs a preceding factorize with fact_mode = skip_phrases");
+        LZ_HIP(hipSetDevice(E.device));
+        const uint64_t b = E.ssszip_gapped();
+        if (size) *size = b;
+        if (out) {
+            if (cap < b) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+            LZ_HIP(hipMemcpy(out, E.ssz_out.p, b, hipMemcpyDeviceToHost));
+        }
     });
 }
 
