@@ -188,6 +188,10 @@ def main():
     _, mism = sess.decode(out=False)
     dec_ms = sess.phase_times().get("decode", float("nan"))
     dec_rounds = sess.stats()[18]
+    # the Huffman factor container of the same factors (csrc/huffman.hip), host copy included
+    t_h0 = time.perf_counter()
+    hbytes = int(sess.huffman().size)
+    t_h = time.perf_counter() - t_h0
 
     if rank == 0:
         avg_ms = sum(kern_ms) / len(kern_ms)
@@ -220,6 +224,7 @@ def main():
                 "pcie_inclusive_mbps": round(n / (dt + t_load + t_out) / 1e6, 2),
                 "device_decode": {"mismatches": int(mism), "ms": round(dec_ms, 3), "jump_rounds": int(dec_rounds),
                                   "mbps": round(n / (dec_ms * 1e-3) / 1e6, 1)},
+                "huffman_container": {"bytes": hbytes, "ms_incl_d2h": round(t_h * 1e3, 3)},
             },
             "roofline": {
                 "kernel": "k_sss_stream",

@@ -161,6 +161,12 @@ int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint64_t base_len
  * codes of misc/vbyte.hpp:62-84, min_lpf_len 64 of cli/ssszip.cpp:37): built in HBM;
  * *size = its byte length; out (host, cap >= *size) may be NULL to query the size. */
 int lz77sss_session_ssszip_gapped(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size);
+/* The Huffman factor container of the last factorization (huff_writer,
+ * include/lz77_sss/misc/huffman.hpp:318-375, as written by
+ * cli/lz77_sss_3_aprx.cpp:71-85): 5 bytes n, then per block of 2^14 factors an
+ * Elias-delta count, two 66-symbol length-limited Huffman tables and the coded
+ * factors.  Built in HBM; out (host) may be NULL to query *size. */
+int lz77sss_session_huffman(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size);
 /* Copies SA_S / LCP_S (suffix order of the sync positions) of the last call. */
 int lz77sss_session_get_sa_s(lz77sss_session* s, uint32_t* sa, uint32_t* lcp, uint64_t cap);
 /* Copies the LPF phrase list (beg,end,src triples) of the last factorize call. */

@@ -374,6 +374,23 @@ LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint6
     });
 }
 
+// Huffman factor container of the last greedy / exact factorization (csrc/huffman.hip)
+LZ77SSS_API int lz77sss_session_huffman(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        lz::engine& E = s->E;
+        if (E.last_fact_mode == LZ77SSS_SKIP_PHRASES)
+            throw lz::error(LZ77SSS_EINVAL, "the Huffman container holds a factorization, not a skip_phrases stream");
+        LZ_HIP(hipSetDevice(E.device));
+        const uint64_t b = E.huffman_container();
+        if (size) *size = b;
+        if (out) {
+            if (cap < b) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+            LZ_HIP(hipMemcpy(out, E.hf_out.p, b, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
 // ssszip's gapped container of the last skip_phrases factorization (csrc/ssszip.hip)
 LZ77SSS_API int lz77sss_session_ssszip_gapped(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size) {
     if (!s) return LZ77SSS_EINVAL;

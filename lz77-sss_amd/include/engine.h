@@ -158,6 +158,7 @@ struct engine {
     u64 num_fact = 0;
     int last_fact_mode = -1;  // fact_mode of the last factorize call
     dbuf<u8> ssz_out;         // ssszip gapped container (csrc/ssszip.hip)
+    dbuf<u8> hf_tabs, hf_words, hf_out;  // Huffman factor container (csrc/huffman.hip)
     u64 ssz_size = 0;
     std::vector<u64> stats;
 
@@ -187,6 +188,7 @@ struct engine {
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode = 1);
     u64 emit_skip_phrases();  // fact_mode = skip_phrases (csrc/engine.hip)
     u64 ssszip_gapped();      // csrc/ssszip.hip
+    u64 huffman_container();  // csrc/huffman.hip
     void build_sa_full(const u8* T);
     u64 factorize_exact(bool log);  // csrc/exact.hip
     u64 decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cmp);

@@ -61,6 +61,7 @@ _SYMBOLS = {
                                                  ctypes.POINTER(ctypes.c_int)]),
     "lz77sss_session_get_sss64": (ctypes.c_int, [_P, _P, _U64]),
     "lz77sss_session_copy_sss64_device": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_huffman": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_ssszip_gapped": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_gen_genome": (ctypes.c_int, [_P, _U64, _U64, ctypes.c_double, ctypes.c_uint32, _U64]),
     "lz77sss_session_get_sa_s": (ctypes.c_int, [_P, _P, _P, _U64]),
@@ -203,6 +204,14 @@ class Session:
     def copy_sync_set64(self, dst_ptr: int, cap: int):
         """Device-to-device copy of the sss_range result to a device address (same device)."""
         _check(load_library().lz77sss_session_copy_sss64_device(self._h, _P(dst_ptr), cap))
+
+    def huffman(self) -> np.ndarray:
+        """Huffman factor container (bytes) of the last factorization (csrc/huffman.hip)."""
+        sz = _U64()
+        _check(load_library().lz77sss_session_huffman(self._h, None, 0, ctypes.byref(sz)))
+        out = np.empty(max(sz.value, 1), np.uint8)
+        _check(load_library().lz77sss_session_huffman(self._h, out.ctypes.data_as(_P), sz.value, ctypes.byref(sz)))
+        return out[:sz.value]
 
     def ssszip_gapped(self) -> np.ndarray:
         """ssszip's gapped container (bytes) of the last skip_phrases factorization (csrc/ssszip.hip)."""

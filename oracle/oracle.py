@@ -207,3 +207,28 @@ def gap_bases(rk_seed: int) -> list[int]:
 
 def num_threads() -> int:
     return int(lib().oracle_num_threads())
+
+
+def huffman(F, n: int) -> bytes:
+    """The Huffman factor container (misc/huffman.hpp huff_writer) of a factor stream (oracle_huffman.cpp)."""
+    f = np.ascontiguousarray(np.asarray(F, dtype=np.uint32).reshape(-1, 2))
+    L = lib()
+    L.oracle_huffman.restype = ctypes.c_int64
+    L.oracle_huffman.argtypes = [_P, _U64, _U64, _P, _U64]
+    size = L.oracle_huffman(f.ctypes.data_as(_P), f.shape[0], n, None, 0)
+    out = np.zeros(max(size, 1), np.uint8)
+    L.oracle_huffman(f.ctypes.data_as(_P), f.shape[0], n, out.ctypes.data_as(_P), size)
+    return out[:size].tobytes()
+
+
+def huffman_decode(buf, cap: int) -> np.ndarray:
+    """Factors back from a Huffman container (huff_factor_iterator restated)."""
+    b = np.frombuffer(bytes(buf), np.uint8)
+    out = np.zeros((max(cap, 1), 2), np.uint32)
+    L = lib()
+    L.oracle_huffman_decode.restype = ctypes.c_int64
+    L.oracle_huffman_decode.argtypes = [_P, _U64, _P, _U64]
+    z = L.oracle_huffman_decode(b.ctypes.data_as(_P), b.size, out.ctypes.data_as(_P), cap)
+    if z < 0:
+        raise RuntimeError("invalid Huffman container")
+    return out[:z].copy()
