@@ -122,7 +122,10 @@ __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __res
 // no atomics), packed into a bitmap with per-word popcounts; id = rank of the slot.
 __global__ void k_slot_presence(const u32* __restrict__ keys, u64 m, u8* __restrict__ pf) {
     const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < m) pf[keys[e]] = 1;
+    if (e < m) {
+        const u32 k = keys[e];
+        if (!pf[k]) pf[k] = 1;  // a hot slot's byte is read (cached) far more often than written
+    }
 }
 __global__ void k_presence_pack(const u8* __restrict__ pf, u64 nw, u32* __restrict__ pbm, u32* __restrict__ c) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -145,6 +148,16 @@ __global__ void k_dense_keys(const u32* __restrict__ keys, u64 m, const u32* __r
                              const u32* __restrict__ pwp, u32* __restrict__ dk) {
     const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (e < m) dk[e] = slot_rank(pbm, pwp, keys[e]);
+}
+// k_pred and k_dense_heads in one pass over the sorted dense ids
+__global__ void k_pred_heads(const u32* __restrict__ sdk, const u32* __restrict__ svals, u64 m, u32 D,
+                             u32* __restrict__ pred5, u32* __restrict__ dstart) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > m) return;
+    if (t == m) { dstart[D] = (u32)m; return; }
+    const bool head = t == 0 || sdk[t - 1] != sdk[t];
+    if (head) dstart[sdk[t]] = (u32)t;
+    if (pred5) pred5[svals[t]] = head ? NONE : svals[t - 1];
 }
 // first sorted index of every dense id (all ids occur), dstart[D] = m
 __global__ void k_dense_heads(const u32* __restrict__ sdk, u64 m, u32 D, u32* __restrict__ dstart) {
@@ -854,41 +867,39 @@ __global__ __launch_bounds__(BMB_T) void k_bmb_count(M mk, u64 nw, u64* __restri
     __syncthreads();
     if (threadIdx.x == 0) bsum[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
-// lane l of a block owns words [w0 + 8l, w0 + 8l + 8) in pass 2 (contiguous, in order)
+// pass 2, coalesced: in round r lane l owns word w0 + 256 r + l; the lanes' counts of
+// a round are scanned across the block (wave scan + 4 wave totals in LDS), so the
+// outputs stay in word order
 template <class M, class OUT>
 __global__ __launch_bounds__(BMB_T) void k_bmb_write(M mk, u64 nw, const u64* __restrict__ bincl, OUT out) {
-    __shared__ u64 part[BMB_T];
-    const u32 l = threadIdx.x;
-    const u64 wb = (u64)blockIdx.x * BMB + (u64)l * BMB_W;
-    u32 ca = 0, cb = 0;
-#pragma unroll
+    __shared__ u64 wsum[BMB_T / 64];
+    const u32 l = threadIdx.x, lane = l & 63, wv = l >> 6;
+    u64 base = blockIdx.x ? bincl[blockIdx.x - 1] : 0ull;
     for (u32 r = 0; r < BMB_W; r++) {
-        if (wb + r < nw) {
-            u32 a, b;
-            mk.masks(wb + r, a, b);
-            ca += __popc(a);
-            cb += __popc(b);
+        const u64 w = (u64)blockIdx.x * BMB + (u64)r * BMB_T + l;
+        u32 a = 0, b = 0;
+        if (w < nw) mk.masks(w, a, b);
+        const u64 mine = ((u64)__popc(a) << 32) | __popc(b);
+        u64 inc = mine;  // inclusive wave scan
+        for (u32 d = 1; d < 64; d <<= 1) {
+            const u64 v = __shfl_up(inc, d);
+            if (lane >= d) inc += v;
         }
-    }
-    const u64 mine = ((u64)ca << 32) | cb;
-    part[l] = mine;
-    __syncthreads();
-    for (u32 d = 1; d < BMB_T; d <<= 1) {
-        const u64 v = l >= d ? part[l - d] : 0ull;
+        if (lane == 63) wsum[wv] = inc;
         __syncthreads();
-        part[l] += v;
-        __syncthreads();
-    }
-    const u64 base = (blockIdx.x ? bincl[blockIdx.x - 1] : 0ull) + part[l] - mine;
-    u32 oa = (u32)(base >> 32), ob = (u32)base;
-#pragma unroll 1
-    for (u32 r = 0; r < BMB_W; r++) {
-        const u64 w = wb + r;
-        if (w >= nw) break;
-        u32 a, b;
-        mk.masks(w, a, b);
+        u64 pre = 0, tot = 0;
+#pragma unroll
+        for (u32 k = 0; k < BMB_T / 64; k++) {
+            const u64 x = wsum[k];
+            if (k < wv) pre += x;
+            tot += x;
+        }
+        const u64 o = base + pre + inc - mine;
+        u32 oa = (u32)(o >> 32), ob = (u32)o;
         while (a) { out.a(oa++, (u32)(32 * w + __builtin_ctz(a)), w); a &= a - 1; }
         while (b) { out.b(ob++, (u32)(32 * w + __builtin_ctz(b))); b &= b - 1; }
+        base += tot;
+        __syncthreads();  // wsum reused by the next round
     }
 }
 struct out_runs {
@@ -1369,7 +1380,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
             u8* t = scan_tmp.get(tb);
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
-            if (W.use_pred && ne5 < (1ull << 27)) {
+            if (dense && ne5 < (1ull << 27)) {
+                // predecessors and dense-id starts in one pass (buckets below reuse dstart)
+                k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, svals, ne5, D, W.use_pred ? pred5 : nullptr,
+                                                                  g_dstart.get((u64)D + 1));
+            } else if (W.use_pred && ne5 < (1ull << 27)) {
                 k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
             } else if (W.use_pred) {
                 // pred5[e] = predecessor of entry e in its slot: a radix sort by entry id of the
@@ -1388,7 +1403,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         lap("base sort + pred");
         if (dense) {
             u32* dstart = g_dstart.get((u64)D + 1);
-            k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
+            if (ne5 >= (1ull << 27)) k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
             k_bstart_rank<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
                                                                       g_bstart.get((u64)nslots + 1));
         } else {
