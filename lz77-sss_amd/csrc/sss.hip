@@ -409,11 +409,29 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     // windows and past the last full window).  q holds the Q intervals of the block's 5 anchors (s_k/128 + 0..4), loaded
     // by the whole wave as one scalar load: the per-lane test runs only when one
     // of them is non-empty
-    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
+    // block k lies entirely in Q (every window T[j..j+512) is periodic): its Phi' is
+    // INF at all 512 positions.  Uniform test on the anchors' intervals: anchor 0
+    // must cover rel 127 (offset 0), anchors 1-3 all of rel 0..127, anchor 4 rel 0..126
+    auto fullq = [&](uint4 q) -> bool {
+        const u32 a0 = q.x & 0xFFFFu, a4 = q.z & 0xFFFFu;
+        const bool m0 = (a0 >> 8) <= 127u && (a0 & 255u) >= 127u;
+        const bool m1 = (q.x >> 24) == 0u && ((q.x >> 16) & 255u) >= 127u;
+        const bool m2 = (q.y >> 8 & 255u) == 0u && (q.y & 255u) >= 127u;
+        const bool m3 = (q.y >> 24) == 0u && ((q.y >> 16) & 255u) >= 127u;
+        const bool m4 = (a4 >> 8) == 0u && (a4 & 255u) >= 126u;
+        return m0 && m1 && m2 && m3 && m4;
+    };
+    // returns true when the block is all INF (uniform)
+    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) -> bool {
+        const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
+        if (__builtin_amdgcn_readfirstlane((int)anyq) && fullq(q)) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = INF32;
+            return true;
+        }
 #pragma unroll
         for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
         const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
-        const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
         if (__builtin_amdgcn_readfirstlane((int)(anyq || endblk))) {
             // anchor r (0..4) of the block covers offsets (128r - 128, 128r]; its Q interval
             // [lo, hi] (rel = offset + 127 - 128r) is an offset interval, uniform per block:
@@ -437,6 +455,7 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
 #pragma unroll
             for (int e = 0; e < 8; e++) v[e] |= 0u - ((bits >> e) & 1u);
         }
+        return false;
     };
     // Q intervals of the anchors of block k (uniform address: a scalar load)
     auto loadq = [&](u64 k) -> uint4 { return *(const uint4*)(qinfo + ((i0 + k * TAU) >> 7)); };
@@ -449,17 +468,19 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     u32 hA[8], hB[8], xA[8], xB[8];
     block_prefix(load8(0), carry, hA);
     block_prefix(load8(1), carry, hB);
-    phi_block(0, hA, hB, qa, xA);
+    bool fA = phi_block(0, hA, hB, qa, xA), fB = false;
     u32 nout = 0;       // outputs of this stripe so far (uniform)
     u32* out = s_out + w * SCAP;
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
     // one decision block: x = Phi'(block c) (in), y = Phi'(block c+1) (out),
     // h0 = Hp(block c+1) (in), h1 <- Hp(block c+2); B = bytes of block c+2
-    auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn) {
+    auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn, bool fx, bool& fy) {
         const uint4 qc = loadq(c + 2);
         block_prefix(B, carry, h1);
-        phi_block(c + 1, h0, h1, qn, y);
+        fy = phi_block(c + 1, h0, h1, qn, y);
         qn = qc;
+        // both blocks all INF: every window minimum is INF, no decision of block c is in S
+        if (fx && fy) return;
         // window minima for decisions of block c
         u32 sx[8], py[8];
         sx[7] = x[7];
@@ -502,11 +523,11 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     };
     for (u32 c = 0; c < nblk; c += 2) {
         u64 Bn = load8(c + 4);  // prefetch (the text pad covers the stripe's end)
-        step(c, xA, xB, hB, hA, Ba, qb);
+        step(c, xA, xB, hB, hA, Ba, qb, fA, fB);
         Ba = Bn;
         if (c + 1 >= nblk) break;
         Bn = load8(c + 5);
-        step(c + 1, xB, xA, hA, hB, Bb, qb);
+        step(c + 1, xB, xA, hA, hB, Bb, qb, fB, fA);
         Bb = Bn;
     }
     if (lane == 0) {
