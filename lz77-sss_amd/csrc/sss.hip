@@ -360,6 +360,10 @@ __device__ __forceinline__ u32 wave_suffix_min(u32 v, u32 lane) {  // inclusive,
     return min(v, lane < 16 ? a0 : lane < 32 ? a1 : lane < 48 ? r3 : INF32);
 }
 
+// QSKIP: the text has Q windows (k_q_anchors found one): blocks entirely inside Q
+// skip their hashing and minima (without Q the plain instantiation runs, whose code
+// is not burdened by the per-block test)
+template <bool QSKIP>
 __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict__ T, u64 n, u64 last_i,
                                                            const u16* __restrict__ qinfo, u64 nstripes,
                                                            u32* __restrict__ s_out, u32* __restrict__ s_cnt,
@@ -421,14 +425,14 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
         const bool m4 = (a4 >> 8) == 0u && (a4 & 255u) >= 126u;
         return m0 && m1 && m2 && m3 && m4;
     };
-    // returns true when the block is all INF (uniform)
-    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) -> bool {
+    // all-Q test of a block (uniform; one per block, carried from step to step)
+    auto allq = [&](uint4 q) -> bool {
+        if constexpr (!QSKIP) return false;
         const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
-        if (__builtin_amdgcn_readfirstlane((int)anyq) && fullq(q)) {
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = INF32;
-            return true;
-        }
+        return __builtin_amdgcn_readfirstlane((int)anyq) && fullq(q);
+    };
+    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
+        const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
 #pragma unroll
         for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
         const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
@@ -455,7 +459,14 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
 #pragma unroll
             for (int e = 0; e < 8; e++) v[e] |= 0u - ((bits >> e) & 1u);
         }
-        return false;
+    };
+    auto phi_or_inf = [&](bool full, u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
+        if (full) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = INF32;
+        } else {
+            phi_block(k, h0, h1, q, v);
+        }
     };
     // Q intervals of the anchors of block k (uniform address: a scalar load)
     auto loadq = [&](u64 k) -> uint4 { return *(const uint4*)(qinfo + ((i0 + k * TAU) >> 7)); };
@@ -468,16 +479,29 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     u32 hA[8], hB[8], xA[8], xB[8];
     block_prefix(load8(0), carry, hA);
     block_prefix(load8(1), carry, hB);
-    bool fA = phi_block(0, hA, hB, qa, xA), fB = false;
+    bool fA = allq(qa), fB = false;
+    bool fq = allq(qb);  // all-Q flag of the block whose Phi' the next step computes
+    bool hvalid = true;  // the prefix hash carry continues the last computed block
+    phi_or_inf(fA, 0, hA, hB, qa, xA);
     u32 nout = 0;       // outputs of this stripe so far (uniform)
     u32* out = s_out + w * SCAP;
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
     // one decision block: x = Phi'(block c) (in), y = Phi'(block c+1) (out),
     // h0 = Hp(block c+1) (in), h1 <- Hp(block c+2); B = bytes of block c+2
+    // Phi(j) = Hp(j+512) - b^512 Hp(j) does not depend on where the prefix hash starts
+    // (the start's contribution cancels): the prefix hash of block k is needed only when
+    // block k-1 or k is not all Q, and restarts from 0 after skipped blocks
     auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn, bool fx, bool& fy) {
         const uint4 qc = loadq(c + 2);
-        block_prefix(B, carry, h1);
-        fy = phi_block(c + 1, h0, h1, qn, y);
+        const bool f1 = fq, f2 = allq(qc);
+        if (!(f1 && f2)) {
+            if (!hvalid) carry = 0;
+            block_prefix(B, carry, h1);
+        }
+        hvalid = !(f1 && f2);
+        phi_or_inf(f1, c + 1, h0, h1, qn, y);
+        fy = f1;
+        fq = f2;
         qn = qc;
         // both blocks all INF: every window minimum is INF, no decision of block c is in S
         if (fx && fy) return;
@@ -629,6 +653,7 @@ void engine::build_sss(const u8* T) {
         runs_valid = true;
     }
 
+    const bool any_q = rd1(ctr, st) != 0;  // picks the stream kernel's instantiation
     const u64 nlanes = last_i / SD + 1;  // stripes
     u32* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
@@ -643,8 +668,12 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipEventCreate(&e0));
     LZ_HIP(hipEventCreate(&e1));
     LZ_HIP(hipEventRecord(e0, st));
-    k_sss_stream<<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
-                                                               (u32)SSS_BASE, PW);
+    if (any_q)
+        k_sss_stream<true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
+                                                                       (u32)SSS_BASE, PW);
+    else
+        k_sss_stream<false><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
+                                                                        (u32)SSS_BASE, PW);
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipEventRecord(e1, st));
 
