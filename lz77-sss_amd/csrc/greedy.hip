@@ -1231,7 +1231,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     const unsigned bmb_blocks = (unsigned)std::max<u64>(1, (nw + BMB - 1) / BMB);
 
     // ---- default segments: gaps + chunk boundaries of long gaps
-    const u32 CH = std::getenv("LZ77SSS_NO_CHUNK") ? 0x0FFFFFFFu : 512u;
+    const char* ch_env = std::getenv("LZ77SSS_GAP_CHUNK");  // tuning knob (walk length per segment)
+    const u32 CH = std::getenv("LZ77SSS_NO_CHUNK") ? 0x0FFFFFFFu : ch_env ? (u32)std::max(16, std::atoi(ch_env)) : 512u;
     u32* cnt_seg = g_tmp1.get(m + 2);
     u32* cnt_cb = g_tmp2.get(m + 2);
     u32* off_seg = g_tmp3.get(m + 2);

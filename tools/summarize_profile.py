@@ -42,7 +42,7 @@ def counter(path, name):
 
 fetch, nf = counter(src / f"pmc_{tag}_{wl}_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
 write, nw = counter(src / f"pmc_{tag}_{wl}_write" / "run_counter_collection.csv", "WRITE_SIZE")
-sss_avg_ns = [float(r["AverageNs"]) for r in rows if r["Name"].startswith("lz::k_sss_stream")][0]
+sss_avg_ns = [float(r["AverageNs"]) for r in rows if "k_sss_stream" in r["Name"]][0]
 hbm = 2 * fetch * 1024 + write * 1024
 out = {"kernel": "k_sss_stream", "workload": wl, "n": n, "launches": {"fetch": nf, "write": nw},
        "fetch_size_kib": fetch, "write_size_kib": write, "fetch_correction": 2.0,
