@@ -151,7 +151,40 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
     // agrees over its whole chunk is verified from its two successors' chunks
     // when they test the same shift (inside a run: every anchor), so each byte
     // of a run is compared about once instead of 340/128 times
-    const int c = p1 ? ext_fwd(oa, oa + (int)QA, (int)p1) - oa : 0;
+    // agreement of shift p1 over the anchor's own 128 bytes, 16 bytes per step (oa is
+    // word aligned): inside a run every anchor runs the whole chunk, so the LDS loads
+    // of a step are issued together and the exit test is taken once per 4 words
+    auto chunk_agree = [&](int p) -> int {
+        const int w0 = oa >> 2;
+        const int q0 = (oa + p) >> 2;
+        const u32 sh = (u32)(p & 3);
+        u32 lo = word(q0);
+#pragma unroll 1
+        for (int k = 0; k < (int)QA / 4; k += 4) {
+            u32 a[4], b[5];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                a[j] = word(w0 + k + j);
+                b[j + 1] = word(q0 + k + j + 1);
+            }
+            b[0] = lo;
+            u32 d[4];
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                d[j] = a[j] ^ __builtin_amdgcn_alignbyte(b[j + 1], b[j], sh);
+                any |= d[j] != 0;
+            }
+            if (any) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (d[j]) return 4 * (k + j) + (__builtin_ctz(d[j]) >> 3);
+            }
+            lo = b[4];
+        }
+        return (int)QA;
+    };
+    const int c = p1 ? chunk_agree((int)p1) : 0;
     s_p1[i] = (u8)p1;
     s_c[i] = (u8)c;
     __syncthreads();
