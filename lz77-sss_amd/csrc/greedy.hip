@@ -149,6 +149,41 @@ __global__ void k_dense_keys(const u32* __restrict__ keys, u64 m, const u32* __r
     const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (e < m) dk[e] = slot_rank(pbm, pwp, keys[e]);
 }
+// pred5[e] = pv[t] for the permutation e = svals[t] without a radix sort by e: bucket
+// b holds the 2^PB_SH consecutive ids [b << PB_SH, (b+1) << PB_SH), so its size is known;
+// pass 1 moves (e, pv) pairs into their buckets (per tile: an LDS histogram, one global
+// atomic per non-empty bucket, LDS cursors), pass 2 scatters each bucket's pairs inside
+// its own 1 MiB window of pred5 (L2-local writes)
+constexpr u32 PB_SH = 18;
+constexpr int PB_T = 1024;
+__global__ void k_pb_init(u32* __restrict__ cursor, u32 nb) {
+    const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < nb) cursor[b] = b << PB_SH;
+}
+__global__ __launch_bounds__(PB_T) void k_pb_move(const u32* __restrict__ svals, const u32* __restrict__ pv, u64 m,
+                                                  u64 tile, u32 nb, u32* __restrict__ cursor, u64* __restrict__ tmp) {
+    __shared__ u32 h[1u << 14];  // nb <= 2^32 >> PB_SH
+    const int tid = (int)threadIdx.x;
+    for (u32 b = tid; b < nb; b += PB_T) h[b] = 0;
+    __syncthreads();
+    const u64 t0 = (u64)blockIdx.x * tile, t1 = min(m, t0 + tile);
+    for (u64 t = t0 + tid; t < t1; t += PB_T) atomicAdd(&h[svals[t] >> PB_SH], 1u);
+    __syncthreads();
+    for (u32 b = tid; b < nb; b += PB_T)
+        if (h[b]) h[b] = atomicAdd(&cursor[b], h[b]);
+    __syncthreads();
+    for (u64 t = t0 + tid; t < t1; t += PB_T) {
+        const u32 e = svals[t];
+        const u32 p = atomicAdd(&h[e >> PB_SH], 1u);
+        tmp[p] = ((u64)e << 32) | pv[t];
+    }
+}
+__global__ void k_pb_apply(const u64* __restrict__ tmp, u64 m, u32* __restrict__ pred5) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const u64 x = tmp[i];
+    pred5[x >> 32] = (u32)x;
+}
 // k_pred and k_dense_heads in one pass over the sorted dense ids
 __global__ void k_pred_heads(const u32* __restrict__ sdk, const u32* __restrict__ svals, u64 m, u32 D,
                              u32* __restrict__ pred5, u32* __restrict__ dstart) {
@@ -1327,6 +1362,10 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         if (nch) k_iv_chunks<<<cdiv(nch, 256), 256, 0, st>>>(a, b, ni, choff, nch, chl, rk, ch);
         return ch;
     };
+    // base sets this large get their predecessors in sorted order and moved back to
+    // entry order in buckets (random 4-byte scatters over the whole array are slower)
+    const char* psm = std::getenv("LZ77SSS_PRED_SORTED_MIN");
+    const u64 pred_sorted_min = psm ? std::strtoull(psm, nullptr, 10) : (1ull << 27);
     auto build_base = [&](const u32* bm) {
         if (bm != bmIb) LZ_HIP(hipMemcpyAsync(bmIb, bm, nw * 4, hipMemcpyDeviceToDevice, st));
         u32 ni, nch;
@@ -1381,30 +1420,41 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
             u8* t = scan_tmp.get(tb);
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
-            if (dense && ne5 < (1ull << 27)) {
+            if (dense && ne5 < pred_sorted_min) {
                 // predecessors and dense-id starts in one pass (buckets below reuse dstart)
                 k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, svals, ne5, D, W.use_pred ? pred5 : nullptr,
                                                                   g_dstart.get((u64)D + 1));
-            } else if (W.use_pred && ne5 < (1ull << 27)) {
+            } else if (W.use_pred && ne5 < pred_sorted_min) {
                 k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
             } else if (W.use_pred) {
                 // pred5[e] = predecessor of entry e in its slot: a radix sort by entry id of the
                 // sorted-order predecessors (a random scatter of 4-byte writes is ~3x slower)
                 u32* pv = vals;  // the unsorted values are no longer needed
-                u32* kdump = g_predk.get(ne5 + 1);
                 k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
-                int eb = 1;
-                while (eb < 32 && (1ull << eb) < ne5) eb++;
-                size_t tb2 = 0;
-                LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
-                u8* t2 = scan_tmp.get(tb2);
-                LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
+                if (std::getenv("LZ77SSS_PRED_RADIX")) {  // reference path: radix sort by entry id
+                    u32* kdump = g_predk.get(ne5 + 1);
+                    int eb = 1;
+                    while (eb < 32 && (1ull << eb) < ne5) eb++;
+                    size_t tb2 = 0;
+                    LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
+                    u8* t2 = scan_tmp.get(tb2);
+                    LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
+                } else {
+                    const u32 nbk = (u32)((ne5 + (1ull << PB_SH) - 1) >> PB_SH);
+                    u32* cursor = g_pbcur.get(nbk + 1);
+                    u64* tmp = g_pbtmp.get(ne5);
+                    const u32 ntile = (u32)std::min<u64>(1024, cdiv(ne5, PB_T));
+                    const u64 tile = (ne5 + ntile - 1) / ntile;
+                    k_pb_init<<<cdiv(nbk, 256), 256, 0, st>>>(cursor, nbk);
+                    k_pb_move<<<ntile, PB_T, 0, st>>>(svals, pv, ne5, tile, nbk, cursor, tmp);
+                    k_pb_apply<<<cdiv(ne5, 256), 256, 0, st>>>(tmp, ne5, pred5);
+                }
             }
         }
         lap("base sort + pred");
         if (dense) {
             u32* dstart = g_dstart.get((u64)D + 1);
-            if (ne5 >= (1ull << 27)) k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
+            if (ne5 >= pred_sorted_min) k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
             k_bstart_rank<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
                                                                       g_bstart.get((u64)nslots + 1));
         } else {

@@ -142,7 +142,8 @@ struct engine {
     dbuf<u64> l_tmp64;
     dbuf<u32> g_predk, g_wk, g_ids2;
     dbuf<u32> g_brev;
-    dbuf<u64> g_bsum, g_bincl;
+    dbuf<u64> g_bsum, g_bincl, g_pbtmp;
+    dbuf<u32> g_pbcur;  // predecessor bucket scatter
     dbuf<u32> g_pbm, g_pwp, g_pcnt, g_sdk, g_dstart, g_pflag;  // dense slot ids of the base set  // per-block bitmap counts and their inclusive scan
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
     dbuf<u64> g_xk, g_xk2;

@@ -285,3 +285,18 @@ def test_dense_slot_ids_match_slot_sort(session, lz, kind, mib, monkeypatch):
     monkeypatch.setenv("LZ77SSS_NO_DENSE", "1")
     _, F0 = run(session, T)
     assert F1.shape == F0.shape and np.array_equal(F1, F0)
+
+
+@pytest.mark.parametrize("kind,mib", [("genome", 16), ("rr", 32)])
+def test_sorted_predecessor_paths_vs_oracle(session, orc, lz, kind, mib, monkeypatch):
+    """Base sets above LZ77SSS_PRED_SORTED_MIN move their predecessors back by bucket scatter
+    (default) or by a radix sort (LZ77SSS_PRED_RADIX): both equal the oracle stream."""
+    n = mib << 20
+    T = lz.gen_genome(n, 2 << 20, 0.001, 11) if kind == "genome" else lz.gen_random_repetitive(n, n, 5, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    monkeypatch.setenv("LZ77SSS_PRED_SORTED_MIN", "1")
+    _, F1 = run(session, T)
+    assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    monkeypatch.setenv("LZ77SSS_PRED_RADIX", "1")
+    _, F2 = run(session, T)
+    assert np.array_equal(F2, F_ref)
