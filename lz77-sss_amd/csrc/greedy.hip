@@ -30,6 +30,8 @@
 #include "../include/lce_dev.h"
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 #include <array>
@@ -1389,7 +1391,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u32* pbm = g_pbm.get(npw + 1);
         u32* pwp = g_pwp.get(npw + 1);
         if (nch) {
-            k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, vals, ipos);
+            k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos);
             lap("base slots");
             // distinct slots -> dense ids when that saves radix passes
             // (tried below 2^28 entries: a base set that large comes from a non-repetitive
@@ -1417,9 +1419,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy base: %u distinct slots, %s sort on %u bits\n", D,
                                   dense ? "dense-id" : "slot", sbits);
             size_t tb = 0;
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
+            // values = entry ids: a counting iterator, so the ids are never written or read
+            const rocprim::counting_iterator<u32> ids(0);
+            LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
             u8* t = scan_tmp.get(tb);
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, sk_in, skeys, vals, svals, (int)ne5, 0, (int)sbits, st));
+            LZ_HIP(rocprim::radix_sort_pairs(t, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
             if (dense && ne5 < pred_sorted_min) {
                 // predecessors and dense-id starts in one pass (buckets below reuse dstart)
                 k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, svals, ne5, D, W.use_pred ? pred5 : nullptr,
