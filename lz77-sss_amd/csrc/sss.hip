@@ -297,7 +297,9 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
     }
     __syncthreads();
     // one atomic per block: same-address atomics from every anchor serialize
-    if (i == 0 && s_anyq) atomicOr(any_q, 1u);
+    // (and none once the flag is visible: on run-heavy text every block has a Q window)
+    if (i == 0 && s_anyq && __hip_atomic_load(any_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicOr(any_q, 1u);
 }
 
 // run chains: anchor t continues into t+1 (same run) when both have period p
