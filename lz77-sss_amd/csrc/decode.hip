@@ -10,16 +10,15 @@
 // factors, not positions.
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
-
-#include <hipcub/hipcub.hpp>
+#include "../include/prim.h"
 
 namespace lz {
 
-__global__ void k_dec_lens(const u32* __restrict__ F, u64 nf, u32* __restrict__ len) {
+__global__ void k_dec_lens(const u32* __restrict__ F, u64 nf, u64* __restrict__ len) {
     const u64 f = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (f < nf) len[f] = F[2 * f + 1] ? F[2 * f + 1] : 1u;
 }
-__global__ void k_dec_heads(const u32* __restrict__ start, u64 nf, u64 n, u32* __restrict__ head) {
+__global__ void k_dec_heads(const u64* __restrict__ start, u64 nf, u64 n, u32* __restrict__ head) {
     const u64 f = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (f < nf && start[f] < n) head[start[f]] = (u32)f;
 }
@@ -27,14 +26,14 @@ struct max_u32 {
     __device__ __forceinline__ u32 operator()(const u32& a, const u32& b) const { return a > b ? a : b; }
 };
 // ref[p]: p for literals, the source position for copies; err on a forward reference
-__global__ void k_dec_refs(const u32* __restrict__ F, const u32* __restrict__ start, const u32* __restrict__ fid, u64 n,
+__global__ void k_dec_refs(const u32* __restrict__ F, const u64* __restrict__ start, const u32* __restrict__ fid, u64 n,
                            u32* __restrict__ ref, u32* __restrict__ err) {
     const u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const u32 f = fid[p];
     const u32 len = F[2 * (u64)f + 1];
     if (len == 0) { ref[p] = (u32)p; return; }
-    const u32 src = F[2 * (u64)f], st = start[f];
+    const u32 src = F[2 * (u64)f], st = (u32)start[f];
     if (src >= st) { atomicOr(err, 1u); ref[p] = (u32)p; return; }  // only on an invalid stream
     // a self-overlapping copy (distance d < len) is d-periodic: fold the offset
     // into the first period so the reference lands before the factor start
@@ -97,27 +96,18 @@ u64 engine::decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cm
     }
     if (nf == 0 || nf > n_out) throw error(LZ77SSS_EINVAL, "factor count does not fit the text length");
     if (n_out > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
-    u32* len = dec_len.get(nf + 1);
-    u32* start = dec_start.get(nf + 1);
+    // starts in 64 bits: lengths of an invalid stream may sum past 2^32 (the sum check must see it)
+    u64* len = dec_len64.get(nf + 1);
+    u64* start = dec_start64.get(nf + 1);
     k_dec_lens<<<cdiv(nf, 256), 256, 0, st>>>(F, nf, len);
-    LZ_HIP(hipMemsetAsync(len + nf, 0, 4, st));
-    {
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len, start, (int)(nf + 1), st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, len, start, (int)(nf + 1), st));
-    }
+    LZ_HIP(hipMemsetAsync(len + nf, 0, 8, st));
+    excl_sum64(len, start, (u64)0, nf + 1, scan_tmp, st);
     if (rd1(start + nf, st) != n_out) throw error(LZ77SSS_EINVAL, "factor lengths do not sum to n");
     u32* head = dec_fid.get(n_out);
     u32* fid = dec_ref2.get(n_out);
     LZ_HIP(hipMemsetAsync(head, 0, n_out * 4, st));
     k_dec_heads<<<cdiv(nf, 256), 256, 0, st>>>(start, nf, n_out, head);
-    {
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, head, fid, max_u32{}, (int)n_out, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, head, fid, max_u32{}, (int)n_out, st));
-    }
+    incl_scan64(head, fid, n_out, max_u32{}, scan_tmp, st);
     u32* ref = dec_ref.get(n_out);
     u32* ref2 = head;  // free after the scan
     u32* flags = counters.get(16);

@@ -675,6 +675,141 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
     count_out[1] = nins;
 }
 
+// ---------------------------------------------------------------------------
+// Bounded-cost completion: the reference loop itself (greedy.cpp:46-134 with
+// longest_prev_occ, factorize/common.cpp:33-61) on one thread, against a
+// materialized single-slot table H and the literal rolling_hash_index_107
+// semantics (reinit / roll / advance / advance_and_get_occ, including stale and
+// zeroed fingerprints at the text end, rolling_hash_index_107.hpp:80-150).  It
+// starts from an exact chain state (a segment start whose predecessors were all
+// exact) with H holding the last insert per slot below that state, so its output
+// continues the confirmed prefix.  Used when the speculation does not reach its
+// fixed point within the round budget, or a walk reports an internal overflow.
+__global__ void k_h_fill(const u8* __restrict__ T, gap_cfg G, const u32* __restrict__ bm, u32 y, u32* __restrict__ H) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w * 32 >= y) return;
+    u32 bits = bm[w];
+    while (bits) {
+        const u32 q = (u32)(32 * w) + (u32)__builtin_ctz(bits);
+        bits &= bits - 1;
+        if (q >= y) break;
+        // confirmed inserts lie below the tail region: all 5 fingerprints are full windows
+        for (int x = 0; x < 5; x++)
+            atomicMax(&H[(u32)((u64)kr_direct(T, q, G.lens[x], G.base[x]) & G.mask)], q + 1);
+    }
+}
+__global__ void k_h_fix(u32* __restrict__ H, u64 m) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) H[k] = H[k] ? H[k] - 1 : NONE;
+}
+__global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __restrict__ P, lce_view L,
+                           u32* __restrict__ H, seg_in in, u32* __restrict__ fact, u64 off, u64* __restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const u32 n = G.n;
+    u128 fp[5];
+    u32 cur = in.idxpos;
+    for (int x = 0; x < 5; x++) {  // fingerprint state at cur
+        const u32 len = G.lens[x];
+        if (((in.zmask >> x) & 1) || len > n) fp[x] = 0;
+        else fp[x] = kr_direct(T, (u64)cur + len <= n ? cur : n - len, len, G.base[x]);
+    }
+    auto slot_of = [&](int x) -> u32 { return (u32)((u64)fp[x] & G.mask); };
+    auto roll1 = [&](int x) {
+        if ((u64)cur + G.lens[x] < n) fp[x] = kr_roll(fp[x], G.base[x], G.negpow[x * 256 + T[cur]], T[cur + G.lens[x]]);
+    };
+    auto roll = [&]() {
+        for (int x = 0; x < 5; x++) roll1(x);
+        cur++;
+    };
+    auto reinit = [&](u32 pos) {
+        cur = pos;
+        for (int x = 0; x < 5; x++) fp[x] = ((u64)pos + G.lens[x] < n) ? kr_direct(T, pos, G.lens[x], G.base[x]) : 0;
+    };
+    auto advance = [&]() {
+        for (int x = 0; x < 5; x++)
+            if ((u64)cur + G.lens[x] < n) {
+                H[slot_of(x)] = cur;
+                roll1(x);
+            }
+        cur++;
+    };
+    auto longest_prev_occ = [&](u32 pos, u32& fsrc, u32& flen) {
+        fsrc = T[pos];
+        flen = 0;
+        for (int x = 4; x >= 0; x--) {
+            if (flen == 0) {  // advance_and_get_occ<x>: always inserts
+                const u32 sl = slot_of(x), occ = H[sl];
+                H[sl] = cur;
+                roll1(x);
+                if (occ < pos && T[occ] == T[pos]) {
+                    flen = (u32)dev_lce(L, occ, pos);
+                    fsrc = occ;
+                }
+            } else if ((u64)cur + G.lens[x] < n) {  // advance<x>
+                H[slot_of(x)] = cur;
+                roll1(x);
+            }
+        }
+        cur++;
+    };
+    u64 nf = 0, guard = 0;
+    auto emit = [&](u32 src, u32 len) {
+        fact[2 * (off + nf)] = src;
+        fact[2 * (off + nf) + 1] = len;
+        nf++;
+    };
+    u32 i = in.start, p = in.p;
+    out[1] = 0;
+    for (;;) {
+        if (++guard > 4ull * n + 1024 || i > n) { out[1] = 1; break; }
+        u32 gap_end = P[3 * p];
+        if (i < gap_end) {
+            if (cur < i) {
+                if (i - cur <= G.thr) {
+                    do roll(); while (cur < i);
+                } else {
+                    reinit(i);
+                }
+            }
+            do {
+                u32 fsrc, flen;
+                longest_prev_occ(i, fsrc, flen);
+                i += flen ? flen : 1;
+                if (i > gap_end) {
+                    if (i <= P[3 * p + 1]) {
+                        flen -= i - gap_end;
+                        i = gap_end;
+                    } else {
+                        do { p++; } while (P[3 * p + 1] <= i);
+                        while (cur < gap_end) advance();
+                        gap_end = P[3 * p];
+                    }
+                }
+                emit(fsrc, flen);
+                while (cur < i) advance();
+            } while (i < gap_end);
+        }
+        if (i == n) break;
+        const u32 exc = i - gap_end;
+        u32 lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
+        if (cur == i) {
+            u32 fsrc, flen;
+            longest_prev_occ(i, fsrc, flen);
+            if (flen > llen) { lsrc = fsrc; llen = flen; }
+        }
+        emit(lsrc, llen);
+        i += llen;
+        while (P[3 * p + 1] <= i) p++;
+    }
+    out[0] = nf;
+}
+// first set bit of a bitmap (NONE if none), one atomic per workgroup
+__global__ void k_first_bit(const u32* __restrict__ bm, u64 nw, u32* __restrict__ out) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 v = (w < nw && bm[w]) ? (u32)(32 * w) + (u32)__builtin_ctz(bm[w]) : NONE;
+    block_min(out, v);
+}
+
 // phrase statistics (approximate/common.cpp:98-157, p = 1)
 __global__ void k_phrase_info(const u32* __restrict__ P, u32 m, u32 n, u32* __restrict__ acc) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1155,6 +1290,37 @@ __global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cn
     bm_set_range_wave(bm, a, b, lane);
     if (lane < o.nsingle && lane < 4 && o.single[lane] < nt) atomicOr(&bm[o.single[lane] >> 5], 1u << (o.single[lane] & 31));
 }
+// completion start: the last chain node whose start is <= y0 (the first position where
+// the speculated insert set and the chain's differ): every lookup of its predecessors
+// happened below y0, so its start state is exact (index state from its predecessor)
+struct chain_cut { u32 k, pad; seg_in in; };
+__global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, const u32* __restrict__ y0p,
+                            chain_cut* __restrict__ out) {
+    const u32 y0 = *y0p;
+    chain_cut c{};
+    if (nall == 0 || y0 == 0) {
+        c.k = 0;
+        c.in = make_seg_in(S, 0);
+        *out = c;
+        return;
+    }
+    u32 lo = 0, hi = nall;  // first k with start > y0
+    while (lo < hi) {
+        const u32 mid = (lo + hi) >> 1;
+        if (S.sin[chain[mid]].start <= y0) lo = mid + 1; else hi = mid;
+    }
+    c.k = lo - 1;  // chain[0] starts at 0 <= y0
+    c.in = S.sin[chain[c.k]];
+    if (c.k > 0) {
+        const seg_out& pv = S.sout[chain[c.k - 1]];
+        c.in.idxpos = pv.idxpos;
+        c.in.zmask = pv.zmask;
+    } else {
+        c.in.idxpos = 0;
+        c.in.zmask = S.zmask0;
+    }
+    *out = c;
+}
 __global__ void k_set_pairs(const u32* __restrict__ pairs, u32 np, u32* __restrict__ bm) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < np) bm_set_range(bm, pairs[2 * k], pairs[2 * k + 1]);
@@ -1314,12 +1480,50 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     LZ_HIP(hipStreamSynchronize(st));
     lap("greedy setup");
 
-    // ---- base set (entries sorted by slot) and delta
+    // ---- bounded completion (k_seq_walk): the chain prefix [0, k*) is written by
+    // the segment walks, the rest by the exact sequential walk from chain node k*
+    const char* mo_env = std::getenv("LZ77SSS_GREEDY_MAX_OUTER");  // test knob (0: sequential only)
+    const int max_outer = mo_env ? std::max(0, std::atoi(mo_env)) : 256;
+    const u64 nslots_all = (u64)G.mask + 1;
     walk_ctx W{};
     W.T = T;
     W.G = G;
     W.P = P;
     W.L = view(T);
+    const lce_view& Lv = W.L;
+    u64* d_sq = (u64*)g_cut.get(sizeof(chain_cut) + 64);
+    chain_cut* d_cutp = (chain_cut*)(d_sq + 4);
+    u32* d_y0 = (u32*)(d_sq + 2);
+    auto seq_complete = [&](const u32* chain, u32 nall, const u64* offs, const u32* ins_bm, bool from_zero) -> u64 {
+        if (from_zero) LZ_HIP(hipMemsetAsync(d_y0, 0, 4, st));
+        k_chain_cut<<<1, 1, 0, st>>>(S, chain, from_zero ? 0u : nall, d_y0, d_cutp);
+        chain_cut cut;
+        LZ_HIP(hipMemcpyAsync(&cut, d_cutp, sizeof(cut), hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        const u64 offk = cut.k ? rd1(offs + cut.k, st) : 0;
+        u32* fo = fact.get(2 * (offk + (u64)(N - cut.in.start) + 2) + 2);
+        if (cut.k) {
+            k_walk<true><<<cdiv(cut.k, 64), 64, 0, st>>>(W, S, chain, cut.k, offs, fo);
+            LZ_HIP(hipGetLastError());
+        }
+        u32* H = g_H.get((u64)nslots_all);
+        LZ_HIP(hipMemsetAsync(H, 0, (u64)nslots_all * 4, st));
+        if (cut.in.start && ins_bm)
+            k_h_fill<<<cdiv(((u64)cut.in.start + 31) / 32, 256), 256, 0, st>>>(T, G, ins_bm, cut.in.start, H);
+        k_h_fix<<<cdiv(nslots_all, 256), 256, 0, st>>>(H, nslots_all);
+        k_seq_walk<<<1, 64, 0, st>>>(T, G, P, Lv, H, cut.in, fo, offk, d_sq);
+        LZ_HIP(hipGetLastError());
+        u64 hc[2];
+        LZ_HIP(hipMemcpyAsync(hc, d_sq, 16, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        if (hc[1]) throw error(-6, "greedy: sequential completion guard tripped (internal error)");
+        stats[19] = 1;
+        stats[20] = cut.in.start;
+        lap("sequential completion");
+        return offk + hc[0];
+    };
+
+    // ---- base set (entries sorted by slot) and delta
     u64 nb = 0;
     const u32 nslots = G.mask + 1;
     auto build_buckets = [&](auto key, u64 mk, dbuf<u32>& bk) {
@@ -1440,9 +1644,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
                     int eb = 1;
                     while (eb < 32 && (1ull << eb) < ne5) eb++;
                     size_t tb2 = 0;
-                    LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
+                    LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u, (unsigned)eb, st));
                     u8* t2 = scan_tmp.get(tb2);
-                    LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, svals, kdump, pv, pred5, (int)ne5, 0, eb, st));
+                    LZ_HIP(rocprim::radix_sort_pairs(t2, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u, (unsigned)eb, st));
                 } else {
                     const u32 nbk = (u32)((ne5 + (1ull << PB_SH) - 1) >> PB_SH);
                     u32* cursor = g_pbcur.get(nbk + 1);
@@ -1490,9 +1694,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u64* ak2 = kb.get(5 * na);
         k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
         size_t tb = 0;
-        LZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, ak, ak2, (int)(5 * na), 0, 63, st));
+        LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, ak, ak2, (size_t)(5 * na), 0u, 63u, st));
         u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, ak, ak2, (int)(5 * na), 0, 63, st));
+        LZ_HIP(rocprim::radix_sort_keys(t, tb, ak, ak2, (size_t)(5 * na), 0u, 63u, st));
         keys_out = ak2;
         nkeys = 5 * na;
         build_buckets(key_u64{ak2}, 5 * na, bucket);
@@ -1518,6 +1722,18 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         rebuild_added(true);
     };
     W.use_pred = std::getenv("LZ77SSS_NO_PRED") ? 0 : 1;
+    auto finish_call = [&](u64 z, int outer_rounds, int link_rounds, u64 walked, u32 nseg_end) {
+        k_seg_at_clear<<<cdiv(nseg_end, 256), 256, 0, st>>>(S, nseg_end);
+        seg_at_clean = true;
+        stats[12] = outer_rounds;
+        stats[13] = link_rounds;
+        stats[14] = stats_fallback_lanes;
+        stats[15] = walked;
+        stats[16] = nseg_end;
+        stats[17] = nseg0;
+        return z;
+    };
+    if (max_outer == 0) return finish_call(seq_complete(nullptr, 0, nullptr, nullptr, true), 0, 0, 0, nseg0);
     build_base(bmT);  // superset: gaps + short phrase interiors
     set_state();
 
@@ -1530,11 +1746,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     jump_levels JL{};
     u64 total_fact = 0, walked_total = 0;
     int outer = 0, rounds_total = 0;
+    bool restart_seq = false;  // a walk overflowed or linking ran away: complete from position 0
     for (;; outer++) {
-        if (outer > 500) throw error(-6, "greedy speculation did not converge");
         for (int round = 0;; round++) {
             rounds_total++;
-            if (round > 100000) throw error(-6, "greedy segment linking did not converge");
+            if (round > 100000) { restart_seq = true; break; }
             LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
             k_todo<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, ids, d_cnt);
             const u32 ntodo = rd1(d_cnt, st);
@@ -1544,9 +1760,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
                 u32* ids2 = g_ids2.get(ntodo);
                 k_walk_keys<<<cdiv(ntodo, 256), 256, 0, st>>>(S, ids, ntodo, wk);
                 size_t tb = 0;
-                LZ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, wk, wk + ntodo, ids, ids2, (int)ntodo, 0, 32, st));
+                LZ_HIP(rocprim::radix_sort_pairs_desc(nullptr, tb, wk, wk + ntodo, ids, ids2, (size_t)ntodo, 0u, 32u, st));
                 u8* t = scan_tmp.get(tb);
-                LZ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(t, tb, wk, wk + ntodo, ids, ids2, (int)ntodo, 0, 32, st));
+                LZ_HIP(rocprim::radix_sort_pairs_desc(t, tb, wk, wk + ntodo, ids, ids2, (size_t)ntodo, 0u, 32u, st));
                 wids = ids2;
             }
             if (ntodo) {
@@ -1589,12 +1805,15 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             LZ_HIP(hipMemcpyAsync(&cs, d_cs, sizeof(cs), hipMemcpyDeviceToHost, st));
             LZ_HIP(hipStreamSynchronize(st));
             lap("link");
-            if (cs.err & 2) throw error(-6, "greedy: too many LPF-start queries in one segment");
-            if (cs.err & 4) throw error(-6, "greedy: walk guard tripped (internal error)");
+            if (cs.err & 6) { restart_seq = true; break; }  // 2: LPF-start query overflow, 4: walk guard
             if (dbg)
                 std::fprintf(stderr, "[lz77sss-debug] greedy outer=%d round=%d segs=%u walked=%u chain=%u valid=%u flags=%u\n",
                              outer, round, nseg, ntodo, cs.hops + 1, cs.valid, cs.flags);
             if (cs.valid && ((cs.flags & 1) || cs.next >= N)) break;
+        }
+        if (restart_seq) {
+            total_fact = seq_complete(nullptr, 0, nullptr, nullptr, true);
+            break;
         }
         // ---- the chain, its factor offsets, the tail
         const bool tail = cs.flags & 1;
@@ -1659,6 +1878,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             total_fact = chain_fact + tail_count;
             break;
         }
+        if (outer + 1 >= max_outer) {
+            // round budget spent: the chain is exact up to the first changed position
+            LZ_HIP(hipMemsetAsync(d_y0, 0xFF, 4, st));
+            k_first_bit<<<gw, 256, 0, st>>>(bmT, nw, d_y0);
+            total_fact = seq_complete(chain, nall, offs, bmI2, false);
+            break;
+        }
         // positions that joined (flag 1) or left (0) I
         u32* d_y = dirty_in.get(ny + 1);
         u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
@@ -1704,24 +1930,16 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u32* d_ds = dirty_sorted.get(11 * ny + 1);
         {
             size_t tb = 0;
-            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, d_d, d_ds, (int)(11 * ny), 0, 32, st));
+            LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, d_d, d_ds, (size_t)(11 * ny), 0u, 32u, st));
             u8* t = scan_tmp.get(tb);
-            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, d_d, d_ds, (int)(11 * ny), 0, 32, st));
+            LZ_HIP(rocprim::radix_sort_keys(t, tb, d_d, d_ds, (size_t)(11 * ny), 0u, 32u, st));
         }
         k_stale<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, d_ds, 11 * ny);
         lap("delta + dirty");
         if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy delta: changed=%llu outside=%llu\n",
                               (unsigned long long)ny, (unsigned long long)outside);
     }
-    k_seg_at_clear<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
-    seg_at_clean = true;
-    stats[12] = outer + 1;
-    stats[13] = rounds_total;
-    stats[14] = stats_fallback_lanes;
-    stats[15] = walked_total;
-    stats[16] = nseg;
-    stats[17] = nseg0;
-    return total_fact;
+    return finish_call(total_fact, outer + 1, rounds_total, walked_total, nseg);
 }
 
 }  // namespace lz

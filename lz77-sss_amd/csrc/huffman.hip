@@ -18,6 +18,7 @@
 // spans (fields are <= 32 bits: at most two words).
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
+#include "../include/prim.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -213,10 +214,7 @@ u64 engine::huffman_container() {
     std::vector<hf_tab> ht(std::max<u64>(1, nblk));
     if (z) {
         k_hf_adv<<<g, 256, 0, st>>>(F, z, adv);
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, adv, pos, (int)z, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, adv, pos, (int)z, st));
+        excl_sum64(adv, pos, (u64)0, z, scan_tmp, st);
         u32* hist = x_idx.get(nblk * 2 * HF_SIGMA);
         k_hf_hist<<<(unsigned)nblk, 256, 0, st>>>(F, z, pos, hist);
         std::vector<u32> hh(nblk * 2 * HF_SIGMA);
@@ -234,10 +232,7 @@ u64 engine::huffman_container() {
         LZ_HIP(hipMemcpyAsync(dt, ht.data(), nblk * sizeof(hf_tab), hipMemcpyHostToDevice, st));
         k_hf_bits<<<g, 256, 0, st>>>(F, z, pos, dt, bits);
         LZ_HIP(hipMemsetAsync(bits + z, 0, 8, st));
-        tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, bits, off, (int)(z + 1), st));
-        t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, bits, off, (int)(z + 1), st));
+        excl_sum64(bits, off, (u64)0, z + 1, scan_tmp, st);
         total_bits = rd1(off + z, st);
         const u64 nw = total_bits / 32 + 2;
         u32* words = (u32*)hf_words.get(nw * 4);

@@ -3,20 +3,24 @@
 // patched-files/external/lce/include/ds/lce_sss.hpp:53; its source is absent
 // upstream, the definition pinned here is DESIGN.md section 4.1):
 //
-//   Phi(j)  = KR fingerprint of T[j..j+tau) mod 2^31-1 (base SSS_BASE)
+//   Phi(j)  = sum_k T[j+k] b^(tau-1-k) mod 2^32, b = SSS_BASE (a polynomial
+//             Karp-Rabin hash over Z/2^32, not over a prime: DESIGN.md 4.1 states
+//             what that choice costs on hash-adversarial text)
 //   Q       = { j : T[j..j+tau) has a period <= floor(tau/3) }
-//   S       = { i <= n-2tau : min Phi'[i..i+tau] < inf at i or at i+tau }
+//   Phi'(j) = INF (2^32-1) for j in Q, else Phi(j)
+//   S       = { i <= n-2tau : m_i != INF and m_i in {Phi'(i), Phi'(i+tau)} },
+//             m_i = min Phi'[i..i+tau]
 //
 // Launches:
 //   k_q_anchors  -- per anchor a (every 128 positions) the smallest period <= 170
 //                   of T[a..a+340), the Q interval it induces on (a-128, a], and
 //                   the local extent of the periodic run (run table, lce_dev.h)
 //   k_run_elems + 2 scans + k_run_finish -- exact run ends/starts along chains
-//   k_sss_stream -- one wave per stripe of 16384 decisions, walked in 512-blocks
+//   k_sss_stream -- one wave per stripe of 32768 decisions, walked in 512-blocks
 //                   with bytes, prefix hashes and Phi' in registers: lane Horner +
 //                   wave scan, 7 rolls per lane, van Herk minima by lane-local
 //                   and wave scans, ordered per-stripe output
-//   k_sss_fallback -- exact slow path for stripes with more than SCAP outputs
+//   k_sss_fallback -- exact workgroup-parallel path for stripes with more than SCAP outputs
 //   k_sss_compact-- per-stripe outputs -> sorted S
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
@@ -403,7 +407,7 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
                                                            const u16* __restrict__ qinfo, u64 nstripes,
                                                            u32* __restrict__ s_out, u32* __restrict__ s_cnt,
                                                            u32* __restrict__ s_flag, u32* __restrict__ any_flag,
-                                                           u32 b, sss_pow32 PW) {
+                                                           u32 b, sss_pow32 PW, u32 scap) {
     const u32 lane = threadIdx.x & 63;
     // the stripe index is wave-uniform: keep it (and every address derived from it) in SGPRs
     const u64 w = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -591,48 +595,98 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     }
     if (lane == 0) {
         s_cnt[w] = nout;
-        s_flag[w] = nout > (u32)SCAP;
-        if (nout > (u32)SCAP) atomicOr(any_flag, 1u);
+        s_flag[w] = nout > scap;
+        if (nout > scap) atomicOr(any_flag, 1u);
     }
 }
 
-// Exact slow path for stripes whose output buffer overflowed: one workgroup
-// recomputes the stripe's Phi' values and the window minima directly.
-__global__ __launch_bounds__(256) void k_sss_fallback(const u8* __restrict__ T, u64 n, u64 last_i,
-                                                      const u16* __restrict__ qinfo, const u32* __restrict__ lanes,
-                                                      u32* __restrict__ scratch, u8* __restrict__ member,
-                                                      u32* __restrict__ ovf_out, u32* __restrict__ lane_cnt, u32 b,
-                                                      u32 bpow) {
+// Exact path for stripes whose output buffer overflowed (dense sync sets, e.g.
+// hash-adversarial text): one 256-thread workgroup per stripe, everything
+// parallel.  (1) Phi' of the stripe's windows: thread t hashes a contiguous run
+// of ~130 windows (one direct 512-byte hash, then rolls), Q windows -> INF;
+// (2) van Herk / Gil-Werman 512-block prefix and suffix minima (one thread per
+// block and direction); (3) m_i = min(suf[i], pre[i + 511], Phi'[i + 512]) and the
+// membership test per decision; (4) ordered compaction: each thread owns 128
+// consecutive decisions, a block scan of their counts gives the offsets.
+constexpr int FB_T = 256;
+constexpr int FB_DEC = SD / FB_T;  // decisions per thread (128)
+__global__ __launch_bounds__(FB_T) void k_sss_fallback(const u8* __restrict__ T, u64 n, u64 last_i,
+                                                       const u16* __restrict__ qinfo, const u32* __restrict__ lanes,
+                                                       u32* __restrict__ scratch, u32* __restrict__ ovf_out,
+                                                       u32* __restrict__ lane_cnt, u32 b, u32 bpow) {
+    __shared__ u32 s_cnt[FB_T];
     const u64 lane = lanes[blockIdx.x];
     const u64 i0 = lane * SD;
     const u64 i_end = min(i0 + SD, last_i + 1);
-    const u64 j_end = min(i0 + SD + TAU - 1, n - TAU);
-    u32* v = scratch + (u64)blockIdx.x * (SD + TAU);
-    u8* mem = member + (u64)blockIdx.x * SD;
-    if (threadIdx.x == 0) {
-        u32 fp = 0;
-        for (u64 k = 0; k < TAU; k++) fp = fp * b + T[i0 + k];
-        for (u64 j = i0; j <= j_end; j++) {
-            const u64 t = (j + 127) >> 7;
-            const u16 qi = qinfo[t];
-            const u32 rel = (u32)(j + 127 - (t << 7));
-            v[j - i0] = (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) ? INF32 : fp;
-            if (j < j_end) fp = fp * b + T[j + TAU] - bpow * T[j];
+    const u64 j_end = min(i0 + SD + TAU - 1, n - TAU);  // last window needed (a full one)
+    const u64 L = j_end - i0 + 1;
+    const u32 t = threadIdx.x;
+    u32* v = scratch + (u64)blockIdx.x * 3 * (SD + TAU);
+    u32* pre = v + (SD + TAU);
+    u32* suf = pre + (SD + TAU);
+    {
+        const u64 C = (L + FB_T - 1) / FB_T;
+        const u64 a = min<u64>(L, t * C), e = min<u64>(L, a + C);
+        if (a < e) {
+            u32 fp = 0;
+            for (u64 k = 0; k < TAU; k++) fp = fp * b + T[i0 + a + k];
+            for (u64 r = a; r < e; r++) {
+                const u64 j = i0 + r;
+                const u64 q = (j + 127) >> 7;
+                const u16 qi = qinfo[q];
+                const u32 rel = (u32)(j + 127 - (q << 7));
+                v[r] = (rel >= (u32)(qi >> 8) && rel <= (u32)(qi & 255)) ? INF32 : fp;
+                if (r + 1 < e) fp = fp * b + T[j + TAU] - bpow * T[j];
+            }
         }
     }
     __syncthreads();
-    for (u64 i = i0 + threadIdx.x; i < i_end; i += blockDim.x) {
-        u32 m = INF32;
-        for (u64 x = 0; x <= TAU; x++) m = min(m, v[i - i0 + x]);
-        mem[i - i0] = (m != INF32 && (v[i - i0] == m || v[i - i0 + TAU] == m));
+    {
+        const u64 nblk = (L + TAU - 1) / TAU;
+        for (u64 k = t; k < 2 * nblk; k += FB_T) {
+            const u64 blk = k >> 1, a = blk * TAU, e = min<u64>(L, a + TAU);
+            if (k & 1) {
+                u32 m = INF32;
+                for (u64 r = e; r > a; r--) suf[r - 1] = m = min(m, v[r - 1]);
+            } else {
+                u32 m = INF32;
+                for (u64 r = a; r < e; r++) pre[r] = m = min(m, v[r]);
+            }
+        }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        u32 c = 0;
-        for (u64 i = i0; i < i_end; i++)
-            if (mem[i - i0]) ovf_out[(u64)blockIdx.x * SD + c++] = (u32)i;
-        lane_cnt[lane] = c;
+    u32 mask[FB_DEC / 32];
+    u32 c = 0;
+    const u64 d0 = (u64)t * FB_DEC;
+#pragma unroll
+    for (int w = 0; w < FB_DEC / 32; w++) {
+        u32 bits = 0;
+        for (int k = 0; k < 32; k++) {
+            const u64 r = d0 + 32 * w + k;
+            if (i0 + r >= i_end) break;
+            const u32 m = min(min(suf[r], pre[r + TAU - 1]), v[r + TAU]);
+            if (m != INF32 && (v[r] == m || v[r + TAU] == m)) bits |= 1u << k;
+        }
+        mask[w] = bits;
+        c += __popc(bits);
     }
+    s_cnt[t] = c;
+    __syncthreads();
+    if (t == 0) {
+        u32 tot = 0;
+        for (int k = 0; k < FB_T; k++) {
+            const u32 x = s_cnt[k];
+            s_cnt[k] = tot;
+            tot += x;
+        }
+        lane_cnt[lane] = tot;
+    }
+    __syncthreads();
+    u32 o = s_cnt[t];
+    u32* out = ovf_out + (u64)blockIdx.x * SD;
+#pragma unroll
+    for (int w = 0; w < FB_DEC / 32; w++)
+        for (u32 bits = mask[w]; bits; bits &= bits - 1) out[o++] = (u32)(i0 + d0 + 32 * w + __builtin_ctz(bits));
 }
 
 __global__ void k_sss_compact(const u32* __restrict__ lane_out, const u32* __restrict__ lane_cnt,
@@ -703,12 +757,15 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipEventCreate(&e0));
     LZ_HIP(hipEventCreate(&e1));
     LZ_HIP(hipEventRecord(e0, st));
+    // test knob: a lower overflow threshold sends more stripes down the exact fallback
+    const char* scap_env = std::getenv("LZ77SSS_TEST_SCAP");
+    const u32 scap = scap_env ? (u32)std::min<long>(SCAP, std::max<long>(0, std::atol(scap_env))) : (u32)SCAP;
     if (any_q)
         k_sss_stream<true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
-                                                                       (u32)SSS_BASE, PW);
+                                                                       (u32)SSS_BASE, PW, scap);
     else
         k_sss_stream<false><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
-                                                                        (u32)SSS_BASE, PW);
+                                                                        (u32)SSS_BASE, PW, scap);
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipEventRecord(e1, st));
 
@@ -734,11 +791,10 @@ void engine::build_sss(const u8* T) {
         u32* d_lanes = u32d.get(lanes.size());
         LZ_HIP(hipMemcpy(d_lanes, lanes.data(), lanes.size() * 4, hipMemcpyHostToDevice));
         LZ_HIP(hipMemcpy(ovf_slot, slot.data(), nlanes * 4, hipMemcpyHostToDevice));
-        u32* scratch = (u32*)u64a.get(lanes.size() * (SD + TAU));
-        u8* member = tmp_bytes.get(lanes.size() * SD);
+        u32* scratch = (u32*)u64a.get((lanes.size() * 3 * (SD + TAU) + 1) / 2);
         ovf_out = u32b.get(lanes.size() * SD);
-        k_sss_fallback<<<(unsigned)lanes.size(), 256, 0, st>>>(T, n, last_i, qi, d_lanes, scratch, member, ovf_out,
-                                                               lc, (u32)SSS_BASE, bpow);
+        k_sss_fallback<<<(unsigned)lanes.size(), FB_T, 0, st>>>(T, n, last_i, qi, d_lanes, scratch, ovf_out, lc,
+                                                                (u32)SSS_BASE, bpow);
         LZ_HIP(hipGetLastError());
         stats_fallback_lanes = lanes.size();
     } else {

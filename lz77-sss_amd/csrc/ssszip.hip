@@ -15,6 +15,7 @@
 // offsets are scans; every record then writes its bytes independently.
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
+#include "../include/prim.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -142,25 +143,13 @@ u64 engine::ssszip_gapped() {
     u64 off_end = 0, tail = 0;
     if (z) {
         k_ssz_prep<<<g, 256, 0, st>>>(F, z, adv, dec);
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, adv, pos, (int)z, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, adv, pos, (int)z, st));
-        tb = 0;
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, dec, lastdec, max_u32_op{}, (int)z, st));
-        t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, dec, lastdec, max_u32_op{}, (int)z, st));
+        excl_sum64(adv, pos, (u64)0, z, scan_tmp, st);
+        incl_scan64(dec, lastdec, z, max_u32_op{}, scan_tmp, st);
         k_ssz_merged<<<g, 256, 0, st>>>(F, z, lastdec, merged, rs, pos);
-        tb = 0;
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, rs, runst, max_u64_op{}, (int)z, st));
-        t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, rs, runst, max_u64_op{}, (int)z, st));
+        incl_scan64(rs, runst, z, max_u64_op{}, scan_tmp, st);
         k_ssz_size<<<g, 256, 0, st>>>(F, z, merged, runst, pos, sz);
         LZ_HIP(hipMemsetAsync(sz + z, 0, 8, st));
-        tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sz, off, (int)(z + 1), st));
-        t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, sz, off, (int)(z + 1), st));
+        excl_sum64(sz, off, (u64)0, z + 1, scan_tmp, st);
         off_end = rd1(off + z, st);
         u8 mlast = 0;
         u64 rlast = 0;

@@ -146,6 +146,8 @@ struct engine {
     dbuf<u32> g_pbcur;  // predecessor bucket scatter
     dbuf<u32> g_pbm, g_pwp, g_pcnt, g_sdk, g_dstart, g_pflag;  // dense slot ids of the base set  // per-block bitmap counts and their inclusive scan
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
+    dbuf<u32> g_H;      // materialized gap-index table of the sequential completion
+    dbuf<u8> g_cut;     // chain_cut + completion counters
     dbuf<u64> g_xk, g_xk2;
     // exact mode (csrc/exact.hip)
     dbuf<u64> x_key, x_key2, x_off, x_wide;
@@ -153,7 +155,8 @@ struct engine {
     const u32* sa_full = nullptr;    // suffix array of the text (x_sa) after build_sa_full
     u32 x_rounds = 0;
     // device decode (csrc/decode.hip)
-    dbuf<u32> dec_len, dec_start, dec_fid, dec_ref, dec_ref2;
+    dbuf<u32> dec_fid, dec_ref, dec_ref2;
+    dbuf<u64> dec_len64, dec_start64;
     dbuf<u8> dec_out;
     u32 dec_rounds = 0;
     u64 num_fact = 0;

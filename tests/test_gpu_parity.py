@@ -255,7 +255,20 @@ def test_device_decode_rejects_invalid(lz):
         lz.decode_device(np.array([[97, 0], [0, 2]], np.uint32), 5)
     with pytest.raises(lz.Lz77SssError):
         lz.decode_device(np.array([[97, 0]], np.uint32), 0)
+    with pytest.raises(lz.Lz77SssError):  # lengths sum to n + 2^32: a 32-bit running sum would wrap to n
+        lz.decode_device(np.array([[97, 0], [0, 4], [0, 0xFFFFFFFF], [0, 1]], np.uint32), 5)
     assert lz.decode_device(np.zeros((0, 2), np.uint32), 0).size == 0
+
+
+@pytest.mark.slow
+def test_device_decode_past_2g(lz):
+    """n just above 2^31: every device scan of the decode runs on 64-bit item counts."""
+    n = (1 << 31) + 7
+    F = np.array([[ord("x"), 0], [ord("y"), 0], [0, n - 2]], np.uint32)
+    out = lz.decode_device(F, n)
+    assert out.size == n and out[0] == ord("x") and out[1] == ord("y")
+    assert out[-1] == (ord("x") if (n - 1) % 2 == 0 else ord("y"))
+    assert np.array_equal(out[:1 << 20], np.resize(np.array([ord("x"), ord("y")], np.uint8), 1 << 20))
 
 
 @pytest.mark.parametrize("name", golden_names())
@@ -300,3 +313,50 @@ def test_sorted_predecessor_paths_vs_oracle(session, orc, lz, kind, mib, monkeyp
     monkeypatch.setenv("LZ77SSS_PRED_RADIX", "1")
     _, F2 = run(session, T)
     assert np.array_equal(F2, F_ref)
+
+
+# ---- bounded greedy completion (k_seq_walk): the exact sequential walk from the confirmed chain prefix
+
+@pytest.mark.parametrize("max_outer", [0, 1, 2])
+@pytest.mark.parametrize("seed", [1, 2, 3, 5, 8, 13])
+def test_greedy_bounded_completion_c1(session, orc, lz, seed, max_outer, monkeypatch):
+    """LZ77SSS_GREEDY_MAX_OUTER caps the speculation rounds; past the cap the chain prefix that is exact
+    (up to the first position where the speculated and the actual insert sets differ) is kept and the
+    rest is walked sequentially (0: the whole text).  Either way the stream is the p = 1 oracle's."""
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    monkeypatch.setenv("LZ77SSS_GREEDY_MAX_OUTER", str(max_outer))
+    s, F = run(session, T)
+    assert np.array_equal(F, orc.factorize(T)[0])
+    st = s.stats()
+    if max_outer == 0:
+        assert st[19] == 1 and st[20] == 0
+    else:
+        assert st[12] <= max_outer
+
+
+@pytest.mark.parametrize("n", [1, 2, 511, 1024, 1537, 4097, 65537])
+def test_greedy_sequential_edges(session, orc, n, monkeypatch):
+    """The sequential walk's tail semantics (stale / zeroed fingerprints, conditional inserts) at edge sizes."""
+    rng = np.random.Generator(np.random.PCG64(n))
+    T = rng.integers(0, 3, n, dtype=np.uint8)
+    if n > 3000:
+        T[1000:2500] = T[100:1600]
+    monkeypatch.setenv("LZ77SSS_GREEDY_MAX_OUTER", "0")
+    _, F = run(session, T)
+    assert np.array_equal(F, orc.factorize(T)[0])
+
+
+@pytest.mark.parametrize("max_outer", [1, 2, 3])
+def test_greedy_bounded_completion_genome(session, orc, lz, max_outer, monkeypatch):
+    """A genome-like text needs several speculation rounds; cutting them short must not change the stream."""
+    n = 4 << 20
+    T = lz.gen_genome(n, 1 << 20, 0.001, 21)
+    F_ref, _ = orc.factorize(T)
+    s0, F0 = run(session, T)
+    rounds = s0.stats()[12]
+    assert np.array_equal(F0, F_ref)
+    monkeypatch.setenv("LZ77SSS_GREEDY_MAX_OUTER", str(max_outer))
+    s, F = run(session, T)
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+    st = s.stats()
+    assert st[19] == (1 if rounds > max_outer else 0)
