@@ -8,15 +8,23 @@
  *   lz77sss_factorize_approx_u32  <- lz77_sss<uint32_t>::factorize_approximate
  *                                    <fact_mode, phr_mode, tau>(input, n, output, params)
  *                                    include/lz77_sss/lz77_sss.hpp:176-186
+ *   lz77sss_factorize_approx_u64  <- lz77_sss<uint64_t>::factorize_approximate (same lines;
+ *                                    pos_t = uint64_t per lz77_sss.hpp:72-75, selected by the CLI
+ *                                    for n > 2^32 - 1, cli/lz77_sss_3_aprx.cpp:73-83)
  *   lz77sss_factorize_exact_u32   <- lz77_sss<uint32_t>::factorize_exact
  *                                    <fact_mode, phr_mode, transf_mode, range_ds_t, tau>(input, n, output, params)
  *                                    include/lz77_sss/lz77_sss.hpp:188-200,333-357
  *   lz77sss_decode_u32            <- lz77_sss<uint32_t>::decode(fact_it, out_it, n)
  *                                    include/lz77_sss/lz77_sss.hpp:202-203,
  *                                    include/lz77_sss/algorithms/common.cpp:31-54
+ *   lz77sss_factorize_exact_u64,
+ *   lz77sss_decode_u64            <- the same with pos_t = uint64_t
  *   lz77sss_factor32              <- lz77_sss<uint32_t>::factor {src, len}
  *                                    include/lz77_sss/lz77_sss.hpp:129-147 (8-byte layout;
  *                                    literal <=> len == 0, src = (uint8_t)char)
+ *   lz77sss_factor64              <- lz77_sss<uint64_t>::factor {src, len} (in memory; its
+ *                                    10-byte stream form, lz77_sss.hpp:149-173, is written by
+ *                                    lz77sss_serialize_factors64)
  *   lz77sss_params                <- struct parameters {num_threads, log}
  *                                    include/lz77_sss/lz77_sss.hpp:67-70, plus the knobs the
  *                                    reference leaves to std::random_device / malloc_count
@@ -60,6 +68,7 @@ enum {
 };
 
 typedef struct { uint32_t src; uint32_t len; } lz77sss_factor32;
+typedef struct { uint64_t src; uint64_t len; } lz77sss_factor64;
 
 typedef struct {
     int32_t phr_mode;        /* default LZ77SSS_LPF_OPT, lz77_sss.hpp:77 */
@@ -83,6 +92,7 @@ void lz77sss_default_params(lz77sss_params* prm);
 
 /* Batched, in-order factor sink.  Return 0 to continue, non-zero to abort. */
 typedef int (*lz77sss_emit_fn)(const lz77sss_factor32* batch, uint64_t count, void* user);
+typedef int (*lz77sss_emit64_fn)(const lz77sss_factor64* batch, uint64_t count, void* user);
 
 /* One-shot: factorize text[0..n) (host memory).  LPF/LNF modes do NOT modify
  * `text` (the reference reverses the caller's buffer in place and restores
@@ -90,6 +100,13 @@ typedef int (*lz77sss_emit_fn)(const lz77sss_factor32* batch, uint64_t count, vo
  * past n is required. */
 int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
                                  lz77sss_emit_fn emit, void* user);
+/* The same with pos_t = uint64_t: any n up to 2^40 (texts past 2^32 - 16 bytes need this
+ * one).  The gap index is sized by the reference's formula for 8-byte entries
+ * (rolling_hash_index_107.hpp:59-70), so the stream is the reference's pos_t = uint64_t
+ * stream, which differs from the uint32_t one in general.  phr_mode: lpf_opt or
+ * lpf_naive (the LPF/LNF modes are built for uint32_t only). */
+int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
+                                 lz77sss_emit64_fn emit, void* user);
 
 /* One-shot exact factorization (greedy LZ77: every factor is a longest previous
  * factor; a copy {src, len >= 1} or the literal {char, 0} when the character is
@@ -103,6 +120,9 @@ int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_
  * Requires n < 2^31. */
 int lz77sss_factorize_exact_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm, int transf_mode,
                                 lz77sss_emit_fn emit, void* user);
+/* pos_t = uint64_t form of the exact factorization (same algorithm and limit n < 2^31). */
+int lz77sss_factorize_exact_u64(const uint8_t* text, uint64_t n, const lz77sss_params* prm, int transf_mode,
+                                lz77sss_emit64_fn emit, void* user);
 
 /* Decode nf factors into out[0..n) (host memory), algorithms/common.cpp:31-54. */
 int lz77sss_decode_u32(const lz77sss_factor32* factors, uint64_t nf, uint8_t* out, uint64_t n);
@@ -111,12 +131,26 @@ int lz77sss_decode_u32(const lz77sss_factor32* factors, uint64_t nf, uint8_t* ou
  * references, O(n log depth) work).  Stricter than the host decode: the factor
  * lengths must sum to exactly n. */
 int lz77sss_decode_u32_device(const lz77sss_factor32* factors, uint64_t nf, uint8_t* out, uint64_t n, int device);
+int lz77sss_decode_u64(const lz77sss_factor64* factors, uint64_t nf, uint8_t* out, uint64_t n);
+int lz77sss_decode_u64_device(const lz77sss_factor64* factors, uint64_t nf, uint8_t* out, uint64_t n, int device);
+/* The reference's pos_t = uint64_t factor stream (lz77_sss.hpp:149-173): 5 bytes src, 5
+ * bytes len, little endian; out holds 10 * nf bytes.  Returns LZ77SSS_EINVAL if a value
+ * needs more than 40 bits. */
+int lz77sss_serialize_factors64(const lz77sss_factor64* factors, uint64_t nf, uint8_t* out);
+int lz77sss_deserialize_factors64(const uint8_t* in, uint64_t nf, lz77sss_factor64* factors);
 
 /* ---- device-resident session (text stays in HBM across calls) ---- */
 typedef struct lz77sss_session lz77sss_session;
 
-/* Creates a session on `device` able to hold texts of up to max_n bytes. */
+/* Creates a session on `device` able to hold texts of up to max_n bytes (pos_t = uint32_t:
+ * n <= 2^32 - 16). */
 int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out);
+/* A pos_t = uint64_t session (lz77_sss<uint64_t>): any n up to 2^40.  Supports load,
+ * gen_genome, factorize (lpf_opt / lpf_naive, greedy / skip_phrases), get_factors64,
+ * decode, sss, get_sss64, get_sa_s, get_lpf64, phase_times, stats, sss_kernel_time;
+ * the 32-bit accessors and the exact / LNF / container entry points return LZ77SSS_EINVAL. */
+int lz77sss_session_create64(int device, uint64_t max_n, lz77sss_session** out);
+int lz77sss_session_is64(const lz77sss_session* s);
 /* Copies text[0..n) host -> HBM (not part of the timed factorization). */
 int lz77sss_session_load(lz77sss_session* s, const uint8_t* text, uint64_t n);
 /* Factorizes the loaded text; factors stay in HBM. */
@@ -126,6 +160,8 @@ int lz77sss_session_factorize_exact(lz77sss_session* s, const lz77sss_params* pr
                                     uint64_t* num_factors);
 /* Copies the factors HBM -> host (cap >= num_factors). */
 int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32* out, uint64_t cap);
+/* 64-bit factors (any session; a 32-bit session's factors are widened). */
+int lz77sss_session_get_factors64(lz77sss_session* s, lz77sss_factor64* out, uint64_t cap);
 /* Decodes the factors of the last factorize call on the device.  out (host,
  * cap >= n) may be NULL; when mismatches is given it receives the number of
  * positions where the decoded text differs from the loaded one (0 = round trip
@@ -146,7 +182,7 @@ int lz77sss_session_get_sss(lz77sss_session* s, uint32_t* out, uint64_t cap);
  * The result stays in HBM until get_sss64 / copy_sss64_device. */
 int lz77sss_session_sss_range(lz77sss_session* s, uint64_t first, uint64_t end, uint64_t base, uint64_t window,
                               uint64_t* size_sss, int* has_runs);
-int lz77sss_session_get_sss64(lz77sss_session* s, uint64_t* out, uint64_t cap);
+int lz77sss_session_get_sss64(lz77sss_session* s, uint64_t* out, uint64_t cap);  /* also a 64-bit session's S */
 /* Device-to-device copy of the sss_range result into `dst`, a device buffer on the
  * session's device (e.g. a collective's send buffer); cap in elements. */
 int lz77sss_session_copy_sss64_device(lz77sss_session* s, void* dst, uint64_t cap);
@@ -171,6 +207,7 @@ int lz77sss_session_huffman(lz77sss_session* s, uint8_t* out, uint64_t cap, uint
 int lz77sss_session_get_sa_s(lz77sss_session* s, uint32_t* sa, uint32_t* lcp, uint64_t cap);
 /* Copies the LPF phrase list (beg,end,src triples) of the last factorize call. */
 int lz77sss_session_get_lpf(lz77sss_session* s, uint32_t* out3, uint64_t cap, uint64_t* count);
+int lz77sss_session_get_lpf64(lz77sss_session* s, uint64_t* out3, uint64_t cap, uint64_t* count);
 /* Per-phase times (ms, hipEvent-timed) of the last call; returns the count. */
 int lz77sss_session_phase_times(lz77sss_session* s, double* ms, const char** names, int cap);
 /* Statistics of the last factorize call: [size_sss, has_runs, num_lpf, len_lpf_phr,
@@ -190,6 +227,9 @@ int64_t lz77sss_gen_random_repetitive(uint32_t min_size, uint32_t max_size, uint
                                       double rep_knob, double run_knob, uint8_t* out, uint64_t cap);
 /* chr19-style: random ACGT base block repeated with point mutations. */
 int64_t lz77sss_gen_genome(uint64_t n, uint64_t base_len, double mut_rate, uint32_t seed, uint8_t* out);
+/* The text of lz77sss_session_gen_genome (position-hashed), generated on the host. */
+int lz77sss_gen_genome_pos(uint64_t n, uint64_t base_len, double mut_rate, uint32_t seed, uint64_t offset,
+                           uint8_t* out);
 
 const char* lz77sss_last_error(void);
 /* Number of visible HIP devices (0 if none); does not create a context. */

@@ -12,9 +12,9 @@
 #include "../include/engine.h"
 #include "../include/prim.h"
 
-namespace lz {
+namespace LZ_NS {
 
-__global__ void k_dec_lens(const u32* __restrict__ F, u64 nf, u64* __restrict__ len) {
+__global__ void k_dec_lens(const pos_t* __restrict__ F, u64 nf, u64* __restrict__ len) {
     const u64 f = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (f < nf) len[f] = F[2 * f + 1] ? F[2 * f + 1] : 1u;
 }
@@ -26,19 +26,19 @@ struct max_u32 {
     __device__ __forceinline__ u32 operator()(const u32& a, const u32& b) const { return a > b ? a : b; }
 };
 // ref[p]: p for literals, the source position for copies; err on a forward reference
-__global__ void k_dec_refs(const u32* __restrict__ F, const u64* __restrict__ start, const u32* __restrict__ fid, u64 n,
-                           u32* __restrict__ ref, u32* __restrict__ err) {
+__global__ void k_dec_refs(const pos_t* __restrict__ F, const u64* __restrict__ start, const u32* __restrict__ fid, u64 n,
+                           pos_t* __restrict__ ref, u32* __restrict__ err) {
     const u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const u32 f = fid[p];
-    const u32 len = F[2 * (u64)f + 1];
-    if (len == 0) { ref[p] = (u32)p; return; }
-    const u32 src = F[2 * (u64)f], st = (u32)start[f];
-    if (src >= st) { atomicOr(err, 1u); ref[p] = (u32)p; return; }  // only on an invalid stream
+    const pos_t len = F[2 * (u64)f + 1];
+    if (len == 0) { ref[p] = (pos_t)p; return; }
+    const pos_t src = F[2 * (u64)f], st = (pos_t)start[f];
+    if (src >= st) { atomicOr(err, 1u); ref[p] = (pos_t)p; return; }  // only on an invalid stream
     // a self-overlapping copy (distance d < len) is d-periodic: fold the offset
     // into the first period so the reference lands before the factor start
-    const u32 d = st - src;
-    u32 off = (u32)(p - st);
+    const pos_t d = st - src;
+    pos_t off = (pos_t)(p - st);
     if (off >= d) off %= d;
     ref[p] = src + off;
 }
@@ -46,7 +46,7 @@ __global__ void k_dec_refs(const u32* __restrict__ F, const u64* __restrict__ st
 // flag costs one atomic per block: millions of same-address atomics (even one
 // per wave) serialize at ~10 ns each.
 constexpr unsigned DEC_GRID = 4096;
-__global__ void __launch_bounds__(256) k_dec_jump(const u32* __restrict__ ref, u64 n, u32* __restrict__ out,
+__global__ void __launch_bounds__(256) k_dec_jump(const pos_t* __restrict__ ref, u64 n, pos_t* __restrict__ out,
                                                   u32* __restrict__ changed) {
     __shared__ u32 any;
     if (threadIdx.x == 0) any = 0;
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) k_dec_jump(const u32* __restrict__ ref, u
     const u64 stride = (u64)gridDim.x * blockDim.x;
     u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     for (; p + 3 * stride < n; p += 4 * stride) {  // 4 independent gathers in flight per lane
-        u32 r[4], rr[4];
+        pos_t r[4], rr[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) r[k] = ref[p + k * stride];
 #pragma unroll
@@ -67,8 +67,8 @@ __global__ void __launch_bounds__(256) k_dec_jump(const u32* __restrict__ ref, u
         }
     }
     for (; p < n; p += stride) {
-        const u32 r = ref[p];
-        const u32 rr = ref[r];
+        const pos_t r = ref[p];
+        const pos_t rr = ref[r];
         out[p] = rr;
         ch |= rr != r;
     }
@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(256) k_dec_jump(const u32* __restrict__ ref, u
     __syncthreads();
     if (threadIdx.x == 0 && any) atomicOr(changed, 1u);
 }
-__global__ void k_dec_bytes(const u32* __restrict__ F, const u32* __restrict__ fid, const u32* __restrict__ ref, u64 n,
+__global__ void k_dec_bytes(const pos_t* __restrict__ F, const u32* __restrict__ fid, const pos_t* __restrict__ ref, u64 n,
                             const u8* __restrict__ cmp, u8* __restrict__ out, u32* __restrict__ mism) {
     const u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
@@ -89,13 +89,14 @@ __global__ void k_dec_bytes(const u32* __restrict__ F, const u32* __restrict__ f
 // the text to out (device, may be null) and, when cmp is given, counts the
 // positions where it differs from cmp.  Returns the mismatch count, or throws
 // on an invalid stream (lengths not summing to n, forward references).
-u64 engine::decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cmp) {
+u64 engine::decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* cmp) {
     if (n_out == 0) {
         if (nf) throw error(LZ77SSS_EINVAL, "factors for an empty text");
         return 0;
     }
     if (nf == 0 || nf > n_out) throw error(LZ77SSS_EINVAL, "factor count does not fit the text length");
-    if (n_out > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
+    if (n_out > POS_MAX_N) throw error(LZ77SSS_EINVAL, "n too large for pos_t");
+    if (nf >= (1ull << 32)) throw error(LZ77SSS_EINVAL, "too many factors for the device decode (factor ids are 32-bit)");
     // starts in 64 bits: lengths of an invalid stream may sum past 2^32 (the sum check must see it)
     u64* len = dec_len64.get(nf + 1);
     u64* start = dec_start64.get(nf + 1);
@@ -104,12 +105,12 @@ u64 engine::decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cm
     excl_sum64(len, start, (u64)0, nf + 1, scan_tmp, st);
     if (rd1(start + nf, st) != n_out) throw error(LZ77SSS_EINVAL, "factor lengths do not sum to n");
     u32* head = dec_fid.get(n_out);
-    u32* fid = dec_ref2.get(n_out);
+    u32* fid = dec_fid2.get(n_out);
     LZ_HIP(hipMemsetAsync(head, 0, n_out * 4, st));
     k_dec_heads<<<cdiv(nf, 256), 256, 0, st>>>(start, nf, n_out, head);
     incl_scan64(head, fid, n_out, max_u32{}, scan_tmp, st);
-    u32* ref = dec_ref.get(n_out);
-    u32* ref2 = head;  // free after the scan
+    pos_t* ref = dec_ref.get(n_out);
+    pos_t* ref2 = dec_ref2.get(n_out);
     u32* flags = counters.get(16);
     LZ_HIP(hipMemsetAsync(flags, 0, 8, st));
     k_dec_refs<<<cdiv(n_out, 256), 256, 0, st>>>(F, start, fid, n_out, ref, flags);
@@ -128,4 +129,4 @@ u64 engine::decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cm
     return cmp ? rd1(flags + 2, st) : 0;
 }
 
-}  // namespace lz
+}  // namespace LZ_NS

@@ -4,15 +4,17 @@
 // for fact_mode = greedy, phr_mode = lpf_opt, p = 1.
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
+#include "../include/engine_if.h"
 
 #include <hipcub/hipcub.hpp>
 
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 
-namespace lz {
+namespace LZ_NS {
 
 void engine::init(int dev, u64 maxn) {
     device = dev;
@@ -58,12 +60,12 @@ void engine::destroy() {
 // (approximate/factorize/skip_gaps.cpp:31-61): {beg of the first phrase, 0}, then
 // per phrase {src, len} followed by {gap length, 0} when the next phrase (or the
 // sentinel {n, n+1, 0}) starts after its end
-__global__ void k_skip_counts(const u32* __restrict__ P, u32 m, u32* __restrict__ cnt) {
+__global__ void k_skip_counts(const pos_t* __restrict__ P, u32 m, u32* __restrict__ cnt) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
     cnt[k] = k == m ? 1u : 1u + (P[3 * (k + 1)] > P[3 * k + 1] ? 1u : 0u);  // slot m: the leading gap record
 }
-__global__ void k_skip_write(const u32* __restrict__ P, u32 m, const u32* __restrict__ off, u32* __restrict__ F) {
+__global__ void k_skip_write(const pos_t* __restrict__ P, u32 m, const u32* __restrict__ off, pos_t* __restrict__ F) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
     if (k == m) {
@@ -72,7 +74,7 @@ __global__ void k_skip_write(const u32* __restrict__ P, u32 m, const u32* __rest
         return;
     }
     const u64 o = 1 + off[k];
-    const u32 beg = P[3 * k], end = P[3 * k + 1], src = P[3 * k + 2], nb = P[3 * (k + 1)];
+    const pos_t beg = P[3 * k], end = P[3 * k + 1], src = P[3 * k + 2], nb = P[3 * (k + 1)];
     F[2 * o] = src;
     F[2 * o + 1] = end - beg;
     if (nb > end) {
@@ -82,9 +84,10 @@ __global__ void k_skip_write(const u32* __restrict__ P, u32 m, const u32* __rest
 }
 u64 engine::emit_skip_phrases() {
     const u32 m = num_phr;
-    u32* P = lpf.get((u64)(m + 1) * 3);
-    const u32 sent[3] = {(u32)n, (u32)n + 1, 0};
-    LZ_HIP(hipMemcpyAsync(P + 3 * (u64)m, sent, 12, hipMemcpyHostToDevice, st));
+    pos_t* P = lpf.get((u64)(m + 1) * 3);
+    const pos_t sent[3] = {(pos_t)n, (pos_t)n + 1, 0};
+    LZ_HIP(hipMemcpyAsync(P + 3 * (u64)m, sent, sizeof(sent), hipMemcpyHostToDevice, st));
+    LZ_HIP(hipStreamSynchronize(st));  // sent is a stack array
     u32* cnt = u32a.get((u64)m + 2);
     u32* off = u32b.get((u64)m + 2);
     k_skip_counts<<<cdiv((u64)m + 1, 256), 256, 0, st>>>(P, m, cnt);
@@ -94,7 +97,7 @@ u64 engine::emit_skip_phrases() {
     LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, cnt, off, (int)(m + 1), st));
     const u32 last = rd1(off + m, st);  // records of the m phrases (slot m is the leading record)
     const u64 z = (u64)last + 1;
-    u32* F = fact.get(2 * z + 2);
+    pos_t* F = fact.get(2 * z + 2);
     k_skip_write<<<cdiv((u64)m + 1, 256), 256, 0, st>>>(P, m, off, F);
     LZ_HIP(hipGetLastError());
     return z;
@@ -103,7 +106,8 @@ u64 engine::emit_skip_phrases() {
 u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode) {
     LZ_HIP(hipSetDevice(device));
     if (phr_mode < LZ77SSS_LPF_NAIVE || phr_mode > LZ77SSS_LPF_LNF_OPT) throw error(LZ77SSS_EINVAL, "unsupported phrase mode");
-    if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
+    if (n > POS_MAX_N)
+        throw error(LZ77SSS_EINVAL, sizeof(pos_t) == 4 ? "n too large for pos_t = uint32_t" : "n too large");
     num_fact = 0;
     last_fact_mode = fact_mode;
     stats.assign(24, 0);
@@ -130,8 +134,12 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         timer.mark("lpf");
         trace("lpf");
     } else {
+#ifdef LZ_POS64
+        throw error(LZ77SSS_EINVAL, "LPF/LNF phrase modes are built for pos_t = uint32_t only");
+#else
         build_lpf_lnf(phr_mode == LZ77SSS_LPF_LNF_OPT ? 1 : 0);
         trace("lpf_lnf");
+#endif
     }
     if (fact_mode == LZ77SSS_SKIP_PHRASES) {
         num_fact = emit_skip_phrases();
@@ -151,13 +159,72 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
     return num_fact;
 }
 
-}  // namespace lz
+}  // namespace LZ_NS
 
+#ifdef LZ_POS64
+// ===========================================================================
+// the pos_t = uint64_t engine behind the C-ABI's 64-bit sessions (engine_if.h)
+// ===========================================================================
+namespace lz64 {
+struct engine64_impl final : lz::engine_if {
+    engine E;
+    ~engine64_impl() override { E.destroy(); }
+    int device() const override { return E.device; }
+    u64 n() const override { return E.n; }
+    u64 max_n() const override { return E.max_n; }
+    u8* text() override { return E.d_text; }
+    hipStream_t stream() override { return E.st; }
+    void set_n(u64 n) override { E.n = n; }
+    void load(const u8* t, u64 n) override { E.load(t, n); }
+    u64 factorize(int phr, u32 seed, int log2, bool log, int fact_mode) override {
+        return E.factorize(phr, seed, log2, log, fact_mode);
+    }
+    u64 num_fact() const override { return E.num_fact; }
+    const u64* factors() const override { return E.fact.p; }
+    u64* factors_buf(u64 nf) override { return E.fact.get(2 * nf + 2); }
+    u64 decode(const u64* F, u64 nf, u64 n_out, u8* d_out, bool cmp) override {
+        return E.decode_device(F, nf, n_out, d_out, cmp ? E.d_text : nullptr);
+    }
+    u8* dec_out(u64 n) override { return E.dec_out.get(n); }
+    void sss(u64* size, int* has_runs) override {
+        LZ_HIP(hipSetDevice(E.device));
+        E.build_sss(E.d_text);
+        LZ_HIP(hipStreamSynchronize(E.st));
+        *size = E.s;
+        *has_runs = E.has_runs;
+    }
+    u64 sss_size() const override { return E.s; }
+    const u64* sss_ptr() const override { return E.S.p; }
+    u64 num_phr() const override { return E.num_phr; }
+    const u64* lpf_ptr() const override { return E.lpf.p; }
+    const u32* sa_ptr() const override { return E.SA.p; }
+    const u32* lcp_ptr() const override { return E.lcp_rmq[0].p; }
+    std::vector<u64>& stats() override { return E.stats; }
+    lz::phase_timer& timer() override { return E.timer; }
+    double sss_kernel_ms() const override { return E.sss_kernel_ms; }
+    u64 sss_kernel_bytes() const override { return E.sss_kernel_bytes; }
+    u32 dec_rounds() const override { return E.dec_rounds; }
+};
+}  // namespace lz64
+namespace lz {
+engine_if* make_engine64(int dev, u64 maxn) {
+    auto* p = new lz64::engine64_impl();
+    try {
+        p->E.init(dev, maxn);
+    } catch (...) {
+        delete p;
+        throw;
+    }
+    return p;
+}
+}  // namespace lz
+#else
 // ===========================================================================
 // C-ABI
 // ===========================================================================
 struct lz77sss_session {
-    lz::engine E;
+    lz::engine E;                          // pos_t = uint32_t sessions
+    std::unique_ptr<lz::engine_if> E64;    // pos_t = uint64_t sessions (lz77sss_session_create64)
 };
 
 static thread_local std::string g_err;
@@ -177,6 +244,9 @@ static int guarded(F&& f) {
         g_err = e.what();
         return LZ77SSS_EINTERNAL;
     }
+}
+static void need32(lz77sss_session* s, const char* what) {
+    if (s->E64) throw lz::error(LZ77SSS_EINVAL, std::string(what) + " is not available on a pos_t = uint64_t session");
 }
 
 extern "C" {
@@ -238,16 +308,38 @@ LZ77SSS_API int lz77sss_session_create(int device, uint64_t max_n, lz77sss_sessi
     return LZ77SSS_OK;
 }
 
+LZ77SSS_API int lz77sss_session_create64(int device, uint64_t max_n, lz77sss_session** out) {
+    if (!out) return LZ77SSS_EINVAL;
+    *out = nullptr;
+    lz77sss_session* s = new (std::nothrow) lz77sss_session();
+    if (!s) return LZ77SSS_ENOMEM;
+    int rc = guarded([&] { s->E64.reset(lz::make_engine64(device, max_n)); });
+    if (rc) {
+        delete s;
+        return rc;
+    }
+    *out = s;
+    return LZ77SSS_OK;
+}
+
+LZ77SSS_API int lz77sss_session_is64(const lz77sss_session* s) { return s && s->E64 ? 1 : 0; }
+
 LZ77SSS_API int lz77sss_session_load(lz77sss_session* s, const uint8_t* text, uint64_t n) {
     if (!s || (!text && n)) return LZ77SSS_EINVAL;
-    return guarded([&] { s->E.load(text, n); });
+    return guarded([&] {
+        if (s->E64) s->E64->load(text, n);
+        else s->E.load(text, n);
+    });
 }
 
 LZ77SSS_API int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_params* prm, uint64_t* num_factors) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
         check_params(prm);
-        uint64_t z = s->E.factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0, prm->fact_mode);
+        uint64_t z = s->E64 ? s->E64->factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0,
+                                                 prm->fact_mode)
+                            : s->E.factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0,
+                                             prm->fact_mode);
         if (num_factors) *num_factors = z;
     });
 }
@@ -256,6 +348,7 @@ LZ77SSS_API int lz77sss_session_factorize_exact(lz77sss_session* s, const lz77ss
                                                 uint64_t* num_factors) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        need32(s, "session_factorize_exact");
         check_exact_params(prm, transf_mode);
         uint64_t z = s->E.factorize_exact(prm->log != 0);
         if (num_factors) *num_factors = z;
@@ -263,11 +356,32 @@ LZ77SSS_API int lz77sss_session_factorize_exact(lz77sss_session* s, const lz77ss
 }
 
 LZ77SSS_API int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32* out, uint64_t cap) {
-    if (!s || (!out && s->E.num_fact)) return LZ77SSS_EINVAL;
+    if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        need32(s, "get_factors (32-bit layout)");
+        if (!out && s->E.num_fact) throw lz::error(LZ77SSS_EINVAL, "out is NULL");
         if (cap < s->E.num_fact) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
         if (s->E.num_fact)
             LZ_HIP(hipMemcpy(out, s->E.fact.p, s->E.num_fact * sizeof(lz77sss_factor32), hipMemcpyDeviceToHost));
+    });
+}
+
+// the 10-byte serialized pos_t = uint64_t factor of lz77_sss.hpp:149-173 is a storage
+// format; in memory a factor is {uint64_t src, uint64_t len} (lz77_sss.hpp:129-147)
+LZ77SSS_API int lz77sss_session_get_factors64(lz77sss_session* s, lz77sss_factor64* out, uint64_t cap) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        const uint64_t z = s->E64 ? s->E64->num_fact() : s->E.num_fact;
+        if (!out && z) throw lz::error(LZ77SSS_EINVAL, "out is NULL");
+        if (cap < z) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (!z) return;
+        if (s->E64) {
+            LZ_HIP(hipMemcpy(out, s->E64->factors(), z * sizeof(lz77sss_factor64), hipMemcpyDeviceToHost));
+        } else {
+            std::vector<lz77sss_factor32> tmp(z);
+            LZ_HIP(hipMemcpy(tmp.data(), s->E.fact.p, z * sizeof(lz77sss_factor32), hipMemcpyDeviceToHost));
+            for (uint64_t k = 0; k < z; k++) out[k] = lz77sss_factor64{tmp[k].src, tmp[k].len};
+        }
     });
 }
 
@@ -275,6 +389,20 @@ LZ77SSS_API int lz77sss_session_get_factors(lz77sss_session* s, lz77sss_factor32
 LZ77SSS_API int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* mismatches) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        if (s->E64) {
+            lz::engine_if& E = *s->E64;
+            LZ_HIP(hipSetDevice(E.device()));
+            if (out && cap < E.n()) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+            lz::u8* d_out = out && E.n() ? E.dec_out(E.n()) : nullptr;
+            E.timer().begin(E.stream());
+            const uint64_t bad = E.decode(E.factors(), E.num_fact(), E.n(), d_out, mismatches != nullptr);
+            E.timer().mark("decode");
+            if (E.stats().size() > 18) E.stats()[18] = E.dec_rounds();
+            if (mismatches) *mismatches = bad;
+            if (d_out) LZ_HIP(hipMemcpyAsync(out, d_out, E.n(), hipMemcpyDeviceToHost, E.stream()));
+            LZ_HIP(hipStreamSynchronize(E.stream()));
+            return;
+        }
         lz::engine& E = s->E;
         LZ_HIP(hipSetDevice(E.device));
         if (out && cap < E.n) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
@@ -292,6 +420,14 @@ LZ77SSS_API int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_
 LZ77SSS_API int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        if (s->E64) {
+            uint64_t sz = 0;
+            int hr = 0;
+            s->E64->sss(&sz, &hr);
+            if (size_sss) *size_sss = sz;
+            if (has_runs) *has_runs = hr;
+            return;
+        }
         LZ_HIP(hipSetDevice(s->E.device));
         s->E.build_sss(s->E.d_text);
         LZ_HIP(hipStreamSynchronize(s->E.st));
@@ -304,6 +440,7 @@ LZ77SSS_API int lz77sss_session_sss_range(lz77sss_session* s, uint64_t first, ui
                                           uint64_t window, uint64_t* size_sss, int* has_runs) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        need32(s, "sss_range");
         LZ_HIP(hipSetDevice(s->E.device));
         s->E.build_sss_range(first, end, base, window);
         if (size_sss) *size_sss = s->E.s64;
@@ -311,21 +448,43 @@ LZ77SSS_API int lz77sss_session_sss_range(lz77sss_session* s, uint64_t first, ui
     });
 }
 
+// 64-bit sync set: of the last sss_range call (32-bit session) or of the last sss /
+// factorize call (64-bit session)
+static void sss64_src(lz77sss_session* s, const uint64_t*& p, uint64_t& cnt) {
+    if (s->E64) {
+        p = s->E64->sss_ptr();
+        cnt = s->E64->sss_size();
+    } else {
+        p = s->E.S64.p;
+        cnt = s->E.s64;
+    }
+}
+
 LZ77SSS_API int lz77sss_session_get_sss64(lz77sss_session* s, uint64_t* out, uint64_t cap) {
-    if (!s || (!out && s->E.s64)) return LZ77SSS_EINVAL;
+    if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
-        if (cap < s->E.s64) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
-        if (s->E.s64) LZ_HIP(hipMemcpy(out, s->E.S64.p, s->E.s64 * 8, hipMemcpyDeviceToHost));
+        const uint64_t* p;
+        uint64_t cnt;
+        sss64_src(s, p, cnt);
+        if (!out && cnt) throw lz::error(LZ77SSS_EINVAL, "out is NULL");
+        if (cap < cnt) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (cnt) LZ_HIP(hipMemcpy(out, p, cnt * 8, hipMemcpyDeviceToHost));
     });
 }
 
 LZ77SSS_API int lz77sss_session_copy_sss64_device(lz77sss_session* s, void* dst, uint64_t cap) {
-    if (!s || (!dst && s->E.s64)) return LZ77SSS_EINVAL;
+    if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
-        if (cap < s->E.s64) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
-        LZ_HIP(hipSetDevice(s->E.device));
-        if (s->E.s64) LZ_HIP(hipMemcpyAsync(dst, s->E.S64.p, s->E.s64 * 8, hipMemcpyDeviceToDevice, s->E.st));
-        LZ_HIP(hipStreamSynchronize(s->E.st));
+        const uint64_t* p;
+        uint64_t cnt;
+        sss64_src(s, p, cnt);
+        if (!dst && cnt) throw lz::error(LZ77SSS_EINVAL, "dst is NULL");
+        if (cap < cnt) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        const int dev = s->E64 ? s->E64->device() : s->E.device;
+        hipStream_t st = s->E64 ? s->E64->stream() : s->E.st;
+        LZ_HIP(hipSetDevice(dev));
+        if (cnt) LZ_HIP(hipMemcpyAsync(dst, p, cnt * 8, hipMemcpyDeviceToDevice, st));
+        LZ_HIP(hipStreamSynchronize(st));
     });
 }
 
@@ -362,15 +521,19 @@ LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint6
                                            uint32_t seed, uint64_t offset) {
     if (!s || base_len == 0 || !(mut_rate >= 0.0 && mut_rate <= 1.0)) return LZ77SSS_EINVAL;
     return guarded([&] {
-        lz::engine& E = s->E;
-        if (n > E.max_n) throw lz::error(LZ77SSS_EINVAL, "text larger than the session capacity");
-        LZ_HIP(hipSetDevice(E.device));
-        E.n = n;
+        const int dev = s->E64 ? s->E64->device() : s->E.device;
+        const uint64_t cap = s->E64 ? s->E64->max_n() : s->E.max_n;
+        lz::u8* text = s->E64 ? s->E64->text() : s->E.d_text;
+        hipStream_t st = s->E64 ? s->E64->stream() : s->E.st;
+        if (n > cap) throw lz::error(LZ77SSS_EINVAL, "text larger than the session capacity");
+        LZ_HIP(hipSetDevice(dev));
+        if (s->E64) s->E64->set_n(n);
+        else s->E.n = n;
         const lz::u64 thr = mut_rate >= 1.0 ? ~0ull : (lz::u64)(mut_rate * 18446744073709551616.0);
-        if (n) k_gen_genome<<<(unsigned)((n + 4095) / 4096), 256, 0, E.st>>>(E.d_text, n, offset, base_len, thr, seed);
+        if (n) k_gen_genome<<<(unsigned)((n + 4095) / 4096), 256, 0, st>>>(text, n, offset, base_len, thr, seed);
         LZ_HIP(hipGetLastError());
-        LZ_HIP(hipMemsetAsync(E.d_text + n, 0, lz::TEXT_PAD, E.st));
-        LZ_HIP(hipStreamSynchronize(E.st));
+        LZ_HIP(hipMemsetAsync(text + n, 0, lz::TEXT_PAD, st));
+        LZ_HIP(hipStreamSynchronize(st));
     });
 }
 
@@ -378,6 +541,7 @@ LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint6
 LZ77SSS_API int lz77sss_session_huffman(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        need32(s, "huffman");
         lz::engine& E = s->E;
         if (E.last_fact_mode == LZ77SSS_SKIP_PHRASES)
             throw lz::error(LZ77SSS_EINVAL, "the Huffman container holds a factorization, not a skip_phrases stream");
@@ -395,6 +559,7 @@ LZ77SSS_API int lz77sss_session_huffman(lz77sss_session* s, uint8_t* out, uint64
 LZ77SSS_API int lz77sss_session_ssszip_gapped(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* size) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        need32(s, "ssszip_gapped");
         lz::engine& E = s->E;
         if (E.last_fact_mode != LZ77SSS_SKIP_PHRASES)
             throw lz::error(LZ77SSS_EINVAL, "ssszip_gapped needs a preceding factorize with fact_mode = skip_phrases");
@@ -411,6 +576,7 @@ LZ77SSS_API int lz77sss_session_ssszip_gapped(lz77sss_session* s, uint8_t* out, 
 LZ77SSS_API int lz77sss_session_get_sss(lz77sss_session* s, uint32_t* out, uint64_t cap) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        need32(s, "get_sss (32-bit positions)");
         if (cap < s->E.s) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
         if (s->E.s) LZ_HIP(hipMemcpy(out, s->E.S.p, (size_t)s->E.s * 4, hipMemcpyDeviceToHost));
     });
@@ -419,20 +585,41 @@ LZ77SSS_API int lz77sss_session_get_sss(lz77sss_session* s, uint32_t* out, uint6
 LZ77SSS_API int lz77sss_session_get_sa_s(lz77sss_session* s, uint32_t* sa, uint32_t* lcp, uint64_t cap) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
-        if (cap < s->E.s) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
-        if (!s->E.s) return;
-        if (sa) LZ_HIP(hipMemcpy(sa, s->E.SA.p, (size_t)s->E.s * 4, hipMemcpyDeviceToHost));
-        if (lcp) LZ_HIP(hipMemcpy(lcp, s->E.lcp_rmq[0].p, (size_t)s->E.s * 4, hipMemcpyDeviceToHost));
+        const uint64_t cnt = s->E64 ? s->E64->sss_size() : s->E.s;
+        if (cap < cnt) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (!cnt) return;
+        const uint32_t* psa = s->E64 ? s->E64->sa_ptr() : s->E.SA.p;
+        const uint32_t* plcp = s->E64 ? s->E64->lcp_ptr() : s->E.lcp_rmq[0].p;
+        if (sa) LZ_HIP(hipMemcpy(sa, psa, (size_t)cnt * 4, hipMemcpyDeviceToHost));
+        if (lcp) LZ_HIP(hipMemcpy(lcp, plcp, (size_t)cnt * 4, hipMemcpyDeviceToHost));
     });
 }
 
 LZ77SSS_API int lz77sss_session_get_lpf(lz77sss_session* s, uint32_t* out3, uint64_t cap, uint64_t* count) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
+        need32(s, "get_lpf (32-bit positions)");
         if (count) *count = s->E.num_phr;
         if (!out3) return;
         if (cap < s->E.num_phr) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
         if (s->E.num_phr) LZ_HIP(hipMemcpy(out3, s->E.lpf.p, (size_t)s->E.num_phr * 12, hipMemcpyDeviceToHost));
+    });
+}
+
+LZ77SSS_API int lz77sss_session_get_lpf64(lz77sss_session* s, uint64_t* out3, uint64_t cap, uint64_t* count) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        const uint64_t m = s->E64 ? s->E64->num_phr() : s->E.num_phr;
+        if (count) *count = m;
+        if (!out3 || !m) return;
+        if (cap < m) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        if (s->E64) {
+            LZ_HIP(hipMemcpy(out3, s->E64->lpf_ptr(), (size_t)m * 24, hipMemcpyDeviceToHost));
+        } else {
+            std::vector<uint32_t> tmp(3 * m);
+            LZ_HIP(hipMemcpy(tmp.data(), s->E.lpf.p, (size_t)m * 12, hipMemcpyDeviceToHost));
+            for (uint64_t k = 0; k < 3 * m; k++) out3[k] = tmp[k];
+        }
     });
 }
 
@@ -441,7 +628,7 @@ LZ77SSS_API int lz77sss_session_phase_times(lz77sss_session* s, double* ms, cons
     int k = 0;
     int rc = guarded([&] {
         static thread_local std::vector<std::string> keep;
-        auto v = s->E.timer.read();
+        auto v = s->E64 ? s->E64->timer().read() : s->E.timer.read();
         keep.clear();
         for (auto& x : v) keep.push_back(x.first);
         for (auto& x : v) {
@@ -456,41 +643,50 @@ LZ77SSS_API int lz77sss_session_phase_times(lz77sss_session* s, double* ms, cons
 
 LZ77SSS_API int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap) {
     if (!s || !out) return LZ77SSS_EINVAL;
+    const std::vector<uint64_t>& st = s->E64 ? s->E64->stats() : s->E.stats;
     int k = 0;
-    for (; k < cap && k < (int)s->E.stats.size(); k++) out[k] = s->E.stats[k];
+    for (; k < cap && k < (int)st.size(); k++) out[k] = st[k];
     return k;
 }
 
 LZ77SSS_API int lz77sss_session_sss_kernel_time(lz77sss_session* s, double* ms, uint64_t* bytes) {
     if (!s) return LZ77SSS_EINVAL;
-    if (ms) *ms = s->E.sss_kernel_ms;
-    if (bytes) *bytes = s->E.sss_kernel_bytes;
+    if (ms) *ms = s->E64 ? s->E64->sss_kernel_ms() : s->E.sss_kernel_ms;
+    if (bytes) *bytes = s->E64 ? s->E64->sss_kernel_bytes() : s->E.sss_kernel_bytes;
     return LZ77SSS_OK;
 }
 
 LZ77SSS_API void lz77sss_session_destroy(lz77sss_session* s) {
     if (!s) return;
+    s->E64.reset();
     s->E.destroy();
     delete s;
 }
 
-LZ77SSS_API int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
-                                             lz77sss_emit_fn emit, void* user) {
+}  // extern "C"
+// one-shot: upload, factorize, stream the factors to the callback in text order
+template <class FACT, class EMIT>
+static int one_shot(const uint8_t* text, uint64_t n, const lz77sss_params* prm, EMIT emit, void* user, bool wide,
+                    bool exact, int transf_mode) {
     if ((!text && n) || !emit) return LZ77SSS_EINVAL;
     lz77sss_session* s = nullptr;
-    int rc = guarded([&] { check_params(prm); });
+    int rc = guarded([&] {
+        if (exact) check_exact_params(prm, transf_mode);
+        else check_params(prm);
+    });
     if (rc) return rc;
-    rc = lz77sss_session_create(prm->device, n, &s);
+    rc = (wide && !exact) ? lz77sss_session_create64(prm->device, n, &s) : lz77sss_session_create(prm->device, n, &s);
     if (rc) return rc;
     rc = lz77sss_session_load(s, text, n);
     uint64_t z = 0;
-    if (!rc) rc = lz77sss_session_factorize(s, prm, &z);
+    if (!rc) rc = exact ? lz77sss_session_factorize_exact(s, prm, transf_mode, &z) : lz77sss_session_factorize(s, prm, &z);
     if (!rc && z) {
-        std::vector<lz77sss_factor32> buf;
-        rc = guarded([&] {
-            buf.resize(z);
-            LZ_HIP(hipMemcpy(buf.data(), s->E.fact.p, z * sizeof(lz77sss_factor32), hipMemcpyDeviceToHost));
-        });
+        std::vector<FACT> buf;
+        rc = guarded([&] { buf.resize(z); });
+        if (!rc) {
+            if constexpr (sizeof(FACT) == 16) rc = lz77sss_session_get_factors64(s, buf.data(), z);
+            else rc = lz77sss_session_get_factors(s, buf.data(), z);
+        }
         const uint64_t B = 1 << 16;
         for (uint64_t o = 0; !rc && o < z; o += B) {
             if (emit(buf.data() + o, std::min(B, z - o), user) != 0) {
@@ -503,33 +699,25 @@ LZ77SSS_API int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, co
     return rc;
 }
 
+extern "C" {
+LZ77SSS_API int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
+                                             lz77sss_emit_fn emit, void* user) {
+    return one_shot<lz77sss_factor32>(text, n, prm, emit, user, false, false, 0);
+}
+
+LZ77SSS_API int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
+                                             lz77sss_emit64_fn emit, void* user) {
+    return one_shot<lz77sss_factor64>(text, n, prm, emit, user, true, false, 0);
+}
+
 LZ77SSS_API int lz77sss_factorize_exact_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
                                             int transf_mode, lz77sss_emit_fn emit, void* user) {
-    if ((!text && n) || !emit) return LZ77SSS_EINVAL;
-    lz77sss_session* s = nullptr;
-    int rc = guarded([&] { check_exact_params(prm, transf_mode); });
-    if (rc) return rc;
-    rc = lz77sss_session_create(prm->device, n, &s);
-    if (rc) return rc;
-    rc = lz77sss_session_load(s, text, n);
-    uint64_t z = 0;
-    if (!rc) rc = lz77sss_session_factorize_exact(s, prm, transf_mode, &z);
-    if (!rc && z) {
-        std::vector<lz77sss_factor32> buf;
-        rc = guarded([&] {
-            buf.resize(z);
-            LZ_HIP(hipMemcpy(buf.data(), s->E.fact.p, z * sizeof(lz77sss_factor32), hipMemcpyDeviceToHost));
-        });
-        const uint64_t B = 1 << 16;
-        for (uint64_t o = 0; !rc && o < z; o += B) {
-            if (emit(buf.data() + o, std::min(B, z - o), user) != 0) {
-                g_err = "emit callback aborted";
-                rc = LZ77SSS_ECALLBACK;
-            }
-        }
-    }
-    lz77sss_session_destroy(s);
-    return rc;
+    return one_shot<lz77sss_factor32>(text, n, prm, emit, user, false, true, transf_mode);
+}
+
+LZ77SSS_API int lz77sss_factorize_exact_u64(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
+                                            int transf_mode, lz77sss_emit64_fn emit, void* user) {
+    return one_shot<lz77sss_factor64>(text, n, prm, emit, user, true, true, transf_mode);
 }
 
 // decode on a device: upload, pointer-jumping decode (csrc/decode.hip), download
@@ -552,20 +740,41 @@ LZ77SSS_API int lz77sss_decode_u32_device(const lz77sss_factor32* f, uint64_t nf
     return rc;
 }
 
+LZ77SSS_API int lz77sss_decode_u64_device(const lz77sss_factor64* f, uint64_t nf, uint8_t* out, uint64_t n,
+                                          int device) {
+    if ((!f && nf) || (!out && n)) return LZ77SSS_EINVAL;
+    lz77sss_session* s = nullptr;
+    int rc = lz77sss_session_create64(device, n, &s);
+    if (rc) return rc;
+    rc = guarded([&] {
+        lz::engine_if& E = *s->E64;
+        lz::u64* F = E.factors_buf(nf);
+        if (nf) LZ_HIP(hipMemcpyAsync(F, f, nf * sizeof(lz77sss_factor64), hipMemcpyHostToDevice, E.stream()));
+        lz::u8* d_out = n ? E.dec_out(n) : nullptr;
+        E.decode(F, nf, n, d_out, false);
+        if (n) LZ_HIP(hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, E.stream()));
+        LZ_HIP(hipStreamSynchronize(E.stream()));
+    });
+    lz77sss_session_destroy(s);
+    return rc;
+}
+
+}  // extern "C"
 // decode: algorithms/common.cpp:31-54 (sequential; forward byte copy allows overlap)
-LZ77SSS_API int lz77sss_decode_u32(const lz77sss_factor32* f, uint64_t nf, uint8_t* out, uint64_t n) {
+template <class FACT>
+static int host_decode(const FACT* f, uint64_t nf, uint8_t* out, uint64_t n) {
     if ((!f && nf) || (!out && n)) return LZ77SSS_EINVAL;
     uint64_t pos = 0, k = 0;
     while (pos < n && k < nf) {
-        const lz77sss_factor32 x = f[k++];
+        const FACT x = f[k++];
         if (x.len == 0) {
             out[pos++] = (uint8_t)x.src;
         } else {
-            if ((uint64_t)x.src >= pos || pos + x.len > n) {
+            if ((uint64_t)x.src >= pos || x.len > n - pos) {
                 g_err = "invalid factor during decode";
                 return LZ77SSS_EINVAL;
             }
-            for (uint32_t i = 0; i < x.len; i++) out[pos + i] = out[x.src + i];
+            for (uint64_t i = 0; i < x.len; i++) out[pos + i] = out[x.src + i];
             pos += x.len;
         }
     }
@@ -576,4 +785,14 @@ LZ77SSS_API int lz77sss_decode_u32(const lz77sss_factor32* f, uint64_t nf, uint8
     return LZ77SSS_OK;
 }
 
+extern "C" {
+LZ77SSS_API int lz77sss_decode_u32(const lz77sss_factor32* f, uint64_t nf, uint8_t* out, uint64_t n) {
+    return host_decode(f, nf, out, n);
+}
+
+LZ77SSS_API int lz77sss_decode_u64(const lz77sss_factor64* f, uint64_t nf, uint8_t* out, uint64_t n) {
+    return host_decode(f, nf, out, n);
+}
+
 }  // extern "C"
+#endif  // LZ_POS64

@@ -42,7 +42,7 @@
 #include <random>
 #include <unordered_map>
 
-namespace lz {
+namespace LZ_NS {
 
 // ---------------------------------------------------------------------------
 // 107-bit Mersenne arithmetic (rolling_hash.hpp relies on mersenne::mod, absent
@@ -72,7 +72,7 @@ static u128 powmod107_host(u128 b, u64 e) {
 }
 
 struct gap_cfg {
-    u32 n, nt;          // text length, start of the tail region
+    pos_t n, nt;        // text length, start of the tail region
     u32 lens[5];
     u64 base[5];
     u32 thr;            // roll_threshold
@@ -93,13 +93,13 @@ __device__ __forceinline__ u128 kr_direct(const u8* T, u64 q, u32 len, u64 b) {
 // ---------------------------------------------------------------------------
 // entries: e = 5*rank + (4 - x); entries of one position are generated in the
 // order of longest_prev_occ (x = 4 .. 0)
-struct ichunk { u32 q0, q1, rank0; };
+struct ichunk { pos_t q0, q1; u32 rank0; };
 
 // one thread per (chunk, x): the 5 fingerprint chains of a chunk run on 5 adjacent
 // lanes (5x the threads of a chunk-per-thread walk for latency hiding, and the 5
 // entries of a position are written by adjacent lanes)
 __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __restrict__ chunks, u32 nch,
-                        u32* __restrict__ keys, u32* __restrict__ vals, u32* __restrict__ ipos) {
+                        u32* __restrict__ keys, u32* __restrict__ vals, pos_t* __restrict__ ipos) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= 5ull * nch) return;
     const u64 c = g / 5;
@@ -109,7 +109,7 @@ __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __res
     const u64 b = G.base[x];
     const u128* np = G.negpow + x * 256;
     u128 fp = kr_direct(T, ch.q0, len, b);
-    for (u32 q = ch.q0; q < ch.q1; q++) {
+    for (pos_t q = ch.q0; q < ch.q1; q++) {
         const u32 rank = ch.rank0 + (q - ch.q0);
         if (ipos && x == 4) ipos[rank] = q;
         const u32 e = 5 * rank + (4 - x);
@@ -254,11 +254,14 @@ __global__ void k_pred_sorted(const u32* __restrict__ skeys, const u32* __restri
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < m) pv[t] = (t > 0 && skeys[t - 1] == skeys[t]) ? svals[t - 1] : NONE;
 }
-// added entries -> 64-bit keys (slot << 35 | pos << 3 | order)
-__global__ void k_pack_added(const u32* __restrict__ keys, const u32* __restrict__ ipos, u64 m, u64* __restrict__ out) {
+// added entries -> 64-bit keys (slot << 35 | x << 3 | order); x = the position for
+// pos_t = uint32_t, the entry's rank in its (position-ordered) list for pos_t = uint64_t
+// (ranks are monotone in position, so the key order is the same)
+__global__ void k_pack_added(const u32* __restrict__ keys, const pos_t* __restrict__ ipos, u64 m, u64* __restrict__ out) {
     const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
-    out[e] = ((u64)keys[e] << 35) | ((u64)ipos[e / 5] << 3) | (e % 5);
+    const u64 x = sizeof(pos_t) == 4 ? (u64)ipos[e / 5] : e / 5;
+    out[e] = ((u64)keys[e] << 35) | (x << 3) | (e % 5);
 }
 __global__ void k_set_rem(u8* __restrict__ rem, const u32* __restrict__ ranks, u64 m, u8 v) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -269,17 +272,17 @@ __global__ void k_set_rem(u8* __restrict__ rem, const u32* __restrict__ ranks, u
 struct walk_ctx {
     const u8* T;
     gap_cfg G;
-    const u32* P;        // phrases (beg,end,src) + sentinel
+    const pos_t* P;      // phrases (beg,end,src) + sentinel
     // base set
-    const u32* istart;   // interval starts (sorted)
-    const u32* iend;     // interval ends (exclusive)
+    const pos_t* istart; // interval starts (sorted)
+    const pos_t* iend;   // interval ends (exclusive)
     const u32* irank;    // rank of istart
     u32 nint;
     const u32* keys;     // slot of entry e (position order)
     const u32* skeys;    // sorted slots
     const u32* svals;    // entry ids in sorted order
     const u32* pred5;    // predecessor entry in the same slot
-    const u32* ipos;     // rank -> position
+    const pos_t* ipos;   // rank -> position
     u64 nentries;
     const u32* bstart;   // slot -> first sorted base entry (nslots + 1)
     // delta
@@ -287,16 +290,20 @@ struct walk_ctx {
     const u64* akeys;    // sorted added keys (main list)
     u64 nadd;
     const u32* abeg;     // slot -> first added key (nslots + 1)
+    const pos_t* apos;   // positions of the main list (rank -> position, pos_t = uint64_t keys)
+    u64 napos;
     const u64* akeys2;   // sorted added keys (extra list, positions joined after the main build)
     u64 nadd2;
     const u32* abeg2;
+    const pos_t* apos2;
+    u64 napos2;
     const u32* bmI;      // current insert set (membership of added positions)
     int use_pred;        // base lookups via pred5 (else bucket search)
     lce_view L;
 };
 
-__device__ __forceinline__ u32 base_rank(const walk_ctx& W, u32 q, int& hint) {
-    if (hint >= 0 && q >= W.istart[hint] && q < W.iend[hint]) return W.irank[hint] + (q - W.istart[hint]);
+__device__ __forceinline__ u32 base_rank(const walk_ctx& W, pos_t q, int& hint) {
+    if (hint >= 0 && q >= W.istart[hint] && q < W.iend[hint]) return W.irank[hint] + (u32)(q - W.istart[hint]);
     u32 lo = 0, hi = W.nint;
     while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
@@ -306,38 +313,59 @@ __device__ __forceinline__ u32 base_rank(const walk_ctx& W, u32 q, int& hint) {
     const u32 k = lo - 1;
     if (q >= W.iend[k]) return NONE;
     hint = (int)k;
-    return W.irank[k] + (q - W.istart[k]);
+    return W.irank[k] + (u32)(q - W.istart[k]);
 }
-__device__ __forceinline__ u32 occ_max(u32 a, u32 b) {
-    if (a == NONE) return b;
-    if (b == NONE) return a;
+__device__ __forceinline__ pos_t occ_max(pos_t a, pos_t b) {
+    if (a == POS_NONE) return b;
+    if (b == POS_NONE) return a;
     return max(a, b);
 }
-__device__ __forceinline__ u32 occ_min(u32 a, u32 b) {
-    if (a == NONE) return b;
-    if (b == NONE) return a;
+__device__ __forceinline__ pos_t occ_min(pos_t a, pos_t b) {
+    if (a == POS_NONE) return b;
+    if (b == POS_NONE) return a;
     return min(a, b);
 }
 // last base entry strictly before (slot, q, ord) in processing order, skipping removed
-__device__ u32 base_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
+__device__ pos_t base_last_before(const walk_ctx& W, u32 slot, pos_t q, u32 ord) {
     const u64 beg = W.bstart[slot], end = W.bstart[slot + 1];
     // within [beg, end) entries are in (position, order) order: first >= (q, ord)
     u64 lo = beg, hi = end;
     while (lo < hi) {
         const u64 mid = (lo + hi) >> 1;
         const u32 e = W.svals[mid];
-        const u32 pq = W.ipos[e / 5], po = e % 5;
+        const pos_t pq = W.ipos[e / 5];
+        const u32 po = e % 5;
         if (pq < q || (pq == q && po < ord)) lo = mid + 1; else hi = mid;
     }
     for (u64 t = lo; t > beg; t--) {
         const u32 rk = W.svals[t - 1] / 5;
         if (!W.rem[rk] || W.ipos[rk] == q) return W.ipos[rk];
     }
-    return NONE;
+    return POS_NONE;
 }
-__device__ __forceinline__ bool in_I(const walk_ctx& W, u32 q) { return (W.bmI[q >> 5] >> (q & 31)) & 1; }
-__device__ u32 added_last_before_1(const walk_ctx& W, const u64* ak, const u32* ab, u32 slot, u32 q, u32 ord) {
-    const u64 key = ((u64)slot << 35) | ((u64)q << 3) | ord;
+__device__ __forceinline__ bool in_I(const walk_ctx& W, pos_t q) { return (W.bmI[q >> 5] >> (q & 31)) & 1; }
+// key field of position q in an added list: q itself (u32) or the number of list
+// positions below q (u64; first_ge) / at or below q (!first_ge)
+__device__ __forceinline__ u64 added_x(const pos_t* apos, u64 na, pos_t q, bool first_ge) {
+    if (sizeof(pos_t) == 4) return (u64)q + (first_ge ? 0 : 1);
+    u64 lo = 0, hi = na;
+    while (lo < hi) {
+        const u64 mid = (lo + hi) >> 1;
+        if (first_ge ? apos[mid] < q : apos[mid] <= q) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ pos_t added_pos(const pos_t* apos, u64 key) {
+    const u64 x = (key >> 3) & 0xFFFFFFFFull;
+    return sizeof(pos_t) == 4 ? (pos_t)x : apos[x];
+}
+__device__ pos_t added_last_before_1(const walk_ctx& W, const u64* ak, const u32* ab, const pos_t* apos, u64 na,
+                                     u32 slot, pos_t q, u32 ord) {
+    // rank keys (pos_t = uint64_t): when q is not in the list, the entries of rank
+    // lower_bound(q) lie after q whatever their order, so the search key takes order 0
+    const u64 x = added_x(apos, na, q, true);
+    const u32 o = (sizeof(pos_t) == 4 || (x < na && apos[x] == q)) ? ord : 0u;
+    const u64 key = ((u64)slot << 35) | (x << 3) | o;
     u64 lo = ab[slot], hi = ab[slot + 1];  // first >= key
     const u64 beg = lo;
     while (lo < hi) {
@@ -345,29 +373,30 @@ __device__ u32 added_last_before_1(const walk_ctx& W, const u64* ak, const u32* 
         if (ak[mid] < key) lo = mid + 1; else hi = mid;
     }
     for (u64 t = lo; t > beg; t--) {
-        const u32 pq = (u32)((ak[t - 1] >> 3) & 0xFFFFFFFFull);
+        const pos_t pq = added_pos(apos, ak[t - 1]);
         if (pq == q || in_I(W, pq)) return pq;
     }
-    return NONE;
+    return POS_NONE;
 }
-__device__ u32 added_last_before(const walk_ctx& W, u32 slot, u32 q, u32 ord) {
-    u32 r = NONE;
-    if (W.nadd) r = added_last_before_1(W, W.akeys, W.abeg, slot, q, ord);
-    if (W.nadd2) r = occ_max(r, added_last_before_1(W, W.akeys2, W.abeg2, slot, q, ord));
+__device__ pos_t added_last_before(const walk_ctx& W, u32 slot, pos_t q, u32 ord) {
+    pos_t r = POS_NONE;
+    if (W.nadd) r = added_last_before_1(W, W.akeys, W.abeg, W.apos, W.napos, slot, q, ord);
+    if (W.nadd2) r = occ_max(r, added_last_before_1(W, W.akeys2, W.abeg2, W.apos2, W.napos2, slot, q, ord));
     return r;
 }
 // H[slot of (q,x)] just before longest_prev_occ's advance_and_get_occ<x> at q
-__device__ u32 lookup(const walk_ctx& W, u32 q, int x, int& hint) {
+__device__ pos_t lookup(const walk_ctx& W, pos_t q, int x, int& hint) {
     const u32 ord = 4 - x;
     const u32 rk = base_rank(W, q, hint);
-    u32 slot, cb;
+    u32 slot;
+    pos_t cb;
     if (rk != NONE) {
         const u32 e = 5 * rk + ord;
         slot = W.keys[e];
         if (W.use_pred) {
             u32 p = W.pred5[e];
             while (p != NONE && W.rem[p / 5] && W.ipos[p / 5] != q) p = W.pred5[p];
-            cb = p == NONE ? NONE : W.ipos[p / 5];
+            cb = p == NONE ? POS_NONE : W.ipos[p / 5];
         } else {
             // entries of a bucket are in ascending entry order: locate e, then walk back
             const u64 beg = W.bstart[slot];
@@ -376,7 +405,7 @@ __device__ u32 lookup(const walk_ctx& W, u32 q, int x, int& hint) {
                 const u64 mid = (lo + hi) >> 1;
                 if (W.svals[mid] < e) lo = mid + 1; else hi = mid;
             }
-            cb = NONE;
+            cb = POS_NONE;
             for (u64 t = lo; t > beg; t--) {
                 const u32 r2 = W.svals[t - 1] / 5;
                 if (!W.rem[r2] || W.ipos[r2] == q) { cb = W.ipos[r2]; break; }
@@ -392,14 +421,15 @@ __device__ u32 lookup(const walk_ctx& W, u32 q, int x, int& hint) {
 // ---------------------------------------------------------------------------
 // walks
 template <bool WRITE>
-__device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__ og, u32* fout) {
+__device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__ og, pos_t* fout) {
     // outputs go straight to the table entry og (the bnd/single lists are indexed
     // dynamically: a local copy of seg_out would live in scratch memory)
     const u8* T = W.T;
-    const u32 n = W.G.n, nt = W.G.nt;
-    const u32* P = W.P;
-    u32 i = in.start, p = in.p, idx = in.idxpos, zm = in.zmask;
-    u32 nf = 0, ns = 0, flags = 0, e = in.start, nb = 0, next = n;
+    const pos_t n = W.G.n, nt = W.G.nt;
+    const pos_t* P = W.P;
+    pos_t i = in.start, idx = in.idxpos, e = in.start, next = n;
+    u32 p = in.p, zm = in.zmask;
+    u32 nf = 0, ns = 0, flags = 0, nb = 0;
     bool first_gap = true;
     int hint = -1;
     u64 guard = 0;
@@ -415,24 +445,24 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__
         og->flags = flags;
         og->nbnd = nb;
     };
-    auto emit = [&](u32 src, u32 len) {
+    auto emit = [&](pos_t src, pos_t len) {
         if (WRITE) { fout[2 * nf] = src; fout[2 * nf + 1] = len; }
         nf++;
     };
-    auto query = [&](u32 q, u32& fsrc, u32& flen) {
+    auto query = [&](pos_t q, pos_t& fsrc, pos_t& flen) {
         fsrc = T[q];
         flen = 0;
         for (int x = 4; x >= 0; x--) {
-            const u32 occ = lookup(W, q, x, hint);
-            if (occ != NONE && occ < q && T[occ] == T[q]) {
-                flen = (u32)dev_lce(W.L, occ, q);
+            const pos_t occ = lookup(W, q, x, hint);
+            if (occ != POS_NONE && occ < q && T[occ] == T[q]) {
+                flen = (pos_t)dev_lce(W.L, occ, q);
                 fsrc = occ;
                 return;
             }
         }
     };
     for (;;) {
-        u32 gap_end = P[3 * p];
+        pos_t gap_end = P[3 * p];
         if (i < gap_end) {
             if (idx < i) {
                 if (i - idx > W.G.thr) {  // reinit (matters only in the tail region)
@@ -451,7 +481,7 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__
                 if (i >= nt) { flags |= 1; finish(); return; }
                 if (++guard > guard_max || i > n) { flags |= 4; finish(); return; }
                 if (!WRITE && first_gap && nb < SEG_NBND) og->bnd[nb++] = i;
-                u32 fsrc, flen;
+                pos_t fsrc, flen;
                 query(i, fsrc, flen);
                 idx = i + 1;
                 i += flen ? flen : 1;
@@ -471,11 +501,11 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__
         }
         first_gap = false;
         if (i == n) break;
-        const u32 exc = i - gap_end;
-        u32 lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
+        const pos_t exc = i - gap_end;
+        pos_t lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
         if (idx == i) {
             if (i >= nt) { flags |= 1; finish(); return; }
-            u32 fsrc, flen;
+            pos_t fsrc, flen;
             query(i, fsrc, flen);
             idx = i + 1;
             if (ns < 4) { if (!WRITE) og->single[ns] = i; } else flags |= 2;
@@ -493,14 +523,14 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__
 
 // successor insert (next position of the same slot after y) in the current set:
 // the only query whose lookup can change when y joins or leaves I
-__global__ void k_dirty(walk_ctx W, const u32* __restrict__ ys, u64 m, u32* __restrict__ out) {
+__global__ void k_dirty(walk_ctx W, const pos_t* __restrict__ ys, u64 m, pos_t* __restrict__ out) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
-    const u32 y = ys[k];
+    const pos_t y = ys[k];
 #pragma unroll 1
     for (int x = 0; x < 5; x++) {
         const u32 slot = (u32)((u64)kr_direct(W.T, y, W.G.lens[x], W.G.base[x]) & W.G.mask);
-        u32 best = NONE;
+        pos_t best = POS_NONE;
         const u64 bend = W.bstart[slot + 1];
         u64 lo = W.bstart[slot], hi = bend;  // first entry after (slot, y)
         while (lo < hi) {
@@ -514,8 +544,9 @@ __global__ void k_dirty(walk_ctx W, const u32* __restrict__ ys, u64 m, u32* __re
         for (int li = 0; li < 2; li++) {
             const u64* ak = li ? W.akeys2 : W.akeys;
             const u32* ab = li ? W.abeg2 : W.abeg;
+            const pos_t* ap = li ? W.apos2 : W.apos;
             if (!(li ? W.nadd2 : W.nadd)) continue;
-            const u64 key = ((u64)slot << 35) | ((u64)(y + 1) << 3);
+            const u64 key = ((u64)slot << 35) | (added_x(ap, li ? W.napos2 : W.napos, y, false) << 3);
             u64 a = ab[slot], b = ab[slot + 1];
             const u64 aend = b;
             while (a < b) {
@@ -523,7 +554,7 @@ __global__ void k_dirty(walk_ctx W, const u32* __restrict__ ys, u64 m, u32* __re
                 if (ak[mid] < key) a = mid + 1; else b = mid;
             }
             for (; a < aend; a++) {
-                const u32 pq = (u32)((ak[a] >> 3) & 0xFFFFFFFFull);
+                const pos_t pq = added_pos(ap, ak[a]);
                 if (in_I(W, pq)) { best = occ_min(best, pq); break; }
             }
         }
@@ -533,7 +564,7 @@ __global__ void k_dirty(walk_ctx W, const u32* __restrict__ ys, u64 m, u32* __re
 
 // incremental delta: y joined (flag 1) or left (flag 0) I; base positions flip
 // their removed bit, others are reported as additions to maintain on the host
-__global__ void k_flip(walk_ctx W, const u32* __restrict__ ys, const u8* __restrict__ joined, u64 m,
+__global__ void k_flip(walk_ctx W, const pos_t* __restrict__ ys, const u8* __restrict__ joined, u64 m,
                        u8* __restrict__ rem, u8* __restrict__ in_base) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
@@ -545,55 +576,56 @@ __global__ void k_flip(walk_ctx W, const u32* __restrict__ ys, const u8* __restr
 // ---------------------------------------------------------------------------
 // exact single-thread walk from a segment start to the end of the text, with
 // a local model of the inserts in the tail region (last 64 positions)
-struct tail_ins { u32 slot, pos; };
+struct tail_ins { u32 slot; pos_t pos; };
 constexpr int TAIL_CAP = 64 * 5 + 8;
 
-__global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u64* __restrict__ count_out,
-                       u32* __restrict__ ins_out /* [a, b) pairs below the tail region, cap 8 */) {
+__global__ void k_tail(walk_ctx W, seg_in in, pos_t* __restrict__ fact, u64 off, u64* __restrict__ count_out,
+                       pos_t* __restrict__ ins_out /* [a, b) pairs below the tail region, cap 8 */) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const u8* T = W.T;
-    const u32 n = W.G.n, nt = W.G.nt;
-    const u32* P = W.P;
+    const pos_t n = W.G.n, nt = W.G.nt;
+    const pos_t* P = W.P;
     tail_ins loc[TAIL_CAP];
     int nloc = 0;
-    u32 i = in.start, p = in.p, idx = in.idxpos, zm = in.zmask;
+    pos_t i = in.start, idx = in.idxpos;
+    u32 p = in.p, zm = in.zmask;
     u64 nf = 0;
     int hint = -1;
     u32 nins = 0;
-    auto fp_slot = [&](u32 q, int x) -> u32 {
+    auto fp_slot = [&](pos_t q, int x) -> u32 {
         const u32 len = W.G.lens[x];
         if ((zm >> x & 1) || (u64)len > n) return 0;
         const u64 qq = ((u64)q + len <= n) ? q : n - len;
         return (u32)((u64)kr_direct(T, qq, len, W.G.base[x]) & W.G.mask);
     };
-    auto tail_lookup = [&](u32 slot) -> u32 {
+    auto tail_lookup = [&](u32 slot) -> pos_t {
         for (int k = nloc - 1; k >= 0; k--)
             if (loc[k].slot == slot) return loc[k].pos;
         // every base / added entry lies below nt
         return occ_max(base_last_before(W, slot, nt, 0), added_last_before(W, slot, nt, 0));
     };
-    auto insert = [&](u32 q, u32 slot) {
+    auto insert = [&](pos_t q, u32 slot) {
         if (nloc < TAIL_CAP) loc[nloc++] = {slot, q};
     };
-    auto query = [&](u32 q, u32& fsrc, u32& flen) {
+    auto query = [&](pos_t q, pos_t& fsrc, pos_t& flen) {
         fsrc = T[q];
         flen = 0;
         bool hit = false;
         for (int x = 4; x >= 0; x--) {
             if (q < nt) {
                 if (hit) continue;
-                const u32 occ = lookup(W, q, x, hint);
-                if (occ != NONE && occ < q && T[occ] == T[q]) {
-                    flen = (u32)dev_lce(W.L, occ, q);
+                const pos_t occ = lookup(W, q, x, hint);
+                if (occ != POS_NONE && occ < q && T[occ] == T[q]) {
+                    flen = (pos_t)dev_lce(W.L, occ, q);
                     fsrc = occ;
                     hit = true;
                 }
             } else if (!hit) {
                 const u32 slot = fp_slot(q, x);
-                const u32 occ = tail_lookup(slot);
+                const pos_t occ = tail_lookup(slot);
                 insert(q, slot);  // advance_and_get_occ always inserts
-                if (occ != NONE && occ < q && T[occ] == T[q]) {
-                    flen = (u32)dev_lce(W.L, occ, q);
+                if (occ != POS_NONE && occ < q && T[occ] == T[q]) {
+                    flen = (pos_t)dev_lce(W.L, occ, q);
                     fsrc = occ;
                     hit = true;
                 }
@@ -602,18 +634,18 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
             }
         }
     };
-    auto advance_to = [&](u32 target) {
+    auto advance_to = [&](pos_t target) {
         for (; idx < target; idx++)
             if (idx >= nt)
                 for (int x = 0; x < 5; x++)
                     if ((u64)idx + W.G.lens[x] < n) insert(idx, fp_slot(idx, x));
     };
-    auto emit = [&](u32 src, u32 len) {
+    auto emit = [&](pos_t src, pos_t len) {
         fact[2 * (off + nf)] = src;
         fact[2 * (off + nf) + 1] = len;
         nf++;
     };
-    auto record = [&](u32 a, u32 b) {
+    auto record = [&](pos_t a, pos_t b) {
         b = min(b, nt);
         if (a >= b) return;
         if (nins > 0 && ins_out[2 * (nins - 1) + 1] >= a) {
@@ -627,7 +659,7 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
     u64 guard = 0;
     for (;;) {
         if (++guard > 4ull * n + 1024 || i > n) { count_out[2] = 2; break; }
-        u32 gap_end = P[3 * p];
+        pos_t gap_end = P[3 * p];
         if (i < gap_end) {
             if (idx < i) {
                 if (i - idx > W.G.thr) {
@@ -636,9 +668,9 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
                 }
                 idx = i;  // roll: fingerprints advance, nothing inserted
             }
-            const u32 walk_start = i;
+            const pos_t walk_start = i;
             do {
-                u32 fsrc, flen;
+                pos_t fsrc, flen;
                 query(i, fsrc, flen);
                 idx = i + 1;
                 i += flen ? flen : 1;
@@ -658,10 +690,10 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
             record(walk_start, i);
         }
         if (i == n) break;
-        const u32 exc = i - gap_end;
-        u32 lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
+        const pos_t exc = i - gap_end;
+        pos_t lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
         if (idx == i) {
-            u32 fsrc, flen;
+            pos_t fsrc, flen;
             query(i, fsrc, flen);
             idx = i + 1;
             record(i, i + 1);
@@ -685,29 +717,33 @@ __global__ void k_tail(walk_ctx W, seg_in in, u32* __restrict__ fact, u64 off, u
 // exact) with H holding the last insert per slot below that state, so its output
 // continues the confirmed prefix.  Used when the speculation does not reach its
 // fixed point within the round budget, or a walk reports an internal overflow.
-__global__ void k_h_fill(const u8* __restrict__ T, gap_cfg G, const u32* __restrict__ bm, u32 y, u32* __restrict__ H) {
+__device__ __forceinline__ void atomic_max_pos(pos_t* a, pos_t v) {
+    if constexpr (sizeof(pos_t) == 4) atomicMax((u32*)a, (u32)v);
+    else atomicMax((unsigned long long*)a, (unsigned long long)v);
+}
+__global__ void k_h_fill(const u8* __restrict__ T, gap_cfg G, const u32* __restrict__ bm, pos_t y, pos_t* __restrict__ H) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (w * 32 >= y) return;
     u32 bits = bm[w];
     while (bits) {
-        const u32 q = (u32)(32 * w) + (u32)__builtin_ctz(bits);
+        const pos_t q = (pos_t)(32 * w) + (pos_t)__builtin_ctz(bits);
         bits &= bits - 1;
         if (q >= y) break;
         // confirmed inserts lie below the tail region: all 5 fingerprints are full windows
         for (int x = 0; x < 5; x++)
-            atomicMax(&H[(u32)((u64)kr_direct(T, q, G.lens[x], G.base[x]) & G.mask)], q + 1);
+            atomic_max_pos(&H[(u32)((u64)kr_direct(T, q, G.lens[x], G.base[x]) & G.mask)], q + 1);
     }
 }
-__global__ void k_h_fix(u32* __restrict__ H, u64 m) {
+__global__ void k_h_fix(pos_t* __restrict__ H, u64 m) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < m) H[k] = H[k] ? H[k] - 1 : NONE;
+    if (k < m) H[k] = H[k] ? H[k] - 1 : POS_NONE;
 }
-__global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __restrict__ P, lce_view L,
-                           u32* __restrict__ H, seg_in in, u32* __restrict__ fact, u64 off, u64* __restrict__ out) {
+__global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __restrict__ P, lce_view L,
+                           pos_t* __restrict__ H, seg_in in, pos_t* __restrict__ fact, u64 off, u64* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const u32 n = G.n;
+    const pos_t n = G.n;
     u128 fp[5];
-    u32 cur = in.idxpos;
+    pos_t cur = in.idxpos;
     for (int x = 0; x < 5; x++) {  // fingerprint state at cur
         const u32 len = G.lens[x];
         if (((in.zmask >> x) & 1) || len > n) fp[x] = 0;
@@ -721,7 +757,7 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __res
         for (int x = 0; x < 5; x++) roll1(x);
         cur++;
     };
-    auto reinit = [&](u32 pos) {
+    auto reinit = [&](pos_t pos) {
         cur = pos;
         for (int x = 0; x < 5; x++) fp[x] = ((u64)pos + G.lens[x] < n) ? kr_direct(T, pos, G.lens[x], G.base[x]) : 0;
     };
@@ -733,16 +769,17 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __res
             }
         cur++;
     };
-    auto longest_prev_occ = [&](u32 pos, u32& fsrc, u32& flen) {
+    auto longest_prev_occ = [&](pos_t pos, pos_t& fsrc, pos_t& flen) {
         fsrc = T[pos];
         flen = 0;
         for (int x = 4; x >= 0; x--) {
             if (flen == 0) {  // advance_and_get_occ<x>: always inserts
-                const u32 sl = slot_of(x), occ = H[sl];
+                const u32 sl = slot_of(x);
+                const pos_t occ = H[sl];
                 H[sl] = cur;
                 roll1(x);
                 if (occ < pos && T[occ] == T[pos]) {
-                    flen = (u32)dev_lce(L, occ, pos);
+                    flen = (pos_t)dev_lce(L, occ, pos);
                     fsrc = occ;
                 }
             } else if ((u64)cur + G.lens[x] < n) {  // advance<x>
@@ -753,16 +790,17 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __res
         cur++;
     };
     u64 nf = 0, guard = 0;
-    auto emit = [&](u32 src, u32 len) {
+    auto emit = [&](pos_t src, pos_t len) {
         fact[2 * (off + nf)] = src;
         fact[2 * (off + nf) + 1] = len;
         nf++;
     };
-    u32 i = in.start, p = in.p;
+    pos_t i = in.start;
+    u32 p = in.p;
     out[1] = 0;
     for (;;) {
         if (++guard > 4ull * n + 1024 || i > n) { out[1] = 1; break; }
-        u32 gap_end = P[3 * p];
+        pos_t gap_end = P[3 * p];
         if (i < gap_end) {
             if (cur < i) {
                 if (i - cur <= G.thr) {
@@ -772,7 +810,7 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __res
                 }
             }
             do {
-                u32 fsrc, flen;
+                pos_t fsrc, flen;
                 longest_prev_occ(i, fsrc, flen);
                 i += flen ? flen : 1;
                 if (i > gap_end) {
@@ -790,10 +828,10 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __res
             } while (i < gap_end);
         }
         if (i == n) break;
-        const u32 exc = i - gap_end;
-        u32 lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
+        const pos_t exc = i - gap_end;
+        pos_t lsrc = P[3 * p + 2] + exc, llen = (P[3 * p + 1] - P[3 * p]) - exc;
         if (cur == i) {
-            u32 fsrc, flen;
+            pos_t fsrc, flen;
             longest_prev_occ(i, fsrc, flen);
             if (flen > llen) { lsrc = fsrc; llen = flen; }
         }
@@ -803,25 +841,25 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const u32* __res
     }
     out[0] = nf;
 }
-// first set bit of a bitmap (NONE if none), one atomic per workgroup
-__global__ void k_first_bit(const u32* __restrict__ bm, u64 nw, u32* __restrict__ out) {
+// first set bit of a bitmap (~0 if none), one atomic per workgroup
+__global__ void k_first_bit(const u32* __restrict__ bm, u64 nw, u64* __restrict__ out) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    const u32 v = (w < nw && bm[w]) ? (u32)(32 * w) + (u32)__builtin_ctz(bm[w]) : NONE;
-    block_min(out, v);
+    const u64 v = (w < nw && bm[w]) ? 32 * w + (u64)__builtin_ctz(bm[w]) : ~0ull;
+    block_min64(out, v);
 }
 
 // phrase statistics (approximate/common.cpp:98-157, p = 1)
-__global__ void k_phrase_info(const u32* __restrict__ P, u32 m, u32 n, u32* __restrict__ acc) {
+__global__ void k_phrase_info(const pos_t* __restrict__ P, u32 m, pos_t n, u64* __restrict__ acc) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    u32 len = 0, gaps = 0;
+    u64 len = 0, gaps = 0;
     if (k < m) {
-        const u32 b = P[3 * k], e = P[3 * k + 1];
+        const pos_t b = P[3 * k], e = P[3 * k + 1];
         len = e - b;
         if (k == 0 ? b > 0 : b > P[3 * (k - 1) + 1]) gaps++;
         if (k == m - 1 && e < n) gaps++;
     }
-    block_add(&acc[0], len);
-    block_add(&acc[1], gaps);
+    block_add64(&acc[0], len);
+    block_add64(&acc[1], gaps);
 }
 
 // ---------------------------------------------------------------------------
@@ -832,16 +870,16 @@ struct gap_params_h {
     u32 log2_size_h = 0;
 };
 
-// lz77_sss.hpp:99-122, 425-461 and rolling_hash_index_107.hpp:59-70 (pos_t =
-// uint32_t, malloc_count_peak() - malloc_count_current() == 0)
-static gap_params_h choose_gap_params(u32 n, u32 num_lpf, u32 len_lpf_phr, u32 num_gaps) {
+// lz77_sss.hpp:99-122, 425-461 and rolling_hash_index_107.hpp:59-70 (the entry
+// counts depend on sizeof(pos_t); malloc_count_peak() - malloc_count_current() == 0)
+static gap_params_h choose_gap_params(pos_t n, u64 num_lpf, pos_t len_lpf_phr, u64 num_gaps) {
     static const std::array<std::pair<double, std::array<u32, 5>>, 10> table{{
         {6, {2, 3, 4, 5, 6}}, {8, {2, 3, 4, 6, 8}}, {12, {2, 3, 4, 8, 12}}, {16, {2, 4, 6, 9, 16}},
         {32, {2, 4, 6, 10, 20}}, {64, {2, 4, 7, 12, 28}}, {128, {2, 4, 8, 16, 36}},
         {256, {2, 5, 10, 20, 42}}, {1024, {2, 6, 12, 24, 48}},
         {std::numeric_limits<double>::max(), {2, 8, 16, 32, 64}}}};
     gap_params_h g;
-    const u32 len_gaps = n - len_lpf_phr;
+    const pos_t len_gaps = n - len_lpf_phr;
     const double rel_len_gaps = len_gaps / (double)n;
     const double avg_gap_len = len_gaps / (double)num_gaps;
     const double avg_lpf_phr_len = len_lpf_phr / (double)num_lpf;
@@ -853,9 +891,9 @@ static gap_params_h choose_gap_params(u32 n, u32 num_lpf, u32 len_lpf_phr, u32 n
     for (int j = 0; j < 5; j++) rt += g.patt_lens[j];
     g.roll_threshold = rt / 5;
     const int64_t rk_bytes = (int64_t)(80 + 16 * 256 * 256) * 5;  // rk_prime<107>::byte_size() * 5
-    const int64_t min_index_size = std::max<u32>(1u << 20, (u32)(n * 0.1)) / sizeof(u32);
-    const int64_t max_index_size = (1ll << 30) / (int64_t)sizeof(u32);
-    const int64_t target_entries = std::max<int64_t>(0, (int64_t)target - rk_bytes) / (int64_t)sizeof(u32);
+    const int64_t min_index_size = (int64_t)(std::max<pos_t>(1u << 20, (pos_t)(n * 0.1)) / sizeof(pos_t));
+    const int64_t max_index_size = (1ll << 30) / (int64_t)sizeof(pos_t);
+    const int64_t target_entries = std::max<int64_t>(0, (int64_t)target - rk_bytes) / (int64_t)sizeof(pos_t);
     const uint64_t target_size_h = std::min<int64_t>(max_index_size, std::max<int64_t>(min_index_size, target_entries));
     g.log2_size_h = (u8)std::round(std::log2(target_size_h));
     return g;
@@ -873,15 +911,16 @@ struct seg_tab {
     u32* seg_at;     // text position -> segment id (NONE / PENDING)
     u32* nseg;       // device counter
     u32 cap;
-    const u32* cbv;  // chunk boundaries (sorted)
+    const pos_t* cbv;  // chunk boundaries (sorted)
     u32 ncb;
-    const u32* P;    // phrases (beg, end, src) + sentinel
+    const pos_t* P;  // phrases (beg, end, src) + sentinel
     u32 m;
-    u32 N, zmask0;
+    pos_t N;
+    u32 zmask0;
     u32* err;        // bit 1: table full, 2: too many LPF-start queries, 4: walk guard
 };
 
-__device__ __forceinline__ u32 first_phrase_after(const u32* P, u32 m, u32 a) {  // smallest k: end_k > a
+__device__ __forceinline__ u32 first_phrase_after(const pos_t* P, u32 m, pos_t a) {  // smallest k: end_k > a
     u32 lo = 0, hi = m;
     while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
@@ -889,7 +928,7 @@ __device__ __forceinline__ u32 first_phrase_after(const u32* P, u32 m, u32 a) { 
     }
     return lo;
 }
-__device__ __forceinline__ u32 upper_cb(const seg_tab& S, u32 a) {  // first chunk boundary > a (N if none)
+__device__ __forceinline__ pos_t upper_cb(const seg_tab& S, pos_t a) {  // first chunk boundary > a (N if none)
     u32 lo = 0, hi = S.ncb;
     while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
@@ -897,47 +936,48 @@ __device__ __forceinline__ u32 upper_cb(const seg_tab& S, u32 a) {  // first chu
     }
     return lo < S.ncb ? S.cbv[lo] : S.N;
 }
-__device__ __forceinline__ seg_in make_seg_in(const seg_tab& S, u32 a) {
+__device__ __forceinline__ seg_in make_seg_in(const seg_tab& S, pos_t a) {
     return seg_in{a, first_phrase_after(S.P, S.m, a), a, S.zmask0, upper_cb(S, a)};
 }
 
 // default segments: one per gap (phrase k's gap [end_{k-1}, beg_k)) + chunk
 // boundaries inside long gaps; also the initial speculation I_0 and the base
 // superset (gaps + the LPF-start query position, + interiors of short phrases)
-__device__ __forceinline__ void gap_of(const u32* P, u32 k, u32& a, u32& b) {
+__device__ __forceinline__ void gap_of(const pos_t* P, u32 k, pos_t& a, pos_t& b) {
     a = k ? P[3 * (k - 1) + 1] : 0;
     b = P[3 * k];
 }
-__device__ __forceinline__ u32 gap_chunks(u32 a, u32 b, u32 CH) {
-    return (b > a && b - a > 2 * CH) ? (b - a - CH / 2 - 1) / CH : 0;
+__device__ __forceinline__ u32 gap_chunks(pos_t a, pos_t b, u32 CH) {
+    return (b > a && b - a > 2 * (pos_t)CH) ? (u32)((b - a - CH / 2 - 1) / CH) : 0;
 }
-__global__ void k_gap_counts(const u32* __restrict__ P, u32 m, u32 CH, u32* __restrict__ nsegs, u32* __restrict__ ncbs) {
+__global__ void k_gap_counts(const pos_t* __restrict__ P, u32 m, u32 CH, u32* __restrict__ nsegs, u32* __restrict__ ncbs) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
-    u32 a, b;
+    pos_t a, b;
     gap_of(P, (u32)k, a, b);
     const u32 K = gap_chunks(a, b, CH);
     nsegs[k] = (a < b) ? 1 + K : 0;
     ncbs[k] = K;
 }
-__global__ void k_gap_cbv(const u32* __restrict__ P, u32 m, u32 CH, const u32* __restrict__ cb_off, u32* __restrict__ cbv) {
+__global__ void k_gap_cbv(const pos_t* __restrict__ P, u32 m, u32 CH, const u32* __restrict__ cb_off, pos_t* __restrict__ cbv) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
-    u32 a, b;
+    pos_t a, b;
     gap_of(P, (u32)k, a, b);
     const u32 K = gap_chunks(a, b, CH);
-    for (u32 t = 1; t <= K; t++) cbv[cb_off[k] + t - 1] = a + t * CH;
+    for (u32 t = 1; t <= K; t++) cbv[cb_off[k] + t - 1] = a + (pos_t)t * CH;
 }
 __global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off) {
     const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per gap
     const u32 lane = threadIdx.x & 63;
     if (k > S.m) return;
-    u32 a, b;
+    pos_t a, b;
     gap_of(S.P, (u32)k, a, b);
     if (a >= b) return;
     const u32 K = gap_chunks(a, b, CH);
     for (u32 t = lane; t <= K; t += 64) {
-        const u32 x = a + t * CH, id = seg_off[k] + t;
+        const pos_t x = a + (pos_t)t * CH;
+        const u32 id = seg_off[k] + t;
         S.sin[id] = seg_in{x, (u32)k, x, S.zmask0, upper_cb(S, x)};
         S.valid[id] = 0;
         S.succ[id] = NONE;
@@ -945,39 +985,40 @@ __global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off) {
     }
 }
 // bitmaps over text positions (bit q of word q >> 5)
-__device__ __forceinline__ void bm_set_range(u32* bm, u32 a, u32 b) {  // [a, b)
+__device__ __forceinline__ void bm_set_range(u32* bm, pos_t a, pos_t b) {  // [a, b)
     while (a < b) {
-        const u32 w = a >> 5, lo = a & 31, hi = min(32u, lo + (b - a));
+        const u64 w = a >> 5;
+        const u32 lo = a & 31, hi = (u32)min<u64>(32u, lo + (u64)(b - a));
         const u32 mask = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & ~((1u << lo) - 1);
         atomicOr(&bm[w], mask);
         a += hi - lo;
     }
 }
 // one wave sets [a, b): lanes stride over the 32-bit words
-__device__ __forceinline__ void bm_set_range_wave(u32* bm, u32 a, u32 b, u32 lane) {
+__device__ __forceinline__ void bm_set_range_wave(u32* bm, pos_t a, pos_t b, u32 lane) {
     if (a >= b) return;
-    const u32 w0 = a >> 5, w1 = (b - 1) >> 5;
-    for (u32 w = w0 + lane; w <= w1; w += 64) {
+    const u64 w0 = a >> 5, w1 = (b - 1) >> 5;
+    for (u64 w = w0 + lane; w <= w1; w += 64) {
         u32 mask = 0xFFFFFFFFu;
         if (w == w0) mask &= ~((1u << (a & 31)) - 1);
         if (w == w1 && (b & 31)) mask &= (1u << (b & 31)) - 1;
         atomicOr(&bm[w], mask);
     }
 }
-__global__ void k_gap_bitmaps(const u32* __restrict__ P, u32 m, u32 N, u32 nt, u32* __restrict__ bmI,
+__global__ void k_gap_bitmaps(const pos_t* __restrict__ P, u32 m, pos_t N, pos_t nt, u32* __restrict__ bmI,
                               u32* __restrict__ bmSup) {
     const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per phrase
     const u32 lane = threadIdx.x & 63;
     if (k > m) return;
-    u32 a, b;
+    pos_t a, b;
     gap_of(P, (u32)k, a, b);
     if (a < b) {
-        const u32 e = min(min(b + 1, N), nt);
+        const pos_t e = min(min((pos_t)(b + 1), N), nt);
         bm_set_range_wave(bmI, a, e, lane);
         bm_set_range_wave(bmSup, a, e, lane);
     }
     if (k < m) {
-        const u32 pb = P[3 * k], pe = P[3 * k + 1];
+        const pos_t pb = P[3 * k], pe = P[3 * k + 1];
         if (pe - pb <= 48 && pb < nt) bm_set_range_wave(bmSup, pb, min(pe, nt), lane);
     }
 }
@@ -1068,27 +1109,27 @@ __global__ __launch_bounds__(BMB_T) void k_bmb_write(M mk, u64 nw, const u64* __
         }
         const u64 o = base + pre + inc - mine;
         u32 oa = (u32)(o >> 32), ob = (u32)o;
-        while (a) { out.a(oa++, (u32)(32 * w + __builtin_ctz(a)), w); a &= a - 1; }
-        while (b) { out.b(ob++, (u32)(32 * w + __builtin_ctz(b))); b &= b - 1; }
+        while (a) { out.a(oa++, (pos_t)(32 * w + __builtin_ctz(a)), w); a &= a - 1; }
+        while (b) { out.b(ob++, (pos_t)(32 * w + __builtin_ctz(b))); b &= b - 1; }
         base += tot;
         __syncthreads();  // wsum reused by the next round
     }
 }
 struct out_runs {
-    u32* st;
-    u32* en;
-    __device__ __forceinline__ void a(u32 o, u32 p, u64) const { st[o] = p; }
-    __device__ __forceinline__ void b(u32 o, u32 p) const { en[o] = p; }
+    pos_t* st;
+    pos_t* en;
+    __device__ __forceinline__ void a(u32 o, pos_t p, u64) const { st[o] = p; }
+    __device__ __forceinline__ void b(u32 o, pos_t p) const { en[o] = p; }
 };
 struct out_list {  // positions + a flag bit from a second bitmap
-    u32* pos;
+    pos_t* pos;
     u8* flag;
     const u32* flagbm;
-    __device__ __forceinline__ void a(u32 o, u32 p, u64 w) const {
+    __device__ __forceinline__ void a(u32 o, pos_t p, u64 w) const {
         pos[o] = p;
         if (flag) flag[o] = (flagbm[w] >> (p & 31)) & 1;
     }
-    __device__ __forceinline__ void b(u32, u32) const {}
+    __device__ __forceinline__ void b(u32, pos_t) const {}
 };
 // totals of the two masks; bincl holds the inclusive block scan afterwards
 template <class M>
@@ -1108,17 +1149,17 @@ static u64 bmb_scan(M mk, u64 nw, dbuf<u64>& bs, dbuf<u64>& bi, dbuf<u8>& tmp, h
 // fingerprint of <= 64 bytes per pattern, then rolls) wide on the device: the
 // chunk length is 128, or 32 when that leaves fewer than ~2^18 chunks.
 constexpr u32 SLOT_CHUNK_LONG = 128, SLOT_CHUNK_SHORT = 32;
-__global__ void k_iv_chunk_counts(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, u32* __restrict__ nch,
+__global__ void k_iv_chunk_counts(const pos_t* __restrict__ st, const pos_t* __restrict__ en, u32 ni, u32* __restrict__ nch,
                                   u32* __restrict__ nch_short, u32* __restrict__ len) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ni) return;
-    const u32 l = en[k] - st[k];
+    const u32 l = (u32)(en[k] - st[k]);  // intervals hold < 2^32 / 5 positions (entry ids are 32-bit)
     len[k] = l;
     nch[k] = (l + SLOT_CHUNK_LONG - 1) / SLOT_CHUNK_LONG;
     nch_short[k] = (l + SLOT_CHUNK_SHORT - 1) / SLOT_CHUNK_SHORT;
 }
 // one thread per chunk; its interval by binary search over the chunk offsets
-__global__ void k_iv_chunks(const u32* __restrict__ st, const u32* __restrict__ en, u32 ni, const u32* __restrict__ choff,
+__global__ void k_iv_chunks(const pos_t* __restrict__ st, const pos_t* __restrict__ en, u32 ni, const u32* __restrict__ choff,
                             u32 nch, u32 chl, const u32* __restrict__ rank, ichunk* __restrict__ ch) {
     const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nch) return;
@@ -1127,21 +1168,21 @@ __global__ void k_iv_chunks(const u32* __restrict__ st, const u32* __restrict__ 
         const u32 mid = (lo + hi) >> 1;
         if (choff[mid] <= c) lo = mid; else hi = mid;
     }
-    const u32 q = st[lo] + (u32)(c - choff[lo]) * chl;
-    ch[c] = ichunk{q, min(en[lo], q + chl), rank[lo] + (q - st[lo])};
+    const pos_t q = st[lo] + (pos_t)(c - choff[lo]) * chl;
+    ch[c] = ichunk{q, min(en[lo], (pos_t)(q + chl)), rank[lo] + (u32)(q - st[lo])};
 }
 // rem[r] = base position r not in I
-__global__ void k_rem_from_bm(const u32* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, u8* __restrict__ rem) {
+__global__ void k_rem_from_bm(const pos_t* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, u8* __restrict__ rem) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nb) return;
-    const u32 q = ipos[r];
+    const pos_t q = ipos[r];
     rem[r] = ((bmI[q >> 5] >> (q & 31)) & 1) ? 0 : 1;
 }
 
 // walks over a list of segment ids (outputs in the table; WRITE: factors at offs)
 template <bool WRITE>
 __global__ void k_walk(walk_ctx W, seg_tab S, const u32* __restrict__ ids, u32 cnt, const u64* __restrict__ offs,
-                       u32* __restrict__ fact) {
+                       pos_t* __restrict__ fact) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const u32 g = ids[t];
@@ -1160,8 +1201,8 @@ __global__ void k_walk_keys(seg_tab S, const u32* __restrict__ ids, u32 cnt, u32
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const seg_in si = S.sin[ids[t]];
-    const u32 ge = min(S.P[3 * si.p], si.lim);
-    keys[t] = ge > si.start ? ge - si.start : 0u;
+    const pos_t ge = min(S.P[3 * si.p], si.lim);
+    keys[t] = ge > si.start ? (u32)min<u64>(ge - si.start, 0xFFFFFFFFull) : 0u;
 }
 __global__ void k_todo(seg_tab S, u32 nseg, u32* __restrict__ ids, u32* __restrict__ cnt) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1170,7 +1211,7 @@ __global__ void k_todo(seg_tab S, u32 nseg, u32* __restrict__ ids, u32* __restri
     if (todo) ids[slot] = (u32)g;
 }
 // claim the segment starting at x (created by this thread iff *mine)
-__device__ u32 seg_claim(const seg_tab& S, u32 x, bool& mine) {
+__device__ u32 seg_claim(const seg_tab& S, pos_t x, bool& mine) {
     mine = false;
     const u32 old = atomicCAS(&S.seg_at[x], NONE, PENDING);
     if (old != NONE) return old;
@@ -1191,7 +1232,7 @@ __global__ void k_link(seg_tab S, u32 nseg) {
     if (g >= nseg || !S.valid[g] || S.succ[g] != NONE) return;
     const seg_out& o = S.sout[g];
     if ((o.flags & 1) || o.next >= S.N) return;
-    const u32 x = o.next;
+    const pos_t x = o.next;
     const u32 s = S.seg_at[x];
     if (s == PENDING) return;
     if (s != NONE) { S.succ[g] = s; return; }
@@ -1256,7 +1297,7 @@ __global__ void k_jumpk(const u32* __restrict__ J, const u32* __restrict__ D, u3
     J2[g] = J[j];
     D2[g] = D[g] + D[j];
 }
-struct chain_status { u32 term, hops, valid, flags, next, err, nseg, pad; };
+struct chain_status { u32 term, hops, valid, flags; pos_t next; u32 err, nseg; };
 __global__ void k_chain_status(seg_tab S, const u32* __restrict__ J, const u32* __restrict__ D, chain_status* out) {
     const u32 t = J[0];
     chain_status c{};
@@ -1280,13 +1321,13 @@ __global__ void k_chain_expand(jump_levels JL, u32 len, u32* __restrict__ chain)
     chain[k] = g;
 }
 // I' bitmap: what the chain inserted below nt ([start, e) + LPF-start queries)
-__global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, u32 nt, u32* __restrict__ bm) {
+__global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, pos_t nt, u32* __restrict__ bm) {
     const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per chain node
     const u32 lane = threadIdx.x & 63;
     if (k >= cnt) return;
     const u32 g = chain[k];
     const seg_out& o = S.sout[g];
-    const u32 a = S.sin[g].start, b = min(o.e, nt);
+    const pos_t a = S.sin[g].start, b = min(o.e, nt);
     bm_set_range_wave(bm, a, b, lane);
     if (lane < o.nsingle && lane < 4 && o.single[lane] < nt) atomicOr(&bm[o.single[lane] >> 5], 1u << (o.single[lane] & 31));
 }
@@ -1294,9 +1335,9 @@ __global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cn
 // the speculated insert set and the chain's differ): every lookup of its predecessors
 // happened below y0, so its start state is exact (index state from its predecessor)
 struct chain_cut { u32 k, pad; seg_in in; };
-__global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, const u32* __restrict__ y0p,
+__global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, const u64* __restrict__ y0p,
                             chain_cut* __restrict__ out) {
-    const u32 y0 = *y0p;
+    const u64 y0 = *y0p;
     chain_cut c{};
     if (nall == 0 || y0 == 0) {
         c.k = 0;
@@ -1321,7 +1362,7 @@ __global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, 
     }
     *out = c;
 }
-__global__ void k_set_pairs(const u32* __restrict__ pairs, u32 np, u32* __restrict__ bm) {
+__global__ void k_set_pairs(const pos_t* __restrict__ pairs, u32 np, u32* __restrict__ bm) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < np) bm_set_range(bm, pairs[2 * k], pairs[2 * k + 1]);
 }
@@ -1330,11 +1371,11 @@ __global__ void k_chain_nfact(seg_tab S, const u32* __restrict__ chain, u32 cnt,
     if (k < cnt) nf[k] = S.sout[chain[k]].nfact;
 }
 // a walked segment is stale iff a dirty position lies in its covered range
-__global__ void k_stale(seg_tab S, u32 nseg, const u32* __restrict__ dirty, u64 nd) {
+__global__ void k_stale(seg_tab S, u32 nseg, const pos_t* __restrict__ dirty, u64 nd) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nseg || !S.valid[g]) return;
     const seg_out& o = S.sout[g];
-    const u32 a = S.sin[g].start, b = (o.flags & 1) ? S.N : max(o.next, o.e + 1);
+    const pos_t a = S.sin[g].start, b = (o.flags & 1) ? S.N : max(o.next, (pos_t)(o.e + 1));
     u64 l = 0, h = nd;
     while (l < h) {
         const u64 mid = (l + h) >> 1;
@@ -1353,7 +1394,7 @@ __global__ void k_invalidate_all(seg_tab S, u32 nseg) {
     S.succ[g] = NONE;
 }
 
-__global__ void k_put3(u32* p, u32 a, u32 b, u32 c) {
+__global__ void k_put3(pos_t* p, pos_t a, pos_t b, pos_t c) {
     p[0] = a;
     p[1] = b;
     p[2] = c;
@@ -1383,19 +1424,24 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         std::fprintf(stderr, "[lz77sss-debug]   %-28s %9.3f ms\n", what, t - t_mark);
         t_mark = t;
     };
-    const u32 N = (u32)n;
+    const pos_t N = (pos_t)n;
     const u32 m = num_phr;  // phrases; P[m] = sentinel
-    u32* P = lpf.get((u64)(m + 1) * 3);
+    pos_t* P = lpf.get((u64)(m + 1) * 3);
     k_put3<<<1, 1, 0, st>>>(P + 3 * (u64)m, N, N + 1, 0);
     // ---- phrase statistics -> parameters (lz77_sss.hpp:420-461)
-    u32 num_lpf = m, len_lpf_phr = 0, num_gaps = 1;
+    u64 num_lpf = m, num_gaps = 1;
+    pos_t len_lpf_phr = 0;
     if (m > 0) {
-        u32* acc = counters.get(16);
-        LZ_HIP(hipMemsetAsync(acc, 0, 8, st));
+        u64* acc = counters64.get(4) + 2;
+        LZ_HIP(hipMemsetAsync(acc, 0, 16, st));
         k_phrase_info<<<cdiv(m, 256), 256, 0, st>>>(P, m, N, acc);
-        len_lpf_phr = rd1(acc, st);
+        len_lpf_phr = (pos_t)rd1(acc, st);
         num_gaps = rd1(acc + 1, st);
     }
+    // entry ids are 32-bit: the base superset (gaps + LPF-start queries + short phrase
+    // interiors) must hold fewer than 2^32 / 5 positions
+    if (sizeof(pos_t) > 4 && ((u64)(N - len_lpf_phr) + 49ull * (m + 1)) * 5 >= (1ull << 32))
+        throw error(-1, "gap region too large for 32-bit entry ids");
     gap_params_h gp = choose_gap_params(N, num_lpf, len_lpf_phr, num_gaps);
     if (log2_override > 0) gp.log2_size_h = (u32)log2_override;
     // bases: rk_prime::random64(257, 2^20-1) from mt19937_64(rk_seed) (rolling_hash.hpp:127-130)
@@ -1443,7 +1489,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     k_gap_counts<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, cnt_seg, cnt_cb);
     const u32 nseg0 = excl_scan(cnt_seg, off_seg, m + 1, scan_tmp, st);
     const u32 ncb = excl_scan(cnt_cb, off_cb, m + 1, scan_tmp, st);
-    u32* cbv = g_cbv.get(ncb + 1);
+    pos_t* cbv = g_cbv.get(ncb + 1);
     k_gap_cbv<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, off_cb, cbv);
     u32 cap = nseg0 + nseg0 / 2 + (1u << 16);
     seg_tab S{};
@@ -1493,21 +1539,21 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     const lce_view& Lv = W.L;
     u64* d_sq = (u64*)g_cut.get(sizeof(chain_cut) + 64);
     chain_cut* d_cutp = (chain_cut*)(d_sq + 4);
-    u32* d_y0 = (u32*)(d_sq + 2);
+    u64* d_y0 = d_sq + 2;
     auto seq_complete = [&](const u32* chain, u32 nall, const u64* offs, const u32* ins_bm, bool from_zero) -> u64 {
-        if (from_zero) LZ_HIP(hipMemsetAsync(d_y0, 0, 4, st));
+        if (from_zero) LZ_HIP(hipMemsetAsync(d_y0, 0, 8, st));
         k_chain_cut<<<1, 1, 0, st>>>(S, chain, from_zero ? 0u : nall, d_y0, d_cutp);
         chain_cut cut;
         LZ_HIP(hipMemcpyAsync(&cut, d_cutp, sizeof(cut), hipMemcpyDeviceToHost, st));
         LZ_HIP(hipStreamSynchronize(st));
         const u64 offk = cut.k ? rd1(offs + cut.k, st) : 0;
-        u32* fo = fact.get(2 * (offk + (u64)(N - cut.in.start) + 2) + 2);
+        pos_t* fo = fact.get(2 * (offk + (u64)(N - cut.in.start) + 2) + 2);
         if (cut.k) {
             k_walk<true><<<cdiv(cut.k, 64), 64, 0, st>>>(W, S, chain, cut.k, offs, fo);
             LZ_HIP(hipGetLastError());
         }
-        u32* H = g_H.get((u64)nslots_all);
-        LZ_HIP(hipMemsetAsync(H, 0, (u64)nslots_all * 4, st));
+        pos_t* H = g_H.get((u64)nslots_all);
+        LZ_HIP(hipMemsetAsync(H, 0, (u64)nslots_all * sizeof(pos_t), st));
         if (cut.in.start && ins_bm)
             k_h_fill<<<cdiv(((u64)cut.in.start + 31) / 32, 256), 256, 0, st>>>(T, G, ins_bm, cut.in.start, H);
         k_h_fix<<<cdiv(nslots_all, 256), 256, 0, st>>>(H, nslots_all);
@@ -1543,12 +1589,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         }
     };
     // runs of a bitmap -> intervals (st, en), ranks, chunks for k_slots
-    auto runs_to_chunks = [&](const u32* bm, dbuf<u32>& dst, dbuf<u32>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
+    auto runs_to_chunks = [&](const u32* bm, dbuf<pos_t>& dst, dbuf<pos_t>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
                               u64& npos, u32& nch) -> ichunk* {
         const u64 tot = bmb_scan(bm_runs{bm}, nw, g_bsum, g_bincl, scan_tmp, st);
         ni = (u32)(tot >> 32);  // run starts (= run ends)
-        u32* a = dst.get(ni + 1);
-        u32* b = den.get(ni + 1);
+        pos_t* a = dst.get(ni + 1);
+        pos_t* b = den.get(ni + 1);
         k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_runs{bm}, nw, g_bincl.p, out_runs{a, b});
         u32* len = g_tmp5.get(ni + 1);
         u32* nc = g_tmp6.get(ni + 1);
@@ -1585,7 +1631,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         u32* vals = evals.get(ne5 + 1);
         u32* skeys = ekeys2.get(ne5 + 1);
         u32* svals = evals2.get(ne5 + 1);
-        u32* ipos = ipos_buf.get(nb + 1);
+        pos_t* ipos = ipos_buf.get(nb + 1);
         u32* pred5 = occ_buf.get(ne5 + 1);
         u8* rem = rem_buf.get(nb + 1);
         LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
@@ -1679,16 +1725,21 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     // positions that join later and are missing from it go to the small extra list.
     u32* bmA = g_bmA.get(nw);
     u64 na_main = 0;
-    auto build_list = [&](const u32* bm, dbuf<u32>& k32, dbuf<u32>& kpos, dbuf<u64>& ka, dbuf<u64>& kb,
-                          dbuf<u32>& bucket, const u64*& keys_out, u64& nkeys, const u32*& bk_out) -> u64 {
+    auto build_list = [&](const u32* bm, dbuf<u32>& k32, dbuf<pos_t>& kpos, dbuf<u64>& ka, dbuf<u64>& kb,
+                          dbuf<u32>& bucket, const u64*& keys_out, u64& nkeys, const u32*& bk_out,
+                          const pos_t*& apos_out, u64& napos_out) -> u64 {
         u32 ni, nch;
         u64 na;
         ichunk* ch = runs_to_chunks(bm, g_ast, g_aen, g_ark, chunk_buf2, ni, na, nch);
         nkeys = 0;
         keys_out = nullptr;
+        apos_out = nullptr;
+        napos_out = 0;
         if (!na) return 0;
         u32* akey32 = k32.get(5 * na);
-        u32* apos = kpos.get(na);
+        pos_t* apos = kpos.get(na);
+        apos_out = apos;
+        napos_out = na;
         k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
         u64* ak = ka.get(5 * na);
         u64* ak2 = kb.get(5 * na);
@@ -1705,7 +1756,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     };
     auto rebuild_main = [&]() {
         k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmA);
-        na_main = build_list(bmA, add_keys32, add_pos, add_keys, add_keys2, g_abeg, W.akeys, W.nadd, W.abeg);
+        na_main = build_list(bmA, add_keys32, add_pos, add_keys, add_keys2, g_abeg, W.akeys, W.nadd, W.abeg, W.apos,
+                             W.napos);
         W.nadd2 = 0;
         W.akeys2 = nullptr;
     };
@@ -1713,7 +1765,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         if (main_list) return rebuild_main();
         k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmT);
         k_bm_andnot<<<gw, 256, 0, st>>>(bmT, bmA, nw, bmT);
-        const u64 nx = build_list(bmT, g_x32, g_xpos, g_xk, g_xk2, g_abeg2, W.akeys2, W.nadd2, W.abeg2);
+        const u64 nx = build_list(bmT, g_x32, g_xpos, g_xk, g_xk2, g_abeg2, W.akeys2, W.nadd2, W.abeg2, W.apos2,
+                                  W.napos2);
         if (nx * 4 > na_main + (1u << 16)) rebuild_main();
     };
     auto set_state = [&]() {  // rem + added for the current I
@@ -1828,7 +1881,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             chain_fact = excl_scan(nf, offs, nchain, scan_tmp, st);
         }
         u64 tail_count = 0, tail_bound = 0;
-        u32 tail_pairs[16];
+        pos_t tail_pairs[16];
         u64 hc[3] = {0, 0, 0};
         if (tail) {
             seg_in tin;
@@ -1844,13 +1897,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             tin.idxpos = nall >= 2 ? prev.idxpos : 0;  // exact chain state entering the tail walk
             tin.zmask = nall >= 2 ? prev.zmask : zmask0;
             tail_bound = (u64)N - tin.start + 1;
-            u32* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
+            pos_t* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
             u64* d_tc = (u64*)g_tailc.get(4 * sizeof(u64));
-            u32* d_tins = tail_ins_buf.get(16);
+            pos_t* d_tins = tail_ins_buf.get(16);
             k_tail<<<1, 64, 0, st>>>(W, tin, fo, chain_fact, d_tc, d_tins);
             LZ_HIP(hipGetLastError());
             LZ_HIP(hipMemcpyAsync(hc, d_tc, 24, hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipMemcpyAsync(tail_pairs, d_tins, 64, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipMemcpyAsync(tail_pairs, d_tins, sizeof(tail_pairs), hipMemcpyDeviceToHost, st));
             LZ_HIP(hipStreamSynchronize(st));
             if (hc[2]) throw error(-6, "greedy tail: insert overflow or guard tripped");
             tail_count = hc[0];
@@ -1862,7 +1915,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
         if (nchain) k_chain_inserts<<<cdiv((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, G.nt, bmI2);
         if (tail && hc[1]) {
-            u32* d_tins = tail_ins_buf.p;
+            pos_t* d_tins = tail_ins_buf.p;
             k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], bmI2);
         }
         k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
@@ -1880,13 +1933,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         }
         if (outer + 1 >= max_outer) {
             // round budget spent: the chain is exact up to the first changed position
-            LZ_HIP(hipMemsetAsync(d_y0, 0xFF, 4, st));
+            LZ_HIP(hipMemsetAsync(d_y0, 0xFF, 8, st));
             k_first_bit<<<gw, 256, 0, st>>>(bmT, nw, d_y0);
             total_fact = seq_complete(chain, nall, offs, bmI2, false);
             break;
         }
         // positions that joined (flag 1) or left (0) I
-        u32* d_y = dirty_in.get(ny + 1);
+        pos_t* d_y = dirty_in.get(ny + 1);
         u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
         k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_bits{bmT, nullptr}, nw, g_bincl.p, out_list{d_y, d_j, bmI2});
         // many positions outside the base set: rebuild it as I' u I_b, re-walk everything
@@ -1915,8 +1968,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
             continue;
         }
         // dirty = changed positions + their same-slot successors before and after the update
-        u32* d_d = dirty_out.get(11 * ny + 1);
-        LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * 4, hipMemcpyDeviceToDevice, st));
+        pos_t* d_d = dirty_out.get(11 * ny + 1);
+        LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
         k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + ny);
         k_flip<<<cdiv(ny, 256), 256, 0, st>>>(W, d_y, d_j, ny, (u8*)W.rem, d_j + ny);
         std::swap(g_bmI.p, g_bmI2.p);
@@ -1927,12 +1980,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         W.bmI = bmI;
         if (rd1(d_cnt, st)) rebuild_added(false);
         k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + 6 * ny);
-        u32* d_ds = dirty_sorted.get(11 * ny + 1);
+        pos_t* d_ds = dirty_sorted.get(11 * ny + 1);
         {
+            constexpr unsigned PB = 8 * sizeof(pos_t);
             size_t tb = 0;
-            LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, d_d, d_ds, (size_t)(11 * ny), 0u, 32u, st));
+            LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, d_d, d_ds, (size_t)(11 * ny), 0u, PB, st));
             u8* t = scan_tmp.get(tb);
-            LZ_HIP(rocprim::radix_sort_keys(t, tb, d_d, d_ds, (size_t)(11 * ny), 0u, 32u, st));
+            LZ_HIP(rocprim::radix_sort_keys(t, tb, d_d, d_ds, (size_t)(11 * ny), 0u, PB, st));
         }
         k_stale<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, d_ds, 11 * ny);
         lap("delta + dirty");
@@ -1942,4 +1996,4 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     return finish_call(total_fact, outer + 1, rounds_total, walked_total, nseg);
 }
 
-}  // namespace lz
+}  // namespace LZ_NS

@@ -18,7 +18,7 @@
 
 #include <hipcub/hipcub.hpp>
 
-namespace lz {
+namespace LZ_NS {
 
 __global__ void k_sa_min_level(const u32* __restrict__ prev, u32 cnt, u32 half, u32* __restrict__ out) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -54,23 +54,23 @@ __global__ void k_psv_nsv(const u32* __restrict__ SA, u32 s, sa_min_levels M, u3
 constexpr int CREC = 8;
 
 __global__ void k_lpf_candidates(lce_view L, const u32* __restrict__ SA, const u32* __restrict__ PSV,
-                                 const u32* __restrict__ NSV, u32* __restrict__ cand) {
+                                 const u32* __restrict__ NSV, pos_t* __restrict__ cand) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const u32 s = L.s;
     if (i >= s) return;
-    const u32* S = L.S;
+    const pos_t* S = L.S;
     const u32 r = L.ISA[i];
-    const u32 Si = S[i];
-    const u32 capmax = i >= 2 ? Si - S[i - 1] : Si;
-    u32 rec[CREC] = {0, 0, 0, 0, 0, 0, 0, 0};
-    u32 E = 0;
+    const pos_t Si = S[i];
+    const pos_t capmax = i >= 2 ? Si - S[i - 1] : Si;
+    pos_t rec[CREC] = {0, 0, 0, 0, 0, 0, 0, 0};
+    pos_t E = 0;
 #pragma unroll
     for (int side = 0; side < 2; side++) {
         const u32 nb = side == 0 ? PSV[r] : NSV[r];
         if (nb == s) continue;
-        const u32 src = S[SA[nb]];
-        const u32 end = Si + (u32)dev_lce(L, src, Si);
-        u32 l = 0;
+        const pos_t src = S[SA[nb]];
+        const pos_t end = Si + (pos_t)dev_lce(L, src, Si);
+        pos_t l = 0;
         if (src != 0 && Si != 0) l = dev_lce_left(L.T, L.R, src - 1, Si - 1, capmax);
         rec[side * 3 + 0] = src;
         rec[side * 3 + 1] = end;
@@ -84,11 +84,11 @@ __global__ void k_lpf_candidates(lce_view L, const u32* __restrict__ SA, const u
 }
 
 // next processed index after i (lpf_opt.cpp:61-63): max(i+1, last k: S[k] <= E_i)
-__global__ void k_next(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand, u32* __restrict__ nxt) {
+__global__ void k_next(const pos_t* __restrict__ S, u32 s, const pos_t* __restrict__ cand, u32* __restrict__ nxt) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > s) return;
     if (i == s) { nxt[s] = s; return; }
-    const u32 E = cand[i * CREC + 7];
+    const pos_t E = cand[i * CREC + 7];
     u32 nx = (u32)i + 1;
     if (i + 1 < s && S[i + 1] <= E) {
         u32 lo = (u32)i + 1, hi = s;  // last k with S[k] <= E: first k with S[k] > E, minus 1
@@ -117,36 +117,36 @@ __global__ void k_mark(const u32* __restrict__ C, u32 cnt, u32 s, u32* __restric
     const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (m < cnt && C[m] < s) mark[C[m]] = 1;
 }
-__global__ void k_masked_E(const u32* __restrict__ cand, const u32* __restrict__ mark, u32 s, u32* __restrict__ Em) {
+__global__ void k_masked_E(const pos_t* __restrict__ cand, const u32* __restrict__ mark, u32 s, pos_t* __restrict__ Em) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < s) Em[i] = mark[i] ? cand[i * CREC + 7] : 0u;
+    if (i < s) Em[i] = mark[i] ? cand[i * CREC + 7] : (pos_t)0;
 }
 
 // phrase of a processed index given lst_end (lpf_opt.cpp:65-144)
-__global__ void k_phrase(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand, const u32* __restrict__ mark,
-                         const u32* __restrict__ lst, u32* __restrict__ ph, u32* __restrict__ push) {
+__global__ void k_phrase(const pos_t* __restrict__ S, u32 s, const pos_t* __restrict__ cand, const u32* __restrict__ mark,
+                         const pos_t* __restrict__ lst, pos_t* __restrict__ ph, u32* __restrict__ push) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= s) return;
     u32 pu = 0;
-    u32 pb = 0, pe = 0, ps = 0;
+    pos_t pb = 0, pe = 0, ps = 0;
     if (mark[i]) {
-        const u32* c = cand + i * CREC;
-        const u32 lst_end = lst[i];
-        const u32 Si = S[i];
-        const u32 has = c[6];
+        const pos_t* c = cand + i * CREC;
+        const pos_t lst_end = lst[i];
+        const pos_t Si = S[i];
+        const u32 has = (u32)c[6];
         for (int side = 0; side < 2; side++) {
             if (!(has >> side & 1)) continue;
-            u32 src = c[side * 3 + 0];
-            const u32 end = c[side * 3 + 1];
+            pos_t src = c[side * 3 + 0];
+            const pos_t end = c[side * 3 + 1];
             if (end > lst_end) {
-                u32 beg = Si;
+                pos_t beg = Si;
                 if (Si > lst_end && src != 0 && Si != 0) {
-                    const u32 l = min(c[side * 3 + 2], Si - lst_end);
+                    const pos_t l = min(c[side * 3 + 2], (pos_t)(Si - lst_end));
                     beg -= l;
                     src -= l;
                 }
                 if (beg < lst_end) {
-                    const u32 exc = lst_end - beg;
+                    const pos_t exc = lst_end - beg;
                     beg += exc;
                     src += exc;
                 }
@@ -164,8 +164,8 @@ __global__ void k_phrase(const u32* __restrict__ S, u32 s, const u32* __restrict
     ph[i * 3 + 2] = ps;
     push[i] = pu;
 }
-__global__ void k_compact3(const u32* __restrict__ ph, const u32* __restrict__ push, const u32* __restrict__ off,
-                           u32 s, u32* __restrict__ out) {
+__global__ void k_compact3(const pos_t* __restrict__ ph, const u32* __restrict__ push, const u32* __restrict__ off,
+                           u32 s, pos_t* __restrict__ out) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= s || !push[i]) return;
     const u32 o = off[i];
@@ -175,7 +175,7 @@ __global__ void k_compact3(const u32* __restrict__ ph, const u32* __restrict__ p
 }
 
 struct max_op {
-    __device__ u32 operator()(const u32& a, const u32& b) const { return a > b ? a : b; }
+    __device__ pos_t operator()(const pos_t& a, const pos_t& b) const { return a > b ? a : b; }
 };
 
 // ---------------------------------------------------------------------------
@@ -185,18 +185,19 @@ struct max_op {
 // (lpf_naive.cpp:104-108), so the processed indices are again a path from 0.
 // cand2[i] = (src, len)
 __global__ void k_lpf_naive_cand(lce_view L, const u32* __restrict__ SA, const u32* __restrict__ PSV,
-                                 const u32* __restrict__ NSV, u32* __restrict__ cand2) {
+                                 const u32* __restrict__ NSV, pos_t* __restrict__ cand2) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const u32 s = L.s;
     if (i >= s) return;
-    const u32 r = L.ISA[i], Si = L.S[i];
-    u32 src = 0, len = 0;
+    const u32 r = L.ISA[i];
+    const pos_t Si = L.S[i];
+    pos_t src = 0, len = 0;
 #pragma unroll
     for (int side = 0; side < 2; side++) {
         const u32 nb = side == 0 ? PSV[r] : NSV[r];
         if (nb == s) continue;
-        const u32 sc = L.S[SA[nb]];
-        const u32 lc = (u32)dev_lce(L, sc, Si);
+        const pos_t sc = L.S[SA[nb]];
+        const pos_t lc = (pos_t)dev_lce(L, sc, Si);
         if (lc > len) {
             src = sc;
             len = lc;
@@ -205,7 +206,7 @@ __global__ void k_lpf_naive_cand(lce_view L, const u32* __restrict__ SA, const u
     cand2[2 * i] = src;
     cand2[2 * i + 1] = len;
 }
-__global__ void k_next_naive(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand2, u32* __restrict__ nxt) {
+__global__ void k_next_naive(const pos_t* __restrict__ S, u32 s, const pos_t* __restrict__ cand2, u32* __restrict__ nxt) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i > s) return;
     if (i == s) { nxt[s] = s; return; }
@@ -217,11 +218,11 @@ __global__ void k_next_naive(const u32* __restrict__ S, u32 s, const u32* __rest
     }
     nxt[i] = lo;
 }
-__global__ void k_phrase_naive(const u32* __restrict__ S, u32 s, const u32* __restrict__ cand2,
-                               const u32* __restrict__ mark, u32* __restrict__ ph, u32* __restrict__ push) {
+__global__ void k_phrase_naive(const pos_t* __restrict__ S, u32 s, const pos_t* __restrict__ cand2,
+                               const u32* __restrict__ mark, pos_t* __restrict__ ph, u32* __restrict__ push) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= s) return;
-    const u32 len = cand2[2 * i + 1];
+    const pos_t len = cand2[2 * i + 1];
     const bool pu = mark[i] && len > 0;
     ph[i * 3 + 0] = S[i];
     ph[i * 3 + 1] = S[i] + len;
@@ -270,12 +271,12 @@ void engine::build_lpf_naive(const u8* T) {
     if (s == 0) return;
     const unsigned g = cdiv(s, 256);
     psv_nsv_s();
-    u32* cd = cand.get((u64)s * 2);
+    pos_t* cd = cand.get((u64)s * 2);
     k_lpf_naive_cand<<<g, 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, cd);
     k_next_naive<<<cdiv(s + 1, 256), 256, 0, st>>>(S.p, s, cd, jump[0].get(s + 1));
     u32* mark = u32c.get(s);
     mark_path(mark);
-    u32* ph3 = u32e.get((u64)s * 3);
+    pos_t* ph3 = p_ph3.get((u64)s * 3);
     u32* push = u32d.get(s);
     k_phrase_naive<<<g, 256, 0, st>>>(S.p, s, cd, mark, ph3, push);
     u32* off = mark;  // mark no longer needed
@@ -286,7 +287,7 @@ void engine::build_lpf_naive(const u8* T) {
         LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, push, off, (int)s, st));
     }
     num_phr = rd1(off + s - 1, st) + rd1(push + s - 1, st);
-    u32* out = lpf.get((u64)(num_phr + 1) * 3);
+    pos_t* out = lpf.get((u64)(num_phr + 1) * 3);
     k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);
     LZ_HIP(hipGetLastError());
 }
@@ -312,7 +313,7 @@ void engine::build_lpf_opt(const u8* T) {
         k_psv_nsv<<<g, 256, 0, st>>>(SA.p, s, M, PSV.get(s), NSV.get(s));
     }
     // 2. candidates
-    u32* cd = cand.get((u64)s * CREC);
+    pos_t* cd = cand.get((u64)s * CREC);
     k_lpf_candidates<<<g, 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, cd);
     // 3. skip chain: pointer doubling over next[], nodes 0..s (s = end)
     const u32 m = s + 1;
@@ -334,20 +335,18 @@ void engine::build_lpf_opt(const u8* T) {
     LZ_HIP(hipMemsetAsync(mark, 0, (size_t)s * 4, st));
     k_mark<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, s, mark);
     // running max_end before each processed index
-    u32* Em = u32d.get(s);
+    pos_t* Em = p_Em.get(s);
     k_masked_E<<<g, 256, 0, st>>>(cd, mark, s, Em);
-    u32* lst = (C == u32a.p) ? u32b.p : u32a.p;  // reuse the free expansion buffer (>= s entries)
+    pos_t* lst = p_lst.get(s);
     {
         size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, Em, lst, max_op{}, 0u, (int)s, st));
+        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, Em, lst, max_op{}, (pos_t)0, (int)s, st));
         u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(t, tb, Em, lst, max_op{}, 0u, (int)s, st));
+        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(t, tb, Em, lst, max_op{}, (pos_t)0, (int)s, st));
     }
     // 4. phrases + compaction
-    u32* ph = PSV.p;  // PSV/NSV no longer needed: reuse as scratch (3 words per index needs 3s)
-    u32* ph3 = u32e.get((u64)s * 3);
-    (void)ph;
-    u32* push = Em;
+    pos_t* ph3 = p_ph3.get((u64)s * 3);
+    u32* push = u32d.get(s);
     k_phrase<<<g, 256, 0, st>>>(S.p, s, cd, mark, lst, ph3, push);
     u32* off = mark;  // mark no longer needed after k_phrase
     {
@@ -358,9 +357,9 @@ void engine::build_lpf_opt(const u8* T) {
     }
     const u32 last_off = rd1(off + s - 1, st), last_push = rd1(push + s - 1, st);
     num_phr = last_off + last_push;
-    u32* out = lpf.get((u64)(num_phr + 1) * 3);
+    pos_t* out = lpf.get((u64)(num_phr + 1) * 3);
     k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);
     LZ_HIP(hipGetLastError());
 }
 
-}  // namespace lz
+}  // namespace LZ_NS

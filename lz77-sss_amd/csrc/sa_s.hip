@@ -15,17 +15,17 @@
 
 #include <hipcub/hipcub.hpp>
 
-namespace lz {
+namespace LZ_NS {
 
-__global__ void k_key_len(const u32* __restrict__ S, u32 s, u64 n, u32* __restrict__ KL) {
+__global__ void k_key_len(const pos_t* __restrict__ S, u32 s, u64 n, pos_t* __restrict__ KL) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s) return;
     const u64 beg = S[k];
     u64 len = (k + 1 < s) ? max<u64>(3 * TAU, (u64)S[k + 1] - S[k] + 2 * TAU) : n - beg;
-    KL[k] = (u32)min<u64>(len, n - beg);
+    KL[k] = (pos_t)min<u64>(len, n - beg);
 }
 
-__device__ __forceinline__ int dev_key_cmp(const u8* T, const u32* S, const u32* KL, u32 a, u32 b) {
+__device__ __forceinline__ int dev_key_cmp(const u8* T, const pos_t* S, const pos_t* KL, u32 a, u32 b) {
     const u64 la = KL[a], lb = KL[b], m = min(la, lb);
     const u64 c = dev_naive_lce(T, S[a], S[b], m);
     if (c < m) return T[(u64)S[a] + c] < T[(u64)S[b] + c] ? -1 : 1;
@@ -34,8 +34,8 @@ __device__ __forceinline__ int dev_key_cmp(const u8* T, const u32* S, const u32*
 
 struct key_less {
     const u8* T;
-    const u32* S;
-    const u32* KL;
+    const pos_t* S;
+    const pos_t* KL;
     __device__ bool operator()(const u32& a, const u32& b) const { return dev_key_cmp(T, S, KL, a, b) < 0; }
 };
 
@@ -43,7 +43,7 @@ __global__ void k_iota(u32* __restrict__ x, u32 m) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < m) x[k] = (u32)k;
 }
-__global__ void k_key_diff(const u8* T, const u32* S, const u32* KL, const u32* __restrict__ idx, u32 s,
+__global__ void k_key_diff(const u8* T, const pos_t* S, const pos_t* KL, const u32* __restrict__ idx, u32 s,
                            u32* __restrict__ flag) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= s) return;
@@ -80,7 +80,7 @@ struct rank_levels {
 };
 
 // LCP[r] = LCE(S[SA[r-1]], S[SA[r]]), r >= 1; LCP[0] = 0
-__global__ void k_lcp(const u8* __restrict__ T, u64 n, const u32* __restrict__ S, const u32* __restrict__ KL,
+__global__ void k_lcp(const u8* __restrict__ T, u64 n, const pos_t* __restrict__ S, const pos_t* __restrict__ KL,
                       const u32* __restrict__ SA, u32 s, rank_levels RL, run_tab R, u32* __restrict__ LCP) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= s) return;
@@ -99,7 +99,7 @@ __global__ void k_lcp(const u8* __restrict__ T, u64 n, const u32* __restrict__ S
         const u64 m = min(KL[ka], KL[kb]);
         v = ((u64)S[ka] - S[a]) + dev_lce_fwd(T, R, S[ka], S[kb], m);
     }
-    LCP[r] = (u32)v;
+    LCP[r] = (u32)min<u64>(v, LCP_SAT);
 }
 
 __global__ void k_min_level(const u32* __restrict__ prev, u32 cnt, u32 half, u32* __restrict__ out) {
@@ -107,7 +107,7 @@ __global__ void k_min_level(const u32* __restrict__ prev, u32 cnt, u32 half, u32
     if (k < cnt) out[k] = min(prev[k], prev[k + half]);
 }
 
-__global__ void k_succ_table(const u32* __restrict__ S, u32 s, u64 nb, u32* __restrict__ tab) {
+__global__ void k_succ_table(const pos_t* __restrict__ S, u32 s, u64 nb, u32* __restrict__ tab) {
     const u64 bkt = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (bkt >= nb) return;
     const u64 x = bkt << 9;
@@ -132,7 +132,7 @@ __device__ __forceinline__ u64 mix64(u64 z) {
 // serialize on one wave.  k_key_prep sets H = mix(len) and the piece counts.
 constexpr u32 KH_CHUNK = 16384;
 constexpr u32 KH_WAVES = 16384;
-__global__ void k_key_prep(const u32* __restrict__ KL, u32 s, u64* __restrict__ H, u32* __restrict__ CC) {
+__global__ void k_key_prep(const pos_t* __restrict__ KL, u32 s, u64* __restrict__ H, u32* __restrict__ CC) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s) return;
     const u64 len = KL[k];
@@ -140,8 +140,8 @@ __global__ void k_key_prep(const u32* __restrict__ KL, u32 s, u64* __restrict__ 
     CC[k] = (u32)max<u64>(1, (len + KH_CHUNK - 1) / KH_CHUNK);
 }
 // OFF = inclusive scan of the piece counts; wave w hashes pieces [w*per, (w+1)*per)
-__global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, const u32* __restrict__ S,
-                                                  const u32* __restrict__ KL, const u32* __restrict__ OFF, u32 s,
+__global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, const pos_t* __restrict__ S,
+                                                  const pos_t* __restrict__ KL, const u32* __restrict__ OFF, u32 s,
                                                   u64* __restrict__ H) {
     const u32 wave = (u32)(((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const u32 lane = threadIdx.x & 63;
@@ -182,13 +182,13 @@ __device__ __forceinline__ u64 key_word_be(const u8* T, u64 beg, u64 len, u32 i)
     if (r < 8) x &= (1ull << (8 * r)) - 1;
     return __builtin_bswap64(x);
 }
-__global__ void k_word_keys(const u8* __restrict__ T, const u32* __restrict__ S, const u32* __restrict__ KL,
+__global__ void k_word_keys(const u8* __restrict__ T, const pos_t* __restrict__ S, const pos_t* __restrict__ KL,
                             const u32* __restrict__ v, u32 d, u32 i, u64* __restrict__ key) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < d) key[t] = key_word_be(T, S[v[t]], KL[v[t]], i);
 }
 // wave-parallel exact comparison of two keys (all 64 lanes must call it)
-__device__ int wave_key_cmp(const u8* T, const run_tab& R, const u32* S, const u32* KL, u32 a, u32 b, u32 lane) {
+__device__ int wave_key_cmp(const u8* T, const run_tab& R, const pos_t* S, const pos_t* KL, u32 a, u32 b, u32 lane) {
     const u64 la = KL[a], lb = KL[b], m = min(la, lb);
     const u64 pa = S[a], pb = S[b];
     const u64 c = wave_lce_fwd(T, R, pa, pb, m, lane);
@@ -196,7 +196,7 @@ __device__ int wave_key_cmp(const u8* T, const run_tab& R, const u32* S, const u
     return la < lb ? -1 : (la > lb ? 1 : 0);
 }
 // flags: new group where the hash changes; exact check of equal-hash neighbours
-__global__ __launch_bounds__(256) void k_group_verify(const u8* T, run_tab R, const u32* S, const u32* KL,
+__global__ __launch_bounds__(256) void k_group_verify(const u8* T, run_tab R, const pos_t* S, const pos_t* KL,
                                                       const u64* __restrict__ Hs, const u32* __restrict__ idx,
                                                       u32 s, u32* __restrict__ flag, u32* __restrict__ collide) {
     const u64 t = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -221,7 +221,7 @@ __global__ void k_reps(const u32* __restrict__ flag, const u32* __restrict__ grp
 // (LSD: one stable 64-bit radix pass per word); keys equal on that prefix form
 // tie segments finished by exact wave comparisons below
 constexpr u32 PRESORT_WORDS = 4;
-__global__ void k_prefix_ties(const u8* __restrict__ T, const u32* __restrict__ S, const u32* __restrict__ KL,
+__global__ void k_prefix_ties(const u8* __restrict__ T, const pos_t* __restrict__ S, const pos_t* __restrict__ KL,
                               const u32* __restrict__ srt, u32 d, u8* __restrict__ tie) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= d) return;
@@ -244,7 +244,7 @@ __global__ void k_seg_units(const u32* __restrict__ sbeg, u32 nseg, u32 opw, u32
     if (k < nseg) units[k] = (sbeg[k + 1] - sbeg[k] + opw - 1) / opw;
     if (k == nseg) units[k] = 0;  // exclusive scan over nseg + 1 -> uoff[nseg] = total
 }
-__global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const u32* S, const u32* KL,
+__global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const pos_t* S, const pos_t* KL,
                                                   const u32* __restrict__ sbeg, const u32* __restrict__ uoff, u32 nseg,
                                                   u32 nunits, const u32* __restrict__ in, u32* __restrict__ out, u32 w,
                                                   u32 opw) {
@@ -408,8 +408,8 @@ void engine::build_sa_s(const u8* T) {
     (void)sa_dbg_t;
     nlev_rank = 0;
     if (s == 0) return;
-    const u32* dS = S.p;
-    u32* KL = key_len.get(s);
+    const pos_t* dS = S.p;
+    pos_t* KL = key_len.get(s);
     const unsigned g = cdiv(s, 256);
     k_key_len<<<g, 256, 0, st>>>(dS, s, n, KL);
     // ---- R_0: lexicographic rank of the keys (equal keys share a rank)
@@ -624,4 +624,4 @@ lce_view engine::view(const u8* T) const {
     return L;
 }
 
-}  // namespace lz
+}  // namespace LZ_NS

@@ -28,7 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 
-namespace lz {
+namespace LZ_NS {
 
 // ---------------------------------------------------------------------------
 // Q anchors.  A workgroup of 256 lanes covers anchors tb-1 .. tb+254 (lane i ->
@@ -43,8 +43,8 @@ constexpr u32 RUN_LCAP = 256;
 
 __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__ T, u64 n, u64 nanch,
                                                           u16* __restrict__ qinfo, u32* __restrict__ any_q,
-                                                          u8* __restrict__ run_p, u32* __restrict__ run_hi,
-                                                          u32* __restrict__ run_lo, u8* __restrict__ run_cap) {
+                                                          u8* __restrict__ run_p, pos_t* __restrict__ run_hi,
+                                                          pos_t* __restrict__ run_lo, u8* __restrict__ run_cap) {
     // LDS text with one pad word per 128 bytes: the anchors of a wave sit 128 bytes
     // apart, so unpadded their accesses would all hit the same bank
     __shared__ __attribute__((aligned(16))) u32 b32[QT_LDS / 4 + QT_LDS / 128 + 2];
@@ -249,7 +249,8 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
     // ---- 3. owned anchors: Q interval on (a-128, a] and the local run extent
     if (i >= 1 && i <= QT_OWN && (u64)t < nanch) {
         u16 res = 0xFF00;  // empty interval
-        u32 rp = 0, rhi = 0, rlo = 0;
+        u32 rp = 0;
+        pos_t rhi = 0, rlo = 0;
         u8 rcap = 0;
         const u32 p = per;
         if (p) {
@@ -275,21 +276,21 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
             // inside a chain of same-period anchors the values only need to mark the chain
             rp = p;
             if (contf) {
-                rhi = (u32)(a + RUN_HCAP);
+                rhi = (pos_t)(a + RUN_HCAP);
                 rcap |= 1;
             } else {
                 const u64 h2_cap = min(a + RUN_HCAP - p, n - p);
                 const u64 h2 = hi < hi_cap ? hi : (u64)(base + ext_fwd(o_hi, (int)((int64_t)h2_cap - base), (int)p));
-                rhi = (u32)(h2 + p);
+                rhi = (pos_t)(h2 + p);
                 rcap |= h2 == a + RUN_HCAP - p ? 1 : 0;
             }
             if (contb) {
-                rlo = (u32)(a >= RUN_LCAP ? a - RUN_LCAP : a - QA);
+                rlo = (pos_t)(a >= RUN_LCAP ? a - RUN_LCAP : a - QA);
                 rcap |= 2;
             } else {
                 const u64 l2_cap = a >= RUN_LCAP ? a - RUN_LCAP : 0;
                 const u64 l2 = (lo > lo_cap) ? lo : (u64)(base + ext_bwd(o_lo, (int)((int64_t)l2_cap - base), (int)p));
-                rlo = (u32)l2;
+                rlo = (pos_t)l2;
                 rcap |= (l2 == a - RUN_LCAP && a >= RUN_LCAP) ? 2 : 0;
             }
         }
@@ -309,7 +310,9 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
 // run chains: anchor t continues into t+1 (same run) when both have period p
 // and t's run covers t+1's window; a chain's exact hi is its last anchor's local
 // hi (exact unless capped), its exact lo its first anchor's local lo.
-__global__ void k_run_elems(const u8* __restrict__ rp, const u32* __restrict__ rhi, const u32* __restrict__ rlo,
+// an unknown run start reads as larger than every position (lce_dev.h: "lo > x" skips the jump)
+constexpr u64 RUN_LO_UNKNOWN = sizeof(pos_t) == 4 ? 0xFFFFFFFFull : (1ull << 62);
+__global__ void k_run_elems(const u8* __restrict__ rp, const pos_t* __restrict__ rhi, const pos_t* __restrict__ rlo,
                             const u8* __restrict__ rcap, u64 na, u64* __restrict__ ehi_rev, u64* __restrict__ elo) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= na) return;
@@ -317,10 +320,10 @@ __global__ void k_run_elems(const u8* __restrict__ rp, const u32* __restrict__ r
     const u64 a = t * QA;
     const bool cont_f = p && t + 1 < na && rp[t + 1] == p && (u64)rhi[t] >= a + QA + QM;
     const bool cont_b = p && t >= 1 && rp[t - 1] == p && (u64)rlo[t] + QA <= a;
-    u64 vh = 0, vl = 0xFFFFFFFFull;
+    u64 vh = 0, vl = RUN_LO_UNKNOWN;
     if (p) {
         vh = (!cont_f && (rcap[t] & 1)) ? 0 : rhi[t];
-        vl = (!cont_b && (rcap[t] & 2)) ? 0xFFFFFFFFull : rlo[t];
+        vl = (!cont_b && (rcap[t] & 2)) ? RUN_LO_UNKNOWN : rlo[t];
     }
     ehi_rev[na - 1 - t] = ((u64)(!cont_f) << 63) | vh;
     elo[t] = ((u64)(!cont_b) << 63) | vl;
@@ -329,11 +332,11 @@ struct last_marked {
     __device__ __forceinline__ u64 operator()(const u64& x, const u64& y) const { return (y >> 63) ? y : x; }
 };
 __global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restrict__ slo, u64 na,
-                             u32* __restrict__ rhi, u32* __restrict__ rlo) {
+                             pos_t* __restrict__ rhi, pos_t* __restrict__ rlo) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= na) return;
-    rhi[t] = (u32)shi_rev[na - 1 - t];
-    rlo[t] = (u32)slo[t];
+    rhi[t] = (pos_t)(shi_rev[na - 1 - t] & ~(1ull << 63));
+    rlo[t] = (pos_t)(slo[t] & ~(1ull << 63));
 }
 
 // ---------------------------------------------------------------------------
@@ -405,7 +408,7 @@ __device__ __forceinline__ u32 wave_suffix_min(u32 v, u32 lane) {  // inclusive,
 template <bool QSKIP>
 __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict__ T, u64 n, u64 last_i,
                                                            const u16* __restrict__ qinfo, u64 nstripes,
-                                                           u32* __restrict__ s_out, u32* __restrict__ s_cnt,
+                                                           pos_t* __restrict__ s_out, u32* __restrict__ s_cnt,
                                                            u32* __restrict__ s_flag, u32* __restrict__ any_flag,
                                                            u32 b, sss_pow32 PW, u32 scap) {
     const u32 lane = threadIdx.x & 63;
@@ -523,7 +526,7 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
     bool hvalid = true;  // the prefix hash carry continues the last computed block
     phi_or_inf(fA, 0, hA, hB, qa, xA);
     u32 nout = 0;       // outputs of this stripe so far (uniform)
-    u32* out = s_out + w * SCAP;
+    pos_t* out = s_out + w * SCAP;
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
     // one decision block: x = Phi'(block c) (in), y = Phi'(block c+1) (out),
     // h0 = Hp(block c+1) (in), h1 <- Hp(block c+2); B = bytes of block c+2
@@ -568,13 +571,13 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict
         if (U) {
             // ordered emission (lanes ascending, then e) by a scalar loop over the
             // few emitting lanes (~2 per block)
-            const u32 base = (u32)(i0 + c * TAU);
+            const pos_t base = (pos_t)(i0 + c * TAU);
             for (u64 u = U; u; u &= u - 1) {
                 const u32 L = (u32)__builtin_ctzll(u);
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
                     if ((M[e] >> L) & 1) {
-                        const u32 pos = base + 8 * L + e;
+                        const pos_t pos = base + 8 * L + e;
                         if ((u64)pos - i0 <= ilim) {
                             if (lane == 0 && nout < (u32)SCAP) out[nout] = pos;
                             nout++;
@@ -612,7 +615,7 @@ constexpr int FB_T = 256;
 constexpr int FB_DEC = SD / FB_T;  // decisions per thread (128)
 __global__ __launch_bounds__(FB_T) void k_sss_fallback(const u8* __restrict__ T, u64 n, u64 last_i,
                                                        const u16* __restrict__ qinfo, const u32* __restrict__ lanes,
-                                                       u32* __restrict__ scratch, u32* __restrict__ ovf_out,
+                                                       u32* __restrict__ scratch, pos_t* __restrict__ ovf_out,
                                                        u32* __restrict__ lane_cnt, u32 b, u32 bpow) {
     __shared__ u32 s_cnt[FB_T];
     const u64 lane = lanes[blockIdx.x];
@@ -683,20 +686,20 @@ __global__ __launch_bounds__(FB_T) void k_sss_fallback(const u8* __restrict__ T,
     }
     __syncthreads();
     u32 o = s_cnt[t];
-    u32* out = ovf_out + (u64)blockIdx.x * SD;
+    pos_t* out = ovf_out + (u64)blockIdx.x * SD;
 #pragma unroll
     for (int w = 0; w < FB_DEC / 32; w++)
-        for (u32 bits = mask[w]; bits; bits &= bits - 1) out[o++] = (u32)(i0 + d0 + 32 * w + __builtin_ctz(bits));
+        for (u32 bits = mask[w]; bits; bits &= bits - 1) out[o++] = (pos_t)(i0 + d0 + 32 * w + __builtin_ctz(bits));
 }
 
-__global__ void k_sss_compact(const u32* __restrict__ lane_out, const u32* __restrict__ lane_cnt,
+__global__ void k_sss_compact(const pos_t* __restrict__ lane_out, const u32* __restrict__ lane_cnt,
                               const u32* __restrict__ lane_off, const u32* __restrict__ lane_flag,
-                              const u32* __restrict__ ovf_slot, const u32* __restrict__ ovf_out, u64 nlanes,
-                              u32* __restrict__ S) {
+                              const u32* __restrict__ ovf_slot, const pos_t* __restrict__ ovf_out, u64 nlanes,
+                              pos_t* __restrict__ S) {
     const u64 lane = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= nlanes) return;
     const u32 c = lane_cnt[lane], o = lane_off[lane];
-    const u32* src = lane_flag[lane] ? ovf_out + (u64)ovf_slot[lane] * SD : lane_out + lane * SCAP;
+    const pos_t* src = lane_flag[lane] ? ovf_out + (u64)ovf_slot[lane] * SD : lane_out + lane * SCAP;
     for (u32 x = 0; x < c; x++) S[o + x] = src[x];
 }
 
@@ -723,8 +726,8 @@ void engine::build_sss(const u8* T) {
     u32* ctr = counters.get(16);
     LZ_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st));
     u8* rp = run_p.get(nanch);
-    u32* rhi = run_hi.get(nanch);
-    u32* rlo = run_lo.get(nanch);
+    pos_t* rhi = run_hi.get(nanch);
+    pos_t* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
     k_q_anchors<<<cdiv(nanch, QT_OWN), QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap);
     LZ_HIP(hipGetLastError());
@@ -744,7 +747,7 @@ void engine::build_sss(const u8* T) {
 
     const bool any_q = rd1(ctr, st) != 0;  // picks the stream kernel's instantiation
     const u64 nlanes = last_i / SD + 1;  // stripes
-    u32* lo = lane_out.get(nlanes * SCAP);
+    pos_t* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
     sss_pow32 PW;
@@ -781,7 +784,7 @@ void engine::build_sss(const u8* T) {
 
     // overflowing tiles -> exact slow path
     u32* ovf_slot = u32c.get(nlanes);
-    u32* ovf_out = nullptr;
+    pos_t* ovf_out = nullptr;
     if (h_ctr[1]) {
         std::vector<u32> hf(nlanes);
         LZ_HIP(hipMemcpy(hf.data(), lf, nlanes * sizeof(u32), hipMemcpyDeviceToHost));
@@ -792,7 +795,7 @@ void engine::build_sss(const u8* T) {
         LZ_HIP(hipMemcpy(d_lanes, lanes.data(), lanes.size() * 4, hipMemcpyHostToDevice));
         LZ_HIP(hipMemcpy(ovf_slot, slot.data(), nlanes * 4, hipMemcpyHostToDevice));
         u32* scratch = (u32*)u64a.get((lanes.size() * 3 * (SD + TAU) + 1) / 2);
-        ovf_out = u32b.get(lanes.size() * SD);
+        ovf_out = sss_ovf.get(lanes.size() * SD);
         k_sss_fallback<<<(unsigned)lanes.size(), FB_T, 0, st>>>(T, n, last_i, qi, d_lanes, scratch, ovf_out, lc,
                                                                 (u32)SSS_BASE, bpow);
         LZ_HIP(hipGetLastError());
@@ -810,12 +813,13 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipMemsetAsync(lc + nlanes, 0, sizeof(u32), st));
     LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, lc, off, (int)(nlanes + 1), st));
     s = rd1(off + nlanes, st);
-    sss_kernel_bytes = n + 4ull * s;
-    u32* dS = S.get((u64)s + 1);
+    sss_kernel_bytes = n + sizeof(pos_t) * (u64)s;
+    pos_t* dS = S.get((u64)s + 1);
     k_sss_compact<<<cdiv(nlanes, 256), 256, 0, st>>>(lo, lc, off, lf, ovf_slot, ovf_out, nlanes, dS);
     LZ_HIP(hipGetLastError());
 }
 
+#ifndef LZ_POS64  // the u32 engine's windowed 64-bit sync set (the u64 engine builds S directly)
 // ---------------------------------------------------------------------------
 // pos_t = uint64_t sync set of a decision range (lce_sss.hpp:53 instantiated with
 // pos_t = uint64_t, lz77_sss.hpp:72-75).  Phi and Q are functions of window contents
@@ -888,4 +892,6 @@ void engine::build_sss_range(u64 first, u64 end, u64 base, u64 window) {
     LZ_HIP(hipStreamSynchronize(st));
 }
 
-}  // namespace lz
+#endif
+
+}  // namespace LZ_NS

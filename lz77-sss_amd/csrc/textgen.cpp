@@ -10,6 +10,7 @@
 //    the string the reference would produce for that random_device value.
 //  * lz77sss_gen_genome: a "chr19-style" text: a random ACGT
 //    base block, repeated with independent point mutations per copy.
+#include "../../include/lz77sss.h"
 #include "../include/lz77sss_internal.h"
 
 #include <algorithm>
@@ -17,6 +18,8 @@
 #include <cstdint>
 #include <cstring>
 #include <random>
+#include <thread>
+#include <vector>
 
 extern "C" {
 
@@ -82,4 +85,67 @@ LZ77SSS_API int64_t lz77sss_gen_genome(uint64_t n, uint64_t base_len, double mut
     return (int64_t)n;
 }
 
+// the position-hashed chr19-style text of lz77sss_session_gen_genome, on the host
+// (same bytes: byte p is a function of (p, seed) only), so the oracle can check a
+// text the device generated in HBM
+static inline uint64_t gen_mix_host(uint64_t x) {  // splitmix64 finalizer
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+LZ77SSS_API int lz77sss_gen_genome_pos(uint64_t n, uint64_t base_len, double mut_rate, uint32_t seed, uint64_t offset,
+                                       uint8_t* out) {
+    if ((!out && n) || base_len == 0 || !(mut_rate >= 0.0 && mut_rate <= 1.0)) return LZ77SSS_EINVAL;
+    const uint64_t thr = mut_rate >= 1.0 ? ~0ull : (uint64_t)(mut_rate * 18446744073709551616.0);
+    auto part = [&](uint64_t a, uint64_t b) {
+        for (uint64_t i = a; i < b; i++) {
+            const uint64_t p = offset + i;
+            uint32_t c = (uint32_t)(gen_mix_host((p % base_len) ^ ((uint64_t)seed << 40)) >> 62);
+            if (p >= base_len) {
+                const uint64_t h = gen_mix_host(p ^ ((uint64_t)seed * 0xD6E8FEB86659FD93ull) ^ 0x5851F42D4C957F2Dull);
+                if (h < thr) c = (c + 1 + (uint32_t)((h >> 7) % 3)) & 3;
+            }
+            out[i] = (uint8_t)"ACGT"[c];
+        }
+    };
+    const uint64_t nt = std::max<uint64_t>(1, std::min<uint64_t>(16, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    const uint64_t chunk = (n + nt - 1) / nt;
+    for (uint64_t t = 0; t < nt; t++) {
+        const uint64_t a = std::min(n, t * chunk), b = std::min(n, a + chunk);
+        if (a < b) th.emplace_back(part, a, b);
+    }
+    for (auto& x : th) x.join();
+    return LZ77SSS_OK;
+}
+
 }  // extern "C"
+
+// lz77_sss<uint64_t>::factor stream form (include/lz77_sss/lz77_sss.hpp:149-173): the low
+// 5 bytes of src, then of len, little endian
+extern "C" __attribute__((visibility("default"))) int lz77sss_serialize_factors64(const lz77sss_factor64* f,
+                                                                                 uint64_t nf, uint8_t* out) {
+    if ((!f || !out) && nf) return LZ77SSS_EINVAL;
+    for (uint64_t k = 0; k < nf; k++) {
+        if ((f[k].src >> 40) || (f[k].len >> 40)) return LZ77SSS_EINVAL;
+        for (int b = 0; b < 5; b++) {
+            out[10 * k + b] = (uint8_t)(f[k].src >> (8 * b));
+            out[10 * k + 5 + b] = (uint8_t)(f[k].len >> (8 * b));
+        }
+    }
+    return LZ77SSS_OK;
+}
+extern "C" __attribute__((visibility("default"))) int lz77sss_deserialize_factors64(const uint8_t* in, uint64_t nf,
+                                                                                   lz77sss_factor64* f) {
+    if ((!f || !in) && nf) return LZ77SSS_EINVAL;
+    for (uint64_t k = 0; k < nf; k++) {
+        uint64_t s = 0, l = 0;
+        for (int b = 0; b < 5; b++) {
+            s |= (uint64_t)in[10 * k + b] << (8 * b);
+            l |= (uint64_t)in[10 * k + 5 + b] << (8 * b);
+        }
+        f[k] = lz77sss_factor64{s, l};
+    }
+    return LZ77SSS_OK;
+}

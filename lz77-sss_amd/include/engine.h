@@ -3,66 +3,33 @@
 #pragma once
 #include "lz77sss_internal.h"
 #include "lce_dev.h"
+#include "timer.h"
 
 #include <array>
 #include <string>
 #include <utility>
 #include <vector>
 
-namespace lz {
+namespace LZ_NS {
 
-struct lpf3 { u32 beg, end, src; };
+struct lpf3 { pos_t beg, end, src; };
 
 // greedy walk segments (csrc/greedy.hip)
 // walk segment input: start position, first phrase index, gap-index state, and
 // the position at or after which the gap walk stops (a chunk boundary; n = none)
-struct seg_in { u32 start, p, idxpos, zmask, lim; };
+struct seg_in { pos_t start; u32 p; pos_t idxpos; u32 zmask; pos_t lim; };
 constexpr int SEG_NBND = 16;  // factor starts recorded per gap walk (chunk convergence)
 struct seg_out {
-    u32 next;        // start of the next gap (or n)
-    u32 e;           // end of this segment's gap walk (positions [start, e) inserted)
+    pos_t next;      // start of the next gap (or n)
+    pos_t e;         // end of this segment's gap walk (positions [start, e) inserted)
     u32 nfact;
-    u32 idxpos;      // gap index position after the segment
+    pos_t idxpos;    // gap index position after the segment
     u32 zmask;
     u32 nsingle;     // extra inserted positions (LPF-start queries)
-    u32 single[4];
+    pos_t single[4];
     u32 flags;       // 1: reached the tail region, 2: single overflow
     u32 nbnd;        // recorded factor starts of the first gap walk
-    u32 bnd[SEG_NBND];
-};
-
-struct phase_timer {
-    hipStream_t st = nullptr;
-    std::vector<std::pair<std::string, hipEvent_t>> marks;
-    bool on = false;
-    void begin(hipStream_t s) {
-        st = s;
-        clear();
-        mark("start");
-    }
-    void mark(const char* name) {
-        hipEvent_t e;
-        LZ_HIP(hipEventCreate(&e));
-        LZ_HIP(hipEventRecord(e, st));
-        marks.emplace_back(name, e);
-    }
-    void clear() {
-        for (auto& m : marks) (void)hipEventDestroy(m.second);
-        marks.clear();
-    }
-    // (name, ms since previous mark)
-    std::vector<std::pair<std::string, double>> read() {
-        std::vector<std::pair<std::string, double>> out;
-        if (marks.empty()) return out;
-        LZ_HIP(hipEventSynchronize(marks.back().second));
-        for (size_t i = 1; i < marks.size(); i++) {
-            float ms = 0;
-            LZ_HIP(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));
-            out.emplace_back(marks[i].first, ms);
-        }
-        return out;
-    }
-    ~phase_timer() { clear(); }
+    pos_t bnd[SEG_NBND];
 };
 
 struct engine {
@@ -74,8 +41,10 @@ struct engine {
 
     // ---- string synchronizing set ----
     dbuf<u16> q_info;          // per anchor: Q interval (start<<8 | end) of (a-128, a]
-    dbuf<u32> lane_out, lane_cnt, lane_flag;
-    dbuf<u32> S;               // sync positions (sorted)
+    dbuf<pos_t> lane_out;      // per-stripe sync positions (k_sss_stream)
+    dbuf<u32> lane_cnt, lane_flag;
+    dbuf<pos_t> sss_ovf;       // fallback outputs
+    dbuf<pos_t> S;             // sync positions (sorted)
     dbuf<u32> counters;        // small scratch counters
     u32 s = 0;
     bool has_runs = false;
@@ -83,7 +52,7 @@ struct engine {
     u64 sss_kernel_bytes = 0;  // its algorithmic bytes (text + 4|S|) per launch
     u64 stats_fallback_lanes = 0;
     dbuf<u8> run_p;            // periodic-run table per Q anchor (lce_dev.h run_tab)
-    dbuf<u32> run_hi, run_lo;
+    dbuf<pos_t> run_hi, run_lo;
     dbuf<u64> run_scan_a, run_scan_b;
     bool runs_valid = false;
     // pos_t = uint64_t sync set of a decision range (build_sss_range): any n, windowed
@@ -98,7 +67,8 @@ struct engine {
     }
 
     // ---- suffix order of sync positions / LCE ----
-    dbuf<u32> SA, ISA, LCP, key_len;
+    dbuf<u32> SA, ISA, LCP;
+    dbuf<pos_t> key_len;
     dbuf<u32> rank_lv[MAX_LV];       // R_h per doubling level (for LCP binary lifting)
     dbuf<u32> lcp_rmq[MAX_LV];       // sparse table levels over LCP
     u32 nlev_rank = 0, nlev_rmq = 0;
@@ -113,19 +83,22 @@ struct engine {
     dbuf<u32> sa_min[MAX_LV];        // sparse table over SA (PSV/NSV)
     dbuf<u32> jump[MAX_LV];          // pointer-doubling tables (skip chain)
     dbuf<u32> PSV, NSV;
-    dbuf<u32> cand;                  // per sync index candidate data
-    dbuf<u32> lpf;                   // phrases as (beg,end,src) triples + sentinel
+    dbuf<pos_t> cand;                // per sync index candidate data
+    dbuf<pos_t> p_Em, p_lst, p_ph3;  // running max_end scan and phrase scratch (csrc/lpf.hip)
+    dbuf<pos_t> lpf;                 // phrases as (beg,end,src) triples + sentinel
     u32 num_phr = 0;
 
     // ---- greedy ----
-    dbuf<u32> fact;                  // output factors (src,len) pairs
+    dbuf<pos_t> fact;                // output factors (src,len) pairs
     dbuf<u8> tmp_greedy, chunk_buf, chunk_buf2, rem_buf;
-    dbuf<u32> add_keys32, add_pos, dirty_in, dirty_out, dirty_sorted, seg_lo, seg_hi;
+    dbuf<u32> add_keys32;
+    dbuf<pos_t> add_pos, dirty_in, dirty_out, dirty_sorted;
     dbuf<u8> tmp_greedy2, tmp_greedy3;
     dbuf<u64> add_keys, add_keys2;
     dbuf<seg_in> seg_in_buf;
     dbuf<seg_out> seg_out_buf;
-    dbuf<u32> seg_ids, ist, iend, irank, ekeys, evals, ekeys2, evals2, ipos_buf, occ_buf, tail_ins_buf;
+    dbuf<u32> seg_ids, irank, ekeys, evals, ekeys2, evals2, occ_buf;
+    dbuf<pos_t> ist, iend, ipos_buf, tail_ins_buf;
     dbuf<u64> seg_offs, counters64;
     // device-resident greedy orchestration (csrc/greedy.hip)
     dbuf<seg_in> g_sin;
@@ -133,9 +106,11 @@ struct engine {
     dbuf<u8> g_valid, g_cs, g_tailc;
     bool seg_at_clean = false;  // g_seg_at is all NONE
     u64 seg_at_n = 0;
-    dbuf<u32> g_succ, g_seg_at, g_cbv, g_ids, g_chain, g_dist[2];
+    dbuf<u32> g_succ, g_seg_at, g_ids, g_chain, g_dist[2];
+    dbuf<pos_t> g_cbv;
     dbuf<u32> g_bmI, g_bmI2, g_bmIb, g_bmT;
-    dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_tmp8, g_ast, g_aen, g_ark;
+    dbuf<u32> g_tmp1, g_tmp2, g_tmp3, g_tmp4, g_tmp5, g_tmp6, g_tmp7, g_tmp8, g_ark;
+    dbuf<pos_t> g_ast, g_aen;
     dbuf<u64> g_offs;
     // LPF/LNF mode (csrc/lnf.hip)
     dbuf<u32> l_V, l_b, l_d, l_e, l_r, l_sflag_lnf, l_slots_lnf, l_sflag, l_slots, l_off, l_P, l_Q;
@@ -145,8 +120,9 @@ struct engine {
     dbuf<u64> g_bsum, g_bincl, g_pbtmp;
     dbuf<u32> g_pbcur;  // predecessor bucket scatter
     dbuf<u32> g_pbm, g_pwp, g_pcnt, g_sdk, g_dstart, g_pflag;  // dense slot ids of the base set  // per-block bitmap counts and their inclusive scan
-    dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32, g_xpos;
-    dbuf<u32> g_H;      // materialized gap-index table of the sequential completion
+    dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32;
+    dbuf<pos_t> g_xpos;
+    dbuf<pos_t> g_H;    // materialized gap-index table of the sequential completion
     dbuf<u8> g_cut;     // chain_cut + completion counters
     dbuf<u64> g_xk, g_xk2;
     // exact mode (csrc/exact.hip)
@@ -155,7 +131,8 @@ struct engine {
     const u32* sa_full = nullptr;    // suffix array of the text (x_sa) after build_sa_full
     u32 x_rounds = 0;
     // device decode (csrc/decode.hip)
-    dbuf<u32> dec_fid, dec_ref, dec_ref2;
+    dbuf<u32> dec_fid, dec_fid2;
+    dbuf<pos_t> dec_ref, dec_ref2;
     dbuf<u64> dec_len64, dec_start64;
     dbuf<u8> dec_out;
     u32 dec_rounds = 0;
@@ -195,7 +172,7 @@ struct engine {
     u64 huffman_container();  // csrc/huffman.hip
     void build_sa_full(const u8* T);
     u64 factorize_exact(bool log);  // csrc/exact.hip
-    u64 decode_device(const u32* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
+    u64 decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
     lce_view view(const u8* T) const;
 };
 
@@ -209,4 +186,4 @@ static inline T rd1(const T* dptr, hipStream_t st) {
 }
 static inline unsigned cdiv(u64 a, u64 b) { return (unsigned)((a + b - 1) / b); }
 
-}  // namespace lz
+}  // namespace LZ_NS

@@ -8,9 +8,10 @@
 #pragma once
 #include "lz77sss_internal.h"
 
-namespace lz {
+namespace LZ_NS {
 
 constexpr int MAX_LV = 32;
+constexpr u32 LCP_SAT = 0xFFFFFFFFu;  // stored LCP values saturate here (pos_t = uint64_t only)
 
 // Periodic runs seen by the Q anchors (csrc/sss.hip): for anchor t (position
 // 128t) whose window T[128t..128t+340) has smallest period p <= 170: p[t] = p,
@@ -22,8 +23,8 @@ constexpr int MAX_LV = 32;
 // ends are at different offsets.
 struct run_tab {
     const u8* p = nullptr;
-    const u32* hi = nullptr;
-    const u32* lo = nullptr;
+    const pos_t* hi = nullptr;
+    const pos_t* lo = nullptr;
 };
 
 // exact LCE of T[i..] and T[j..], at most lim (caller guarantees i+lim, j+lim <= n)
@@ -118,7 +119,7 @@ struct lce_view {
     const u8* T;
     u64 n;
     u32 s;
-    const u32* S;
+    const pos_t* S;
     const u32* ISA;
     const u32* succ;  // bucket (x >> 9) -> first sync index with S >= bucket*512
     u32 nlev;
@@ -160,7 +161,10 @@ __device__ __forceinline__ u64 dev_lce(const lce_view& L, u64 i, u64 j) {
             const u64 e = dev_lce_fwd(L.T, L.R, l + c, r + c, dl - c);
             if (e < dl - c) return c + e;
         }
-        return dl + dev_lce_sync(L, kl, kr);
+        const u64 v = dev_lce_sync(L, kl, kr);
+        if (sizeof(pos_t) > 4 && v == LCP_SAT)  // saturated LCP: finish by comparison
+            return dl + v + dev_lce_fwd(L.T, L.R, l + dl + v, r + dl + v, lmax - dl - v);
+        return dl + v;
     }
     const u64 bound = min(min(dl, dr) + 2 * TAU - 1, lmax);
     if (bound > c) c += dev_lce_fwd(L.T, L.R, l + c, r + c, bound - c);
@@ -169,10 +173,10 @@ __device__ __forceinline__ u64 dev_lce(const lce_view& L, u64 i, u64 j) {
 
 // leftward LCE, exact semantics of lce_l_64 (include/lz77_sss/algorithms/lce_l.hpp:33-83):
 // min(cap', #equal chars going left from i and j), cap' = min(cap, min(i,j)+1)
-__device__ __forceinline__ u32 dev_lce_left(const u8* T, const run_tab& R, u32 i, u32 j, u32 cap) {
-    const u32 cp = min(cap, min(i, j) + 1);
+__device__ __forceinline__ pos_t dev_lce_left(const u8* T, const run_tab& R, pos_t i, pos_t j, pos_t cap) {
+    const pos_t cp = min(cap, (pos_t)(min(i, j) + 1));
     if (i == j) return cp;
-    return (u32)dev_lce_bwd(T, R, i, j, cp);
+    return (pos_t)dev_lce_bwd(T, R, i, j, cp);
 }
 
-}  // namespace lz
+}  // namespace LZ_NS

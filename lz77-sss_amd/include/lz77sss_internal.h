@@ -98,6 +98,28 @@ __device__ inline void block_min(u32* acc, u32 v) {
     __syncthreads();
 }
 
+// 64-bit forms of block_add / block_min (sums and positions past 2^32)
+__device__ inline void block_add64(u64* acc, u64 v) {
+    __shared__ u64 s_sum64;
+    if (threadIdx.x == 0) s_sum64 = 0;
+    __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd((unsigned long long*)&s_sum64, (unsigned long long)v);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_sum64) atomicAdd((unsigned long long*)acc, (unsigned long long)s_sum64);
+    __syncthreads();
+}
+__device__ inline void block_min64(u64* acc, u64 v) {
+    __shared__ u64 s_min64;
+    if (threadIdx.x == 0) s_min64 = ~0ull;
+    __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (u64)__shfl_down(v, o, 64));
+    if ((threadIdx.x & 63) == 0 && v != ~0ull) atomicMin((unsigned long long*)&s_min64, (unsigned long long)v);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_min64 != ~0ull) atomicMin((unsigned long long*)acc, (unsigned long long)s_min64);
+    __syncthreads();
+}
+
 struct error : std::runtime_error {
     int code;
     error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
@@ -182,4 +204,26 @@ __device__ __forceinline__ u64 dev_naive_lce(const u8* T, u64 a, u64 b, u64 lim)
 }
 
 }  // namespace lz
+
+// The approximate-factorization pipeline is compiled twice (Makefile): once with
+// pos_t = uint32_t in namespace lz, and once with -DLZ_POS64, pos_t = uint64_t in
+// namespace lz64 (lz77_sss<pos_t> with pos_t in {uint32_t, uint64_t},
+// include/lz77_sss/lz77_sss.hpp:72-75).  Text positions and lengths are pos_t;
+// sync indices, ranks, segment and entry ids stay 32-bit.
+#ifdef LZ_POS64
+#define LZ_NS lz64
+namespace lz64 {
+using namespace lz;
+using pos_t = uint64_t;
+}  // namespace lz64
+#else
+#define LZ_NS lz
+namespace lz {
+using pos_t = uint32_t;
+}  // namespace lz
+#endif
+namespace LZ_NS {
+constexpr pos_t POS_NONE = ~(pos_t)0;
+constexpr u64 POS_MAX_N = sizeof(pos_t) == 4 ? 0xFFFFFFF0ull : (1ull << 40);  // largest supported n
+}  // namespace LZ_NS
 #endif

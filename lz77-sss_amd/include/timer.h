@@ -1,0 +1,45 @@
+// timer.h -- hipEvent phase timer shared by the pos_t = uint32_t and uint64_t engines.
+#pragma once
+#include "lz77sss_internal.h"
+
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace lz {
+
+struct phase_timer {
+    hipStream_t st = nullptr;
+    std::vector<std::pair<std::string, hipEvent_t>> marks;
+    bool on = false;
+    void begin(hipStream_t s) {
+        st = s;
+        clear();
+        mark("start");
+    }
+    void mark(const char* name) {
+        hipEvent_t e;
+        LZ_HIP(hipEventCreate(&e));
+        LZ_HIP(hipEventRecord(e, st));
+        marks.emplace_back(name, e);
+    }
+    void clear() {
+        for (auto& m : marks) (void)hipEventDestroy(m.second);
+        marks.clear();
+    }
+    // (name, ms since previous mark)
+    std::vector<std::pair<std::string, double>> read() {
+        std::vector<std::pair<std::string, double>> out;
+        if (marks.empty()) return out;
+        LZ_HIP(hipEventSynchronize(marks.back().second));
+        for (size_t i = 1; i < marks.size(); i++) {
+            float ms = 0;
+            LZ_HIP(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));
+            out.emplace_back(marks[i].first, ms);
+        }
+        return out;
+    }
+    ~phase_timer() { clear(); }
+};
+
+}  // namespace lz

@@ -1,13 +1,13 @@
 """Python mirror of the reference API over the C-ABI of liblz77sss_hip.so.
 
-Mirrors ``lz77_sss<uint32_t>`` (include/lz77_sss/lz77_sss.hpp:72-203 of
-LukasNalbach/lz77-sss):
+Mirrors ``lz77_sss<pos_t>`` for pos_t in {uint32_t, uint64_t} (include/lz77_sss/lz77_sss.hpp:72-203
+of LukasNalbach/lz77-sss; ``pos64=True`` selects uint64_t, which texts past 2^32 - 16 bytes need):
 
 * ``factorize_approximate(text, fact_mode=GREEDY, phr_mode=LPF_OPT, ...)``
   <- ``lz77_sss<>::factorize_approximate<fact_mode, phr_mode, tau>`` (:176-186)
 * ``decode(factors, n)`` <- ``lz77_sss<>::decode`` (:202-203, algorithms/common.cpp:31-54)
-* factors are an ``(z, 2)`` uint32 array of ``(src, len)`` = ``lz77_sss<>::factor``
-  (:129-147); a literal has ``len == 0`` and ``src`` = the byte.
+* factors are an ``(z, 2)`` uint32 (uint64 for pos64) array of ``(src, len)`` =
+  ``lz77_sss<>::factor`` (:129-147); a literal has ``len == 0`` and ``src`` = the byte.
 
 There is no CPU fallback: if the HIP library or a gfx950 device is missing,
 every compute call raises ``Lz77SssError``.
@@ -46,6 +46,16 @@ _SYMBOLS = {
     "lz77sss_default_params": (None, [ctypes.POINTER(Params)]),
     "lz77sss_factorize_approx_u32": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), _P, _P]),
     "lz77sss_factorize_exact_u32": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), ctypes.c_int, _P, _P]),
+    "lz77sss_factorize_approx_u64": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), _P, _P]),
+    "lz77sss_factorize_exact_u64": (ctypes.c_int, [_P, _U64, ctypes.POINTER(Params), ctypes.c_int, _P, _P]),
+    "lz77sss_decode_u64": (ctypes.c_int, [_P, _U64, _P, _U64]),
+    "lz77sss_decode_u64_device": (ctypes.c_int, [_P, _U64, _P, _U64, ctypes.c_int]),
+    "lz77sss_serialize_factors64": (ctypes.c_int, [_P, _U64, _P]),
+    "lz77sss_deserialize_factors64": (ctypes.c_int, [_P, _U64, _P]),
+    "lz77sss_session_create64": (ctypes.c_int, [ctypes.c_int, _U64, ctypes.POINTER(_P)]),
+    "lz77sss_session_is64": (ctypes.c_int, [_P]),
+    "lz77sss_session_get_factors64": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_get_lpf64": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_factorize_exact": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.c_int,
                                                        ctypes.POINTER(_U64)]),
     "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
@@ -73,6 +83,7 @@ _SYMBOLS = {
     "lz77sss_gen_random_repetitive": (ctypes.c_int64, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                        ctypes.c_double, ctypes.c_double, _P, _U64]),
     "lz77sss_gen_genome": (ctypes.c_int64, [_U64, _U64, ctypes.c_double, ctypes.c_uint32, _P]),
+    "lz77sss_gen_genome_pos": (ctypes.c_int, [_U64, _U64, ctypes.c_double, ctypes.c_uint32, _U64, _P]),
     "lz77sss_last_error": (ctypes.c_char_p, []),
     "lz77sss_device_count": (ctypes.c_int, []),
 }
@@ -125,12 +136,14 @@ def params(phr_mode=LPF_OPT, fact_mode=GREEDY, tau=DEFAULT_TAU, rk_seed=42, inde
 class Session:
     """Device-resident session: the text stays in HBM across calls."""
 
-    def __init__(self, max_n: int, device: int = 0):
+    def __init__(self, max_n: int, device: int = 0, pos64: bool = False):
         lib = load_library()
         h = _P()
-        _check(lib.lz77sss_session_create(device, max_n, ctypes.byref(h)))
+        create = lib.lz77sss_session_create64 if pos64 else lib.lz77sss_session_create
+        _check(create(device, max_n, ctypes.byref(h)))
         self._h = h
         self.n = 0
+        self.pos64 = pos64
 
     def close(self):
         if self._h:
@@ -168,6 +181,10 @@ class Session:
         return z.value
 
     def factors(self, z: int) -> np.ndarray:
+        if self.pos64:
+            out = np.empty((max(z, 1), 2), np.uint64)
+            _check(load_library().lz77sss_session_get_factors64(self._h, out.ctypes.data_as(_P), z))
+            return out[:z]
         out = np.empty((max(z, 1), 2), np.uint32)
         _check(load_library().lz77sss_session_get_factors(self._h, out.ctypes.data_as(_P), z))
         return out[:z]
@@ -184,6 +201,8 @@ class Session:
     def sss(self):
         s, r = _U64(), ctypes.c_int()
         _check(load_library().lz77sss_session_sss(self._h, ctypes.byref(s), ctypes.byref(r)))
+        if self.pos64:
+            return self.sync_set64(s.value), bool(r.value)
         out = np.empty(max(s.value, 1), np.uint32)
         _check(load_library().lz77sss_session_get_sss(self._h, out.ctypes.data_as(_P), s.value))
         return out[:s.value], bool(r.value)
@@ -239,6 +258,11 @@ class Session:
 
     def lpf(self) -> np.ndarray:
         c = _U64()
+        if self.pos64:
+            _check(load_library().lz77sss_session_get_lpf64(self._h, None, 0, ctypes.byref(c)))
+            out = np.empty((max(c.value, 1), 3), np.uint64)
+            _check(load_library().lz77sss_session_get_lpf64(self._h, out.ctypes.data_as(_P), c.value, ctypes.byref(c)))
+            return out[:c.value]
         _check(load_library().lz77sss_session_get_lpf(self._h, None, 0, ctypes.byref(c)))
         out = np.empty((max(c.value, 1), 3), np.uint32)
         _check(load_library().lz77sss_session_get_lpf(self._h, out.ctypes.data_as(_P), c.value, ctypes.byref(c)))
@@ -264,10 +288,10 @@ class Session:
 
 
 def factorize_approximate(text, fact_mode=GREEDY, phr_mode=LPF_OPT, tau=DEFAULT_TAU, rk_seed=42, device=0,
-                          log=False) -> np.ndarray:
-    """lz77_sss<>::factorize_approximate: returns the (z, 2) uint32 factor array."""
+                          log=False, pos64=False) -> np.ndarray:
+    """lz77_sss<pos_t>::factorize_approximate: returns the (z, 2) uint32 (pos64: uint64) factor array."""
     a = _as_u8(text)
-    with Session(max(a.size, 1), device) as s:
+    with Session(max(a.size, 1), device, pos64=pos64) as s:
         s.load(a)
         z = s.factorize(phr_mode=phr_mode, fact_mode=fact_mode, tau=tau, rk_seed=rk_seed, device=device, log=log)
         return s.factors(z)
@@ -285,20 +309,39 @@ def factorize_exact(text, transf_mode=None, fact_mode=GREEDY, phr_mode=LPF_OPT, 
 
 
 def decode(factors: np.ndarray, n: int) -> np.ndarray:
-    """lz77_sss<>::decode (host, sequential as in the reference)."""
-    f = np.ascontiguousarray(factors, dtype=np.uint32)
+    """lz77_sss<>::decode (host, sequential as in the reference); uint64 factors use pos_t = uint64_t."""
+    wide = np.asarray(factors).dtype == np.uint64
+    f = np.ascontiguousarray(factors, dtype=np.uint64 if wide else np.uint32).reshape(-1, 2)
     out = np.empty(max(n, 1), np.uint8)
-    _check(load_library().lz77sss_decode_u32(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P), n))
+    fn = load_library().lz77sss_decode_u64 if wide else load_library().lz77sss_decode_u32
+    _check(fn(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P), n))
     return out[:n]
 
 
 def decode_device(factors: np.ndarray, n: int, device: int = 0) -> np.ndarray:
     """Same as decode, on the device (pointer jumping, csrc/decode.hip)."""
-    f = np.ascontiguousarray(factors, dtype=np.uint32).reshape(-1, 2)
+    wide = np.asarray(factors).dtype == np.uint64
+    f = np.ascontiguousarray(factors, dtype=np.uint64 if wide else np.uint32).reshape(-1, 2)
     out = np.empty(max(n, 1), np.uint8)
-    _check(load_library().lz77sss_decode_u32_device(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P), n,
-                                                     device))
+    fn = load_library().lz77sss_decode_u64_device if wide else load_library().lz77sss_decode_u32_device
+    _check(fn(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P), n, device))
     return out[:n]
+
+
+def serialize_factors64(factors: np.ndarray) -> bytes:
+    """The reference's pos_t = uint64_t factor stream: 5 + 5 bytes per factor (lz77_sss.hpp:149-173)."""
+    f = np.ascontiguousarray(factors, dtype=np.uint64).reshape(-1, 2)
+    out = np.empty(max(10 * f.shape[0], 1), np.uint8)
+    _check(load_library().lz77sss_serialize_factors64(f.ctypes.data_as(_P), f.shape[0], out.ctypes.data_as(_P)))
+    return out[:10 * f.shape[0]].tobytes()
+
+
+def deserialize_factors64(data: bytes) -> np.ndarray:
+    b = np.frombuffer(data, np.uint8)
+    nf = b.size // 10
+    out = np.empty((max(nf, 1), 2), np.uint64)
+    _check(load_library().lz77sss_deserialize_factors64(b.ctypes.data_as(_P), nf, out.ctypes.data_as(_P)))
+    return out[:nf]
 
 
 def gen_random_repetitive(min_size: int, max_size: int, seed: int, rep: float = -1.0, run: float = -1.0) -> np.ndarray:
@@ -315,3 +358,10 @@ def gen_genome(n: int, base_len: int, mut_rate: float, seed: int) -> np.ndarray:
     buf = np.empty(max(n, 1), np.uint8)
     load_library().lz77sss_gen_genome(n, base_len, mut_rate, seed, buf.ctypes.data_as(_P))
     return buf[:n]
+
+
+def gen_genome_pos(n: int, base_len: int, mut_rate: float, seed: int, offset: int = 0, pad: int = 0) -> np.ndarray:
+    """The chr19-style text of Session.gen_genome (position-hashed), on the host; `pad` zero bytes follow."""
+    buf = np.zeros(max(n + pad, 1), np.uint8)
+    _check(load_library().lz77sss_gen_genome_pos(n, base_len, mut_rate, seed, offset, buf.ctypes.data_as(_P)))
+    return buf[:n + pad]

@@ -54,8 +54,11 @@ static constexpr u64 TAU = 512;  // lz77_sss.hpp:82 default_tau
 // enums mirror lz77_sss.hpp:48-59
 enum phrase_mode { lpf_naive = 0, lpf_lnf_naive = 1, lpf_opt = 2, lpf_lnf_opt = 3 };
 
-struct factor { u32 src; u32 len; };  // lz77_sss.hpp:129-147 (pos_t = uint32_t)
-struct lpf { u32 beg; u32 end; u32 src; };  // lz77_sss.hpp:206-210
+// the approximate path is templated on pos_t in {uint32_t, uint64_t} (lz77_sss.hpp:72-75)
+template <class P> struct factor_t { P src; P len; };  // lz77_sss.hpp:129-147
+template <class P> struct lpf_t { P beg; P end; P src; };  // lz77_sss.hpp:206-210
+using factor = factor_t<u32>;
+using lpf = lpf_t<u32>;
 
 // ---------------------------------------------------------------------------
 // Naive forward LCE bounded by max_len (role of lce_naive_wordwise_xor, absent;
@@ -76,10 +79,11 @@ static inline u64 naive_lce(const u8* T, u64 n, u64 a, u64 b, u64 max_len) {
 
 // Leftward LCE with cap -- exact semantics of lce_l_64 (lce_l.hpp:33-83):
 // min(cap', #equal chars going left from i and j), cap' = min(cap, min(i,j)+1).
-static inline u32 lce_left(const u8* T, u32 i, u32 j, u32 cap = 0xFFFFFFFFu) {
-    u32 cp = std::min<u32>(cap, std::min(i, j) + 1);
+template <class P>
+static inline P lce_left(const u8* T, P i, P j, P cap = ~(P)0) {
+    P cp = std::min<P>(cap, std::min(i, j) + 1);
     if (i == j) return cp;
-    u32 k = 0;
+    P k = 0;
     while (k < cp && T[i - k] == T[j - k]) k++;
     return k;
 }
@@ -141,15 +145,16 @@ static inline bool q_bruteforce(const u8* T, u64 j) {
 }
 
 // SSS over all positions; OpenMP over blocks of positions.
-static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
-    std::vector<u32> S;
+template <class P = u32>
+static inline std::vector<P> compute_sss(const u8* T, u64 n, bool& has_runs) {
+    std::vector<P> S;
     has_runs = false;
     if (n < 2 * TAU) return S;
     const u64 last_i = n - 2 * TAU;          // sync candidates i in [0, last_i]
     const u64 BLK = 1 << 20;
     const u64 nblk = last_i / BLK + 1;
     const u32 bpow = pow32((u32)SSS_BASE, TAU);
-    std::vector<std::vector<u32>> part(nblk);
+    std::vector<std::vector<P>> part(nblk);
     std::vector<u8> runs_flag(nblk, 0);
 #pragma omp parallel for schedule(dynamic, 1)
     for (u64 bi = 0; bi < nblk; bi++) {
@@ -177,7 +182,7 @@ static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
         // sliding-window minimum over [i, i+tau] (monotone deque of indices)
         std::vector<u64> dq(m);
         u64 h = 0, t = 0;
-        std::vector<u32>& out = part[bi];
+        std::vector<P>& out = part[bi];
         u64 nxt = 0;  // next j to push
         for (u64 i = b; i < ie; i++) {
             while (nxt <= i - b + TAU) {
@@ -188,7 +193,7 @@ static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
             }
             while (dq[h] < i - b) h++;
             u64 mn = phi[dq[h]];
-            if (mn != SSS_INF && (phi[i - b] == mn || phi[i - b + TAU] == mn)) out.push_back((u32)i);
+            if (mn != SSS_INF && (phi[i - b] == mn || phi[i - b + TAU] == mn)) out.push_back((P)i);
         }
     }
     size_t tot = 0;
@@ -205,11 +210,14 @@ static inline std::vector<u32> compute_sss(const u8* T, u64 n, bool& has_runs) {
 //  SA_S / ISA_S / LCP / RMQ / successor / exact LCE
 //  (roles of lce_classic_for_sss.hpp:36-142 and lce_sss.hpp:44-177)
 // ===========================================================================
+template <class P = u32>
 struct lce_structure {
     const u8* T = nullptr;
     u64 n = 0;
-    std::vector<u32> S, SA, ISA, LCP;
-    std::vector<std::vector<u32>> rmq;  // sparse table of LCP minima
+    std::vector<P> S;
+    std::vector<u32> SA, ISA;
+    std::vector<P> LCP;
+    std::vector<std::vector<P>> rmq;  // sparse table of LCP minima
     bool has_runs = false;
 
     u32 s() const { return (u32)S.size(); }
@@ -278,7 +286,7 @@ struct lce_structure {
             if (r != 0) {
                 u32 j = SA[r - 1];
                 cur += naive_lce(T, n, (u64)S[i] + cur, (u64)S[j] + cur, ~0ull);
-                LCP[r] = (u32)cur;
+                LCP[r] = (P)cur;
             }
             if (i + 1 == ns) break;
             u64 diff = (u64)S[i + 1] - S[i];
@@ -289,7 +297,7 @@ struct lce_structure {
         rmq.push_back(LCP);
         for (u32 lv = 1; (1ull << lv) <= ns; lv++) {
             const auto& prev = rmq.back();
-            std::vector<u32> cur_lv(ns - (1u << lv) + 1);
+            std::vector<P> cur_lv(ns - (1u << lv) + 1);
             for (u32 k = 0; k < cur_lv.size(); k++) cur_lv[k] = std::min(prev[k], prev[k + (1u << (lv - 1))]);
             rmq.push_back(std::move(cur_lv));
         }
@@ -297,13 +305,13 @@ struct lce_structure {
 
     void build(const u8* text, u64 size) {
         T = text; n = size;
-        S = compute_sss(T, n, has_runs);
+        S = compute_sss<P>(T, n, has_runs);
         build_sa();
         build_lcp();
     }
 
     // min LCP over ranks (a, b], a < b
-    u32 rmq_min(u32 a, u32 b) const {
+    P rmq_min(u32 a, u32 b) const {
         u32 l = a + 1, len = b - a;
         u32 lv = 31 - std::countl_zero(len);
         return std::min(rmq[lv][l], rmq[lv][b + 1 - (1u << lv)]);
@@ -313,7 +321,7 @@ struct lce_structure {
         if (a > b) std::swap(a, b);
         return rmq_min(a, b);
     }
-    u32 succ(u64 x) const { return (u32)(std::lower_bound(S.begin(), S.end(), (u32)std::min<u64>(x, 0xFFFFFFFFull)) - S.begin()); }
+    u32 succ(u64 x) const { return (u32)(std::lower_bound(S.begin(), S.end(), (P)std::min<u64>(x, (u64)~(P)0)) - S.begin()); }
 
     // exact LCE of suffixes i and j (role of lce_sss::lce, lce_sss.hpp:102-177)
     u64 lce(u64 i, u64 j) const {
@@ -341,7 +349,8 @@ struct lce_structure {
 // ===========================================================================
 //  PSV/NSV and PGV/NGV over SA_S: restates nxv_pxv.cpp:33-92 and :94-156
 // ===========================================================================
-static inline void build_psv_nsv(const lce_structure& L, std::vector<u32>& PSV, std::vector<u32>& NSV) {
+template <class P>
+static inline void build_psv_nsv(const lce_structure<P>& L, std::vector<u32>& PSV, std::vector<u32>& NSV) {
     const u32 s = L.s();
     PSV.assign(s, 0); NSV.assign(s, 0);
     if (!s) return;
@@ -354,7 +363,8 @@ static inline void build_psv_nsv(const lce_structure& L, std::vector<u32>& PSV, 
         if (j != s) NSV[j] = s;
     }
 }
-static inline void build_pgv_ngv(const lce_structure& L, std::vector<u32>& PGV, std::vector<u32>& NGV) {
+template <class P>
+static inline void build_pgv_ngv(const lce_structure<P>& L, std::vector<u32>& PGV, std::vector<u32>& NGV) {
     const u32 s = L.s();
     PGV.assign(s, 0); NGV.assign(s, 0);
     if (!s) return;
@@ -371,42 +381,44 @@ static inline void build_pgv_ngv(const lce_structure& L, std::vector<u32>& PGV, 
 // ===========================================================================
 //  build_LPF_opt for p = 1: restates lpf_opt.cpp:33-157
 // ===========================================================================
-static inline std::vector<lpf> build_lpf_opt(const u8* T, u64 n, const lce_structure& L) {
+template <class P>
+static inline std::vector<lpf_t<P>> build_lpf_opt(const u8* T, u64 n, const lce_structure<P>& L) {
+    using lpf = lpf_t<P>;
     std::vector<u32> PSV, NSV;
     build_psv_nsv(L, PSV, NSV);
     std::vector<lpf> out;
     const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
     const u32 s = L.s();
-    u32 max_end = 0;
+    P max_end = 0;
     const u32 i_min = 0, i_max = s;  // p = 1: b = 0, e = n (lpf_opt.cpp:50-56)
     for (u32 i = i_min; i < i_max; i++) {
         while (i + 1 < i_max && S[i + 1] <= max_end) i++;
-        u32 lst_end = max_end;
+        P lst_end = max_end;
         lpf phr{0, 0, 0};
         if (PSV[ISA[i]] != s) {
-            u32 src = S[SA[PSV[ISA[i]]]];
-            u32 end = S[i] + (u32)L.lce(src, S[i]);
+            P src = S[SA[PSV[ISA[i]]]];
+            P end = S[i] + (P)L.lce(src, S[i]);
             if (end > lst_end) {
-                u32 beg = S[i];
+                P beg = S[i];
                 if (S[i] > lst_end && src != 0 && S[i] != 0) {
-                    u32 l = lce_left(T, src - 1, S[i] - 1, S[i] - lst_end);
+                    P l = lce_left<P>(T, src - 1, S[i] - 1, S[i] - lst_end);
                     beg -= l; src -= l;
                 }
-                if (beg < lst_end) { u32 exc = lst_end - beg; beg += exc; src += exc; }
+                if (beg < lst_end) { P exc = lst_end - beg; beg += exc; src += exc; }
                 if (end > max_end) max_end = end;
                 if (end - beg > 1) phr = {beg, end, src};
             }
         }
         if (NSV[ISA[i]] != s) {
-            u32 src = S[SA[NSV[ISA[i]]]];
-            u32 end = S[i] + (u32)L.lce(src, S[i]);
+            P src = S[SA[NSV[ISA[i]]]];
+            P end = S[i] + (P)L.lce(src, S[i]);
             if (end > lst_end) {
-                u32 beg = S[i];
+                P beg = S[i];
                 if (S[i] > lst_end && src != 0 && S[i] != 0) {
-                    u32 l = lce_left(T, src - 1, S[i] - 1, S[i] - lst_end);
+                    P l = lce_left<P>(T, src - 1, S[i] - 1, S[i] - lst_end);
                     beg -= l; src -= l;
                 }
-                if (beg < lst_end) { u32 exc = lst_end - beg; beg += exc; src += exc; }
+                if (beg < lst_end) { P exc = lst_end - beg; beg += exc; src += exc; }
                 if (end > max_end) max_end = end;
                 if (end - beg > phr.end - phr.beg) phr = {beg, end, src};
             }
@@ -423,24 +435,26 @@ static inline std::vector<lpf> build_lpf_opt(const u8* T, u64 n, const lce_struc
 //  sync position not covered by the previous pushed phrase; no left extension;
 //  phrases of length >= 1 are kept)
 // ===========================================================================
-static inline std::vector<lpf> build_lpf_naive(const u8* T, u64 n, const lce_structure& L) {
+template <class P>
+static inline std::vector<lpf_t<P>> build_lpf_naive(const u8* T, u64 n, const lce_structure<P>& L) {
+    using lpf = lpf_t<P>;
     std::vector<u32> PSV, NSV;
     build_psv_nsv(L, PSV, NSV);
     std::vector<lpf> out;
     const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
     const u32 s = L.s();
     for (u32 i = 0; i < s;) {
-        u32 src = 0, len = 0;
+        P src = 0, len = 0;
         if (PSV[ISA[i]] != s) {
-            const u32 sc = S[SA[PSV[ISA[i]]]], lc = (u32)L.lce(sc, S[i]);
+            const P sc = S[SA[PSV[ISA[i]]]], lc = (P)L.lce(sc, S[i]);
             if (lc > len) { src = sc; len = lc; }
         }
         if (NSV[ISA[i]] != s) {
-            const u32 sc = S[SA[NSV[ISA[i]]]], lc = (u32)L.lce(sc, S[i]);
+            const P sc = S[SA[NSV[ISA[i]]]], lc = (P)L.lce(sc, S[i]);
             if (lc > len) { src = sc; len = lc; }
         }
         if (len > 0) out.push_back({S[i], S[i] + len, src});
-        const u32 pos = S[i];
+        const P pos = S[i];
         do { i++; } while (i < s && S[i] < pos + len);
     }
     (void)T; (void)n;
@@ -451,7 +465,7 @@ static inline std::vector<lpf> build_lpf_naive(const u8* T, u64 n, const lce_str
 //  LPF/LNF (lpf_lnf_opt) for p = 1: restates lpf_lnf.cpp:31-249 and
 //  greedy_phrase_selection (approximate/common.cpp:31-96)
 // ===========================================================================
-static inline void build_lpf_all(const u8* T, u64 n, const lce_structure& L, bool opt, std::vector<lpf>& out) {
+static inline void build_lpf_all(const u8* T, u64 n, const lce_structure<u32>& L, bool opt, std::vector<lpf>& out) {
     std::vector<u32> PSV, NSV;
     build_psv_nsv(L, PSV, NSV);
     const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
@@ -478,7 +492,7 @@ static inline void build_lpf_all(const u8* T, u64 n, const lce_structure& L, boo
     }
 }
 // T here is the REVERSED text; phrases are mapped back to forward coordinates
-static inline void build_lnf_all(const u8* T, u64 n, const lce_structure& L, bool opt, std::vector<lpf>& out) {
+static inline void build_lnf_all(const u8* T, u64 n, const lce_structure<u32>& L, bool opt, std::vector<lpf>& out) {
     std::vector<u32> PGV, NGV;
     build_pgv_ngv(L, PGV, NGV);
     const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
@@ -539,14 +553,17 @@ static inline void greedy_phrase_selection(std::vector<lpf>& P) {
 // ===========================================================================
 //  get_phrase_info (p = 1): restates approximate/common.cpp:98-157
 // ===========================================================================
-struct phrase_info { u32 num_lpf = 0, len_lpf_phr = 0, num_gaps = 0; };
-static inline phrase_info get_phrase_info(const std::vector<lpf>& P, u32 n) {
-    phrase_info r;
-    u32 b = 0, e = n, i = 0;
-    if (!P.empty()) e = std::max<u32>(e, P.back().end);
-    r.num_lpf = (u32)P.size() - i;
+template <class Q>
+struct phrase_info_t { Q num_lpf = 0, len_lpf_phr = 0, num_gaps = 0; };
+using phrase_info = phrase_info_t<u32>;
+template <class Q>
+static inline phrase_info_t<Q> get_phrase_info(const std::vector<lpf_t<Q>>& P, Q n) {
+    phrase_info_t<Q> r;
+    Q b = 0, e = n, i = 0;
+    if (!P.empty()) e = std::max<Q>(e, P.back().end);
+    r.num_lpf = (Q)P.size() - i;
     if (r.num_lpf > 0) {
-        r.len_lpf_phr += P[i].end - std::max<u32>(P[i].beg, b);
+        r.len_lpf_phr += P[i].end - std::max<Q>(P[i].beg, b);
         if (P[i].beg > b) r.num_gaps = 1;
         i++;
         while (i < P.size()) {
@@ -573,14 +590,15 @@ struct gap_params {
     u32 log2_size_h = 0;
     double rel_len_gaps = 0;
 };
-static inline gap_params choose_gap_params(u32 n, const phrase_info& pi) {
+template <class Q>
+static inline gap_params choose_gap_params(Q n, const phrase_info_t<Q>& pi) {
     static const std::array<std::pair<double, std::array<u32, 5>>, 10> table{{
         {6, {2, 3, 4, 5, 6}}, {8, {2, 3, 4, 6, 8}}, {12, {2, 3, 4, 8, 12}}, {16, {2, 4, 6, 9, 16}},
         {32, {2, 4, 6, 10, 20}}, {64, {2, 4, 7, 12, 28}}, {128, {2, 4, 8, 16, 36}},
         {256, {2, 5, 10, 20, 42}}, {1024, {2, 6, 12, 24, 48}},
         {std::numeric_limits<double>::max(), {2, 8, 16, 32, 64}}}};
     gap_params g;
-    u32 len_gaps = n - pi.len_lpf_phr;
+    Q len_gaps = n - pi.len_lpf_phr;
     double rel_len_gaps = len_gaps / (double)n;
     double avg_gap_len = len_gaps / (double)pi.num_gaps;
     double avg_lpf_phr_len = pi.len_lpf_phr / (double)pi.num_lpf;
@@ -592,11 +610,11 @@ static inline gap_params choose_gap_params(u32 n, const phrase_info& pi) {
     u32 rt = 0;
     for (int j = 0; j < 5; j++) rt += g.patt_lens[j];
     g.roll_threshold = rt / 5;
-    // rolling_hash_index_107.hpp:59-70 (pos_t = uint32_t)
+    // rolling_hash_index_107.hpp:59-70 (entries of sizeof(pos_t) bytes)
     const int64_t rk_bytes = (int64_t)(80 + 16 * 256 * 256) * 5;  // rk_prime<107>::byte_size() * 5
-    int64_t min_index_size = std::max<u32>(1u << 20, (u32)(n * 0.1)) / sizeof(u32);
-    int64_t max_index_size = (1ll << 30) / (int64_t)sizeof(u32);
-    int64_t target_index_entries = std::max<int64_t>(0, (int64_t)g.target_index_size - rk_bytes) / (int64_t)sizeof(u32);
+    int64_t min_index_size = (int64_t)(std::max<Q>(1u << 20, (Q)(n * 0.1)) / sizeof(Q));
+    int64_t max_index_size = (1ll << 30) / (int64_t)sizeof(Q);
+    int64_t target_index_entries = std::max<int64_t>(0, (int64_t)g.target_index_size - rk_bytes) / (int64_t)sizeof(Q);
     uint64_t target_size_h = std::min<int64_t>(max_index_size, std::max<int64_t>(min_index_size, target_index_entries));
     g.log2_size_h = (u8)std::round(std::log2(target_size_h));
     return g;
@@ -647,22 +665,23 @@ struct rk107 {
 };
 
 // rolling_hash_index_107 restated (rolling_hash_index_107.hpp:33-172)
+template <class Q>
 struct gap_index {
     const u8* T = nullptr;
-    u32 n = 0;
+    Q n = 0;
     std::array<u32, 5> lens{};
     rk107 rh[5];
-    std::vector<u32> H;
+    std::vector<Q> H;
     u64 mask = 0;
-    u32 cur = 0;
-    void create(const u8* text, u32 size, const std::array<u32, 5>& pl, u32 log2_size, const std::array<u64, 5>& bases) {
+    Q cur = 0;
+    void create(const u8* text, Q size, const std::array<u32, 5>& pl, u32 log2_size, const std::array<u64, 5>& bases) {
         T = text; n = size; lens = pl;
-        H.assign((size_t)1 << log2_size, 0xFFFFFFFFu);
+        H.assign((size_t)1 << log2_size, ~(Q)0);
         mask = ((u64)1 << log2_size) - 1;
         for (int i = 0; i < 5; i++) rh[i].init(bases[i], lens[i]);
         reinit(0);
     }
-    void reinit(u32 pos) {
+    void reinit(Q pos) {
         cur = pos;
         for (int i = 0; i < 5; i++) {
             rh[i].fp = 0;
@@ -679,9 +698,9 @@ struct gap_index {
         if ((u64)cur + lens[i] < n) { H[(u64)rh[i].fp & mask] = cur; roll_i(i); }
     }
     void advance() { for (int i = 0; i < 5; i++) advance_i(i); cur++; }
-    inline u32 advance_and_get_occ(int i) {
+    inline Q advance_and_get_occ(int i) {
         u64 h = (u64)rh[i].fp & mask;
-        u32 occ = H[h];
+        Q occ = H[h];
         H[h] = cur;
         if ((u64)cur + lens[i] < n) roll_i(i);
         return occ;
@@ -693,30 +712,34 @@ struct gap_index {
 //  factorize/common.cpp:31-111, greedy.cpp:34-140)
 // ===========================================================================
 struct approx_stats {
-    u32 size_sss = 0;
+    u64 size_sss = 0;
     bool has_runs = false;
-    u32 num_lpf = 0, len_lpf_phr = 0, num_gaps = 0;
+    u64 num_lpf = 0, len_lpf_phr = 0, num_gaps = 0;
     std::array<u32, 5> patt_lens{};
     u32 roll_threshold = 0, log2_size_h = 0;
 };
 
-template <typename OUT>
-static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed, OUT&& output,
+template <class Q = u32, typename OUT>
+static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, OUT&& output,
                                          approx_stats* st = nullptr, int fact_mode = 1) {
+    using lpf = lpf_t<Q>;
+    using factor = factor_t<Q>;
     if (n == 0) return;
     std::vector<lpf> P;
-    lce_structure L;
+    lce_structure<Q> L;
     if (phr_mode == lpf_opt) {
         L.build(T, n);
         P = build_lpf_opt(T, n, L);
     } else if (phr_mode == lpf_naive) {
         L.build(T, n);
         P = build_lpf_naive(T, n, L);
+    } else if constexpr (sizeof(Q) > 4) {
+        throw std::runtime_error("the oracle's LPF/LNF modes are pos_t = uint32_t only");
     } else if (phr_mode == lpf_lnf_opt || phr_mode == lpf_lnf_naive) {
         bool opt = (phr_mode == lpf_lnf_opt);
         std::reverse(T, T + n);  // lz77_sss.hpp:386 (in place on the caller's buffer)
         {
-            lce_structure LR;
+            lce_structure<u32> LR;
             LR.build(T, n);
             build_lnf_all(T, n, LR, opt, P);
         }
@@ -731,7 +754,7 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
         // skip_phrases: sentinel (lz77_sss.hpp:417-419), then factorize_skip_gaps
         // (approximate/factorize/skip_gaps.cpp:31-61) with next_lpf at p = 1
         P.push_back({n, n + 1, 0});
-        if (st) { st->size_sss = L.s(); st->has_runs = L.has_runs; st->num_lpf = (u32)P.size() - 1; }
+        if (st) { st->size_sss = L.s(); st->has_runs = L.has_runs; st->num_lpf = P.size() - 1; }
         size_t k = 0;
         lpf nxt = P[k];
         output(factor{nxt.beg, 0});
@@ -743,7 +766,7 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
         }
         return;
     }
-    phrase_info pi = get_phrase_info(P, n);
+    phrase_info_t<Q> pi = get_phrase_info<Q>(P, n);
     P.push_back({n, n + 1, 0});  // sentinel, lz77_sss.hpp:423
     gap_params gp = choose_gap_params(n, pi);
     if (st) {
@@ -751,7 +774,7 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
         st->len_lpf_phr = pi.len_lpf_phr; st->num_gaps = pi.num_gaps; st->patt_lens = gp.patt_lens;
         st->roll_threshold = gp.roll_threshold; st->log2_size_h = gp.log2_size_h;
     }
-    gap_index G;
+    gap_index<Q> G;
     G.create(T, n, gp.patt_lens, gp.log2_size_h, gap_bases(rk_seed));
     const u32 thr = gp.roll_threshold;
 
@@ -763,12 +786,12 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
         return phr;
     };
     // longest_prev_occ (factorize/common.cpp:33-61)
-    auto longest_prev_occ = [&](u32 pos) -> factor {
+    auto longest_prev_occ = [&](Q pos) -> factor {
         factor f{T[pos], 0};
         for (int x = 4; x >= 0; x--) {
             if (f.len == 0) {
-                u32 src = G.advance_and_get_occ(x);
-                if (src < pos && T[src] == T[pos]) { f.len = (u32)L.lce(src, pos); f.src = src; }
+                Q src = G.advance_and_get_occ(x);
+                if (src < pos && T[src] == T[pos]) { f.len = (Q)L.lce(src, pos); f.src = src; }
             } else {
                 G.advance_i(x);
             }
@@ -778,8 +801,8 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
     };
 
     lpf p = next_lpf();
-    for (u32 i = 0; true;) {
-        u32 gap_end = p.beg;
+    for (Q i = 0; true;) {
+        Q gap_end = p.beg;
         if (i < gap_end) {
             if (G.cur < i) {
                 if (i - G.cur <= thr) { do { G.roll(); } while (G.cur < i); }
@@ -787,7 +810,7 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
             }
             do {
                 factor f = longest_prev_occ(i);
-                i += std::max<u32>(1, f.len);
+                i += std::max<Q>(1, f.len);
                 if (i > gap_end) {
                     if (i <= p.end) { f.len -= i - gap_end; i = gap_end; }
                     else {
@@ -801,7 +824,7 @@ static inline void factorize_approximate(u8* T, u32 n, int phr_mode, u32 rk_seed
             } while (i < gap_end);
         }
         if (i == n) break;
-        u32 exc = i - gap_end;
+        Q exc = i - gap_end;
         factor lf{p.src + exc, (p.end - p.beg) - exc};
         if (G.cur == i) {
             factor f = longest_prev_occ(i);

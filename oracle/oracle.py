@@ -64,6 +64,12 @@ def lib():
         L.oracle_factorize_exact.argtypes = [_P, _U64, _P, _U64]
         L.oracle_factorize_exact_timed.restype = ctypes.c_int64
         L.oracle_factorize_exact_timed.argtypes = [_P, _U64, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_factorize_approx64.restype = ctypes.c_int64
+        L.oracle_factorize_approx64.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, _P, _U64, _P]
+        L.oracle_sss64.restype = ctypes.c_int64
+        L.oracle_sss64.argtypes = [_P, _U64, _P, _U64, ctypes.POINTER(ctypes.c_int)]
+        L.oracle_lpf_opt64.restype = ctypes.c_int64
+        L.oracle_lpf_opt64.argtypes = [_P, _U64, _P, _U64]
         L.oracle_num_threads.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         _lib = L
@@ -95,6 +101,48 @@ def factorize(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):
     if z < 0:
         raise RuntimeError("oracle factorization failed")
     return out[:z].copy(), st
+
+
+def factorize64(T, phr_mode: int = LPF_OPT, rk_seed: int = 42, fact_mode: int = 1, buf=None):
+    """lz77_sss<u64>::factorize_approximate<fact_mode, phr_mode, 512> at p=1 -> ((z,2) u64 factors, stats[12]).
+    The gap index has the reference's pos_t = uint64_t size (8-byte entries), so the stream differs from the
+    uint32_t one in general.  `buf` may be a pre-padded copy (text + >= 4096 zero bytes) to skip the copy."""
+    n = _u8(T).size
+    if buf is None:
+        buf = _padded(T)
+    cap = n // 32 + 65536
+    st = np.zeros(12, np.uint64)
+    while True:
+        out = np.zeros((cap, 2), np.uint64)
+        z = lib().oracle_factorize_approx64(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, fact_mode,
+                                            out.ctypes.data_as(_P), cap, st.ctypes.data_as(_P))
+        if z >= 0:
+            return out[:z].copy(), st
+        if cap >= n + 4:
+            raise RuntimeError("oracle factorization failed")
+        cap = n + 4
+
+
+def sss64(T):
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros(2 * n // 512 * 4 + 1024, np.uint64)
+    hr = ctypes.c_int()
+    k = lib().oracle_sss64(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), out.size, ctypes.byref(hr))
+    if k < 0:
+        out = np.zeros(n + 1, np.uint64)
+        k = lib().oracle_sss64(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), out.size, ctypes.byref(hr))
+    return out[:k].copy(), bool(hr.value)
+
+
+def lpf_opt64(T):
+    buf = _padded(T)
+    n = _u8(T).size
+    out = np.zeros((n // 64 + 1024, 3), np.uint64)
+    k = lib().oracle_lpf_opt64(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), out.shape[0])
+    if k < 0:
+        raise RuntimeError("oracle lpf failed")
+    return out[:k].copy()
 
 
 def factorize_timed(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):

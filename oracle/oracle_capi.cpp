@@ -39,6 +39,48 @@ int64_t oracle_factorize_approx(uint8_t* T, uint64_t n, int phr_mode, uint32_t r
     }
 }
 
+// pos_t = uint64_t form (lz77_sss<uint64_t>): out 2*cap uint64 pairs, stats 12 x uint64.
+int64_t oracle_factorize_approx64(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed, int fact_mode,
+                                  uint64_t* out, uint64_t cap, uint64_t* stats) {
+    try {
+        uint64_t k = 0;
+        bool overflow = false;
+        approx_stats st;
+        factorize_approximate<u64>(T, (u64)n, phr_mode, rk_seed, [&](factor_t<u64> f) {
+            if (k < cap) { out[2 * k] = f.src; out[2 * k + 1] = f.len; } else overflow = true;
+            k++;
+        }, &st, fact_mode);
+        if (stats) {
+            stats[0] = st.size_sss; stats[1] = st.has_runs; stats[2] = st.num_lpf;
+            stats[3] = st.len_lpf_phr; stats[4] = st.num_gaps;
+            for (int i = 0; i < 5; i++) stats[5 + i] = st.patt_lens[i];
+            stats[10] = st.roll_threshold; stats[11] = st.log2_size_h;
+        }
+        return overflow ? -1 : (int64_t)k;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -1;
+    }
+}
+
+// SSS with 64-bit positions and the LPF_opt phrases of pos_t = uint64_t (tests)
+int64_t oracle_sss64(const uint8_t* T, uint64_t n, uint64_t* out, uint64_t cap, int* has_runs) {
+    bool hr = false;
+    std::vector<u64> S = compute_sss<u64>(T, n, hr);
+    if (has_runs) *has_runs = hr;
+    if (S.size() > cap) return -1;
+    std::copy(S.begin(), S.end(), out);
+    return (int64_t)S.size();
+}
+int64_t oracle_lpf_opt64(const uint8_t* T, uint64_t n, uint64_t* out, uint64_t cap) {
+    lce_structure<u64> L;
+    L.build(T, n);
+    auto P = build_lpf_opt(T, n, L);
+    if (P.size() > cap) return -1;
+    for (size_t k = 0; k < P.size(); k++) { out[3 * k] = P[k].beg; out[3 * k + 1] = P[k].end; out[3 * k + 2] = P[k].src; }
+    return (int64_t)P.size();
+}
+
 // fact_mode = skip_phrases (gapped stream).  Returns the record count or -1.
 int64_t oracle_factorize_skip(uint8_t* T, uint64_t n, int phr_mode, uint32_t* out, uint64_t cap) {
     try {
@@ -116,7 +158,7 @@ void oracle_phi(const uint8_t* T, uint64_t n, uint64_t* phi) {
 
 // SA_S / ISA_S / LCP_S (tests).  Each array has cap entries.
 int64_t oracle_sa_s(const uint8_t* T, uint64_t n, uint32_t* S, uint32_t* SA, uint32_t* LCP, uint64_t cap) {
-    lce_structure L;
+    lce_structure<> L;
     L.build(T, n);
     if (L.s() > cap) return -1;
     std::copy(L.S.begin(), L.S.end(), S);
@@ -127,14 +169,14 @@ int64_t oracle_sa_s(const uint8_t* T, uint64_t n, uint32_t* S, uint32_t* SA, uin
 
 // Exact LCE for query pairs (tests).
 void oracle_lce(const uint8_t* T, uint64_t n, const uint32_t* qi, const uint32_t* qj, uint64_t nq, uint32_t* out) {
-    lce_structure L;
+    lce_structure<> L;
     L.build(T, n);
     for (u64 k = 0; k < nq; k++) out[k] = (u32)L.lce(qi[k], qj[k]);
 }
 
 // LPF phrase list after build_LPF_opt (tests); out: 3*cap (beg,end,src)
 int64_t oracle_lpf_opt(const uint8_t* T, uint64_t n, uint32_t* out, uint64_t cap) {
-    lce_structure L;
+    lce_structure<> L;
     L.build(T, n);
     auto P = build_lpf_opt(T, n, L);
     if (P.size() > cap) return -1;

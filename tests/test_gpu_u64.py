@@ -1,0 +1,182 @@
+"""GPU parity of the pos_t = uint64_t engine (lz77_sss<uint64_t>, include/lz77_sss/lz77_sss.hpp:72-75).
+
+The same HIP sources compiled with 64-bit text positions (namespace lz64) against the oracle's
+pos_t = uint64_t restatement.  The stream of lz77_sss<uint64_t> differs from the uint32_t one only
+through the gap-index size (8-byte entries, rolling_hash_index_107.hpp:59-70); S, SA_S, LCP and the
+LPF phrases are the same.  The 4 GiB + 3 MiB chr19-style text puts positions past 2^32.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def session64(lz):
+    s = {"sess": None, "cap": 0}
+
+    def get(n):
+        if s["sess"] is None or n > s["cap"]:
+            if s["sess"] is not None:
+                s["sess"].close()
+            cap = max(n, 1 << 22)
+            s["sess"], s["cap"] = lz.Session(cap, pos64=True), cap
+        return s["sess"]
+
+    yield get
+    if s["sess"] is not None:
+        s["sess"].close()
+
+
+def run64(session64, T, **kw):
+    s = session64(max(T.size, 1))
+    s.load(T)
+    z = s.factorize(**kw)
+    return s, s.factors(z)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_u64_golden_intermediates(session64, name):
+    g = load_golden(name)
+    s, F = run64(session64, g["text"])
+    assert F.dtype == np.uint64
+    S, has_runs = s.sss()
+    assert np.array_equal(S, g["sss"].astype(np.uint64)) and has_runs == bool(g["has_runs"][0])
+    if S.size:
+        SA, LCP = s.sa_s(S.size)
+        assert np.array_equal(SA, g["sa_s"]) and np.array_equal(LCP, g["lcp"])
+    s.factorize()
+    assert np.array_equal(s.lpf(), g["lpf"].astype(np.uint64))
+
+
+@pytest.mark.parametrize("seed", range(1, 17))
+def test_u64_c1_seeds_vs_oracle(session64, orc, lz, seed):
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    s, F = run64(session64, T)
+    F_ref, st_ref = orc.factorize64(T)
+    assert np.array_equal(F, F_ref)
+    assert s.stats()[:12] == [int(x) for x in st_ref[:12]]
+    assert np.array_equal(lz.decode(F, T.size), T)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 511, 1024, 1025, 1537, 4097, 65537, 262144 + 3])
+def test_u64_edge_sizes(session64, orc, n):
+    rng = np.random.Generator(np.random.PCG64(n))
+    T = rng.integers(0, 3, n, dtype=np.uint8)
+    if n > 3000:
+        T[1000:2500] = T[100:1600]
+    _, F = run64(session64, T)
+    assert np.array_equal(F, orc.factorize64(T)[0])
+
+
+@pytest.mark.parametrize("period", [1, 3, 170, 300])
+def test_u64_runs(session64, orc, period):
+    rng = np.random.Generator(np.random.PCG64(period))
+    unit = rng.integers(0, 256, period, dtype=np.uint8)
+    T = np.concatenate([rng.integers(0, 256, 3000, dtype=np.uint8), np.tile(unit, 200000 // period),
+                        rng.integers(0, 256, 5000, dtype=np.uint8), np.tile(unit, 3000 // period + 1)])
+    _, F = run64(session64, T)
+    assert np.array_equal(F, orc.factorize64(T)[0])
+
+
+@pytest.mark.parametrize("kind,mib", [("genome", 16), ("rr", 64)])
+def test_u64_medium_vs_oracle(session64, orc, lz, kind, mib):
+    n = mib << 20
+    T = lz.gen_genome(n, 2 << 20, 0.001, 11) if kind == "genome" else lz.gen_random_repetitive(n, n, 5, 0.5, 0.05)
+    _, F = run64(session64, T)
+    F_ref, _ = orc.factorize64(T)
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
+@pytest.mark.parametrize("phr_mode", [0, 2])
+@pytest.mark.parametrize("seed", [2, 7])
+def test_u64_phrase_modes_and_skip_phrases(session64, orc, lz, phr_mode, seed):
+    T = lz.gen_random_repetitive(20000, 150000, seed)
+    _, F = run64(session64, T, phr_mode=phr_mode)
+    assert np.array_equal(F, orc.factorize64(T, phr_mode=phr_mode)[0])
+    _, G = run64(session64, T, phr_mode=phr_mode, fact_mode=lz.SKIP_PHRASES)
+    assert np.array_equal(G, orc.factorize64(T, phr_mode=phr_mode, fact_mode=2)[0])
+
+
+@pytest.mark.parametrize("max_outer", [0, 1])
+def test_u64_bounded_completion(session64, orc, lz, max_outer, monkeypatch):
+    T = lz.gen_genome(4 << 20, 1 << 20, 0.001, 21)
+    monkeypatch.setenv("LZ77SSS_GREEDY_MAX_OUTER", str(max_outer))
+    _, F = run64(session64, T)
+    assert np.array_equal(F, orc.factorize64(T)[0])
+
+
+def test_u64_index_size_override_matches_u32(session, session64, lz):
+    """With the slot count forced equal, the 32- and 64-bit engines produce the same stream."""
+    T = lz.gen_random_repetitive(100000, 100000, 12)
+    s32 = session(T.size)
+    s32.load(T)
+    F32 = s32.factors(s32.factorize(index_log2_size=19))
+    _, F64 = run64(session64, T, index_log2_size=19)
+    assert np.array_equal(F64, F32.astype(np.uint64))
+
+
+def test_u64_one_shot_callback_and_device_decode(lz, orc):
+    T = lz.gen_random_repetitive(150000, 150000, 8)
+    got = []
+    EMIT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p)
+
+    def emit(ptr, count, user):
+        got.append(np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint64)), (count, 2)).copy())
+        return 0
+
+    cb = EMIT(emit)
+    p = lz.params()
+    rc = lz.load_library().lz77sss_factorize_approx_u64(T.ctypes.data_as(ctypes.c_void_p), T.size, ctypes.byref(p),
+                                                        cb, None)
+    assert rc == 0
+    F = np.concatenate(got)
+    assert np.array_equal(F, orc.factorize64(T)[0])
+    assert np.array_equal(lz.decode_device(F, T.size), T)
+    # exact mode through the 64-bit entry point (n < 2^31): the 32-bit stream, widened
+    got.clear()
+    rc = lz.load_library().lz77sss_factorize_exact_u64(T.ctypes.data_as(ctypes.c_void_p), T.size, ctypes.byref(p),
+                                                       1, cb, None)
+    assert rc == 0
+    assert np.array_equal(np.concatenate(got), orc.factorize_exact(T).astype(np.uint64))
+
+
+def test_u64_session_rejects_32bit_accessors(session64, lz):
+    s = session64(1 << 16)
+    s.load(lz.gen_random_repetitive(20000, 20000, 1))
+    s.factorize()
+    with pytest.raises(lz.Lz77SssError):
+        s.factorize(phr_mode=lz.LPF_LNF_OPT)
+    with pytest.raises(lz.Lz77SssError):
+        s.factorize_exact()
+    with pytest.raises(lz.Lz77SssError):
+        s.huffman()
+
+
+@pytest.mark.slow
+def test_u64_chr19_past_4gib_vs_oracle(lz, orc):
+    """C4's pos_t = uint64_t path on one GPU: a chr19-style text of 4 GiB + 3 MiB (59 MiB ACGT block,
+    0.01 % mutations) generated in HBM, factorized with 64-bit positions, equal to the oracle's
+    uint64_t stream on the same bytes (generated on the host), and decoded back on the device.
+    (At 0.1 % mutations the gap index's base set passes 2^32 / 5 positions, the limit of its 32-bit
+    entry ids: DESIGN.md 7.)"""
+    n = (1 << 32) + (3 << 20) + 12345
+    base, mut, seed = 59 << 20, 0.0001, 7
+    with lz.Session(n, pos64=True) as s:
+        s.gen_genome(n, base, mut, seed)
+        z = s.factorize()
+        F = s.factors(z)
+        st = s.stats()
+        _, mism = s.decode(out=False)
+        assert mism == 0
+    assert int(F[:, 0].max()) >= (1 << 32) or int(np.max(np.cumsum(np.maximum(F[:, 1], 1)))) == n
+    T = lz.gen_genome_pos(n, base, mut, seed, pad=4096)
+    F_ref, st_ref = orc.factorize64(T[:n], buf=T)
+    assert st[:12] == [int(x) for x in st_ref[:12]]
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)

@@ -248,3 +248,48 @@ def test_oracle_lpf_naive_roundtrip(orc, lz, seed):
     T = lz.gen_random_repetitive(10000, 200000, seed)
     F, st = orc.factorize(T, phr_mode=0)
     assert np.array_equal(orc.decode(F, T.size), T)
+
+
+# ---- pos_t = uint64_t restatement (lz77_sss<uint64_t>, lz77_sss.hpp:72-75)
+
+@pytest.mark.parametrize("seed", range(1, 9))
+def test_oracle_u64_roundtrip_and_shared_intermediates(orc, lz, seed):
+    """S and the LPF phrases do not depend on pos_t; the factor stream does only through the gap-index
+    size (8-byte entries, rolling_hash_index_107.hpp:59-70) and must decode back to the text."""
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    F64, st64 = orc.factorize64(T)
+    F32, st32 = orc.factorize(T)
+    assert F64.dtype == np.uint64 and np.array_equal(lz.decode(F64, T.size), T)
+    assert [int(x) for x in st64[:11]] == [int(x) for x in st32[:11]]
+    assert int(st64[11]) == int(st32[11]) - 1  # 8-byte entries: half the slots of the same byte budget
+    S32, hr32 = orc.sss(T)
+    S64, hr64 = orc.sss64(T)
+    assert np.array_equal(S64, S32.astype(np.uint64)) and hr32 == hr64
+    assert np.array_equal(orc.lpf_opt64(T), orc.lpf_opt(T).astype(np.uint64))
+
+
+def test_serialize_factors64_roundtrip(lz):
+    F = np.array([[97, 0], [0, 5], [(1 << 40) - 1, (1 << 33) + 7], [123456789012, 1]], np.uint64)
+    b = lz.serialize_factors64(F)
+    assert len(b) == 10 * F.shape[0]
+    assert b[:10] == bytes([97, 0, 0, 0, 0, 0, 0, 0, 0, 0])
+    assert np.array_equal(lz.deserialize_factors64(b), F)
+    with pytest.raises(lz.Lz77SssError):
+        lz.serialize_factors64(np.array([[1 << 40, 1]], np.uint64))
+
+
+def test_decode_u64_host(lz):
+    T = lz.gen_random_repetitive(5000, 30000, 3)
+    import oracle
+    F, _ = oracle.factorize64(T)
+    assert np.array_equal(lz.decode(F, T.size), T)
+    bad = F.copy()
+    bad[-1, 1] += 1
+    with pytest.raises(lz.Lz77SssError):
+        lz.decode(bad, T.size)
+
+
+def test_gen_genome_pos_is_position_hashed(lz):
+    a = lz.gen_genome_pos(300000, 70000, 0.01, 5)
+    b = lz.gen_genome_pos(100000, 70000, 0.01, 5, offset=150000)
+    assert np.array_equal(a[150000:250000], b)
