@@ -215,6 +215,39 @@ int lz77sss_session_phase_times(lz77sss_session* s, double* ms, const char** nam
 int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap);
 void lz77sss_session_destroy(lz77sss_session* s);
 
+/* ---- sharded factorization ----
+ * One text, N ranks (one session per rank, the whole text loaded on each):
+ *   1. rank r: lz77sss_session_sss_range on its text block, all-gather the blocks' sync
+ *      sets in rank order, lz77sss_session_set_sss with the gathered set;
+ *   2. every rank: lz77sss_session_prepare(external_sss = 1) -- SA_S, LCP, LCE and the
+ *      phrases (replicated), and the gap-index parameters;
+ *   3. in rank order: rank r receives the chain state and the carried table from r - 1
+ *      (lz77sss_session_carried_copy into its session), runs lz77sss_session_greedy_block
+ *      on [state.start, b_{r+1}) and sends exit state + carried table to r + 1;
+ *   4. the ranks' factors concatenated in rank order are the factorization of the text
+ *      (bit-identical to one lz77sss_session_factorize of the whole text). */
+typedef struct {
+    uint64_t start;       /* in: chain position where the block's walk starts (0 on rank 0) */
+    uint64_t idxpos;      /* in: gap-index position at start (0 on rank 0) */
+    uint32_t zmask;       /* in: zeroed-fingerprint mask (0 on every rank but a text shorter than 65) */
+    int32_t carried;      /* in: 1 = the session's carried table holds the inserts before start */
+    uint64_t end;         /* in: block end: n (last rank) or <= n - 4160 */
+    uint64_t exit_start;  /* out: the next block's start (the first hand-over point >= end) */
+    uint64_t exit_idxpos; /* out */
+    uint32_t exit_zmask;  /* out */
+    uint32_t reserved;
+} lz77sss_block;
+/* Loads an externally computed sync set (host or device pointer, 64-bit positions). */
+int lz77sss_session_set_sss(lz77sss_session* s, const uint64_t* S, uint64_t count, int has_runs);
+/* Phases before the greedy emitter; *carried_bytes = size of the carried table. */
+int lz77sss_session_prepare(lz77sss_session* s, const lz77sss_params* prm, int external_sss,
+                            uint64_t* carried_bytes);
+/* Carried table <-> buf (host or device memory): to_session = 1 loads it, 0 reads it. */
+int lz77sss_session_carried_copy(lz77sss_session* s, void* buf, uint64_t bytes, int to_session);
+/* The greedy chain of one block; its factors replace the session's factors. */
+int lz77sss_session_greedy_block(lz77sss_session* s, const lz77sss_params* prm, lz77sss_block* blk,
+                                 uint64_t* num_factors);
+
 /* Average duration (ms) of the dominant kernel (SSS main pass) over the
  * last call, measured with hipEvents on its own stream; bytes = algorithmic
  * bytes of that launch (n + 4|S|). */

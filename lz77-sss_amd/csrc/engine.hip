@@ -103,16 +103,7 @@ u64 engine::emit_skip_phrases() {
     return z;
 }
 
-u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode) {
-    LZ_HIP(hipSetDevice(device));
-    if (phr_mode < LZ77SSS_LPF_NAIVE || phr_mode > LZ77SSS_LPF_LNF_OPT) throw error(LZ77SSS_EINVAL, "unsupported phrase mode");
-    if (n > POS_MAX_N)
-        throw error(LZ77SSS_EINVAL, sizeof(pos_t) == 4 ? "n too large for pos_t = uint32_t" : "n too large");
-    num_fact = 0;
-    last_fact_mode = fact_mode;
-    stats.assign(24, 0);
-    if (n == 0) return 0;
-    timer.begin(st);
+void engine::prepare_phrases(int phr_mode, bool external_sss) {
     const bool dbg = debug_enabled();
     auto trace = [&](const char* what) {
         if (!dbg) return;
@@ -120,7 +111,11 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         std::fprintf(stderr, "[lz77sss-debug] done %s (|S|=%u phrases=%u)\n", what, s, num_phr);
     };
     if (phr_mode == LZ77SSS_LPF_OPT || phr_mode == LZ77SSS_LPF_NAIVE) {
-        build_sss(d_text);
+        if (external_sss) {
+            build_q_runs(d_text);  // the LCE's run table; S came from set_sss
+        } else {
+            build_sss(d_text);
+        }
         timer.mark("sss");
         trace("sss");
         build_sa_s(d_text);
@@ -134,6 +129,7 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         timer.mark("lpf");
         trace("lpf");
     } else {
+        if (external_sss) throw error(LZ77SSS_EINVAL, "an external sync set needs phr_mode lpf_opt or lpf_naive");
 #ifdef LZ_POS64
         throw error(LZ77SSS_EINVAL, "LPF/LNF phrase modes are built for pos_t = uint32_t only");
 #else
@@ -141,6 +137,29 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         trace("lpf_lnf");
 #endif
     }
+}
+
+void engine::set_sss(const pos_t* S_any, u64 count, bool runs) {
+    LZ_HIP(hipSetDevice(device));
+    if (count >= (1ull << 32)) throw error(LZ77SSS_EINVAL, "sync set too large");
+    pos_t* d = S.get(count + 1);
+    if (count) LZ_HIP(hipMemcpyAsync(d, S_any, count * sizeof(pos_t), hipMemcpyDefault, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    s = (u32)count;
+    has_runs = runs;
+}
+
+u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode) {
+    LZ_HIP(hipSetDevice(device));
+    if (phr_mode < LZ77SSS_LPF_NAIVE || phr_mode > LZ77SSS_LPF_LNF_OPT) throw error(LZ77SSS_EINVAL, "unsupported phrase mode");
+    if (n > POS_MAX_N)
+        throw error(LZ77SSS_EINVAL, sizeof(pos_t) == 4 ? "n too large for pos_t = uint32_t" : "n too large");
+    num_fact = 0;
+    last_fact_mode = fact_mode;
+    stats.assign(24, 0);
+    if (n == 0) return 0;
+    timer.begin(st);
+    prepare_phrases(phr_mode, false);
     if (fact_mode == LZ77SSS_SKIP_PHRASES) {
         num_fact = emit_skip_phrases();
         timer.mark("skip_phrases");
@@ -148,7 +167,7 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         num_fact = factorize_greedy(d_text, rk_seed, log2_override);
         timer.mark("greedy");
     }
-    trace("greedy");
+    if (debug_enabled()) std::fprintf(stderr, "[lz77sss-debug] done greedy (|S|=%u phrases=%u)\n", s, num_phr);
     LZ_HIP(hipStreamSynchronize(st));
     if (log) {
         for (auto& [name, ms] : timer.read()) std::fprintf(stderr, "[lz77sss] %-10s %9.3f ms\n", name.c_str(), ms);
@@ -157,6 +176,40 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
                      (unsigned long long)stats[12], (unsigned long long)stats[13]);
     }
     return num_fact;
+}
+
+// the two halves of lz77sss_session_prepare / _greedy_block (a block of a sharded run)
+static u64 block_prepare(engine& E, int phr_mode, bool external_sss, int log2_override) {
+    LZ_HIP(hipSetDevice(E.device));
+    if (phr_mode != LZ77SSS_LPF_OPT && phr_mode != LZ77SSS_LPF_NAIVE)
+        throw error(LZ77SSS_EINVAL, "a sharded factorization needs phr_mode lpf_opt or lpf_naive");
+    if (E.n > POS_MAX_N) throw error(LZ77SSS_EINVAL, "n too large for pos_t");
+    E.num_fact = 0;
+    E.last_fact_mode = LZ77SSS_GREEDY;
+    E.stats.assign(24, 0);
+    E.timer.begin(E.st);
+    E.prepare_phrases(phr_mode, external_sss);
+    const u64 ent = E.n ? E.carried_entries(log2_override) : 1;
+    E.g_Hs.get(ent);
+    LZ_HIP(hipStreamSynchronize(E.st));
+    return ent * sizeof(pos_t);
+}
+static u64 block_run(engine& E, u32 rk_seed, int log2_override, u64* st) {
+    LZ_HIP(hipSetDevice(E.device));
+    greedy_block b;
+    b.start = (pos_t)st[0];
+    b.idxpos = (pos_t)st[1];
+    b.zmask = (u32)st[2];
+    b.carried = st[3] != 0;
+    b.end = (pos_t)st[4];
+    E.timer.begin(E.st);
+    E.num_fact = E.n ? E.factorize_greedy(E.d_text, rk_seed, log2_override, &b) : 0;
+    E.timer.mark("greedy");
+    LZ_HIP(hipStreamSynchronize(E.st));
+    st[5] = b.exit_start;
+    st[6] = b.exit_idxpos;
+    st[7] = b.exit_zmask;
+    return E.num_fact;
 }
 
 }  // namespace LZ_NS
@@ -204,6 +257,12 @@ struct engine64_impl final : lz::engine_if {
     double sss_kernel_ms() const override { return E.sss_kernel_ms; }
     u64 sss_kernel_bytes() const override { return E.sss_kernel_bytes; }
     u32 dec_rounds() const override { return E.dec_rounds; }
+    void set_sss(const u64* S_any, u64 count, bool runs) override { E.set_sss(S_any, count, runs); }
+    u64 prepare(int phr_mode, bool external_sss, int log2_override) override {
+        return block_prepare(E, phr_mode, external_sss, log2_override);
+    }
+    void* carried_table() override { return E.g_Hs.p; }
+    u64 greedy_block(u32 rk_seed, int log2_override, u64* st) override { return block_run(E, rk_seed, log2_override, st); }
 };
 }  // namespace lz64
 namespace lz {
@@ -661,6 +720,73 @@ LZ77SSS_API void lz77sss_session_destroy(lz77sss_session* s) {
     s->E64.reset();
     s->E.destroy();
     delete s;
+}
+
+// ---- sharded factorization: sync set by text block + all-gather, the
+// phrases on every rank, the greedy chain block by block in rank order
+__global__ void k_narrow_u32(const uint64_t* __restrict__ in, uint64_t m, uint32_t* __restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) out[k] = (uint32_t)in[k];
+}
+
+LZ77SSS_API int lz77sss_session_set_sss(lz77sss_session* s, const uint64_t* S, uint64_t count, int has_runs) {
+    if (!s || (!S && count)) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (s->E64) return s->E64->set_sss(S, count, has_runs != 0);
+        lz::engine& E = s->E;
+        LZ_HIP(hipSetDevice(E.device));
+        if (count && E.n > 0xFFFFFFF0ull) throw lz::error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
+        lz::u64* tmp = E.u64a.get(count + 1);
+        if (count) LZ_HIP(hipMemcpyAsync(tmp, S, count * 8, hipMemcpyDefault, E.st));
+        lz::u32* narrow = E.u32e.get(count + 1);
+        if (count) k_narrow_u32<<<lz::cdiv(count, 256), 256, 0, E.st>>>(tmp, count, narrow);
+        LZ_HIP(hipStreamSynchronize(E.st));
+        E.set_sss(narrow, count, has_runs != 0);
+    });
+}
+
+LZ77SSS_API int lz77sss_session_prepare(lz77sss_session* s, const lz77sss_params* prm, int external_sss,
+                                        uint64_t* carried_bytes) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        check_params(prm);
+        const uint64_t b = s->E64 ? s->E64->prepare(prm->phr_mode, external_sss != 0, prm->index_log2_size)
+                                  : lz::block_prepare(s->E, prm->phr_mode, external_sss != 0, prm->index_log2_size);
+        if (carried_bytes) *carried_bytes = b;
+    });
+}
+
+LZ77SSS_API int lz77sss_session_carried_copy(lz77sss_session* s, void* buf, uint64_t bytes, int to_session) {
+    if (!s || (!buf && bytes)) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        void* tab = s->E64 ? s->E64->carried_table() : (void*)s->E.g_Hs.p;
+        const uint64_t cap = s->E64 ? 0 : s->E.g_Hs.cap * sizeof(lz::pos_t);
+        if (!tab) throw lz::error(LZ77SSS_EINVAL, "no carried table: call lz77sss_session_prepare first");
+        if (!s->E64 && bytes > cap) throw lz::error(LZ77SSS_EINVAL, "carried table smaller than the copy");
+        const int dev = s->E64 ? s->E64->device() : s->E.device;
+        hipStream_t st = s->E64 ? s->E64->stream() : s->E.st;
+        LZ_HIP(hipSetDevice(dev));
+        if (bytes) {
+            if (to_session) LZ_HIP(hipMemcpyAsync(tab, buf, bytes, hipMemcpyDefault, st));
+            else LZ_HIP(hipMemcpyAsync(buf, tab, bytes, hipMemcpyDefault, st));
+        }
+        LZ_HIP(hipStreamSynchronize(st));
+    });
+}
+
+LZ77SSS_API int lz77sss_session_greedy_block(lz77sss_session* s, const lz77sss_params* prm, lz77sss_block* blk,
+                                             uint64_t* num_factors) {
+    if (!s || !blk) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        check_params(prm);
+        uint64_t st[8] = {blk->start, blk->idxpos, blk->zmask, (uint64_t)(blk->carried != 0), blk->end, 0, 0, 0};
+        const uint64_t z = s->E64 ? s->E64->greedy_block(prm->rk_seed, prm->index_log2_size, st)
+                                  : lz::block_run(s->E, prm->rk_seed, prm->index_log2_size, st);
+        blk->exit_start = st[5];
+        blk->exit_idxpos = st[6];
+        blk->exit_zmask = (uint32_t)st[7];
+        if (num_factors) *num_factors = z;
+    });
 }
 
 }  // extern "C"

@@ -26,6 +26,7 @@
 // The last 64 positions (where the reference's stale / zeroed fingerprints and
 // conditional inserts live, rolling_hash_index_107.hpp:80-150) are walked by
 // one thread (k_tail) with an exact local model of the table.
+#include "../../include/lz77sss.h"
 #include "../include/engine.h"
 #include "../include/lce_dev.h"
 
@@ -298,6 +299,8 @@ struct walk_ctx {
     const pos_t* apos2;
     u64 napos2;
     const u32* bmI;      // current insert set (membership of added positions)
+    pos_t bmoff;         // text position of bit 0 of the window bitmaps (a multiple of 32)
+    const pos_t* Hs;     // window mode: slot -> last insert before the window (POS_NONE), or null
     int use_pred;        // base lookups via pred5 (else bucket search)
     lce_view L;
 };
@@ -343,7 +346,10 @@ __device__ pos_t base_last_before(const walk_ctx& W, u32 slot, pos_t q, u32 ord)
     }
     return POS_NONE;
 }
-__device__ __forceinline__ bool in_I(const walk_ctx& W, pos_t q) { return (W.bmI[q >> 5] >> (q & 31)) & 1; }
+__device__ __forceinline__ bool in_I(const walk_ctx& W, pos_t q) {
+    const pos_t r = q - W.bmoff;
+    return (W.bmI[r >> 5] >> (r & 31)) & 1;
+}
 // key field of position q in an added list: q itself (u32) or the number of list
 // positions below q (u64; first_ge) / at or below q (!first_ge)
 __device__ __forceinline__ u64 added_x(const pos_t* apos, u64 na, pos_t q, bool first_ge) {
@@ -384,6 +390,11 @@ __device__ pos_t added_last_before(const walk_ctx& W, u32 slot, pos_t q, u32 ord
     if (W.nadd2) r = occ_max(r, added_last_before_1(W, W.akeys2, W.abeg2, W.apos2, W.napos2, slot, q, ord));
     return r;
 }
+// last insert into the slot before the window (the carried table holds pos + 1, 0 = none)
+__device__ __forceinline__ pos_t carried(const walk_ctx& W, u32 slot) {
+    const pos_t h = W.Hs[slot];
+    return h ? h - 1 : POS_NONE;
+}
 // H[slot of (q,x)] just before longest_prev_occ's advance_and_get_occ<x> at q
 __device__ pos_t lookup(const walk_ctx& W, pos_t q, int x, int& hint) {
     const u32 ord = 4 - x;
@@ -415,7 +426,8 @@ __device__ pos_t lookup(const walk_ctx& W, pos_t q, int x, int& hint) {
         slot = (u32)((u64)kr_direct(W.T, q, W.G.lens[x], W.G.base[x]) & W.G.mask);
         cb = base_last_before(W, slot, q, ord);
     }
-    return occ_max(cb, added_last_before(W, slot, q, ord));
+    const pos_t r = occ_max(cb, added_last_before(W, slot, q, ord));
+    return (r == POS_NONE && W.Hs) ? carried(W, slot) : r;  // inserts of earlier windows are all older
 }
 
 // ---------------------------------------------------------------------------
@@ -602,7 +614,8 @@ __global__ void k_tail(walk_ctx W, seg_in in, pos_t* __restrict__ fact, u64 off,
         for (int k = nloc - 1; k >= 0; k--)
             if (loc[k].slot == slot) return loc[k].pos;
         // every base / added entry lies below nt
-        return occ_max(base_last_before(W, slot, nt, 0), added_last_before(W, slot, nt, 0));
+        const pos_t r = occ_max(base_last_before(W, slot, nt, 0), added_last_before(W, slot, nt, 0));
+        return (r == POS_NONE && W.Hs) ? carried(W, slot) : r;
     };
     auto insert = [&](pos_t q, u32 slot) {
         if (nloc < TAIL_CAP) loc[nloc++] = {slot, q};
@@ -721,12 +734,13 @@ __device__ __forceinline__ void atomic_max_pos(pos_t* a, pos_t v) {
     if constexpr (sizeof(pos_t) == 4) atomicMax((u32*)a, (u32)v);
     else atomicMax((unsigned long long*)a, (unsigned long long)v);
 }
-__global__ void k_h_fill(const u8* __restrict__ T, gap_cfg G, const u32* __restrict__ bm, pos_t y, pos_t* __restrict__ H) {
+__global__ void k_h_fill(const u8* __restrict__ T, gap_cfg G, const u32* __restrict__ bm, pos_t off, pos_t y,
+                         pos_t* __restrict__ H) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (w * 32 >= y) return;
+    if (off + w * 32 >= y) return;
     u32 bits = bm[w];
     while (bits) {
-        const pos_t q = (pos_t)(32 * w) + (pos_t)__builtin_ctz(bits);
+        const pos_t q = off + (pos_t)(32 * w) + (pos_t)__builtin_ctz(bits);
         bits &= bits - 1;
         if (q >= y) break;
         // confirmed inserts lie below the tail region: all 5 fingerprints are full windows
@@ -734,12 +748,18 @@ __global__ void k_h_fill(const u8* __restrict__ T, gap_cfg G, const u32* __restr
             atomic_max_pos(&H[(u32)((u64)kr_direct(T, q, G.lens[x], G.base[x]) & G.mask)], q + 1);
     }
 }
-__global__ void k_h_fix(pos_t* __restrict__ H, u64 m) {
+__global__ void k_h_fix(pos_t* __restrict__ H, u64 m) {  // pos + 1 (0 = none) -> pos (POS_NONE)
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < m) H[k] = H[k] ? H[k] - 1 : POS_NONE;
 }
+__global__ void k_h_unfix(const pos_t* __restrict__ H, u64 m, pos_t* __restrict__ Hs) {  // pos -> pos + 1
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < m) Hs[k] = H[k] == POS_NONE ? 0 : H[k] + 1;
+}
+// out: [0] factors, [1] guard tripped, [2] exit position (>= stop), [3] index position there
 __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __restrict__ P, lce_view L,
-                           pos_t* __restrict__ H, seg_in in, pos_t* __restrict__ fact, u64 off, u64* __restrict__ out) {
+                           pos_t* __restrict__ H, seg_in in, pos_t stop, pos_t* __restrict__ fact, u64 off,
+                           u64* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const pos_t n = G.n;
     u128 fp[5];
@@ -798,9 +818,13 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __r
     pos_t i = in.start;
     u32 p = in.p;
     out[1] = 0;
+    out[2] = n;
     for (;;) {
         if (++guard > 4ull * n + 1024 || i > n) { out[1] = 1; break; }
         pos_t gap_end = P[3 * p];
+        // window end: hand over at a gap start or a gap-walk factor start >= stop (the
+        // segment walks' boundaries), before the index rolls to it
+        if (i >= stop && i < gap_end) { out[2] = i; break; }
         if (i < gap_end) {
             if (cur < i) {
                 if (i - cur <= G.thr) {
@@ -809,7 +833,9 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __r
                     reinit(i);
                 }
             }
+            bool stopped = false;
             do {
+                if (i >= stop) { stopped = true; break; }
                 pos_t fsrc, flen;
                 longest_prev_occ(i, fsrc, flen);
                 i += flen ? flen : 1;
@@ -826,6 +852,7 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __r
                 emit(fsrc, flen);
                 while (cur < i) advance();
             } while (i < gap_end);
+            if (stopped) { out[2] = i; break; }
         }
         if (i == n) break;
         const pos_t exc = i - gap_end;
@@ -840,11 +867,12 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __r
         while (P[3 * p + 1] <= i) p++;
     }
     out[0] = nf;
+    out[3] = cur;
 }
 // first set bit of a bitmap (~0 if none), one atomic per workgroup
-__global__ void k_first_bit(const u32* __restrict__ bm, u64 nw, u64* __restrict__ out) {
+__global__ void k_first_bit(const u32* __restrict__ bm, u64 nw, pos_t off, u64* __restrict__ out) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    const u64 v = (w < nw && bm[w]) ? 32 * w + (u64)__builtin_ctz(bm[w]) : ~0ull;
+    const u64 v = (w < nw && bm[w]) ? off + 32 * w + (u64)__builtin_ctz(bm[w]) : ~0ull;
     block_min64(out, v);
 }
 
@@ -908,14 +936,15 @@ struct seg_tab {
     seg_out* sout;
     u8* valid;       // output exact for the current lookup state
     u32* succ;       // id of the segment starting at sout.next (NONE = unknown)
-    u32* seg_at;     // text position -> segment id (NONE / PENDING)
+    u32* seg_at;     // text position - segoff -> segment id (NONE / PENDING)
+    pos_t segoff;    // window start
     u32* nseg;       // device counter
     u32 cap;
     const pos_t* cbv;  // chunk boundaries (sorted)
     u32 ncb;
     const pos_t* P;  // phrases (beg, end, src) + sentinel
     u32 m;
-    pos_t N;
+    pos_t N;         // end of the window: a segment whose next start is >= N ends the chain
     u32 zmask0;
     u32* err;        // bit 1: table full, 2: too many LPF-start queries, 4: walk guard
 };
@@ -950,20 +979,28 @@ __device__ __forceinline__ void gap_of(const pos_t* P, u32 k, pos_t& a, pos_t& b
 __device__ __forceinline__ u32 gap_chunks(pos_t a, pos_t b, u32 CH) {
     return (b > a && b - a > 2 * (pos_t)CH) ? (u32)((b - a - CH / 2 - 1) / CH) : 0;
 }
-__global__ void k_gap_counts(const pos_t* __restrict__ P, u32 m, u32 CH, u32* __restrict__ nsegs, u32* __restrict__ ncbs) {
+// gap k clipped to the window [lo, hi)
+__device__ __forceinline__ void gap_in(const pos_t* P, u32 k, pos_t lo, pos_t hi, pos_t& a, pos_t& b) {
+    gap_of(P, k, a, b);
+    a = max(a, lo);
+    b = min(b, hi);
+}
+__global__ void k_gap_counts(const pos_t* __restrict__ P, u32 m, u32 CH, pos_t lo, pos_t hi, u32* __restrict__ nsegs,
+                             u32* __restrict__ ncbs) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
     pos_t a, b;
-    gap_of(P, (u32)k, a, b);
+    gap_in(P, (u32)k, lo, hi, a, b);
     const u32 K = gap_chunks(a, b, CH);
     nsegs[k] = (a < b) ? 1 + K : 0;
     ncbs[k] = K;
 }
-__global__ void k_gap_cbv(const pos_t* __restrict__ P, u32 m, u32 CH, const u32* __restrict__ cb_off, pos_t* __restrict__ cbv) {
+__global__ void k_gap_cbv(const pos_t* __restrict__ P, u32 m, u32 CH, pos_t lo, pos_t hi, const u32* __restrict__ cb_off,
+                          pos_t* __restrict__ cbv) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
     pos_t a, b;
-    gap_of(P, (u32)k, a, b);
+    gap_in(P, (u32)k, lo, hi, a, b);
     const u32 K = gap_chunks(a, b, CH);
     for (u32 t = 1; t <= K; t++) cbv[cb_off[k] + t - 1] = a + (pos_t)t * CH;
 }
@@ -972,7 +1009,7 @@ __global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off) {
     const u32 lane = threadIdx.x & 63;
     if (k > S.m) return;
     pos_t a, b;
-    gap_of(S.P, (u32)k, a, b);
+    gap_in(S.P, (u32)k, S.segoff, S.N, a, b);
     if (a >= b) return;
     const u32 K = gap_chunks(a, b, CH);
     for (u32 t = lane; t <= K; t += 64) {
@@ -981,7 +1018,7 @@ __global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off) {
         S.sin[id] = seg_in{x, (u32)k, x, S.zmask0, upper_cb(S, x)};
         S.valid[id] = 0;
         S.succ[id] = NONE;
-        S.seg_at[x] = id;
+        S.seg_at[x - S.segoff] = id;
     }
 }
 // bitmaps over text positions (bit q of word q >> 5)
@@ -1005,21 +1042,24 @@ __device__ __forceinline__ void bm_set_range_wave(u32* bm, pos_t a, pos_t b, u32
         atomicOr(&bm[w], mask);
     }
 }
-__global__ void k_gap_bitmaps(const pos_t* __restrict__ P, u32 m, pos_t N, pos_t nt, u32* __restrict__ bmI,
-                              u32* __restrict__ bmSup) {
+// positions of the window [lo, hi) only, relative to off
+__global__ void k_gap_bitmaps(const pos_t* __restrict__ P, u32 m, pos_t N, pos_t nt, pos_t lo, pos_t hi, pos_t off,
+                              u32* __restrict__ bmI, u32* __restrict__ bmSup) {
     const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per phrase
     const u32 lane = threadIdx.x & 63;
     if (k > m) return;
     pos_t a, b;
     gap_of(P, (u32)k, a, b);
     if (a < b) {
-        const pos_t e = min(min((pos_t)(b + 1), N), nt);
-        bm_set_range_wave(bmI, a, e, lane);
-        bm_set_range_wave(bmSup, a, e, lane);
+        const pos_t s0 = max(a, lo), e = min(min(min((pos_t)(b + 1), N), nt), hi);
+        if (s0 < e) {
+            bm_set_range_wave(bmI, s0 - off, e - off, lane);
+            bm_set_range_wave(bmSup, s0 - off, e - off, lane);
+        }
     }
     if (k < m) {
-        const pos_t pb = P[3 * k], pe = P[3 * k + 1];
-        if (pe - pb <= 48 && pb < nt) bm_set_range_wave(bmSup, pb, min(pe, nt), lane);
+        const pos_t pb = max(P[3 * k], lo), pe = min(min(P[3 * k + 1], nt), hi);
+        if (P[3 * k + 1] - P[3 * k] <= 48 && pb < pe) bm_set_range_wave(bmSup, pb - off, pe - off, lane);
     }
 }
 __global__ void k_bm_xor(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
@@ -1084,7 +1124,7 @@ __global__ __launch_bounds__(BMB_T) void k_bmb_count(M mk, u64 nw, u64* __restri
 // a round are scanned across the block (wave scan + 4 wave totals in LDS), so the
 // outputs stay in word order
 template <class M, class OUT>
-__global__ __launch_bounds__(BMB_T) void k_bmb_write(M mk, u64 nw, const u64* __restrict__ bincl, OUT out) {
+__global__ __launch_bounds__(BMB_T) void k_bmb_write(M mk, u64 nw, const u64* __restrict__ bincl, OUT out, pos_t off) {
     __shared__ u64 wsum[BMB_T / 64];
     const u32 l = threadIdx.x, lane = l & 63, wv = l >> 6;
     u64 base = blockIdx.x ? bincl[blockIdx.x - 1] : 0ull;
@@ -1109,8 +1149,8 @@ __global__ __launch_bounds__(BMB_T) void k_bmb_write(M mk, u64 nw, const u64* __
         }
         const u64 o = base + pre + inc - mine;
         u32 oa = (u32)(o >> 32), ob = (u32)o;
-        while (a) { out.a(oa++, (pos_t)(32 * w + __builtin_ctz(a)), w); a &= a - 1; }
-        while (b) { out.b(ob++, (pos_t)(32 * w + __builtin_ctz(b))); b &= b - 1; }
+        while (a) { out.a(oa++, off + (pos_t)(32 * w + __builtin_ctz(a)), w); a &= a - 1; }
+        while (b) { out.b(ob++, off + (pos_t)(32 * w + __builtin_ctz(b))); b &= b - 1; }
         base += tot;
         __syncthreads();  // wsum reused by the next round
     }
@@ -1127,7 +1167,7 @@ struct out_list {  // positions + a flag bit from a second bitmap
     const u32* flagbm;
     __device__ __forceinline__ void a(u32 o, pos_t p, u64 w) const {
         pos[o] = p;
-        if (flag) flag[o] = (flagbm[w] >> (p & 31)) & 1;
+        if (flag) flag[o] = (flagbm[w] >> (p & 31)) & 1;  // offsets are multiples of 32
     }
     __device__ __forceinline__ void b(u32, pos_t) const {}
 };
@@ -1172,10 +1212,11 @@ __global__ void k_iv_chunks(const pos_t* __restrict__ st, const pos_t* __restric
     ch[c] = ichunk{q, min(en[lo], (pos_t)(q + chl)), rank[lo] + (u32)(q - st[lo])};
 }
 // rem[r] = base position r not in I
-__global__ void k_rem_from_bm(const pos_t* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, u8* __restrict__ rem) {
+__global__ void k_rem_from_bm(const pos_t* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, pos_t off,
+                              u8* __restrict__ rem) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nb) return;
-    const pos_t q = ipos[r];
+    const pos_t q = ipos[r] - off;
     rem[r] = ((bmI[q >> 5] >> (q & 31)) & 1) ? 0 : 1;
 }
 
@@ -1213,12 +1254,12 @@ __global__ void k_todo(seg_tab S, u32 nseg, u32* __restrict__ ids, u32* __restri
 // claim the segment starting at x (created by this thread iff *mine)
 __device__ u32 seg_claim(const seg_tab& S, pos_t x, bool& mine) {
     mine = false;
-    const u32 old = atomicCAS(&S.seg_at[x], NONE, PENDING);
+    const u32 old = atomicCAS(&S.seg_at[x - S.segoff], NONE, PENDING);
     if (old != NONE) return old;
     const u32 id = atomicAdd(S.nseg, 1u);
     if (id >= S.cap) {
         atomicOr(S.err, 1u);
-        atomicExch(&S.seg_at[x], NONE);
+        atomicExch(&S.seg_at[x - S.segoff], NONE);
         return NONE;
     }
     mine = true;
@@ -1233,7 +1274,7 @@ __global__ void k_link(seg_tab S, u32 nseg) {
     const seg_out& o = S.sout[g];
     if ((o.flags & 1) || o.next >= S.N) return;
     const pos_t x = o.next;
-    const u32 s = S.seg_at[x];
+    const u32 s = S.seg_at[x - S.segoff];
     if (s == PENDING) return;
     if (s != NONE) { S.succ[g] = s; return; }
     // alias into the chunk walk that covers x?
@@ -1245,7 +1286,7 @@ __global__ void k_link(seg_tab S, u32 nseg) {
             if (S.cbv[mid] <= x) lo = mid + 1; else hi = mid;
         }
         if (lo > 0 && S.cbv[lo - 1] < x) {
-            const u32 gc = S.seg_at[S.cbv[lo - 1]];
+            const u32 gc = S.seg_at[S.cbv[lo - 1] - S.segoff];
             if (gc < S.cap) {
                 if (!S.valid[gc]) return;  // the chunk walk is stale: walked next round, link again
                 const seg_out& oc = S.sout[gc];
@@ -1269,13 +1310,13 @@ __global__ void k_link(seg_tab S, u32 nseg) {
         S.valid[id] = 0;
     }
     __threadfence();
-    atomicExch(&S.seg_at[x], id);
+    atomicExch(&S.seg_at[x - S.segoff], id);
     S.succ[g] = id;
 }
 // sparse reset of the position -> segment map (every entry set was a segment start)
 __global__ void k_seg_at_clear(seg_tab S, u32 nseg) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < nseg) S.seg_at[S.sin[g].start] = NONE;
+    if (g < nseg) S.seg_at[S.sin[g].start - S.segoff] = NONE;
 }
 // pointer doubling along succ: J = terminal-or-successor, D = hops
 __global__ void k_jump0(seg_tab S, u32 nseg, u32* __restrict__ J, u32* __restrict__ D) {
@@ -1298,11 +1339,12 @@ __global__ void k_jumpk(const u32* __restrict__ J, const u32* __restrict__ D, u3
     D2[g] = D[g] + D[j];
 }
 struct chain_status { u32 term, hops, valid, flags; pos_t next; u32 err, nseg; };
-__global__ void k_chain_status(seg_tab S, const u32* __restrict__ J, const u32* __restrict__ D, chain_status* out) {
-    const u32 t = J[0];
+__global__ void k_chain_status(seg_tab S, const u32* __restrict__ J, const u32* __restrict__ D, u32 c0,
+                               chain_status* out) {
+    const u32 t = J[c0];
     chain_status c{};
     c.term = t;
-    c.hops = D[0];
+    c.hops = D[c0];
     c.valid = S.valid[t];
     c.flags = S.sout[t].flags;
     c.next = S.sout[t].next;
@@ -1312,36 +1354,82 @@ __global__ void k_chain_status(seg_tab S, const u32* __restrict__ J, const u32* 
 }
 // chain[k] = k-th successor of segment 0 (binary lifting over the stored levels)
 struct jump_levels { const u32* J[MAX_LV]; u32 nlv; };
-__global__ void k_chain_expand(jump_levels JL, u32 len, u32* __restrict__ chain) {
+__global__ void k_chain_expand(jump_levels JL, u32 len, u32 c0, u32* __restrict__ chain) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= len) return;
-    u32 g = 0;
+    u32 g = c0;
     for (u32 l = 0; l < JL.nlv; l++)
         if ((k >> l) & 1) g = JL.J[l][g];
     chain[k] = g;
 }
 // I' bitmap: what the chain inserted below nt ([start, e) + LPF-start queries)
-__global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, pos_t nt, u32* __restrict__ bm) {
+// (clipped to the window's bitmap range [off, hi), hi <= nt)
+__global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, pos_t hi, pos_t off,
+                                u32* __restrict__ bm) {
     const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per chain node
     const u32 lane = threadIdx.x & 63;
     if (k >= cnt) return;
     const u32 g = chain[k];
     const seg_out& o = S.sout[g];
-    const pos_t a = S.sin[g].start, b = min(o.e, nt);
-    bm_set_range_wave(bm, a, b, lane);
-    if (lane < o.nsingle && lane < 4 && o.single[lane] < nt) atomicOr(&bm[o.single[lane] >> 5], 1u << (o.single[lane] & 31));
+    const pos_t a = S.sin[g].start, b = min(o.e, hi);
+    if (a < b) bm_set_range_wave(bm, a - off, b - off, lane);
+    if (lane < o.nsingle && lane < 4 && o.single[lane] < hi) {
+        const pos_t r = o.single[lane] - off;
+        atomicOr(&bm[r >> 5], 1u << (r & 31));
+    }
+}
+// the window's entry segment: the exact chain state handed over by the previous window
+// (a default segment starting there takes it over); *c0 = its id
+__global__ void k_entry_seg(seg_tab S, pos_t start, pos_t idxpos, u32 zmask, u32* __restrict__ c0) {
+    u32 g = S.seg_at[start - S.segoff];
+    if (g == NONE) {
+        g = atomicAdd(S.nseg, 1u);
+        S.seg_at[start - S.segoff] = g;
+    }
+    seg_in in = make_seg_in(S, start);
+    in.idxpos = idxpos;
+    in.zmask = zmask;
+    S.sin[g] = in;
+    S.valid[g] = 0;
+    S.succ[g] = NONE;
+    *c0 = g;
+}
+// window exit: the chain's last segment stopped at a start >= the window end
+__global__ void k_exit_state(seg_tab S, u32 term, seg_in* __restrict__ out) {
+    const seg_out& o = S.sout[term];
+    seg_in x{};
+    x.start = o.next;
+    x.idxpos = o.idxpos;
+    x.zmask = o.zmask;
+    *out = x;
+}
+// carried table (pos + 1, 0 = none): every insert of the window's chain, for the next window
+__global__ void k_h_export(const u8* __restrict__ T, gap_cfg G, seg_tab S, const u32* __restrict__ chain, u32 cnt,
+                           pos_t* __restrict__ Hs) {
+    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per chain node
+    const u32 lane = threadIdx.x & 63;
+    if (k >= cnt) return;
+    const u32 g = chain[k];
+    const seg_out& o = S.sout[g];
+    const pos_t a = S.sin[g].start;
+    auto put = [&](pos_t q) {
+        for (int x = 0; x < 5; x++)
+            atomic_max_pos(&Hs[(u32)((u64)kr_direct(T, q, G.lens[x], G.base[x]) & G.mask)], q + 1);
+    };
+    for (pos_t q = a + lane; q < o.e; q += 64) put(q);
+    if (lane < o.nsingle && lane < 4) put(o.single[lane]);
 }
 // completion start: the last chain node whose start is <= y0 (the first position where
 // the speculated insert set and the chain's differ): every lookup of its predecessors
 // happened below y0, so its start state is exact (index state from its predecessor)
 struct chain_cut { u32 k, pad; seg_in in; };
 __global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, const u64* __restrict__ y0p,
-                            chain_cut* __restrict__ out) {
+                            seg_in entry, chain_cut* __restrict__ out) {
     const u64 y0 = *y0p;
     chain_cut c{};
-    if (nall == 0 || y0 == 0) {
+    if (nall == 0 || y0 <= entry.start) {
         c.k = 0;
-        c.in = make_seg_in(S, 0);
+        c.in = entry;
         *out = c;
         return;
     }
@@ -1350,21 +1438,20 @@ __global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, 
         const u32 mid = (lo + hi) >> 1;
         if (S.sin[chain[mid]].start <= y0) lo = mid + 1; else hi = mid;
     }
-    c.k = lo - 1;  // chain[0] starts at 0 <= y0
+    c.k = lo - 1;  // chain[0] starts at the window entry <= y0
     c.in = S.sin[chain[c.k]];
     if (c.k > 0) {
         const seg_out& pv = S.sout[chain[c.k - 1]];
         c.in.idxpos = pv.idxpos;
         c.in.zmask = pv.zmask;
     } else {
-        c.in.idxpos = 0;
-        c.in.zmask = S.zmask0;
+        c.in = entry;
     }
     *out = c;
 }
-__global__ void k_set_pairs(const pos_t* __restrict__ pairs, u32 np, u32* __restrict__ bm) {
+__global__ void k_set_pairs(const pos_t* __restrict__ pairs, u32 np, pos_t off, u32* __restrict__ bm) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < np) bm_set_range(bm, pairs[2 * k], pairs[2 * k + 1]);
+    if (k < np && pairs[2 * k] >= off) bm_set_range(bm, pairs[2 * k] - off, pairs[2 * k + 1] - off);
 }
 __global__ void k_chain_nfact(seg_tab S, const u32* __restrict__ chain, u32 cnt, u64* __restrict__ nf) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1414,7 +1501,27 @@ static T excl_scan(T* cnt, T* off, u64 m, dbuf<u8>& tmp, hipStream_t st) {
     return rd1(off + m, st);
 }
 
-u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
+// gap-index slot count (the carried table's entries) of the current phrases
+u64 engine::carried_entries(int log2_override) {
+    const pos_t N = (pos_t)n;
+    const u32 m = num_phr;
+    pos_t* P = lpf.get((u64)(m + 1) * 3);
+    k_put3<<<1, 1, 0, st>>>(P + 3 * (u64)m, N, N + 1, 0);
+    u64 num_gaps = 1;
+    pos_t len_lpf_phr = 0;
+    if (m > 0) {
+        u64* acc = counters64.get(4) + 2;
+        LZ_HIP(hipMemsetAsync(acc, 0, 16, st));
+        k_phrase_info<<<cdiv(m, 256), 256, 0, st>>>(P, m, N, acc);
+        len_lpf_phr = (pos_t)rd1(acc, st);
+        num_gaps = rd1(acc + 1, st);
+    }
+    gap_params_h gp = choose_gap_params(N, m, len_lpf_phr, num_gaps);
+    if (log2_override > 0) gp.log2_size_h = (u32)log2_override;
+    return 1ull << gp.log2_size_h;
+}
+
+u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy_block* blk) {
     const bool dbg = debug_enabled();
     double t_mark = now_ms();
     auto lap = [&](const char* what) {
@@ -1438,10 +1545,6 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
         len_lpf_phr = (pos_t)rd1(acc, st);
         num_gaps = rd1(acc + 1, st);
     }
-    // entry ids are 32-bit: the base superset (gaps + LPF-start queries + short phrase
-    // interiors) must hold fewer than 2^32 / 5 positions
-    if (sizeof(pos_t) > 4 && ((u64)(N - len_lpf_phr) + 49ull * (m + 1)) * 5 >= (1ull << 32))
-        throw error(-1, "gap region too large for 32-bit entry ids");
     gap_params_h gp = choose_gap_params(N, num_lpf, len_lpf_phr, num_gaps);
     if (log2_override > 0) gp.log2_size_h = (u32)log2_override;
     // bases: rk_prime::random64(257, 2^20-1) from mt19937_64(rk_seed) (rolling_hash.hpp:127-130)
@@ -1475,525 +1578,666 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override) {
     G.negpow = d_negpow;
     u32 zmask0 = 0;
     for (int x = 0; x < 5; x++) zmask0 |= (G.lens[x] >= N) ? (1u << x) : 0u;  // reinit(0) at construction
-    const u64 nw = (u64)N / 32 + 2;  // bitmap words (a zero word past the end)
-    const unsigned gw = cdiv(nw, 256);
-    const unsigned bmb_blocks = (unsigned)std::max<u64>(1, (nw + BMB - 1) / BMB);
-
-    // ---- default segments: gaps + chunk boundaries of long gaps
     const char* ch_env = std::getenv("LZ77SSS_GAP_CHUNK");  // tuning knob (walk length per segment)
     const u32 CH = std::getenv("LZ77SSS_NO_CHUNK") ? 0x0FFFFFFFu : ch_env ? (u32)std::max(16, std::atoi(ch_env)) : 512u;
-    u32* cnt_seg = g_tmp1.get(m + 2);
-    u32* cnt_cb = g_tmp2.get(m + 2);
-    u32* off_seg = g_tmp3.get(m + 2);
-    u32* off_cb = g_tmp4.get(m + 2);
-    k_gap_counts<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, cnt_seg, cnt_cb);
-    const u32 nseg0 = excl_scan(cnt_seg, off_seg, m + 1, scan_tmp, st);
-    const u32 ncb = excl_scan(cnt_cb, off_cb, m + 1, scan_tmp, st);
-    pos_t* cbv = g_cbv.get(ncb + 1);
-    k_gap_cbv<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, off_cb, cbv);
-    u32 cap = nseg0 + nseg0 / 2 + (1u << 16);
-    seg_tab S{};
-    auto bind_tab = [&]() {
-        S.sin = g_sin.p; S.sout = g_sout.p; S.valid = g_valid.p; S.succ = g_succ.p; S.cap = cap;
-    };
-    g_sin.get(cap); g_sout.get(cap); g_valid.get(cap); g_succ.get(cap);
-    bind_tab();
-    {
-        // the position -> segment map is cleared sparsely after each call (k_seg_at_clear);
-        // a fresh or reallocated map, or one left dirty by a failed call, is cleared densely
-        u32* prev = g_seg_at.p;
-        S.seg_at = g_seg_at.get((u64)N + 1);
-        if (S.seg_at != prev || !seg_at_clean || seg_at_n < (u64)N + 1) {
-            LZ_HIP(hipMemsetAsync(S.seg_at, 0xFF, g_seg_at.cap * 4, st));
-            seg_at_n = g_seg_at.cap;
-        }
-        seg_at_clean = false;
-    }
-    S.nseg = (u32*)counters64.get(4);
-    S.err = S.nseg + 1;
-    LZ_HIP(hipMemsetAsync(S.nseg, 0, 8, st));
-    LZ_HIP(hipMemcpyAsync(S.nseg, &nseg0, 4, hipMemcpyHostToDevice, st));
-    S.cbv = cbv; S.ncb = ncb; S.P = P; S.m = m; S.N = N; S.zmask0 = zmask0;
-    k_gap_segs<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(S, CH, off_seg);
-    // bitmaps: I (current speculation), I' (what the chain inserted), Ib (base set), scratch
-    u32* bmI = g_bmI.get(nw);
-    u32* bmI2 = g_bmI2.get(nw);
-    u32* bmIb = g_bmIb.get(nw);
-    u32* bmT = g_bmT.get(nw);
-    LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
-    LZ_HIP(hipMemsetAsync(bmT, 0, nw * 4, st));
-    k_gap_bitmaps<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(P, m, N, G.nt, bmI, bmT);
-    LZ_HIP(hipStreamSynchronize(st));
-    lap("greedy setup");
-
-    // ---- bounded completion (k_seq_walk): the chain prefix [0, k*) is written by
-    // the segment walks, the rest by the exact sequential walk from chain node k*
     const char* mo_env = std::getenv("LZ77SSS_GREEDY_MAX_OUTER");  // test knob (0: sequential only)
     const int max_outer = mo_env ? std::max(0, std::atoi(mo_env)) : 256;
     const u64 nslots_all = (u64)G.mask + 1;
-    walk_ctx W{};
-    W.T = T;
-    W.G = G;
-    W.P = P;
-    W.L = view(T);
-    const lce_view& Lv = W.L;
-    u64* d_sq = (u64*)g_cut.get(sizeof(chain_cut) + 64);
-    chain_cut* d_cutp = (chain_cut*)(d_sq + 4);
-    u64* d_y0 = d_sq + 2;
-    auto seq_complete = [&](const u32* chain, u32 nall, const u64* offs, const u32* ins_bm, bool from_zero) -> u64 {
-        if (from_zero) LZ_HIP(hipMemsetAsync(d_y0, 0, 8, st));
-        k_chain_cut<<<1, 1, 0, st>>>(S, chain, from_zero ? 0u : nall, d_y0, d_cutp);
-        chain_cut cut;
-        LZ_HIP(hipMemcpyAsync(&cut, d_cutp, sizeof(cut), hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
-        const u64 offk = cut.k ? rd1(offs + cut.k, st) : 0;
-        pos_t* fo = fact.get(2 * (offk + (u64)(N - cut.in.start) + 2) + 2);
-        if (cut.k) {
-            k_walk<true><<<cdiv(cut.k, 64), 64, 0, st>>>(W, S, chain, cut.k, offs, fo);
-            LZ_HIP(hipGetLastError());
-        }
-        pos_t* H = g_H.get((u64)nslots_all);
-        LZ_HIP(hipMemsetAsync(H, 0, (u64)nslots_all * sizeof(pos_t), st));
-        if (cut.in.start && ins_bm)
-            k_h_fill<<<cdiv(((u64)cut.in.start + 31) / 32, 256), 256, 0, st>>>(T, G, ins_bm, cut.in.start, H);
-        k_h_fix<<<cdiv(nslots_all, 256), 256, 0, st>>>(H, nslots_all);
-        k_seq_walk<<<1, 64, 0, st>>>(T, G, P, Lv, H, cut.in, fo, offk, d_sq);
-        LZ_HIP(hipGetLastError());
-        u64 hc[2];
-        LZ_HIP(hipMemcpyAsync(hc, d_sq, 16, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
-        if (hc[1]) throw error(-6, "greedy: sequential completion guard tripped (internal error)");
-        stats[19] = 1;
-        stats[20] = cut.in.start;
-        lap("sequential completion");
-        return offk + hc[0];
-    };
-
-    // ---- base set (entries sorted by slot) and delta
-    u64 nb = 0;
-    const u32 nslots = G.mask + 1;
-    auto build_buckets = [&](auto key, u64 mk, dbuf<u32>& bk) {
-        u32* b = bk.get((u64)nslots + 1);
-        if (mk * 16 >= nslots) {
-            u32* rev = g_brev.get(2 * ((u64)nslots + 1));
-            u32* scn = rev + nslots + 1;
-            LZ_HIP(hipMemsetAsync(rev, 0xFF, ((u64)nslots + 1) * 4, st));
-            k_bucket_heads<<<cdiv(mk + 1, 256), 256, 0, st>>>(key, mk, nslots, rev);
-            size_t tb = 0;
-            LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, rev, scn, min_u32_op{}, (int)(nslots + 1), st));
-            u8* t = scan_tmp.get(tb);
-            LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, rev, scn, min_u32_op{}, (int)(nslots + 1), st));
-            k_unreverse<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(scn, nslots, b);
-        } else {
-            k_bucket_search<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
-        }
-    };
-    // runs of a bitmap -> intervals (st, en), ranks, chunks for k_slots
-    auto runs_to_chunks = [&](const u32* bm, dbuf<pos_t>& dst, dbuf<pos_t>& den, dbuf<u32>& drk, dbuf<u8>& dch, u32& ni,
-                              u64& npos, u32& nch) -> ichunk* {
-        const u64 tot = bmb_scan(bm_runs{bm}, nw, g_bsum, g_bincl, scan_tmp, st);
-        ni = (u32)(tot >> 32);  // run starts (= run ends)
-        pos_t* a = dst.get(ni + 1);
-        pos_t* b = den.get(ni + 1);
-        k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_runs{bm}, nw, g_bincl.p, out_runs{a, b});
-        u32* len = g_tmp5.get(ni + 1);
-        u32* nc = g_tmp6.get(ni + 1);
-        u32* rk = drk.get(ni + 1);
-        u32* choff = g_tmp7.get(ni + 1);
-        npos = 0;
-        nch = 0;
-        u32 chl = SLOT_CHUNK_LONG;
-        if (ni) {
-            u32* ncs = g_tmp8.get(ni + 1);
-            k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(a, b, ni, nc, ncs, len);
-            npos = excl_scan(len, rk, ni, scan_tmp, st);
-            if (npos < (u64)SLOT_CHUNK_LONG << 18) chl = SLOT_CHUNK_SHORT;
-            nch = excl_scan(chl == SLOT_CHUNK_LONG ? nc : ncs, choff, ni, scan_tmp, st);
-        }
-        ichunk* ch = (ichunk*)dch.get(std::max<u64>(1, nch) * sizeof(ichunk));
-        if (nch) k_iv_chunks<<<cdiv(nch, 256), 256, 0, st>>>(a, b, ni, choff, nch, chl, rk, ch);
-        return ch;
-    };
-    // base sets this large get their predecessors in sorted order and moved back to
-    // entry order in buckets (random 4-byte scatters over the whole array are slower)
     const char* psm = std::getenv("LZ77SSS_PRED_SORTED_MIN");
     const u64 pred_sorted_min = psm ? std::strtoull(psm, nullptr, 10) : (1ull << 27);
-    auto build_base = [&](const u32* bm) {
-        if (bm != bmIb) LZ_HIP(hipMemcpyAsync(bmIb, bm, nw * 4, hipMemcpyDeviceToDevice, st));
-        u32 ni, nch;
-        ichunk* ch = runs_to_chunks(bmIb, ist, iend, irank, chunk_buf, ni, nb, nch);
-        if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy base: intervals=%u positions=%llu chunks=%u slots=2^%u\n", ni,
-                              (unsigned long long)nb, nch, gp.log2_size_h);
-        lap("base intervals");
-        if (5 * nb >= (1ull << 32)) throw error(-1, "gap region too large for 32-bit entry ids");
-        const u64 ne5 = 5 * nb;
-        u32* keys = ekeys.get(ne5 + 1);
-        u32* vals = evals.get(ne5 + 1);
-        u32* skeys = ekeys2.get(ne5 + 1);
-        u32* svals = evals2.get(ne5 + 1);
-        pos_t* ipos = ipos_buf.get(nb + 1);
-        u32* pred5 = occ_buf.get(ne5 + 1);
-        u8* rem = rem_buf.get(nb + 1);
-        LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
-        bool dense = false;
-        u32 D = 0, dense_bits = 0;
-        const u64 npw = ((u64)nslots + 31) / 32;
-        u32* pbm = g_pbm.get(npw + 1);
-        u32* pwp = g_pwp.get(npw + 1);
-        if (nch) {
-            k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos);
-            lap("base slots");
-            // distinct slots -> dense ids when that saves radix passes
-            // (tried below 2^28 entries: a base set that large comes from a non-repetitive
-            // text, whose slots are all in use)
-            if (ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE")) {
-                u32* pcnt = g_pcnt.get(npw + 1);
-                u8* pf = (u8*)g_pflag.get(npw * 8);
-                LZ_HIP(hipMemsetAsync(pf, 0, npw * 32, st));
-                k_slot_presence<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pf);
-                k_presence_pack<<<cdiv(npw, 256), 256, 0, st>>>(pf, npw, pbm, pcnt);
-                D = excl_scan(pcnt, pwp, npw, scan_tmp, st);
-                u32 dbits = 1;
-                while (dbits < 32 && (1ull << dbits) < D) dbits++;
-                dense = (dbits + 7) / 8 < (gp.log2_size_h + 7) / 8;
-                dense_bits = dbits;
+
+    // ---- windows: the chain is walked window by window; a window gets the
+    // exact chain state at its start and the table of the last insert per slot before it
+    // (pos + 1, 0 = none), and hands both on.  Windows bound the gap-index entry ids
+    // (32-bit) and every position-indexed structure to the window's span.  One window
+    // covers the text unless its base set would not fit (or LZ77SSS_GREEDY_WINDOW asks).
+    const u64 est_base = (u64)(N - len_lpf_phr) + 49ull * (m + 1);  // gap positions + queries + short phrases
+    u64 WS = N;
+    if (const char* we = std::getenv("LZ77SSS_GREEDY_WINDOW")) {
+        WS = std::max<u64>(4096, std::strtoull(we, nullptr, 10));
+    } else if (est_base * 5 >= (1ull << 31)) {
+        // windows of ~2^31 / 10 base positions (uniform gap density assumed; a window whose base
+        // set still overflows the ids fails loudly below)
+        WS = std::max<u64>(1ull << 20, (u64)((double)N * ((double)(1ull << 31) / 10.0) / (double)est_base));
+    }
+    // a block of a sharded factorization: [blk->start, blk->end) from the given chain state
+    const pos_t target_end = blk ? blk->end : N;
+    if (blk && (blk->end > N || blk->start >= blk->end || (blk->end < N && (u64)blk->end + 4096 > (u64)G.nt)))
+        throw error(LZ77SSS_EINVAL, "greedy block: need start < end and end == n or end <= n - 4160");
+    const bool multi = WS < (u64)N;
+    const bool carry = multi || blk;
+    pos_t* Hs = nullptr;
+    if (carry) {
+        if (blk && blk->carried && g_Hs.cap < nslots_all)
+            throw error(LZ77SSS_EINVAL, "greedy block: carried table not loaded (size it with carried_entries)");
+        Hs = g_Hs.get(nslots_all);
+        if (!(blk && blk->carried)) LZ_HIP(hipMemsetAsync(Hs, 0, nslots_all * sizeof(pos_t), st));
+    }
+    seg_in entry{0, 0, 0, zmask0, N};
+    if (blk) {
+        entry.start = blk->start;
+        entry.idxpos = blk->idxpos;
+        entry.zmask = blk->zmask;
+    }
+    u64 total_fact = 0, walked_all = 0;
+    int outer_all = 0, rounds_all = 0, nwin = 0;
+    u32 nseg_last = 0, nseg0_all = 0;
+    lce_view Lv = view(T);
+
+    for (;;) {
+        const pos_t a = entry.start;
+        // the window [a, bw): non-last windows end below the tail region (nt) and leave >= 4096 positions
+        pos_t bw = target_end;
+        if (WS < (u64)(target_end - a) && (u64)a + WS + 4096 <= (u64)G.nt) bw = (pos_t)(a + WS);
+        const bool last = bw == N;
+        const pos_t off = a & ~(pos_t)31;  // bitmap origin (word aligned)
+        const u64 nw = (u64)(bw - off) / 32 + 2;  // bitmap words (a zero word past the end)
+        const unsigned gw = cdiv(nw, 256);
+        const unsigned bmb_blocks = (unsigned)std::max<u64>(1, (nw + BMB - 1) / BMB);
+        const pos_t hi_ins = std::min<pos_t>(bw, G.nt);  // inserts recorded in the window bitmaps: [a, hi_ins)
+
+        // ---- default segments: gaps (clipped to the window) + chunk boundaries of long gaps
+        u32* cnt_seg = g_tmp1.get(m + 2);
+        u32* cnt_cb = g_tmp2.get(m + 2);
+        u32* off_seg = g_tmp3.get(m + 2);
+        u32* off_cb = g_tmp4.get(m + 2);
+        k_gap_counts<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, a, bw, cnt_seg, cnt_cb);
+        const u32 nseg0 = excl_scan(cnt_seg, off_seg, m + 1, scan_tmp, st);
+        const u32 ncb = excl_scan(cnt_cb, off_cb, m + 1, scan_tmp, st);
+        pos_t* cbv = g_cbv.get(ncb + 1);
+        k_gap_cbv<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, a, bw, off_cb, cbv);
+        u32 cap = nseg0 + nseg0 / 2 + (1u << 16);
+        seg_tab S{};
+        auto bind_tab = [&]() {
+            S.sin = g_sin.p; S.sout = g_sout.p; S.valid = g_valid.p; S.succ = g_succ.p; S.cap = cap;
+        };
+        g_sin.get(cap); g_sout.get(cap); g_valid.get(cap); g_succ.get(cap);
+        bind_tab();
+        {
+            // the position -> segment map is cleared sparsely after each window (k_seg_at_clear);
+            // a fresh or reallocated map, or one left dirty by a failed call, is cleared densely
+            const u64 span = (u64)(bw - a) + 1;
+            u32* prev = g_seg_at.p;
+            S.seg_at = g_seg_at.get(span);
+            if (S.seg_at != prev || !seg_at_clean || seg_at_n < span) {
+                LZ_HIP(hipMemsetAsync(S.seg_at, 0xFF, g_seg_at.cap * 4, st));
+                seg_at_n = g_seg_at.cap;
             }
-            u32* sk_in = keys;
-            u32 sbits = gp.log2_size_h;
-            if (dense) {
-                k_dense_keys<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pbm, pwp, skeys);
-                sk_in = skeys;
-                skeys = g_sdk.get(ne5 + 1);
-                sbits = dense_bits;
+            seg_at_clean = false;
+        }
+        S.segoff = a;
+        S.nseg = (u32*)counters64.get(4);
+        S.err = S.nseg + 1;
+        LZ_HIP(hipMemsetAsync(S.nseg, 0, 8, st));
+        LZ_HIP(hipMemcpyAsync(S.nseg, &nseg0, 4, hipMemcpyHostToDevice, st));
+        S.cbv = cbv; S.ncb = ncb; S.P = P; S.m = m; S.N = bw; S.zmask0 = zmask0;
+        k_gap_segs<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(S, CH, off_seg);
+        u32* d_c0 = (u32*)(counters64.p + 1);
+        k_entry_seg<<<1, 1, 0, st>>>(S, a, entry.idxpos, entry.zmask, d_c0);
+        u32 hn[2];
+        LZ_HIP(hipMemcpyAsync(hn, S.nseg, 8, hipMemcpyDeviceToHost, st));
+        u32 c0 = 0;
+        LZ_HIP(hipMemcpyAsync(&c0, d_c0, 4, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        const u32 nseg_init = hn[0];
+        // the exact entry of the window as the completion path sees it
+        seg_in entry_in;
+        LZ_HIP(hipMemcpy(&entry_in, g_sin.p + c0, sizeof(seg_in), hipMemcpyDeviceToHost));
+        // bitmaps: I (current speculation), I' (what the chain inserted), Ib (base set), scratch
+        u32* bmI = g_bmI.get(nw);
+        u32* bmI2 = g_bmI2.get(nw);
+        u32* bmIb = g_bmIb.get(nw);
+        u32* bmT = g_bmT.get(nw);
+        LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
+        LZ_HIP(hipMemsetAsync(bmT, 0, nw * 4, st));
+        k_gap_bitmaps<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmT);
+        LZ_HIP(hipStreamSynchronize(st));
+        lap("greedy setup");
+
+        walk_ctx W{};
+        W.T = T;
+        W.G = G;
+        W.P = P;
+        W.L = Lv;
+        W.bmoff = off;
+        W.Hs = Hs;
+
+        // window exit (the chain state at the first handover point >= bw) and the carried table
+        seg_in exit_in{};
+        // ---- bounded completion (k_seq_walk): the chain prefix [0, k*) is written by the
+        // segment walks, the rest of the window by the exact sequential walk from chain node k*
+        u64* d_sq = (u64*)g_cut.get(sizeof(chain_cut) + 256);
+        chain_cut* d_cutp = (chain_cut*)(d_sq + 8);
+        u64* d_y0 = d_sq + 6;
+        auto seq_complete = [&](const u32* chain, u32 nall, const u64* offs, const u32* ins_bm, bool from_entry) -> u64 {
+            if (from_entry) LZ_HIP(hipMemsetAsync(d_y0, 0, 8, st));
+            k_chain_cut<<<1, 1, 0, st>>>(S, chain, from_entry ? 0u : nall, d_y0, entry_in, d_cutp);
+            chain_cut cut;
+            LZ_HIP(hipMemcpyAsync(&cut, d_cutp, sizeof(cut), hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));
+            const u64 offk = cut.k ? rd1(offs + cut.k, st) : 0;
+            pos_t* fo = fact.get(2 * (offk + (u64)(N - cut.in.start) + 2) + 2);
+            if (cut.k) {
+                k_walk<true><<<cdiv(cut.k, 64), 64, 0, st>>>(W, S, chain, cut.k, offs, fo);
+                LZ_HIP(hipGetLastError());
             }
-            if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy base: %u distinct slots, %s sort on %u bits\n", D,
-                                  dense ? "dense-id" : "slot", sbits);
-            size_t tb = 0;
-            // values = entry ids: a counting iterator, so the ids are never written or read
-            const rocprim::counting_iterator<u32> ids(0);
-            LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
-            u8* t = scan_tmp.get(tb);
-            LZ_HIP(rocprim::radix_sort_pairs(t, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
-            if (dense && ne5 < pred_sorted_min) {
-                // predecessors and dense-id starts in one pass (buckets below reuse dstart)
-                k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, svals, ne5, D, W.use_pred ? pred5 : nullptr,
-                                                                  g_dstart.get((u64)D + 1));
-            } else if (W.use_pred && ne5 < pred_sorted_min) {
-                k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
-            } else if (W.use_pred) {
-                // pred5[e] = predecessor of entry e in its slot: a radix sort by entry id of the
-                // sorted-order predecessors (a random scatter of 4-byte writes is ~3x slower)
-                u32* pv = vals;  // the unsorted values are no longer needed
-                k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
-                if (std::getenv("LZ77SSS_PRED_RADIX")) {  // reference path: radix sort by entry id
-                    u32* kdump = g_predk.get(ne5 + 1);
-                    int eb = 1;
-                    while (eb < 32 && (1ull << eb) < ne5) eb++;
-                    size_t tb2 = 0;
-                    LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u, (unsigned)eb, st));
-                    u8* t2 = scan_tmp.get(tb2);
-                    LZ_HIP(rocprim::radix_sort_pairs(t2, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u, (unsigned)eb, st));
-                } else {
-                    const u32 nbk = (u32)((ne5 + (1ull << PB_SH) - 1) >> PB_SH);
-                    u32* cursor = g_pbcur.get(nbk + 1);
-                    u64* tmp = g_pbtmp.get(ne5);
-                    const u32 ntile = (u32)std::min<u64>(1024, cdiv(ne5, PB_T));
-                    const u64 tile = (ne5 + ntile - 1) / ntile;
-                    k_pb_init<<<cdiv(nbk, 256), 256, 0, st>>>(cursor, nbk);
-                    k_pb_move<<<ntile, PB_T, 0, st>>>(svals, pv, ne5, tile, nbk, cursor, tmp);
-                    k_pb_apply<<<cdiv(ne5, 256), 256, 0, st>>>(tmp, ne5, pred5);
+            pos_t* H = g_H.get((u64)nslots_all);
+            if (Hs) LZ_HIP(hipMemcpyAsync(H, Hs, nslots_all * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+            else LZ_HIP(hipMemsetAsync(H, 0, nslots_all * sizeof(pos_t), st));
+            if (cut.in.start > off && ins_bm)
+                k_h_fill<<<cdiv(((u64)(cut.in.start - off) + 31) / 32, 256), 256, 0, st>>>(T, G, ins_bm, off, cut.in.start,
+                                                                                         H);
+            k_h_fix<<<cdiv(nslots_all, 256), 256, 0, st>>>(H, nslots_all);
+            k_seq_walk<<<1, 64, 0, st>>>(T, G, P, Lv, H, cut.in, last ? N + 1 : bw, fo, offk, d_sq);
+            LZ_HIP(hipGetLastError());
+            u64 hc[4];
+            LZ_HIP(hipMemcpyAsync(hc, d_sq, 32, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));
+            if (hc[1]) throw error(-6, "greedy: sequential completion guard tripped (internal error)");
+            if (!last) {
+                exit_in.start = (pos_t)hc[2];
+                exit_in.idxpos = (pos_t)hc[3];
+                exit_in.zmask = 0;  // below the tail region no fingerprint is zeroed
+                k_h_unfix<<<cdiv(nslots_all, 256), 256, 0, st>>>(H, nslots_all, Hs);
+            }
+            stats[19] = 1;
+            stats[20] = cut.in.start;
+            lap("sequential completion");
+            return offk + hc[0];
+        };
+
+        // ---- base set (entries sorted by slot) and delta
+        u64 nb = 0;
+        const u32 nslots = G.mask + 1;
+        auto build_buckets = [&](auto key, u64 mk, dbuf<u32>& bk) {
+            u32* b = bk.get((u64)nslots + 1);
+            if (mk * 16 >= nslots) {
+                u32* rev = g_brev.get(2 * ((u64)nslots + 1));
+                u32* scn = rev + nslots + 1;
+                LZ_HIP(hipMemsetAsync(rev, 0xFF, ((u64)nslots + 1) * 4, st));
+                k_bucket_heads<<<cdiv(mk + 1, 256), 256, 0, st>>>(key, mk, nslots, rev);
+                size_t tb = 0;
+                LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, rev, scn, min_u32_op{}, (int)(nslots + 1), st));
+                u8* t = scan_tmp.get(tb);
+                LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, rev, scn, min_u32_op{}, (int)(nslots + 1), st));
+                k_unreverse<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(scn, nslots, b);
+            } else {
+                k_bucket_search<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(key, mk, nslots, b);
+            }
+        };
+        // runs of a bitmap -> intervals (st, en), ranks, chunks for k_slots
+        auto runs_to_chunks = [&](const u32* bm, dbuf<pos_t>& dst, dbuf<pos_t>& den, dbuf<u32>& drk, dbuf<u8>& dch,
+                                  u32& ni, u64& npos, u32& nch) -> ichunk* {
+            const u64 tot = bmb_scan(bm_runs{bm}, nw, g_bsum, g_bincl, scan_tmp, st);
+            ni = (u32)(tot >> 32);  // run starts (= run ends)
+            pos_t* ra = dst.get(ni + 1);
+            pos_t* rb = den.get(ni + 1);
+            k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_runs{bm}, nw, g_bincl.p, out_runs{ra, rb}, off);
+            u32* len = g_tmp5.get(ni + 1);
+            u32* nc = g_tmp6.get(ni + 1);
+            u32* rk = drk.get(ni + 1);
+            u32* choff = g_tmp7.get(ni + 1);
+            npos = 0;
+            nch = 0;
+            u32 chl = SLOT_CHUNK_LONG;
+            if (ni) {
+                u32* ncs = g_tmp8.get(ni + 1);
+                k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(ra, rb, ni, nc, ncs, len);
+                npos = excl_scan(len, rk, ni, scan_tmp, st);
+                if (npos < (u64)SLOT_CHUNK_LONG << 18) chl = SLOT_CHUNK_SHORT;
+                nch = excl_scan(chl == SLOT_CHUNK_LONG ? nc : ncs, choff, ni, scan_tmp, st);
+            }
+            ichunk* ch = (ichunk*)dch.get(std::max<u64>(1, nch) * sizeof(ichunk));
+            if (nch) k_iv_chunks<<<cdiv(nch, 256), 256, 0, st>>>(ra, rb, ni, choff, nch, chl, rk, ch);
+            return ch;
+        };
+        // base sets this large get their predecessors in sorted order and moved back to
+        // entry order in buckets (random 4-byte scatters over the whole array are slower)
+        auto build_base = [&](const u32* bm) {
+            if (bm != bmIb) LZ_HIP(hipMemcpyAsync(bmIb, bm, nw * 4, hipMemcpyDeviceToDevice, st));
+            u32 ni, nch;
+            ichunk* ch = runs_to_chunks(bmIb, ist, iend, irank, chunk_buf, ni, nb, nch);
+            if (dbg) {
+                std::fprintf(stderr, "[lz77sss-debug] greedy base: intervals=%u positions=%llu chunks=%u slots=2^%u\n", ni,
+                             (unsigned long long)nb, nch, gp.log2_size_h);
+                pos_t r[4] = {0, 0, 0, 0};
+                if (ni) {
+                    LZ_HIP(hipMemcpy(r, ist.p, sizeof(pos_t) * std::min<u32>(ni, 2), hipMemcpyDeviceToHost));
+                    LZ_HIP(hipMemcpy(r + 2, iend.p, sizeof(pos_t) * std::min<u32>(ni, 2), hipMemcpyDeviceToHost));
+                }
+                std::fprintf(stderr, "[lz77sss-debug] greedy base: window [%llu, %llu) off=%llu nw=%llu runs %llu-%llu %llu-%llu\n",
+                             (unsigned long long)a, (unsigned long long)bw, (unsigned long long)off,
+                             (unsigned long long)nw, (unsigned long long)r[0], (unsigned long long)r[2],
+                             (unsigned long long)r[1], (unsigned long long)r[3]);
+            }
+            lap("base intervals");
+            if (5 * nb >= (1ull << 32))
+                throw error(-1, "gap region of a greedy window too large for 32-bit entry ids (set LZ77SSS_GREEDY_WINDOW)");
+            const u64 ne5 = 5 * nb;
+            u32* keys = ekeys.get(ne5 + 1);
+            u32* vals = evals.get(ne5 + 1);
+            u32* skeys = ekeys2.get(ne5 + 1);
+            u32* svals = evals2.get(ne5 + 1);
+            pos_t* ipos = ipos_buf.get(nb + 1);
+            u32* pred5 = occ_buf.get(ne5 + 1);
+            u8* rem = rem_buf.get(nb + 1);
+            LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
+            bool dense = false;
+            u32 D = 0, dense_bits = 0;
+            const u64 npw = ((u64)nslots + 31) / 32;
+            u32* pbm = g_pbm.get(npw + 1);
+            u32* pwp = g_pwp.get(npw + 1);
+            if (nch) {
+                k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos);
+                lap("base slots");
+                // distinct slots -> dense ids when that saves radix passes
+                // (tried below 2^28 entries: a base set that large comes from a non-repetitive
+                // text, whose slots are all in use)
+                if (ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE")) {
+                    u32* pcnt = g_pcnt.get(npw + 1);
+                    u8* pf = (u8*)g_pflag.get(npw * 8);
+                    LZ_HIP(hipMemsetAsync(pf, 0, npw * 32, st));
+                    k_slot_presence<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pf);
+                    k_presence_pack<<<cdiv(npw, 256), 256, 0, st>>>(pf, npw, pbm, pcnt);
+                    D = excl_scan(pcnt, pwp, npw, scan_tmp, st);
+                    u32 dbits = 1;
+                    while (dbits < 32 && (1ull << dbits) < D) dbits++;
+                    dense = (dbits + 7) / 8 < (gp.log2_size_h + 7) / 8;
+                    dense_bits = dbits;
+                }
+                u32* sk_in = keys;
+                u32 sbits = gp.log2_size_h;
+                if (dense) {
+                    k_dense_keys<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pbm, pwp, skeys);
+                    sk_in = skeys;
+                    skeys = g_sdk.get(ne5 + 1);
+                    sbits = dense_bits;
+                }
+                if (dbg)
+                    std::fprintf(stderr, "[lz77sss-debug] greedy base: %u distinct slots, %s sort on %u bits\n", D,
+                                 dense ? "dense-id" : "slot", sbits);
+                size_t tb = 0;
+                // values = entry ids: a counting iterator, so the ids are never written or read
+                const rocprim::counting_iterator<u32> ids(0);
+                LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
+                u8* t = scan_tmp.get(tb);
+                LZ_HIP(rocprim::radix_sort_pairs(t, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
+                if (dense && ne5 < pred_sorted_min) {
+                    // predecessors and dense-id starts in one pass (buckets below reuse dstart)
+                    k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, svals, ne5, D, W.use_pred ? pred5 : nullptr,
+                                                                      g_dstart.get((u64)D + 1));
+                } else if (W.use_pred && ne5 < pred_sorted_min) {
+                    k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
+                } else if (W.use_pred) {
+                    // pred5[e] = predecessor of entry e in its slot: the sorted-order predecessors
+                    // moved back to entry order (a random scatter of 4-byte writes is ~3x slower)
+                    u32* pv = vals;  // the unsorted values are no longer needed
+                    k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
+                    if (std::getenv("LZ77SSS_PRED_RADIX")) {  // reference path: radix sort by entry id
+                        u32* kdump = g_predk.get(ne5 + 1);
+                        int eb = 1;
+                        while (eb < 32 && (1ull << eb) < ne5) eb++;
+                        size_t tb2 = 0;
+                        LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u,
+                                                         (unsigned)eb, st));
+                        u8* t2 = scan_tmp.get(tb2);
+                        LZ_HIP(rocprim::radix_sort_pairs(t2, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u, (unsigned)eb,
+                                                         st));
+                    } else {
+                        const u32 nbk = (u32)((ne5 + (1ull << PB_SH) - 1) >> PB_SH);
+                        u32* cursor = g_pbcur.get(nbk + 1);
+                        u64* tmp = g_pbtmp.get(ne5);
+                        const u32 ntile = (u32)std::min<u64>(1024, cdiv(ne5, PB_T));
+                        const u64 tile = (ne5 + ntile - 1) / ntile;
+                        k_pb_init<<<cdiv(nbk, 256), 256, 0, st>>>(cursor, nbk);
+                        k_pb_move<<<ntile, PB_T, 0, st>>>(svals, pv, ne5, tile, nbk, cursor, tmp);
+                        k_pb_apply<<<cdiv(ne5, 256), 256, 0, st>>>(tmp, ne5, pred5);
+                    }
                 }
             }
-        }
-        lap("base sort + pred");
-        if (dense) {
-            u32* dstart = g_dstart.get((u64)D + 1);
-            if (ne5 >= pred_sorted_min) k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
-            k_bstart_rank<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
-                                                                      g_bstart.get((u64)nslots + 1));
-        } else {
-            build_buckets(key_u32{skeys}, ne5, g_bstart);
-        }
-        W.istart = ist.p; W.iend = iend.p; W.irank = irank.p; W.nint = ni;
-        W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne5;
-        W.bstart = g_bstart.p;
-        W.rem = rem; W.akeys = nullptr; W.nadd = 0; W.akeys2 = nullptr; W.nadd2 = 0;
-        lap("base buckets");
-    };
-    // added entries: positions of I outside the base set.  The main list is
-    // rebuilt rarely (membership of its positions is read from the I bitmap);
-    // positions that join later and are missing from it go to the small extra list.
-    u32* bmA = g_bmA.get(nw);
-    u64 na_main = 0;
-    auto build_list = [&](const u32* bm, dbuf<u32>& k32, dbuf<pos_t>& kpos, dbuf<u64>& ka, dbuf<u64>& kb,
-                          dbuf<u32>& bucket, const u64*& keys_out, u64& nkeys, const u32*& bk_out,
-                          const pos_t*& apos_out, u64& napos_out) -> u64 {
-        u32 ni, nch;
-        u64 na;
-        ichunk* ch = runs_to_chunks(bm, g_ast, g_aen, g_ark, chunk_buf2, ni, na, nch);
-        nkeys = 0;
-        keys_out = nullptr;
-        apos_out = nullptr;
-        napos_out = 0;
-        if (!na) return 0;
-        u32* akey32 = k32.get(5 * na);
-        pos_t* apos = kpos.get(na);
-        apos_out = apos;
-        napos_out = na;
-        k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
-        u64* ak = ka.get(5 * na);
-        u64* ak2 = kb.get(5 * na);
-        k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
-        size_t tb = 0;
-        LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, ak, ak2, (size_t)(5 * na), 0u, 63u, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(rocprim::radix_sort_keys(t, tb, ak, ak2, (size_t)(5 * na), 0u, 63u, st));
-        keys_out = ak2;
-        nkeys = 5 * na;
-        build_buckets(key_u64{ak2}, 5 * na, bucket);
-        bk_out = bucket.p;
-        return na;
-    };
-    auto rebuild_main = [&]() {
-        k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmA);
-        na_main = build_list(bmA, add_keys32, add_pos, add_keys, add_keys2, g_abeg, W.akeys, W.nadd, W.abeg, W.apos,
-                             W.napos);
-        W.nadd2 = 0;
-        W.akeys2 = nullptr;
-    };
-    auto rebuild_added = [&](bool main_list) {
-        if (main_list) return rebuild_main();
-        k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmT);
-        k_bm_andnot<<<gw, 256, 0, st>>>(bmT, bmA, nw, bmT);
-        const u64 nx = build_list(bmT, g_x32, g_xpos, g_xk, g_xk2, g_abeg2, W.akeys2, W.nadd2, W.abeg2, W.apos2,
-                                  W.napos2);
-        if (nx * 4 > na_main + (1u << 16)) rebuild_main();
-    };
-    auto set_state = [&]() {  // rem + added for the current I
-        W.bmI = bmI;
-        if (nb) k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, (u8*)W.rem);
-        rebuild_added(true);
-    };
-    W.use_pred = std::getenv("LZ77SSS_NO_PRED") ? 0 : 1;
-    auto finish_call = [&](u64 z, int outer_rounds, int link_rounds, u64 walked, u32 nseg_end) {
-        k_seg_at_clear<<<cdiv(nseg_end, 256), 256, 0, st>>>(S, nseg_end);
-        seg_at_clean = true;
-        stats[12] = outer_rounds;
-        stats[13] = link_rounds;
-        stats[14] = stats_fallback_lanes;
-        stats[15] = walked;
-        stats[16] = nseg_end;
-        stats[17] = nseg0;
-        return z;
-    };
-    if (max_outer == 0) return finish_call(seq_complete(nullptr, 0, nullptr, nullptr, true), 0, 0, 0, nseg0);
-    build_base(bmT);  // superset: gaps + short phrase interiors
-    set_state();
-
-    // ---- walk + link until the chain from position 0 is complete, then check I
-    u32 nseg = nseg0;
-    u32* ids = g_ids.get(cap);
-    u32* d_cnt = counters.get(16);
-    chain_status cs{};
-    chain_status* d_cs = (chain_status*)g_cs.get(sizeof(chain_status));
-    jump_levels JL{};
-    u64 total_fact = 0, walked_total = 0;
-    int outer = 0, rounds_total = 0;
-    bool restart_seq = false;  // a walk overflowed or linking ran away: complete from position 0
-    for (;; outer++) {
-        for (int round = 0;; round++) {
-            rounds_total++;
-            if (round > 100000) { restart_seq = true; break; }
-            LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
-            k_todo<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, ids, d_cnt);
-            const u32 ntodo = rd1(d_cnt, st);
-            const u32* wids = ids;
-            if (ntodo >= (1u << 16)) {  // sort the walks by expected length: less divergence per wave
-                u32* wk = g_wk.get(2ull * ntodo);
-                u32* ids2 = g_ids2.get(ntodo);
-                k_walk_keys<<<cdiv(ntodo, 256), 256, 0, st>>>(S, ids, ntodo, wk);
-                size_t tb = 0;
-                LZ_HIP(rocprim::radix_sort_pairs_desc(nullptr, tb, wk, wk + ntodo, ids, ids2, (size_t)ntodo, 0u, 32u, st));
-                u8* t = scan_tmp.get(tb);
-                LZ_HIP(rocprim::radix_sort_pairs_desc(t, tb, wk, wk + ntodo, ids, ids2, (size_t)ntodo, 0u, 32u, st));
-                wids = ids2;
+            lap("base sort + pred");
+            if (dense) {
+                u32* dstart = g_dstart.get((u64)D + 1);
+                if (ne5 >= pred_sorted_min) k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
+                k_bstart_rank<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
+                                                                          g_bstart.get((u64)nslots + 1));
+            } else {
+                build_buckets(key_u32{skeys}, ne5, g_bstart);
             }
-            if (ntodo) {
-                k_walk<false><<<cdiv(ntodo, 64), 64, 0, st>>>(W, S, wids, ntodo, nullptr, nullptr);
-                LZ_HIP(hipGetLastError());
-                walked_total += ntodo;
-            }
-            lap("walk");
-            for (;;) {  // link; grow the table when full
-                k_link<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
-                u32 h2[2];
-                LZ_HIP(hipMemcpyAsync(h2, S.nseg, 8, hipMemcpyDeviceToHost, st));
-                LZ_HIP(hipStreamSynchronize(st));
-                if (!(h2[1] & 1)) { nseg = h2[0]; break; }
-                const u32 ncap = cap * 2;
-                g_sin.grow_keep(ncap, cap, st); g_sout.grow_keep(ncap, cap, st);
-                g_valid.grow_keep(ncap, cap, st); g_succ.grow_keep(ncap, cap, st);
-                g_ids.get(ncap);
-                ids = g_ids.p;
-                cap = ncap;
-                bind_tab();
-                const u32 fix[2] = {cap < h2[0] ? cap : h2[0], h2[1] & ~1u};
-                LZ_HIP(hipMemcpyAsync(S.nseg, fix, 8, hipMemcpyHostToDevice, st));
-                LZ_HIP(hipStreamSynchronize(st));
-            }
-            // pointer doubling along succ from every segment
-            u32* D0 = g_dist[0].get(nseg);
-            u32* D1 = g_dist[1].get(nseg);
-            k_jump0<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, jump[0].get(nseg), D0);
-            u32 nlv = 1;
-            while ((1ull << (nlv - 1)) < nseg) {
-                if (nlv >= (u32)MAX_LV) throw error(-6, "greedy: too many jump levels");
-                k_jumpk<<<cdiv(nseg, 256), 256, 0, st>>>(jump[nlv - 1].p, D0, nseg, jump[nlv].get(nseg), D1);
-                std::swap(D0, D1);
-                nlv++;
-            }
-            JL.nlv = nlv;
-            for (u32 l = 0; l < nlv; l++) JL.J[l] = jump[l].p;
-            k_chain_status<<<1, 1, 0, st>>>(S, jump[nlv - 1].p, D0, d_cs);
-            LZ_HIP(hipMemcpyAsync(&cs, d_cs, sizeof(cs), hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipStreamSynchronize(st));
-            lap("link");
-            if (cs.err & 6) { restart_seq = true; break; }  // 2: LPF-start query overflow, 4: walk guard
-            if (dbg)
-                std::fprintf(stderr, "[lz77sss-debug] greedy outer=%d round=%d segs=%u walked=%u chain=%u valid=%u flags=%u\n",
-                             outer, round, nseg, ntodo, cs.hops + 1, cs.valid, cs.flags);
-            if (cs.valid && ((cs.flags & 1) || cs.next >= N)) break;
-        }
-        if (restart_seq) {
-            total_fact = seq_complete(nullptr, 0, nullptr, nullptr, true);
-            break;
-        }
-        // ---- the chain, its factor offsets, the tail
-        const bool tail = cs.flags & 1;
-        const u32 nall = cs.hops + 1, nchain = nall - (tail ? 1u : 0u);
-        u32* chain = g_chain.get(nall + 1);
-        k_chain_expand<<<cdiv(nall, 256), 256, 0, st>>>(JL, nall, chain);
-        u64* nf = seg_offs.get(nall + 2);
-        u64* offs = g_offs.get(nall + 2);
-        u64 chain_fact = 0;
-        if (nchain) {
-            k_chain_nfact<<<cdiv(nchain, 256), 256, 0, st>>>(S, chain, nchain, nf);
-            chain_fact = excl_scan(nf, offs, nchain, scan_tmp, st);
-        }
-        u64 tail_count = 0, tail_bound = 0;
-        pos_t tail_pairs[16];
-        u64 hc[3] = {0, 0, 0};
-        if (tail) {
-            seg_in tin;
-            LZ_HIP(hipMemcpyAsync(&tin, g_sin.p + cs.term, sizeof(seg_in), hipMemcpyDeviceToHost, st));
-            seg_out prev{};
-            if (nall >= 2) {
-                u32 pg;
-                LZ_HIP(hipMemcpyAsync(&pg, chain + nall - 2, 4, hipMemcpyDeviceToHost, st));
-                LZ_HIP(hipStreamSynchronize(st));
-                LZ_HIP(hipMemcpyAsync(&prev, g_sout.p + pg, sizeof(seg_out), hipMemcpyDeviceToHost, st));
-            }
-            LZ_HIP(hipStreamSynchronize(st));
-            tin.idxpos = nall >= 2 ? prev.idxpos : 0;  // exact chain state entering the tail walk
-            tin.zmask = nall >= 2 ? prev.zmask : zmask0;
-            tail_bound = (u64)N - tin.start + 1;
-            pos_t* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
-            u64* d_tc = (u64*)g_tailc.get(4 * sizeof(u64));
-            pos_t* d_tins = tail_ins_buf.get(16);
-            k_tail<<<1, 64, 0, st>>>(W, tin, fo, chain_fact, d_tc, d_tins);
-            LZ_HIP(hipGetLastError());
-            LZ_HIP(hipMemcpyAsync(hc, d_tc, 24, hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipMemcpyAsync(tail_pairs, d_tins, sizeof(tail_pairs), hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipStreamSynchronize(st));
-            if (hc[2]) throw error(-6, "greedy tail: insert overflow or guard tripped");
-            tail_count = hc[0];
-            lap("tail");
-        } else {
-            fact.get(2 * chain_fact + 2);
-        }
-        // ---- the insert set the chain actually produced vs the speculation
-        LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
-        if (nchain) k_chain_inserts<<<cdiv((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, G.nt, bmI2);
-        if (tail && hc[1]) {
-            pos_t* d_tins = tail_ins_buf.p;
-            k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], bmI2);
-        }
-        k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
-        const u64 ny = bmb_scan(bm_bits{bmT, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
-        lap("insert set");
-        if (ny == 0) {
-            // every lookup of the chain was exact: emit the factors
-            if (nchain) {
-                k_walk<true><<<cdiv(nchain, 64), 64, 0, st>>>(W, S, chain, nchain, offs, fact.p);
-                LZ_HIP(hipGetLastError());
-                lap("write");
-            }
-            total_fact = chain_fact + tail_count;
-            break;
-        }
-        if (outer + 1 >= max_outer) {
-            // round budget spent: the chain is exact up to the first changed position
-            LZ_HIP(hipMemsetAsync(d_y0, 0xFF, 8, st));
-            k_first_bit<<<gw, 256, 0, st>>>(bmT, nw, d_y0);
-            total_fact = seq_complete(chain, nall, offs, bmI2, false);
-            break;
-        }
-        // positions that joined (flag 1) or left (0) I
-        pos_t* d_y = dirty_in.get(ny + 1);
-        u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
-        k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_bits{bmT, nullptr}, nw, g_bincl.p, out_list{d_y, d_j, bmI2});
-        // many positions outside the base set: rebuild it as I' u I_b, re-walk everything
-        const u64 outside = bmb_scan(bm_bits{bmI2, bmIb}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
-        if (outside * 8 > nb) {
-            k_bm_or<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
-            std::swap(g_bmI.p, g_bmI2.p);
-            bmI = g_bmI.p;
-            bmI2 = g_bmI2.p;
-            build_base(bmT);
-            set_state();
-            k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
-            if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy rebuild: outside=%llu\n", (unsigned long long)outside);
-            continue;
-        }
-        if (ny > nseg) {
-            // too many changes for dirty tracking to pay off: new state, re-walk everything
-            std::swap(g_bmI.p, g_bmI2.p);
-            bmI = g_bmI.p;
-            bmI2 = g_bmI2.p;
-            set_state();
-            k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
-            lap("delta (full)");
-            if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy delta (full): changed=%llu outside=%llu\n",
-                                  (unsigned long long)ny, (unsigned long long)outside);
-            continue;
-        }
-        // dirty = changed positions + their same-slot successors before and after the update
-        pos_t* d_d = dirty_out.get(11 * ny + 1);
-        LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
-        k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + ny);
-        k_flip<<<cdiv(ny, 256), 256, 0, st>>>(W, d_y, d_j, ny, (u8*)W.rem, d_j + ny);
-        std::swap(g_bmI.p, g_bmI2.p);
-        bmI = g_bmI.p;
-        bmI2 = g_bmI2.p;
-        LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
-        k_sum_u8<<<cdiv(ny, 256), 256, 0, st>>>(d_j + ny, ny, d_cnt);
-        W.bmI = bmI;
-        if (rd1(d_cnt, st)) rebuild_added(false);
-        k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + 6 * ny);
-        pos_t* d_ds = dirty_sorted.get(11 * ny + 1);
-        {
-            constexpr unsigned PB = 8 * sizeof(pos_t);
+            W.istart = ist.p; W.iend = iend.p; W.irank = irank.p; W.nint = ni;
+            W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne5;
+            W.bstart = g_bstart.p;
+            W.rem = rem; W.akeys = nullptr; W.nadd = 0; W.akeys2 = nullptr; W.nadd2 = 0;
+            lap("base buckets");
+        };
+        // added entries: positions of I outside the base set.  The main list is
+        // rebuilt rarely (membership of its positions is read from the I bitmap);
+        // positions that join later and are missing from it go to the small extra list.
+        u32* bmA = g_bmA.get(nw);
+        u64 na_main = 0;
+        auto build_list = [&](const u32* bm, dbuf<u32>& k32, dbuf<pos_t>& kpos, dbuf<u64>& ka, dbuf<u64>& kb,
+                              dbuf<u32>& bucket, const u64*& keys_out, u64& nkeys, const u32*& bk_out,
+                              const pos_t*& apos_out, u64& napos_out) -> u64 {
+            u32 ni, nch;
+            u64 na;
+            ichunk* ch = runs_to_chunks(bm, g_ast, g_aen, g_ark, chunk_buf2, ni, na, nch);
+            nkeys = 0;
+            keys_out = nullptr;
+            apos_out = nullptr;
+            napos_out = 0;
+            if (!na) return 0;
+            u32* akey32 = k32.get(5 * na);
+            pos_t* apos = kpos.get(na);
+            apos_out = apos;
+            napos_out = na;
+            k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
+            u64* ak = ka.get(5 * na);
+            u64* ak2 = kb.get(5 * na);
+            k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
             size_t tb = 0;
-            LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, d_d, d_ds, (size_t)(11 * ny), 0u, PB, st));
+            LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, ak, ak2, (size_t)(5 * na), 0u, 63u, st));
             u8* t = scan_tmp.get(tb);
-            LZ_HIP(rocprim::radix_sort_keys(t, tb, d_d, d_ds, (size_t)(11 * ny), 0u, PB, st));
+            LZ_HIP(rocprim::radix_sort_keys(t, tb, ak, ak2, (size_t)(5 * na), 0u, 63u, st));
+            keys_out = ak2;
+            nkeys = 5 * na;
+            build_buckets(key_u64{ak2}, 5 * na, bucket);
+            bk_out = bucket.p;
+            return na;
+        };
+        auto rebuild_main = [&]() {
+            k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmA);
+            na_main = build_list(bmA, add_keys32, add_pos, add_keys, add_keys2, g_abeg, W.akeys, W.nadd, W.abeg, W.apos,
+                                 W.napos);
+            W.nadd2 = 0;
+            W.akeys2 = nullptr;
+        };
+        auto rebuild_added = [&](bool main_list) {
+            if (main_list) return rebuild_main();
+            k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmT);
+            k_bm_andnot<<<gw, 256, 0, st>>>(bmT, bmA, nw, bmT);
+            const u64 nx = build_list(bmT, g_x32, g_xpos, g_xk, g_xk2, g_abeg2, W.akeys2, W.nadd2, W.abeg2, W.apos2,
+                                      W.napos2);
+            if (nx * 4 > na_main + (1u << 16)) rebuild_main();
+        };
+        auto set_state = [&]() {  // rem + added for the current I
+            W.bmI = bmI;
+            if (nb) k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem);
+            rebuild_added(true);
+        };
+        W.use_pred = std::getenv("LZ77SSS_NO_PRED") ? 0 : 1;
+
+        // ---- walk + link until the chain from the window entry is complete, then check I
+        u32 nseg = nseg_init;
+        u32* ids = g_ids.get(cap);
+        u32* d_cnt = counters.get(16);
+        chain_status cs{};
+        chain_status* d_cs = (chain_status*)g_cs.get(sizeof(chain_status));
+        jump_levels JL{};
+        u64 wfact = 0, walked_total = 0;
+        int outer = 0, rounds_total = 0;
+        if (max_outer == 0) {
+            wfact = seq_complete(nullptr, 0, nullptr, nullptr, true);
+        } else {
+            build_base(bmT);  // superset: gaps + short phrase interiors
+            set_state();
+            bool restart_seq = false;  // a walk overflowed or linking ran away: complete from the entry
+            for (;; outer++) {
+                for (int round = 0;; round++) {
+                    rounds_total++;
+                    if (round > 100000) { restart_seq = true; break; }
+                    LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
+                    k_todo<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, ids, d_cnt);
+                    const u32 ntodo = rd1(d_cnt, st);
+                    const u32* wids = ids;
+                    if (ntodo >= (1u << 16)) {  // sort the walks by expected length: less divergence per wave
+                        u32* wk = g_wk.get(2ull * ntodo);
+                        u32* ids2 = g_ids2.get(ntodo);
+                        k_walk_keys<<<cdiv(ntodo, 256), 256, 0, st>>>(S, ids, ntodo, wk);
+                        size_t tb = 0;
+                        LZ_HIP(rocprim::radix_sort_pairs_desc(nullptr, tb, wk, wk + ntodo, ids, ids2, (size_t)ntodo, 0u,
+                                                              32u, st));
+                        u8* t = scan_tmp.get(tb);
+                        LZ_HIP(rocprim::radix_sort_pairs_desc(t, tb, wk, wk + ntodo, ids, ids2, (size_t)ntodo, 0u, 32u,
+                                                              st));
+                        wids = ids2;
+                    }
+                    if (ntodo) {
+                        k_walk<false><<<cdiv(ntodo, 64), 64, 0, st>>>(W, S, wids, ntodo, nullptr, nullptr);
+                        LZ_HIP(hipGetLastError());
+                        walked_total += ntodo;
+                    }
+                    lap("walk");
+                    for (;;) {  // link; grow the table when full
+                        k_link<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
+                        u32 h2[2];
+                        LZ_HIP(hipMemcpyAsync(h2, S.nseg, 8, hipMemcpyDeviceToHost, st));
+                        LZ_HIP(hipStreamSynchronize(st));
+                        if (!(h2[1] & 1)) { nseg = h2[0]; break; }
+                        const u32 ncap = cap * 2;
+                        g_sin.grow_keep(ncap, cap, st); g_sout.grow_keep(ncap, cap, st);
+                        g_valid.grow_keep(ncap, cap, st); g_succ.grow_keep(ncap, cap, st);
+                        g_ids.get(ncap);
+                        ids = g_ids.p;
+                        cap = ncap;
+                        bind_tab();
+                        const u32 fix[2] = {cap < h2[0] ? cap : h2[0], h2[1] & ~1u};
+                        LZ_HIP(hipMemcpyAsync(S.nseg, fix, 8, hipMemcpyHostToDevice, st));
+                        LZ_HIP(hipStreamSynchronize(st));
+                    }
+                    // pointer doubling along succ from every segment
+                    u32* D0 = g_dist[0].get(nseg);
+                    u32* D1 = g_dist[1].get(nseg);
+                    k_jump0<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, jump[0].get(nseg), D0);
+                    u32 nlv = 1;
+                    while ((1ull << (nlv - 1)) < nseg) {
+                        if (nlv >= (u32)MAX_LV) throw error(-6, "greedy: too many jump levels");
+                        k_jumpk<<<cdiv(nseg, 256), 256, 0, st>>>(jump[nlv - 1].p, D0, nseg, jump[nlv].get(nseg), D1);
+                        std::swap(D0, D1);
+                        nlv++;
+                    }
+                    JL.nlv = nlv;
+                    for (u32 l = 0; l < nlv; l++) JL.J[l] = jump[l].p;
+                    k_chain_status<<<1, 1, 0, st>>>(S, jump[nlv - 1].p, D0, c0, d_cs);
+                    LZ_HIP(hipMemcpyAsync(&cs, d_cs, sizeof(cs), hipMemcpyDeviceToHost, st));
+                    LZ_HIP(hipStreamSynchronize(st));
+                    lap("link");
+                    if (cs.err & 6) { restart_seq = true; break; }  // 2: LPF-start query overflow, 4: walk guard
+                    if (dbg)
+                        std::fprintf(stderr,
+                                     "[lz77sss-debug] greedy window=%d outer=%d round=%d segs=%u walked=%u chain=%u valid=%u "
+                                     "flags=%u\n",
+                                     nwin, outer, round, nseg, ntodo, cs.hops + 1, cs.valid, cs.flags);
+                    if (cs.valid && ((cs.flags & 1) || cs.next >= bw)) break;
+                }
+                if (restart_seq) {
+                    wfact = seq_complete(nullptr, 0, nullptr, nullptr, true);
+                    break;
+                }
+                // ---- the chain, its factor offsets, the tail
+                const bool tail = cs.flags & 1;
+                const u32 nall = cs.hops + 1, nchain = nall - (tail ? 1u : 0u);
+                u32* chain = g_chain.get(nall + 1);
+                k_chain_expand<<<cdiv(nall, 256), 256, 0, st>>>(JL, nall, c0, chain);
+                u64* nf = seg_offs.get(nall + 2);
+                u64* offs = g_offs.get(nall + 2);
+                u64 chain_fact = 0;
+                if (nchain) {
+                    k_chain_nfact<<<cdiv(nchain, 256), 256, 0, st>>>(S, chain, nchain, nf);
+                    chain_fact = excl_scan(nf, offs, nchain, scan_tmp, st);
+                }
+                u64 tail_count = 0, tail_bound = 0;
+                pos_t tail_pairs[16];
+                u64 hc[3] = {0, 0, 0};
+                if (tail) {
+                    seg_in tin;
+                    LZ_HIP(hipMemcpyAsync(&tin, g_sin.p + cs.term, sizeof(seg_in), hipMemcpyDeviceToHost, st));
+                    seg_out prev{};
+                    if (nall >= 2) {
+                        u32 pg;
+                        LZ_HIP(hipMemcpyAsync(&pg, chain + nall - 2, 4, hipMemcpyDeviceToHost, st));
+                        LZ_HIP(hipStreamSynchronize(st));
+                        LZ_HIP(hipMemcpyAsync(&prev, g_sout.p + pg, sizeof(seg_out), hipMemcpyDeviceToHost, st));
+                    }
+                    LZ_HIP(hipStreamSynchronize(st));
+                    if (nall >= 2) {  // exact chain state entering the tail walk
+                        tin.idxpos = prev.idxpos;
+                        tin.zmask = prev.zmask;
+                    } else {
+                        tin.idxpos = entry_in.idxpos;
+                        tin.zmask = entry_in.zmask;
+                    }
+                    tail_bound = (u64)N - tin.start + 1;
+                    pos_t* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
+                    u64* d_tc = (u64*)g_tailc.get(4 * sizeof(u64));
+                    pos_t* d_tins = tail_ins_buf.get(16);
+                    k_tail<<<1, 64, 0, st>>>(W, tin, fo, chain_fact, d_tc, d_tins);
+                    LZ_HIP(hipGetLastError());
+                    LZ_HIP(hipMemcpyAsync(hc, d_tc, 24, hipMemcpyDeviceToHost, st));
+                    LZ_HIP(hipMemcpyAsync(tail_pairs, d_tins, sizeof(tail_pairs), hipMemcpyDeviceToHost, st));
+                    LZ_HIP(hipStreamSynchronize(st));
+                    if (hc[2]) throw error(-6, "greedy tail: insert overflow or guard tripped");
+                    tail_count = hc[0];
+                    lap("tail");
+                } else {
+                    fact.get(2 * chain_fact + 2);
+                }
+                // ---- the insert set the chain actually produced vs the speculation
+                LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
+                if (nchain)
+                    k_chain_inserts<<<cdiv((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2);
+                if (tail && hc[1]) {
+                    pos_t* d_tins = tail_ins_buf.p;
+                    k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], off, bmI2);
+                }
+                k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
+                const u64 ny = bmb_scan(bm_bits{bmT, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
+                lap("insert set");
+                if (ny == 0) {
+                    // every lookup of the chain was exact: emit the factors
+                    if (nchain) {
+                        k_walk<true><<<cdiv(nchain, 64), 64, 0, st>>>(W, S, chain, nchain, offs, fact.p);
+                        LZ_HIP(hipGetLastError());
+                        lap("write");
+                    }
+                    if (!last) {
+                        seg_in* d_ex = (seg_in*)(d_sq + 16);
+                        k_exit_state<<<1, 1, 0, st>>>(S, cs.term, d_ex);
+                        LZ_HIP(hipMemcpyAsync(&exit_in, d_ex, sizeof(seg_in), hipMemcpyDeviceToHost, st));
+                        k_h_export<<<cdiv((u64)nchain * 64, 256), 256, 0, st>>>(T, G, S, chain, nchain, Hs);
+                        LZ_HIP(hipStreamSynchronize(st));
+                    }
+                    wfact = chain_fact + tail_count;
+                    break;
+                }
+                if (outer + 1 >= max_outer) {
+                    // round budget spent: the chain is exact up to the first changed position
+                    LZ_HIP(hipMemsetAsync(d_y0, 0xFF, 8, st));
+                    k_first_bit<<<gw, 256, 0, st>>>(bmT, nw, off, d_y0);
+                    wfact = seq_complete(chain, nall, offs, bmI2, false);
+                    break;
+                }
+                // positions that joined (flag 1) or left (0) I
+                pos_t* d_y = dirty_in.get(ny + 1);
+                u8* d_j = (u8*)tmp_greedy2.get(2 * ny + 2);
+                k_bmb_write<<<bmb_blocks, BMB_T, 0, st>>>(bm_bits{bmT, nullptr}, nw, g_bincl.p, out_list{d_y, d_j, bmI2},
+                                                          off);
+                // many positions outside the base set: rebuild it as I' u I_b, re-walk everything
+                const u64 outside = bmb_scan(bm_bits{bmI2, bmIb}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
+                if (outside * 8 > nb) {
+                    k_bm_or<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
+                    std::swap(g_bmI.p, g_bmI2.p);
+                    bmI = g_bmI.p;
+                    bmI2 = g_bmI2.p;
+                    build_base(bmT);
+                    set_state();
+                    k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
+                    if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy rebuild: outside=%llu\n", (unsigned long long)outside);
+                    continue;
+                }
+                if (ny > nseg) {
+                    // too many changes for dirty tracking to pay off: new state, re-walk everything
+                    std::swap(g_bmI.p, g_bmI2.p);
+                    bmI = g_bmI.p;
+                    bmI2 = g_bmI2.p;
+                    set_state();
+                    k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
+                    lap("delta (full)");
+                    if (dbg)
+                        std::fprintf(stderr, "[lz77sss-debug] greedy delta (full): changed=%llu outside=%llu\n",
+                                     (unsigned long long)ny, (unsigned long long)outside);
+                    continue;
+                }
+                // dirty = changed positions + their same-slot successors before and after the update
+                pos_t* d_d = dirty_out.get(11 * ny + 1);
+                LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+                k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + ny);
+                k_flip<<<cdiv(ny, 256), 256, 0, st>>>(W, d_y, d_j, ny, (u8*)W.rem, d_j + ny);
+                std::swap(g_bmI.p, g_bmI2.p);
+                bmI = g_bmI.p;
+                bmI2 = g_bmI2.p;
+                LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));
+                k_sum_u8<<<cdiv(ny, 256), 256, 0, st>>>(d_j + ny, ny, d_cnt);
+                W.bmI = bmI;
+                if (rd1(d_cnt, st)) rebuild_added(false);
+                k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + 6 * ny);
+                pos_t* d_ds = dirty_sorted.get(11 * ny + 1);
+                {
+                    constexpr unsigned PB = 8 * sizeof(pos_t);
+                    size_t tb = 0;
+                    LZ_HIP(rocprim::radix_sort_keys(nullptr, tb, d_d, d_ds, (size_t)(11 * ny), 0u, PB, st));
+                    u8* t = scan_tmp.get(tb);
+                    LZ_HIP(rocprim::radix_sort_keys(t, tb, d_d, d_ds, (size_t)(11 * ny), 0u, PB, st));
+                }
+                k_stale<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, d_ds, 11 * ny);
+                lap("delta + dirty");
+                if (dbg)
+                    std::fprintf(stderr, "[lz77sss-debug] greedy delta: changed=%llu outside=%llu\n", (unsigned long long)ny,
+                                 (unsigned long long)outside);
+            }
         }
-        k_stale<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, d_ds, 11 * ny);
-        lap("delta + dirty");
-        if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy delta: changed=%llu outside=%llu\n",
-                              (unsigned long long)ny, (unsigned long long)outside);
+        k_seg_at_clear<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
+        seg_at_clean = true;
+        outer_all += max_outer == 0 ? 0 : outer + 1;
+        rounds_all += rounds_total;
+        walked_all += walked_total;
+        nseg_last = nseg;
+        nseg0_all += nseg0;
+        nwin++;
+        // the window's factors: fact[0, wfact); appended to the stream when there are several windows
+        if (carry) {
+            pos_t* acc = fact_acc.grow_keep(2 * (total_fact + wfact) + 2, 2 * total_fact, st);
+            if (wfact)
+                LZ_HIP(hipMemcpyAsync(acc + 2 * total_fact, fact.p, 2 * wfact * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+        }
+        total_fact += wfact;
+        if (last) {
+            entry.start = N;
+            break;
+        }
+        entry = exit_in;
+        if (dbg)
+            std::fprintf(stderr, "[lz77sss-debug] greedy window %d done: factors=%llu next=%llu\n", nwin - 1,
+                         (unsigned long long)wfact, (unsigned long long)entry.start);
+        if (entry.start >= target_end) break;
     }
-    return finish_call(total_fact, outer + 1, rounds_total, walked_total, nseg);
+    if (blk) {
+        blk->exit_start = entry.start;
+        blk->exit_idxpos = entry.idxpos;
+        blk->exit_zmask = entry.zmask;
+    }
+    if (carry) {
+        // the stream: fact_acc becomes fact
+        std::swap(fact.p, fact_acc.p);
+        std::swap(fact.cap, fact_acc.cap);
+    }
+    stats[12] = outer_all;
+    stats[13] = rounds_all;
+    stats[14] = stats_fallback_lanes;
+    stats[15] = walked_all;
+    stats[16] = nseg_last;
+    stats[17] = nseg0_all;
+    stats[21] = nwin;
+    return total_fact;
 }
 
 }  // namespace LZ_NS

@@ -713,14 +713,11 @@ static u32 pow32_host(u32 b, u64 e) {
     return r;
 }
 
-void engine::build_sss(const u8* T) {
-    s = 0;
-    has_runs = false;
+// Q anchors and the periodic-run table (the part of the SSS pass the LCE needs too);
+// returns whether some window is in Q
+bool engine::build_q_runs(const u8* T) {
     runs_valid = false;
-    sss_kernel_ms = 0;
-    sss_kernel_bytes = 0;
-    if (n < 2 * (u64)TAU) return;
-    const u64 last_i = n - 2 * TAU;
+    if (n < 2 * (u64)TAU) return false;
     const u64 nanch = (n - TAU) / QA + 2;
     u16* qi = q_info.get(nanch + 64);  // k_sss_stream reads 8 anchors per block, up to 2 blocks past n
     u32* ctr = counters.get(16);
@@ -745,7 +742,20 @@ void engine::build_sss(const u8* T) {
         runs_valid = true;
     }
 
-    const bool any_q = rd1(ctr, st) != 0;  // picks the stream kernel's instantiation
+    return rd1(ctr, st) != 0;
+}
+
+void engine::build_sss(const u8* T) {
+    s = 0;
+    has_runs = false;
+    sss_kernel_ms = 0;
+    sss_kernel_bytes = 0;
+    const bool any_q = build_q_runs(T);  // picks the stream kernel's instantiation
+    if (n < 2 * (u64)TAU) return;
+    const u64 last_i = n - 2 * TAU;
+    const u64 nanch = (n - TAU) / QA + 2;
+    const u16* qi = q_info.p;
+    u32* ctr = counters.p;
     const u64 nlanes = last_i / SD + 1;  // stripes
     pos_t* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);

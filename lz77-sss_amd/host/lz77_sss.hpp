@@ -3,20 +3,24 @@
 // C-ABI of liblz77sss_hip.so (include/lz77sss.h).
 //
 // A caller of
-//     lz77_sss<uint32_t>::factorize_approximate<greedy, lpf_opt, 512>(T, n, out, {.num_threads = p});
+//     lz77_sss<pos_t>::factorize_approximate<greedy, lpf_opt, 512>(T, n, out, {.num_threads = p});
 //     lz77_sss<uint32_t>::factorize_exact<greedy, lpf_opt, with_samples>(T, n, out);
 //     lz77_sss<uint32_t>::decode(fact_it, out_it, n);
 // keeps its code and links against the HIP library instead.  Differences:
 //   * the factorization runs on an MI355X (device `parameters::device`) with the
 //     p = 1 output stream of the reference (num_threads is accepted and ignored);
 //   * errors surface as lz77_sss_error (the reference only asserts); no CPU fallback;
-//   * pos_t = uint32_t only (n < 2^32); the factor layout is the reference's
-//     `factor{pos_t src, len}` (8 bytes, literal <=> len == 0, src = the byte);
+//   * pos_t = uint32_t (n < 2^32) or uint64_t (any n up to 2^40; the pos_t = uint64_t
+//     engine, lz77sss_factorize_approx_u64); the factor layout is the reference's
+//     `factor{pos_t src, len}` (literal <=> len == 0, src = the byte), streamed as 8
+//     or 5 + 5 bytes (lz77_sss.hpp:149-173);
 //   * the input is not modified (the reference's LPF/LNF modes reverse it in place
 //     and restore it, lz77_sss.hpp:385-393).
 #pragma once
 
 #include <cstdint>
+#include <istream>
+#include <ostream>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -55,7 +59,10 @@ struct lz77_sss_error : std::runtime_error {
 
 template <typename pos_t = uint32_t>
 class lz77_sss {
-    static_assert(std::is_same_v<pos_t, uint32_t>, "this implementation provides pos_t = uint32_t");
+    static_assert(std::is_same_v<pos_t, uint32_t> || std::is_same_v<pos_t, uint64_t>,
+                  "pos_t is uint32_t or uint64_t (lz77_sss.hpp:72-75)");
+    static constexpr bool wide = std::is_same_v<pos_t, uint64_t>;
+    using cfactor = std::conditional_t<wide, lz77sss_factor64, lz77sss_factor32>;
 
     static void check(int rc) {
         if (rc != LZ77SSS_OK) {
@@ -71,12 +78,33 @@ class lz77_sss {
     template <typename sidx_t> using default_range_ds_t = decomposed_static_weighted_square_grid<sidx_t>;
     static constexpr uint64_t default_tau = 512;
 
-    struct factor {  // lz77_sss.hpp:129-147 (same 8-byte layout as lz77sss_factor32)
+    struct factor {  // lz77_sss.hpp:129-147 (same layout as lz77sss_factor32 / lz77sss_factor64)
         pos_t src;
         pos_t len;
         pos_t length() const { return len > 1 ? len : 1; }
+        static constexpr pos_t size_of() { return wide ? 10 : 8; }
+        // the reference's stream form: 8 bytes (uint32_t), 5 + 5 bytes little endian (uint64_t)
+        friend std::ostream& operator<<(std::ostream& out, const factor& f) {
+            if constexpr (!wide) {
+                out.write(reinterpret_cast<const char*>(&f), 8);
+            } else {
+                out.write(reinterpret_cast<const char*>(&f.src), 5);
+                out.write(reinterpret_cast<const char*>(&f.len), 5);
+            }
+            return out;
+        }
+        friend std::istream& operator>>(std::istream& in, factor& f) {
+            if constexpr (!wide) {
+                in.read(reinterpret_cast<char*>(&f), 8);
+            } else {
+                f.src = f.len = 0;
+                in.read(reinterpret_cast<char*>(&f.src), 5);
+                in.read(reinterpret_cast<char*>(&f.len), 5);
+            }
+            return in;
+        }
     };
-    static_assert(sizeof(factor) == sizeof(lz77sss_factor32));
+    static_assert(sizeof(factor) == sizeof(cfactor));
 
     // lz77_sss.hpp:176-186: factors are handed to `output` by value, in text order,
     // on the calling thread.
@@ -96,12 +124,15 @@ class lz77_sss {
         struct ctx_t {
             output_fnc_t* out;
         } ctx{&output};
-        auto emit = [](const lz77sss_factor32* batch, uint64_t count, void* user) -> int {
+        auto emit = [](const cfactor* batch, uint64_t count, void* user) -> int {
             auto* c = static_cast<ctx_t*>(user);
-            for (uint64_t k = 0; k < count; k++) (*c->out)(factor{batch[k].src, batch[k].len});
+            for (uint64_t k = 0; k < count; k++) (*c->out)(factor{(pos_t)batch[k].src, (pos_t)batch[k].len});
             return 0;
         };
-        check(lz77sss_factorize_approx_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p, emit, &ctx));
+        if constexpr (wide)
+            check(lz77sss_factorize_approx_u64(reinterpret_cast<const uint8_t*>(input), input_size, &p, emit, &ctx));
+        else
+            check(lz77sss_factorize_approx_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p, emit, &ctx));
     }
 
     // lz77_sss.hpp:188-200: exact factorization (greedy LZ77 lengths; sources by the
@@ -124,27 +155,32 @@ class lz77_sss {
         struct ctx_t {
             output_fnc_t* out;
         } ctx{&output};
-        auto emit = [](const lz77sss_factor32* batch, uint64_t count, void* user) -> int {
+        auto emit = [](const cfactor* batch, uint64_t count, void* user) -> int {
             auto* c = static_cast<ctx_t*>(user);
-            for (uint64_t k = 0; k < count; k++) (*c->out)(factor{batch[k].src, batch[k].len});
+            for (uint64_t k = 0; k < count; k++) (*c->out)(factor{(pos_t)batch[k].src, (pos_t)batch[k].len});
             return 0;
         };
-        check(lz77sss_factorize_exact_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p,
-                                          static_cast<int>(transf_mode), emit, &ctx));
+        if constexpr (wide)
+            check(lz77sss_factorize_exact_u64(reinterpret_cast<const uint8_t*>(input), input_size, &p,
+                                              static_cast<int>(transf_mode), emit, &ctx));
+        else
+            check(lz77sss_factorize_exact_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p,
+                                              static_cast<int>(transf_mode), emit, &ctx));
     }
 
     // lz77_sss.hpp:202-203 (algorithms/common.cpp:31-54): sequential host decode
     template <typename fact_it_t, typename out_it_t>
     static void decode(fact_it_t fact_it, out_it_t out_it, pos_t output_size) {
         std::vector<uint8_t> buf(output_size);
-        std::vector<lz77sss_factor32> fs;
+        std::vector<cfactor> fs;
         for (uint64_t pos = 0; pos < output_size;) {
             const factor f = *fact_it;
             ++fact_it;
             fs.push_back({f.src, f.len});
             pos += f.length();
         }
-        check(lz77sss_decode_u32(fs.data(), fs.size(), buf.data(), output_size));
+        if constexpr (wide) check(lz77sss_decode_u64(fs.data(), fs.size(), buf.data(), output_size));
+        else check(lz77sss_decode_u32(fs.data(), fs.size(), buf.data(), output_size));
         for (uint64_t i = 0; i < output_size; i++) *out_it++ = static_cast<char>(buf[i]);
     }
 };

@@ -32,6 +32,18 @@ struct seg_out {
     pos_t bnd[SEG_NBND];
 };
 
+// the greedy chain over a text block [start, end) (csrc/greedy.hip): the
+// exact chain state at start in, the state at the first hand-over point >= end out; the
+// carried table (g_Hs: last insert per slot before the block, pos + 1) in and out
+struct greedy_block {
+    pos_t start = 0, idxpos = 0;
+    u32 zmask = 0;
+    bool carried = false;  // g_Hs holds the inserts before start (else it is zeroed)
+    pos_t end = 0;
+    pos_t exit_start = 0, exit_idxpos = 0;
+    u32 exit_zmask = 0;
+};
+
 struct engine {
     int device = 0;
     hipStream_t st = nullptr;
@@ -123,6 +135,8 @@ struct engine {
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32;
     dbuf<pos_t> g_xpos;
     dbuf<pos_t> g_H;    // materialized gap-index table of the sequential completion
+    dbuf<pos_t> g_Hs;   // greedy windows: last insert per slot before the window (pos + 1)
+    dbuf<pos_t> fact_acc;  // greedy windows: the stream so far
     dbuf<u8> g_cut;     // chain_cut + completion counters
     dbuf<u64> g_xk, g_xk2;
     // exact mode (csrc/exact.hip)
@@ -155,6 +169,8 @@ struct engine {
 
     // pipeline phases (each enqueues on `st`)
     void build_sss(const u8* T);
+    bool build_q_runs(const u8* T);     // Q anchors + periodic-run table only
+    void set_sss(const pos_t* S_any, u64 count, bool runs);  // an externally built (sharded) sync set
     void build_sss_range(u64 first, u64 end, u64 base, u64 window);  // csrc/sss.hip
     void build_sa_s(const u8* T);
     void build_lcp_rmq(const u8* T);
@@ -165,8 +181,10 @@ struct engine {
     void build_lpf_lnf(int opt);  // csrc/lnf.hip
     void all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slots, u32* sflag);
     void path_marks(u32 m, u32* nxt0, u32* marks);
-    u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override);
+    u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy_block* blk = nullptr);
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode = 1);
+    void prepare_phrases(int phr_mode, bool external_sss);  // the phases before the emitter
+    u64 carried_entries(int log2_override);                 // slots of the gap index (carried table size)
     u64 emit_skip_phrases();  // fact_mode = skip_phrases (csrc/engine.hip)
     u64 ssszip_gapped();      // csrc/ssszip.hip
     u64 huffman_container();  // csrc/huffman.hip

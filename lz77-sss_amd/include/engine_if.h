@@ -36,6 +36,12 @@ struct engine_if {
     virtual double sss_kernel_ms() const = 0;
     virtual u64 sss_kernel_bytes() const = 0;
     virtual u32 dec_rounds() const = 0;
+    // sharded factorization (rank-ordered greedy blocks)
+    virtual void set_sss(const u64* S_any, u64 count, bool runs) = 0;
+    virtual u64 prepare(int phr_mode, bool external_sss, int log2_override) = 0;  // returns carried-table bytes
+    virtual void* carried_table() = 0;
+    virtual u64 greedy_block(u32 rk_seed, int log2_override, u64* state /* start, idxpos, zmask, carried, end,
+                                                                        exit_start, exit_idxpos, exit_zmask */) = 0;
 };
 
 // defined in the LZ_POS64 compilation of csrc/engine.hip; throws lz::error

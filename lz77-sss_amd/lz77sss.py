@@ -56,6 +56,10 @@ _SYMBOLS = {
     "lz77sss_session_is64": (ctypes.c_int, [_P]),
     "lz77sss_session_get_factors64": (ctypes.c_int, [_P, _P, _U64]),
     "lz77sss_session_get_lpf64": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    "lz77sss_session_set_sss": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "lz77sss_session_prepare": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(_U64)]),
+    "lz77sss_session_carried_copy": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
+    "lz77sss_session_greedy_block": (ctypes.c_int, [_P, ctypes.POINTER(Params), _P, ctypes.POINTER(_U64)]),
     "lz77sss_session_factorize_exact": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.c_int,
                                                        ctypes.POINTER(_U64)]),
     "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
@@ -133,6 +137,13 @@ def params(phr_mode=LPF_OPT, fact_mode=GREEDY, tau=DEFAULT_TAU, rk_seed=42, inde
     return p
 
 
+class Block(ctypes.Structure):
+    """lz77sss_block: one block of a sharded factorization (include/lz77sss.h)."""
+    _fields_ = [("start", ctypes.c_uint64), ("idxpos", ctypes.c_uint64), ("zmask", ctypes.c_uint32),
+                ("carried", ctypes.c_int32), ("end", ctypes.c_uint64), ("exit_start", ctypes.c_uint64),
+                ("exit_idxpos", ctypes.c_uint64), ("exit_zmask", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
 class Session:
     """Device-resident session: the text stays in HBM across calls."""
 
@@ -179,6 +190,45 @@ class Session:
         z = _U64()
         _check(load_library().lz77sss_session_factorize_exact(self._h, ctypes.byref(p), transf_mode, ctypes.byref(z)))
         return z.value
+
+    # ---- sharded factorization (include/lz77sss.h; lz77-sss_amd/sharded.py drives it)
+    def set_sss(self, S, has_runs: bool, device_ptr: int | None = None):
+        """Loads an externally built sync set (uint64 host array, or a device pointer + len(S))."""
+        if device_ptr is not None:
+            _check(load_library().lz77sss_session_set_sss(self._h, _P(device_ptr), int(S), int(has_runs)))
+            return
+        a = np.ascontiguousarray(S, dtype=np.uint64)
+        _check(load_library().lz77sss_session_set_sss(self._h, a.ctypes.data_as(_P), a.size, int(has_runs)))
+
+    def prepare(self, external_sss: bool = True, **kw) -> int:
+        """Phases before the greedy emitter; returns the carried table's size in bytes."""
+        p = params(**kw)
+        b = _U64()
+        _check(load_library().lz77sss_session_prepare(self._h, ctypes.byref(p), int(external_sss), ctypes.byref(b)))
+        return b.value
+
+    def carried_get(self, nbytes: int, device_ptr: int | None = None) -> np.ndarray | None:
+        if device_ptr is not None:
+            _check(load_library().lz77sss_session_carried_copy(self._h, _P(device_ptr), nbytes, 0))
+            return None
+        out = np.empty(max(nbytes, 1), np.uint8)
+        _check(load_library().lz77sss_session_carried_copy(self._h, out.ctypes.data_as(_P), nbytes, 0))
+        return out[:nbytes]
+
+    def carried_set(self, table=None, nbytes: int = 0, device_ptr: int | None = None):
+        if device_ptr is not None:
+            _check(load_library().lz77sss_session_carried_copy(self._h, _P(device_ptr), nbytes, 1))
+            return
+        a = np.ascontiguousarray(table, dtype=np.uint8)
+        _check(load_library().lz77sss_session_carried_copy(self._h, a.ctypes.data_as(_P), a.size, 1))
+
+    def greedy_block(self, start: int, idxpos: int, zmask: int, carried: bool, end: int, **kw):
+        """The greedy chain of [start, end) -> (factor count, (exit_start, exit_idxpos, exit_zmask))."""
+        p = params(**kw)
+        b = Block(start, idxpos, zmask, int(carried), end, 0, 0, 0, 0)
+        z = _U64()
+        _check(load_library().lz77sss_session_greedy_block(self._h, ctypes.byref(p), ctypes.byref(b), ctypes.byref(z)))
+        return z.value, (b.exit_start, b.exit_idxpos, b.exit_zmask)
 
     def factors(self, z: int) -> np.ndarray:
         if self.pos64:

@@ -1,4 +1,4 @@
-"""Sharded sync set over the ranks of one node (collective (1)).
+"""Sharded sync set and sharded 3-approximation over the ranks of one node.
 
 The decisions of the text are split into contiguous blocks, one per rank.  Rank r
 holds only T[b_r, e_r + 2tau - 1) -- its block plus the 2tau - 1 byte halo that the
@@ -119,3 +119,162 @@ def sss_sharded(text, n: int, rank: int, world: int, device: int | None = None,
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
         any_runs = bool(flag.item())
     return allp.cpu().numpy().astype(np.uint64), any_runs
+
+
+# ---------------------------------------------------------------------------
+# Sharded 3-approximation (SURVEY.md 8e collectives (1)-(4)).
+#   (1) S by text block on every rank + all-gather (sss_sharded above);
+#   (2) SA_S / LCP / LCE and the LPF phrases replicated on every rank from the
+#       gathered S (lz77sss_session_prepare with external_sss);
+#   (3) the greedy chain block by block in rank order: rank r receives the exact
+#       chain state and the carried table (last insert per gap-index slot before its
+#       block) from rank r - 1, walks its block, sends both on;
+#   (4) the blocks' factors gathered to every rank in rank order.
+# The concatenation is bit-identical to a one-GPU factorization of the whole text.
+TAIL_GUARD = 4160  # a non-last chain block ends at or below n - 4160 (greedy.hip)
+
+
+def chain_bounds(n: int, world: int, tau: int = TAU) -> list[int]:
+    """g_0 = 0 <= g_1 <= ... <= g_world = n: the chain blocks [g_r, g_{r+1}) (the sync-set
+    blocks' starts, clamped so a non-last block ends at or below n - 4160)."""
+    parts = partition(n, world, tau)
+    lim = n - TAIL_GUARD if n > TAIL_GUARD else 0
+    inner = [min(b, lim) for b, _ in parts[1:]]
+    return [0] + inner + [n]
+
+
+class HipBlocks:
+    """Block compute on one device through the C-ABI (a session holding the whole text)."""
+
+    def __init__(self, text, n: int, device: int = 0, pos64: bool = False, **params):
+        import lz77sss as L
+
+        self.L = L
+        self.params = params
+        self.s = L.Session(max(n, 1), device, pos64=pos64)
+        if callable(text):
+            text(self.s, 0, n)
+        else:
+            self.s.load(np.ascontiguousarray(text))
+        self.table_bytes = 0
+
+    def prepare(self, S, runs: bool) -> int:
+        self.s.set_sss(S, runs)
+        self.table_bytes = self.s.prepare(external_sss=True, **self.params)
+        return self.table_bytes
+
+    def run(self, state, end: int, table):
+        start, idxpos, zmask = state
+        if table is not None:
+            self.s.carried_set(table)
+        z, ex = self.s.greedy_block(start, idxpos, zmask, table is not None, end, **self.params)
+        F = self.s.factors(z).astype(np.uint64)
+        return F, ex, self.s.carried_get(self.table_bytes)
+
+    def close(self):
+        self.s.close()
+
+
+class OracleBlocks:
+    """The same interface on the CPU oracle (tests; oracle.hpp greedy_block)."""
+
+    def __init__(self, text, n: int, pos64: bool = False, **params):
+        import oracle
+
+        self.o = oracle
+        self.T = np.ascontiguousarray(text)
+        self.wide = pos64
+        self.params = params
+
+    def prepare(self, S, runs: bool) -> int:
+        want, _ = self.o.sss(self.T)
+        assert np.array_equal(np.asarray(S, np.uint64), want.astype(np.uint64)), "gathered sync set differs"
+        return 0
+
+    def run(self, state, end: int, table):
+        start, idxpos, _ = state
+        dt = np.uint64 if self.wide else np.uint32
+        tab = None if table is None else np.frombuffer(np.ascontiguousarray(table).tobytes(), dt)
+        F, (es, ei), tab = self.o.greedy_block(self.T, start, idxpos, end, tab, wide=self.wide, **self.params)
+        return F, (es, ei, 0), tab.view(np.uint8)
+
+    def close(self):
+        pass
+
+
+def _send_bytes(arr: np.ndarray, dst: int, device=None, group=None):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy())
+    n = torch.tensor([t.numel()], dtype=torch.int64)
+    if device is not None:
+        t, n = t.to(device), n.to(device)
+    dist.send(n, dst, group=group)
+    if t.numel():
+        dist.send(t, dst, group=group)
+
+
+def _recv_bytes(src: int, device=None, group=None) -> np.ndarray:
+    import torch
+    import torch.distributed as dist
+
+    n = torch.zeros(1, dtype=torch.int64, device=device)
+    dist.recv(n, src, group=group)
+    t = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
+    if t.numel():
+        dist.recv(t, src, group=group)
+    return t.cpu().numpy()
+
+
+def factorize_sharded(text, n: int, rank: int, world: int, device: int | None = None, blocks=None, group=None,
+                      sss_compute: Callable | None = None, timings: dict | None = None):
+    """The 3-approximation of T (uint64 (z, 2) factors, on every rank) computed with `world`
+    ranks.  `blocks` (HipBlocks / OracleBlocks) holds the whole text; defaults to HipBlocks
+    on `device` (rank if None).  Call on every rank of the process group."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    dev = rank if device is None else device
+    nccl = dist.is_initialized() and dist.get_backend(group) == "nccl"
+    comm_dev = f"cuda:{dev}" if nccl else None
+    t0 = time.perf_counter()
+    # (1) sharded sync set
+    S, runs = sss_sharded(text, n, rank, world, device=dev, compute=sss_compute, group=group)
+    t1 = time.perf_counter()
+    # (2) replicated phrases
+    if blocks is None:
+        blocks = HipBlocks(text, n, device=dev)
+    blocks.prepare(S, runs)
+    t2 = time.perf_counter()
+    # (3) rank-ordered greedy chain
+    g = chain_bounds(n, world)
+    if rank == 0:
+        state, table = (0, 0, 0), None
+    else:
+        st = _recv_bytes(rank - 1, comm_dev, group).view(np.uint64)
+        state = (int(st[0]), int(st[1]), int(st[2]))
+        table = _recv_bytes(rank - 1, comm_dev, group)
+        if table.size == 0:  # no block before this one ran: nothing inserted yet
+            table = None
+    if state[0] < g[rank + 1] or rank == world - 1:
+        F, ex, table = blocks.run(state, g[rank + 1], table)
+    else:  # an earlier block's last factor covered this whole block: pass the state on
+        F, ex = np.zeros((0, 2), np.uint64), state
+    if rank + 1 < world:
+        _send_bytes(np.array(ex, np.uint64), rank + 1, comm_dev, group)
+        _send_bytes(table if table is not None else np.zeros(0, np.uint8), rank + 1, comm_dev, group)
+    t3 = time.perf_counter()
+    # (4) emission: the blocks' factors in rank order
+    if world > 1 and dist.is_initialized():
+        flat = torch.from_numpy(F.reshape(-1).astype(np.int64))
+        if nccl:
+            flat = flat.to(comm_dev)
+        allf = gather_blocks(flat, group).cpu().numpy().astype(np.uint64).reshape(-1, 2)
+    else:
+        allf = F.reshape(-1, 2)
+    if timings is not None:
+        timings.update(sss=t1 - t0, prepare=t2 - t1, greedy_chain=t3 - t2, emit=time.perf_counter() - t3)
+    return allf

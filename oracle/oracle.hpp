@@ -837,6 +837,102 @@ static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, 
 }
 
 // ===========================================================================
+//  One block of the sharded greedy (the device's lz77sss_session_greedy_block):
+//  the reference loop above started at chain position `start` with the gap index
+//  at `idxpos` and its table H taken from the carried table Hc (pos + 1, 0 =
+//  empty), stopped at the first hand-over point >= end (a gap start reached after
+//  LPF factors, or a gap-walk factor start), with H written back to Hc.  Blocks
+//  run in order and concatenated give the p = 1 stream (tests/test_sharded_sss.py).
+//  Non-last blocks must end at or below n - 4160 (no stale fingerprints there).
+// ===========================================================================
+template <class Q = u32, typename OUT>
+static inline void greedy_block(u8* T, Q n, int phr_mode, u32 rk_seed, Q start, Q idxpos, Q end, std::vector<Q>& Hc,
+                                Q& exit_start, Q& exit_idxpos, OUT&& output) {
+    using lpf = lpf_t<Q>;
+    using factor = factor_t<Q>;
+    exit_start = n;
+    exit_idxpos = n;
+    if (n == 0 || start >= end) { exit_start = start; exit_idxpos = idxpos; return; }
+    std::vector<lpf> P;
+    lce_structure<Q> L;
+    L.build(T, n);
+    if (phr_mode == lpf_opt) P = build_lpf_opt(T, n, L);
+    else if (phr_mode == lpf_naive) P = build_lpf_naive(T, n, L);
+    else throw std::runtime_error("greedy_block: phr_mode lpf_opt or lpf_naive");
+    phrase_info_t<Q> pi = get_phrase_info<Q>(P, n);
+    P.push_back({n, n + 1, 0});
+    gap_params gp = choose_gap_params(n, pi);
+    gap_index<Q> G;
+    G.create(T, n, gp.patt_lens, gp.log2_size_h, gap_bases(rk_seed));
+    if (Hc.size() != G.H.size()) Hc.assign(G.H.size(), 0);
+    for (size_t k = 0; k < Hc.size(); k++) G.H[k] = Hc[k] ? Hc[k] - 1 : ~(Q)0;
+    G.reinit(idxpos);  // fingerprints at idxpos (< n - 64: full windows, as rolled)
+    const u32 thr = gp.roll_threshold;
+    size_t li = 0;
+    while (P[li].end <= start) li++;  // the phrase iterator's invariant at a chain position
+    auto next_lpf = [&]() -> lpf {
+        lpf phr = P[li++];
+        if (li == P.size()) li--;
+        return phr;
+    };
+    auto longest_prev_occ = [&](Q pos) -> factor {
+        factor f{T[pos], 0};
+        for (int x = 4; x >= 0; x--) {
+            if (f.len == 0) {
+                Q src = G.advance_and_get_occ(x);
+                if (src < pos && T[src] == T[pos]) { f.len = (Q)L.lce(src, pos); f.src = src; }
+            } else {
+                G.advance_i(x);
+            }
+        }
+        G.cur++;
+        return f;
+    };
+    lpf p = next_lpf();
+    Q i = start;
+    for (;;) {
+        Q gap_end = p.beg;
+        if (i >= end && i < gap_end) break;  // hand-over at a gap start
+        bool stopped = false;
+        if (i < gap_end) {
+            if (G.cur < i) {
+                if (i - G.cur <= thr) { do { G.roll(); } while (G.cur < i); }
+                else G.reinit(i);
+            }
+            do {
+                if (i >= end) { stopped = true; break; }  // hand-over at a gap-walk factor start
+                factor f = longest_prev_occ(i);
+                i += std::max<Q>(1, f.len);
+                if (i > gap_end) {
+                    if (i <= p.end) { f.len -= i - gap_end; i = gap_end; }
+                    else {
+                        do { p = next_lpf(); } while (p.end <= i);
+                        while (G.cur < gap_end) G.advance();
+                        gap_end = p.beg;
+                    }
+                }
+                output(f);
+                while (G.cur < i) G.advance();
+            } while (i < gap_end);
+        }
+        if (stopped) break;
+        if (i == n) break;
+        Q exc = i - gap_end;
+        factor lf{p.src + exc, (p.end - p.beg) - exc};
+        if (G.cur == i) {
+            factor f = longest_prev_occ(i);
+            if (f.len > lf.len) lf = f;
+        }
+        output(lf);
+        i += lf.len;
+        while (p.end <= i) p = next_lpf();
+    }
+    exit_start = i;
+    exit_idxpos = G.cur;
+    for (size_t k = 0; k < Hc.size(); k++) Hc[k] = G.H[k] == ~(Q)0 ? 0 : G.H[k] + 1;
+}
+
+// ===========================================================================
 //  Exact greedy LZ77 (factorize_exact, lz77_sss.hpp:188-200,333-357)
 //
 //  The reference's exact modes refine the 3-approximation until every factor

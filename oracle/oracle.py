@@ -70,6 +70,9 @@ def lib():
         L.oracle_sss64.argtypes = [_P, _U64, _P, _U64, ctypes.POINTER(ctypes.c_int)]
         L.oracle_lpf_opt64.restype = ctypes.c_int64
         L.oracle_lpf_opt64.argtypes = [_P, _U64, _P, _U64]
+        L.oracle_greedy_block.restype = ctypes.c_int64
+        L.oracle_greedy_block.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, _P, _P,
+                                          ctypes.POINTER(_U64), _P, _U64]
         L.oracle_num_threads.restype = ctypes.c_int
         L.oracle_num_threads.argtypes = []
         _lib = L
@@ -143,6 +146,31 @@ def lpf_opt64(T):
     if k < 0:
         raise RuntimeError("oracle lpf failed")
     return out[:k].copy()
+
+
+def greedy_block(T, start: int, idxpos: int, end: int, table=None, wide: bool = False, phr_mode: int = LPF_OPT,
+                 rk_seed: int = 42):
+    """One block of the sharded greedy (oracle.hpp greedy_block) -> (factors (z,2) uint64, (exit_start,
+    exit_idxpos), carried table (uint32 / uint64 array, pos + 1))."""
+    buf = _padded(T)
+    n = _u8(T).size
+    dt = np.uint64 if wide else np.uint32
+    tab = np.zeros(0, dt) if table is None else np.ascontiguousarray(table, dtype=dt).copy()
+    cap = n + 4
+    out = np.zeros((cap, 2), np.uint64)
+    for _ in range(2):
+        state = np.array([start, idxpos, end, 0, 0], np.uint64)
+        ent = _U64(tab.size)
+        z = lib().oracle_greedy_block(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, int(wide), state.ctypes.data_as(_P),
+                                      tab.ctypes.data_as(_P) if tab.size else None, ctypes.byref(ent),
+                                      out.ctypes.data_as(_P), cap)
+        if z == -2:  # the carried table was empty: size it (zeros) and run again
+            tab = np.zeros(ent.value, dt)
+            continue
+        if z < 0:
+            raise RuntimeError("oracle greedy block failed")
+        return out[:z].copy(), (int(state[3]), int(state[4])), tab
+    raise RuntimeError("oracle greedy block: table size")
 
 
 def factorize_timed(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):

@@ -63,6 +63,44 @@ int64_t oracle_factorize_approx64(uint8_t* T, uint64_t n, int phr_mode, uint32_t
     }
 }
 
+// One block of the sharded greedy (oracle.hpp greedy_block).  table: the carried table
+// (pos + 1; uint32 entries, or uint64 for wide), table_entries its length (0: empty, the
+// block sizes it; the needed length is returned in *table_entries when it differs).
+// state: [start, idxpos, end] in, [exit_start, exit_idxpos] out in state[3..4].
+// Returns the factor count (out: 2*cap uint64), -1 on overflow, -2 if the table is too small.
+int64_t oracle_greedy_block(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed, int wide, uint64_t* state,
+                            void* table, uint64_t* table_entries, uint64_t* out, uint64_t cap) {
+    try {
+        uint64_t k = 0;
+        bool overflow = false;
+        auto run = [&](auto zero) -> int64_t {
+            using Q = decltype(zero);
+            std::vector<Q> H;
+            Q* tab = (Q*)table;
+            if (*table_entries) H.assign(tab, tab + *table_entries);
+            Q es = 0, ei = 0;
+            greedy_block<Q>(T, (Q)n, phr_mode, rk_seed, (Q)state[0], (Q)state[1], (Q)state[2], H, es, ei,
+                            [&](factor_t<Q> f) {
+                                if (k < cap) { out[2 * k] = f.src; out[2 * k + 1] = f.len; } else overflow = true;
+                                k++;
+                            });
+            state[3] = es;
+            state[4] = ei;
+            if (H.size() != *table_entries) {
+                const bool fits = tab && H.size() <= *table_entries;
+                *table_entries = H.size();
+                if (!fits) return -2;
+            }
+            std::copy(H.begin(), H.end(), tab);
+            return overflow ? -1 : (int64_t)k;
+        };
+        return wide ? run((u64)0) : run((u32)0);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -3;
+    }
+}
+
 // SSS with 64-bit positions and the LPF_opt phrases of pos_t = uint64_t (tests)
 int64_t oracle_sss64(const uint8_t* T, uint64_t n, uint64_t* out, uint64_t cap, int* has_runs) {
     bool hr = false;

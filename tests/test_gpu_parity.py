@@ -169,7 +169,7 @@ def test_cpp_mirror_roundtrip(tmp_path):
     exe = build_cpp_client(tmp_path)
     r = subprocess.run([str(exe), "8"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count(" ok") == 8
+    assert r.stdout.count(" ok") == 16  # 8 seeds x pos_t in {uint32_t, uint64_t}
 
 
 @pytest.mark.parametrize("name", golden_names())
@@ -360,3 +360,29 @@ def test_greedy_bounded_completion_genome(session, orc, lz, max_outer, monkeypat
     assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
     st = s.stats()
     assert st[19] == (1 if rounds > max_outer else 0)
+
+
+# ---- greedy windows: the chain walked window by window with the exact state and the
+# last-insert-per-slot table handed over; any window size gives the same stream
+
+@pytest.mark.parametrize("window", [4096, 20000, 65536])
+@pytest.mark.parametrize("seed", [1, 4, 9])
+def test_greedy_windows_c1(session, orc, lz, seed, window, monkeypatch):
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    monkeypatch.setenv("LZ77SSS_GREEDY_WINDOW", str(window))
+    s, F = run(session, T)
+    assert np.array_equal(F, orc.factorize(T)[0])
+    assert s.stats()[21] >= (1 if T.size < 2 * window else 2)
+
+
+@pytest.mark.parametrize("window,max_outer", [(1 << 20, 256), (3 << 20, 256), (1 << 20, 1), (1 << 20, 0)])
+def test_greedy_windows_genome(session, orc, lz, window, max_outer, monkeypatch):
+    """Windows on a gap-heavy text, also with the sequential completion inside windows."""
+    n = 8 << 20
+    T = lz.gen_genome(n, 1 << 20, 0.001, 17)
+    monkeypatch.setenv("LZ77SSS_GREEDY_WINDOW", str(window))
+    monkeypatch.setenv("LZ77SSS_GREEDY_MAX_OUTER", str(max_outer))
+    s, F = run(session, T)
+    F_ref, _ = orc.factorize(T)
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+    assert s.stats()[21] >= 2

@@ -180,3 +180,12 @@ def test_u64_chr19_past_4gib_vs_oracle(lz, orc):
     F_ref, st_ref = orc.factorize64(T[:n], buf=T)
     assert st[:12] == [int(x) for x in st_ref[:12]]
     assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
+@pytest.mark.parametrize("window", [4096, 65536, 1 << 20])
+def test_u64_greedy_windows(session64, orc, lz, window, monkeypatch):
+    T = lz.gen_genome(4 << 20, 1 << 20, 0.001, 23)
+    monkeypatch.setenv("LZ77SSS_GREEDY_WINDOW", str(window))
+    s, F = run64(session64, T)
+    assert np.array_equal(F, orc.factorize64(T)[0])
+    assert s.stats()[21] >= 2

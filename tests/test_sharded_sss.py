@@ -211,3 +211,116 @@ def test_gen_genome_blocks_and_past_4gib(lz, orc):
         blk = s.sync_set64(c)
     want = S1[(S1 >= b) & (S1 < e)]
     assert np.array_equal(blk, want)
+
+
+# ---------------------------------------------------------------- sharded 3-approximation
+def test_chain_bounds():
+    for n in [100, 5000, 100000, (1 << 20) + 7]:
+        for world in [1, 2, 3, 8]:
+            g = sharded.chain_bounds(n, world)
+            assert len(g) == world + 1 and g[0] == 0 and g[-1] == n
+            assert all(a <= b for a, b in zip(g, g[1:]))
+            assert all(x <= n - sharded.TAIL_GUARD or x in (0, n) for x in g[1:-1])
+
+
+def _fact_worker(rank, world, port, q, use_gpu, T, wide):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT / "lz77-sss_amd"))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import sharded as SH
+    from test_sharded_sss import _oracle_block
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if use_gpu:
+            blocks = SH.HipBlocks(T, T.size, device=0, pos64=wide)
+            F = SH.factorize_sharded(T, T.size, rank, world, device=0, blocks=blocks)
+            blocks.close()
+        else:
+            blocks = SH.OracleBlocks(T, T.size, pos64=wide)
+            F = SH.factorize_sharded(T, T.size, rank, world, blocks=blocks, sss_compute=_oracle_block)
+        q.put((rank, F))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_fact_ranks(world, use_gpu, T, wide=False):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fact_worker, args=(r, world, port, q, use_gpu, T, wide)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,wide", [(2, False), (3, False), (2, True)])
+def test_gloo_sharded_factorization_oracle_blocks(world, wide):
+    """Collectives (1)-(4) on CPU ranks (gloo) with the oracle as the block compute: sharded
+    sync set + all-gather, replicated phrases, the rank-ordered greedy chain with the carried
+    gap-index table, rank-ordered emission == the one-process p = 1 stream."""
+    import lz77sss
+    import oracle
+
+    T = lz77sss.gen_random_repetitive(60000, 60000, 11)
+    F_ref = oracle.factorize64(T)[0] if wide else oracle.factorize(T)[0].astype(np.uint64)
+    for _, F in _run_fact_ranks(world, False, T, wide):
+        assert np.array_equal(F, F_ref)
+
+
+def test_oracle_greedy_blocks_any_bounds():
+    import lz77sss
+    import oracle
+
+    T = lz77sss.gen_genome(200000, 20000, 0.01, 4)
+    F_ref = oracle.factorize(T)[0].astype(np.uint64)
+    for bounds in [[0, T.size], [0, 5000, T.size], [0, 17000, 23000, 120000, T.size]]:
+        st, tab, parts = (0, 0), None, []
+        for r in range(len(bounds) - 1):
+            F, st, tab = oracle.greedy_block(T, st[0], st[1], bounds[r + 1], tab)
+            parts.append(F)
+        assert np.array_equal(np.concatenate(parts), F_ref), bounds
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,wide", [(2, False), (3, True)])
+def test_sharded_factorization_ranks_on_gpu(lz, orc, world, wide):
+    """The sharded 3-approximation through the C-ABI, ranks sharing the GPU (gloo between them)."""
+    T = lz.gen_genome(3 << 20, 1 << 20, 0.001, 19)
+    F_ref = orc.factorize64(T)[0] if wide else orc.factorize(T)[0].astype(np.uint64)
+    for _, F in _run_fact_ranks(world, True, T, wide):
+        assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bounds_kind", ["two", "many"])
+def test_greedy_blocks_one_session(lz, orc, bounds_kind):
+    """lz77sss_session_greedy_block in sequence on one session == lz77sss_session_factorize."""
+    T = lz.gen_genome(4 << 20, 1 << 20, 0.001, 29)
+    n = T.size
+    bounds = [0, n // 2, n] if bounds_kind == "two" else [0, 100000, 100001, 1 << 20, 3 << 20, n]
+    F_ref = orc.factorize(T)[0]
+    with lz.Session(n) as s:
+        s.load(T)
+        S, runs = s.sss()
+        nb = s.prepare(external_sss=False)
+        state, parts, tab = (0, 0, 0), [], None
+        for b in bounds[1:]:
+            if state[0] >= b and b < n:
+                continue
+            if tab is not None:
+                s.carried_set(tab)
+            z, ex = s.greedy_block(*state, tab is not None, b)
+            parts.append(s.factors(z))
+            tab = s.carried_get(nb)
+            state = ex
+    assert np.array_equal(np.concatenate(parts), F_ref)
