@@ -121,6 +121,10 @@ def main():
     ap.add_argument("--cpu-sample-mib", type=int, default=-1,
                     help="oracle sample size in MiB (default: the full workload text, 2-30 s of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", action="store_true",
+                    help="--mode approx: ONE text split across the ranks (sharded.factorize_sharded_resident: "
+                         "sync set by block + all-gather, replicated phrases, rank-ordered greedy blocks, "
+                         "rank-ordered emission; strong scaling) instead of one independent text per rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,6 +144,10 @@ def main():
 
     if args.mode == "sss":
         return main_sss(args, lz, torch, dist, world, rank, local_rank)
+    if args.shard:
+        if args.mode != "approx" or args.phr_mode != "lpf_opt":
+            raise SystemExit("--shard runs the 3-aprx with lpf_opt (configs[1])")
+        return main_shard(args, lz, torch, dist, world, rank, local_rank)
 
     n = args.size_mib << 20
     T = make_text(lz, args.workload, n, rank)
@@ -220,6 +228,10 @@ def main():
                 "factors": int(z), "comp_ratio": round(n / max(z, 1), 2),
                 "sss_size": int(st[0]) if st else None, "has_runs": bool(st[1]) if st else None,
                 "lpf_phrases": int(st[2]) if st else None,
+                "greedy": None if exact or not st else {
+                    "outer_rounds": int(st[12]), "link_rounds": int(st[13]), "walked": int(st[15]),
+                    "segments": int(st[16]), "completion_used": bool(st[19]),
+                    "completion_start": int(st[20]), "windows": int(st[21])},
                 "phase_ms": {k: round(v, 3) for k, v in phases.items()},
                 "pcie_inclusive_mbps": round(n / (dt + t_load + t_out) / 1e6, 2),
                 "device_decode": {"mismatches": int(mism), "ms": round(dec_ms, 3), "jump_rounds": int(dec_rounds),
@@ -239,6 +251,20 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if not exact and st and phases.get("sss"):
+            # the whole SSS phase (Q anchors + run table + stream + compaction), same algorithmic bytes
+            sb = n + 4 * int(st[0])
+            out["roofline_sss_phase"] = {
+                "phase": "sss (k_q_anchors + run table + k_sss_stream + compaction)", "bound": "hbm",
+                "achieved": round(sb / (phases["sss"] * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(sb / (phases["sss"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes": sb, "ms": round(phases["sss"], 4),
+                "ms_per_gib": round(phases["sss"] * GIB / n, 4)}
+            pipe = sum(v for k, v in phases.items() if k != "decode")
+            out["roofline_pipeline"] = {
+                "bound": "hbm", "note": "text bytes per step over the whole pipeline's phase time",
+                "achieved": round(n / (pipe * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(n / (pipe * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms": round(pipe, 3)}
         if world == 1 and not args.no_cpu_baseline:
             sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else args.size_mib
             if exact:
@@ -246,6 +272,73 @@ def main():
                                                          if args.cpu_sample_mib > 0 else 4)
             else:
                 out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample, PHR[args.phr_mode])
+        print(json.dumps(out), flush=True)
+    sess.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main_shard(args, lz, torch, dist, world, rank, local_rank):
+    """One text (seed 42, the rank-0 text of the default mode) factorized by all ranks
+    together: one step = sharded.factorize_sharded_resident (collectives (1)-(4) of
+    SURVEY.md 8e).  The greedy chain is walked block by block in rank order, so the
+    phases that shard are the sync set and the emission; total work is fixed (strong
+    scaling).  After the timed region rank 0 checks the stream against a one-GPU
+    factorize of the same text in the same session."""
+    import sharded
+
+    n = args.size_mib << 20
+    T = make_text(lz, args.workload, n, 0)
+    sess = lz.Session(n, device=local_rank)
+    sess.load(T)
+    del T
+    tm = {}
+
+    def step():
+        return sharded.factorize_sharded_resident(sess, n, rank, world, local_rank, timings=tm)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    F = None
+    for _ in range(args.steps):
+        F = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    dt, _ = aggregate((t1 - t0) / args.steps, n, world, dist, device="cuda")  # max over ranks
+    phases = {k: round(v * 1e3, 3) for k, v in tm.items()}
+    z = int(F.shape[0])
+    same = None
+    if rank == 0:
+        z1 = sess.factorize(device=local_rank)
+        ref = torch.empty(max(z1, 1) * 2, dtype=torch.int32, device=f"cuda:{local_rank}")
+        if z1:
+            sess.copy_factors(ref.data_ptr(), z1 * 8)
+        same = bool(z1 == z and torch.equal(ref[: 2 * z1].view(-1, 2), F))
+    if rank == 0:
+        out = {
+            "metric": "factorization MB/s (3-aprx LZ77, greedy + lpf_opt, tau=512)",
+            "value": round(n / dt / 1e6, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded restatement of the reference's random_repetitive_string)"
+            if args.workload == "rr" else "synthetic (genome-like: 64 MiB ACGT base block, 0.1% mutations)",
+            "config": {"workload": f"{args.workload} n={n} ({args.size_mib} MiB), ONE text split over {world} rank(s)",
+                       "n": n, "tau": 512, "phr_mode": "lpf_opt", "fact_mode": "greedy",
+                       "parallelism": f"sharded x{world}: S by block + all-gather, replicated phrases, "
+                                      f"rank-ordered greedy blocks, gathered emission",
+                       "factors": z, "equals_one_gpu_stream": same,
+                       "rank0_phase_ms": phases},
+            "roofline": None, "cpu_baseline": None,
+        }
         print(json.dumps(out), flush=True)
     sess.close()
     if dist is not None:

@@ -186,6 +186,13 @@ int lz77sss_session_get_sss64(lz77sss_session* s, uint64_t* out, uint64_t cap); 
 /* Device-to-device copy of the sss_range result into `dst`, a device buffer on the
  * session's device (e.g. a collective's send buffer); cap in elements. */
 int lz77sss_session_copy_sss64_device(lz77sss_session* s, void* dst, uint64_t cap);
+/* Copy of the last factorization (factorize / greedy_block) in the session's own
+ * layout -- lz77sss_factor32 for a 32-bit session, lz77sss_factor64 for a 64-bit
+ * one -- to `dst` (host or device memory; device-to-device for a collective's send
+ * buffer, the emission step of SURVEY.md 8e).  *bytes receives the size; dst NULL
+ * with cap_bytes 0 only queries it.  Replaces reading lz77_sss::factorize's output
+ * vector (lz77_sss.hpp:259-282) on the rank that emits it. */
+int lz77sss_session_copy_factors_device(lz77sss_session* s, void* dst, uint64_t cap_bytes, uint64_t* bytes);
 /* Fills the session text with n bytes of a chr19-style text generated in HBM: a
  * random ACGT block of base_len bytes, repeated, each copy byte mutated to another
  * base with probability mut_rate -- every byte a function of (position, seed), so

@@ -547,6 +547,30 @@ LZ77SSS_API int lz77sss_session_copy_sss64_device(lz77sss_session* s, void* dst,
     });
 }
 
+// device-to-device copy of the last factorization in the session's own layout
+// ({u32 src, u32 len} or {u64 src, u64 len} per factor): the emission step of a
+// sharded run gathers these bytes over RCCL without a host round trip
+LZ77SSS_API int lz77sss_session_copy_factors_device(lz77sss_session* s, void* dst, uint64_t cap_bytes,
+                                                    uint64_t* bytes) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        const uint64_t z = s->E64 ? s->E64->num_fact() : s->E.num_fact;
+        const uint64_t nb = z * (s->E64 ? sizeof(lz77sss_factor64) : sizeof(lz77sss_factor32));
+        if (bytes) *bytes = nb;
+        if (!dst) {
+            if (cap_bytes) throw lz::error(LZ77SSS_EINVAL, "dst is NULL");
+            return;
+        }
+        if (cap_bytes < nb) throw lz::error(LZ77SSS_EINVAL, "output capacity too small");
+        const int dev = s->E64 ? s->E64->device() : s->E.device;
+        hipStream_t st = s->E64 ? s->E64->stream() : s->E.st;
+        const void* src = s->E64 ? (const void*)s->E64->factors() : (const void*)s->E.fact.p;
+        LZ_HIP(hipSetDevice(dev));
+        if (nb) LZ_HIP(hipMemcpyAsync(dst, src, nb, hipMemcpyDefault, st));
+        LZ_HIP(hipStreamSynchronize(st));
+    });
+}
+
 // chr19-style text in HBM: byte p of the text is a function of (p, seed) only
 __device__ __forceinline__ lz::u64 gen_mix(lz::u64 x) {  // splitmix64 finalizer
     x += 0x9E3779B97F4A7C15ull;

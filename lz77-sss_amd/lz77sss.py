@@ -75,6 +75,7 @@ _SYMBOLS = {
                                                  ctypes.POINTER(ctypes.c_int)]),
     "lz77sss_session_get_sss64": (ctypes.c_int, [_P, _P, _U64]),
     "lz77sss_session_copy_sss64_device": (ctypes.c_int, [_P, _P, _U64]),
+    "lz77sss_session_copy_factors_device": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_huffman": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_ssszip_gapped": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_gen_genome": (ctypes.c_int, [_P, _U64, _U64, ctypes.c_double, ctypes.c_uint32, _U64]),
@@ -273,6 +274,18 @@ class Session:
     def copy_sync_set64(self, dst_ptr: int, cap: int):
         """Device-to-device copy of the sss_range result to a device address (same device)."""
         _check(load_library().lz77sss_session_copy_sss64_device(self._h, _P(dst_ptr), cap))
+
+    def factor_bytes(self) -> int:
+        """Size of the last factorization in the session's layout (8 or 16 bytes per factor)."""
+        b = _U64()
+        _check(load_library().lz77sss_session_copy_factors_device(self._h, None, 0, ctypes.byref(b)))
+        return b.value
+
+    def copy_factors(self, dst_ptr: int, cap_bytes: int) -> int:
+        """Copies the last factorization's raw pairs to a device (or host) address; returns the bytes."""
+        b = _U64()
+        _check(load_library().lz77sss_session_copy_factors_device(self._h, _P(dst_ptr), cap_bytes, ctypes.byref(b)))
+        return b.value
 
     def huffman(self) -> np.ndarray:
         """Huffman factor container (bytes) of the last factorization (csrc/huffman.hip)."""

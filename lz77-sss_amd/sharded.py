@@ -278,3 +278,89 @@ def factorize_sharded(text, n: int, rank: int, world: int, device: int | None = 
     if timings is not None:
         timings.update(sss=t1 - t0, prepare=t2 - t1, greedy_chain=t3 - t2, emit=time.perf_counter() - t3)
     return allf
+
+
+def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int, group=None,
+                               timings: dict | None = None, **params):
+    """Collectives (1)-(4) with everything in HBM: `sess` is a 32-bit Session on `device`
+    holding the whole text (every rank loads it; phrases are replicated).  Returns the
+    factors as an int32 (z, 2) torch tensor on `device`, identical on every rank.
+
+    With backend "nccl" the sync-set blocks, the chain state, the carried table and the
+    factor blocks move GPU to GPU (RCCL over xGMI); with "gloo" they go through host
+    memory (several ranks sharing a GPU in the tests).  The session's own stream is
+    synchronized before any buffer changes hands, and torch's current stream before the
+    session reads a received buffer."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    multi = world > 1 and dist.is_initialized()
+    nccl = multi and dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", device)
+    cdev = dev if nccl else torch.device("cpu")
+
+    def ready():  # received device buffers are complete before the session stream reads them
+        torch.cuda.current_stream(dev).synchronize()
+
+    t0 = time.perf_counter()
+    # (1) S n [b_r, e_r) on this rank, all-gathered in rank order
+    b, e = partition(n, world)[rank]
+    cnt, runs = sess.sss_range(b, e) if e > b else (0, False)
+    local = torch.empty(max(cnt, 1), dtype=torch.int64, device=dev)
+    if cnt:
+        sess.copy_sync_set64(local.data_ptr(), cnt)
+    local = local[:cnt]
+    if multi:
+        S = gather_blocks(local.to(cdev), group)
+        flag = torch.tensor([1 if runs else 0], dtype=torch.int64, device=cdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        runs = bool(flag.item())
+        S = S.to(dev)
+    else:
+        S = local
+    ready()
+    sess.set_sss(S.numel(), runs, device_ptr=S.data_ptr())
+    t1 = time.perf_counter()
+    # (2) replicated SA_S / LCP / LPF phrases
+    tab_bytes = sess.prepare(external_sss=True, **params)
+    t2 = time.perf_counter()
+    # (3) the greedy chain in rank order
+    g = chain_bounds(n, world)
+    state, carried = (0, 0, 0), False
+    if rank > 0:
+        hdr = torch.zeros(4, dtype=torch.int64, device=cdev)
+        dist.recv(hdr, rank - 1, group=group)
+        state, carried = (int(hdr[0]), int(hdr[1]), int(hdr[2])), bool(hdr[3])
+        if carried:
+            tab = torch.empty(max(tab_bytes, 1), dtype=torch.uint8, device=cdev)
+            dist.recv(tab, rank - 1, group=group)
+            if nccl:
+                ready()
+            sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
+            del tab
+    z = 0
+    if state[0] < g[rank + 1] or rank == world - 1:
+        z, state = sess.greedy_block(*state, carried, g[rank + 1], **params)
+        carried = True
+    if multi and rank + 1 < world:
+        hdr = torch.tensor([state[0], state[1], state[2], int(carried)], dtype=torch.int64, device=cdev)
+        dist.send(hdr, rank + 1, group=group)
+        if carried:
+            tab = torch.empty(max(tab_bytes, 1), dtype=torch.uint8, device=cdev)
+            sess.carried_get(tab_bytes, device_ptr=tab.data_ptr())
+            dist.send(tab, rank + 1, group=group)
+            del tab
+    t3 = time.perf_counter()
+    # (4) emission: the blocks' factors gathered in rank order
+    fb = sess.factor_bytes() if z else 0
+    F = torch.empty(max(fb // 8, 1), dtype=torch.int64, device=dev)
+    if fb:
+        sess.copy_factors(F.data_ptr(), fb)
+    F = F[: fb // 8]
+    if multi:
+        F = gather_blocks(F.to(cdev), group).to(dev)
+    if timings is not None:
+        timings.update(sss=t1 - t0, prepare=t2 - t1, greedy_chain=t3 - t2, emit=time.perf_counter() - t3)
+    return F.view(torch.int32).view(-1, 2)

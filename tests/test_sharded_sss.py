@@ -324,3 +324,48 @@ def test_greedy_blocks_one_session(lz, orc, bounds_kind):
             tab = s.carried_get(nb)
             state = ex
     assert np.array_equal(np.concatenate(parts), F_ref)
+
+
+def _resident_worker(rank, world, port, q, T):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT / "lz77-sss_amd"))
+    import lz77sss as L
+    import sharded as SH
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        with L.Session(T.size, 0) as s:
+            s.load(T)
+            tm = {}
+            F = SH.factorize_sharded_resident(s, T.size, rank, world, 0, timings=tm)
+            F2 = SH.factorize_sharded_resident(s, T.size, rank, world, 0)  # a second step on the same session
+            q.put((rank, F.cpu().numpy().astype(np.uint64), bool(torch.equal(F, F2)), sorted(tm)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_resident_ranks_on_gpu(lz, orc, world):
+    """factorize_sharded_resident (the bench's --shard step: every buffer stays in HBM, handed
+    over through the process group) == the one-process stream, on every rank, twice."""
+    import torch.multiprocessing as mp
+
+    T = lz.gen_genome(3 << 20, 1 << 20, 0.001, 23)
+    F_ref = orc.factorize(T)[0].astype(np.uint64)
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resident_worker, args=(r, world, port, qq, T)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((qq.get(timeout=300) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, F, same, keys in res:
+        assert same and keys == ["emit", "greedy_chain", "prepare", "sss"]
+        assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
