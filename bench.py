@@ -18,8 +18,10 @@ independent objects, one 1 GiB text per rank (seed 42 + rank); no data-path
 collective, the barrier/max-over-ranks timing only (weak scaling).
 
 Also reported:
-  roofline      the SSS kernel (k_sss_stream), algorithmic bytes n + 4|S| per
-                launch over its HIP-event time on the library's own stream,
+  roofline      the SSS kernel sequence (k_sss_stream pass 1 with the periodicity
+                filter, the exact Q pass on marked tiles, the re-run of stripes that
+                see Q windows), algorithmic bytes n + 4|S| per call over its HIP-event
+                time on the library's own stream,
                 against the 8 TB/s HBM3E peak; ``traffic`` from the committed
                 rocprofv3 PMC summary (profiles/) when one exists for this
                 workload, else null.
@@ -78,18 +80,45 @@ def pmc_traffic(workload: str, n: int):
 PHR = {"lpf_opt": 2, "lpf_lnf_opt": 3}
 
 
-def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2):
+def cpu_model() -> str:
+    """lscpu's model name (read from /proc/cpuinfo, the same field)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2, runs: int = 3):
+    """the oracle timed at p = the host's OpenMP thread count and at
+    p = 1, median of `runs` each; `value` is the p = nproc median."""
+    import statistics
+
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # the CPU port (test/bench infrastructure only)
 
     n = sample_mib << 20
     T = make_text(lz, workload, n, 0)
-    z, sec, _ = oracle.factorize_timed(T, phr_mode=phr_mode)
-    desc = ("full 1 GiB workload text" if n == GIB else f"first {sample_mib} MiB-sized instance of the same generator")
-    return {"value": round(n / sec / 1e6, 2), "unit": "MB/s", "cores": oracle.num_threads(), "kind": "port",
-            "sample": f"{workload}: {desc} (n={n}, z={z}), oracle factorize_approximate<greedy,"
-                      f"{'lpf_opt' if phr_mode == 2 else 'lpf_lnf_opt'}> p=1 "
-                      f"restatement with OpenMP stages, {sec:.2f} s"}
+    p = oracle.num_threads()
+    res = {}
+    for threads in (p, 1):
+        secs, z = [], 0
+        for _ in range(runs):
+            z, sec, _ = oracle.factorize_timed_p(T, threads, phr_mode=phr_mode)
+            secs.append(sec)
+        res[threads] = (statistics.median(secs), z, secs)
+    sec_p, z_p, _ = res[p]
+    sec_1, z_1, _ = res[1]
+    desc = ("full 1 GiB workload text" if n == GIB else f"{sample_mib} MiB instance of the same generator")
+    return {"value": round(n / sec_p / 1e6, 2), "unit": "MB/s", "cores": p, "kind": "port",
+            "cpu_model": cpu_model(), "runs": runs,
+            "p1": {"value": round(n / sec_1 / 1e6, 2), "cores": 1, "median_s": round(sec_1, 3), "factors": z_1},
+            "sample": f"{workload}: {desc} (n={n}), oracle factorize_approximate<greedy,"
+                      f"{'lpf_opt' if phr_mode == 2 else 'lpf_lnf_opt'}> median of {runs}: p={p} threads "
+                      f"{sec_p:.2f} s (z={z_p}; OpenMP SSS/sort stages, LPF in {p} partitions as "
+                      f"lpf_opt.cpp:46-56, sequential greedy), p=1 {sec_1:.2f} s (z={z_1})"}
 
 
 def cpu_baseline_exact(lz, workload: str, sample_mib: int):
@@ -239,7 +268,7 @@ def main():
                 "huffman_container": {"bytes": hbytes, "ms_incl_d2h": round(t_h * 1e3, 3)},
             },
             "roofline": {
-                "kernel": "k_sss_stream",
+                "kernel": "SSS kernels: k_sss_stream pass 1 .. k_sss_stream re-run (DESIGN.md 4.1)",
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,

@@ -30,7 +30,7 @@ void engine::init(int dev, u64 maxn) {
     max_n = maxn;
     LZ_HIP(hipMalloc(&d_text, max_n + TEXT_PAD));
     LZ_HIP(hipMemsetAsync(d_text, 0, max_n + TEXT_PAD, st));
-    LZ_HIP(hipHostMalloc(&h_pin, 64, hipHostMallocDefault));
+    LZ_HIP(hipHostMalloc(&h_pin, 256, hipHostMallocDefault));
     for (auto& e : ev_pin) LZ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     LZ_HIP(hipStreamSynchronize(st));
 }

@@ -2237,6 +2237,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
     stats[16] = nseg_last;
     stats[17] = nseg0_all;
     stats[21] = nwin;
+    stats[22] = stats_sss_tiles;  // anchor tiles the SSS filter marked (exact Q pass)
     return total_fact;
 }
 

@@ -35,23 +35,33 @@ namespace LZ_NS {
 // anchor tb-1+i) and owns tb .. tb+252; the three halo anchors give the owned
 // ones their neighbours' periods.  Text [a(tb-1) - 256, a(tb+254) + 1024) is
 // staged in LDS.
+constexpr int SNB = 64;                       // decision blocks per stripe (k_sss_stream)
+constexpr int SD = SNB * (int)TAU;            // decisions per stripe (32768)
 constexpr int QT_THREADS = 256;
 constexpr int QT_OWN = QT_THREADS - 3;                  // owned anchors per workgroup
 constexpr int QT_LDS = QT_THREADS * (int)QA + 256 + 1024;
 constexpr u32 RUN_HCAP = 640;                           // local run extension: [a-256, a+640)
 constexpr u32 RUN_LCAP = 256;
 
+// tiles: the tiles to compute (tile = 253 owned anchors; nullptr = tile blockIdx.x);
+// sflag/slist/scnt (optional): stripes whose decisions see a Q window of an owned
+// anchor are appended once to slist (the exact re-run of build_sss)
 __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__ T, u64 n, u64 nanch,
                                                           u16* __restrict__ qinfo, u32* __restrict__ any_q,
                                                           u8* __restrict__ run_p, pos_t* __restrict__ run_hi,
-                                                          pos_t* __restrict__ run_lo, u8* __restrict__ run_cap) {
+                                                          pos_t* __restrict__ run_lo, u8* __restrict__ run_cap,
+                                                          const u32* __restrict__ tiles, u32* __restrict__ sflag,
+                                                          u32* __restrict__ slist, u32* __restrict__ scnt,
+                                                          u64 nstripes) {
     // LDS text with one pad word per 128 bytes: the anchors of a wave sit 128 bytes
     // apart, so unpadded their accesses would all hit the same bank
     __shared__ __attribute__((aligned(16))) u32 b32[QT_LDS / 4 + QT_LDS / 128 + 2];
     __shared__ u8 s_p1[QT_THREADS], s_c[QT_THREADS], s_p[QT_THREADS];
-    __shared__ u32 s_anyq;
+    __shared__ u32 s_anyq, s_mark[4];
     const int i = (int)threadIdx.x;
-    const int64_t tb = (int64_t)blockIdx.x * QT_OWN;
+    const int64_t tb = (int64_t)(tiles ? tiles[blockIdx.x] : blockIdx.x) * QT_OWN;
+    // stripes a Q window of this tile can reach: decisions (a - 640, a] of owned anchors a
+    const int64_t w_lo = max<int64_t>(0, (tb * (int64_t)QA - 639) / SD);
     const int64_t base = (tb - 1) * (int64_t)QA - 256;  // LDS offset 0
     {
         // all global loads first (one round trip), then the LDS writes.  Loads are
@@ -83,6 +93,7 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
         }
     }
     if (i == 0) s_anyq = 0;
+    if (i < 4) s_mark[i] = 0;
     __syncthreads();
     // LDS accessors on offsets o = position - base
     auto word = [&](int w) -> u32 { return b32[w + (w >> 5)]; };
@@ -271,6 +282,10 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
                 const int64_t r0 = (int64_t)a - 127;  // rel(j) = j - r0 in [0,127]
                 res = (u16)(((jlo - r0) << 8) | (jhi - r0));
                 s_anyq = 1;
+                if (sflag) {  // decisions [j - 512, j] for j in (a - 128, a]: stripes of (a - 640, a]
+                    const int64_t wa = max<int64_t>(0, ((int64_t)a - 639) / SD), wb = (int64_t)a / SD;
+                    for (int64_t w = wa; w <= wb; w++) s_mark[w - w_lo] = 1;
+                }
             }
             // local extent of the p-periodic run around the window (for run-skipping LCE);
             // inside a chain of same-period anchors the values only need to mark the chain
@@ -305,6 +320,8 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
     // (and none once the flag is visible: on run-heavy text every block has a Q window)
     if (i == 0 && s_anyq && __hip_atomic_load(any_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
         atomicOr(any_q, 1u);
+    if (sflag && i < 4 && s_mark[i] && (u64)(w_lo + i) < nstripes && atomicOr(&sflag[w_lo + i], 1u) == 0u)
+        slist[atomicAdd(scnt, 1u)] = (u32)(w_lo + i);
 }
 
 // run chains: anchor t continues into t+1 (same run) when both have period p
@@ -312,31 +329,47 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
 // hi (exact unless capped), its exact lo its first anchor's local lo.
 // an unknown run start reads as larger than every position (lce_dev.h: "lo > x" skips the jump)
 constexpr u64 RUN_LO_UNKNOWN = sizeof(pos_t) == 4 ? 0xFFFFFFFFull : (1ull << 62);
-__global__ void k_run_elems(const u8* __restrict__ rp, const pos_t* __restrict__ rhi, const pos_t* __restrict__ rlo,
-                            const u8* __restrict__ rcap, u64 na, u64* __restrict__ ehi_rev, u64* __restrict__ elo) {
-    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= na) return;
-    const u32 p = rp[t];
-    const u64 a = t * QA;
-    const bool cont_f = p && t + 1 < na && rp[t + 1] == p && (u64)rhi[t] >= a + QA + QM;
-    const bool cont_b = p && t >= 1 && rp[t - 1] == p && (u64)rlo[t] + QA <= a;
-    u64 vh = 0, vl = RUN_LO_UNKNOWN;
-    if (p) {
-        vh = (!cont_f && (rcap[t] & 1)) ? 0 : rhi[t];
-        vl = (!cont_b && (rcap[t] & 2)) ? RUN_LO_UNKNOWN : rlo[t];
-    }
-    ehi_rev[na - 1 - t] = ((u64)(!cont_f) << 63) | vh;
-    elo[t] = ((u64)(!cont_b) << 63) | vl;
+// element e of the run-chain scans is anchor t(e): e itself, or with a tile list the
+// anchors of the listed (sorted) tiles back to back.  Chains never cross a tile that
+// is not listed (its anchors have period 0), so the scans over the concatenation are
+// exact.  Elements past the last anchor are chain ends with unknown values.
+__device__ __forceinline__ u64 run_elem_anchor(const u32* __restrict__ tiles, u64 e) {
+    return tiles ? (u64)tiles[e / QT_OWN] * QT_OWN + e % QT_OWN : e;
 }
-struct last_marked {
-    __device__ __forceinline__ u64 operator()(const u64& x, const u64& y) const { return (y >> 63) ? y : x; }
-};
-__global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restrict__ slo, u64 na,
-                             pos_t* __restrict__ rhi, pos_t* __restrict__ rlo) {
-    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= na) return;
-    rhi[t] = (pos_t)(shi_rev[na - 1 - t] & ~(1ull << 63));
-    rlo[t] = (pos_t)(slo[t] & ~(1ull << 63));
+// chain keys: kend_rev[m-1-e] = e at a chain end (else ~0), kstart[e] = e + 1 at a
+// chain start (else 0); an inclusive min-scan over kend_rev and a max-scan over kstart
+// give every element its chain's last and first element
+__global__ void k_run_keys(const u8* __restrict__ rp, const pos_t* __restrict__ rhi, const pos_t* __restrict__ rlo,
+                           u64 na, const u32* __restrict__ tiles, u64 m, u32* __restrict__ kend_rev,
+                           u32* __restrict__ kstart) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const u64 t = run_elem_anchor(tiles, e);
+    bool cont_f = false, cont_b = false;
+    if (t < na) {
+        const u32 p = rp[t];
+        const u64 a = t * QA;
+        cont_f = p && t + 1 < na && rp[t + 1] == p && (u64)rhi[t] >= a + QA + QM;
+        cont_b = p && t >= 1 && rp[t - 1] == p && (u64)rlo[t] + QA <= a;
+    }
+    kend_rev[m - 1 - e] = cont_f ? 0xFFFFFFFFu : (u32)e;
+    kstart[e] = cont_b ? 0u : (u32)e + 1;
+}
+// exact run ends / starts: the chain's last anchor's local hi (unknown = 0 when capped) and
+// its first anchor's local lo (unknown when capped).  In place: an end (start) anchor
+// rewrites its own entry by the same rule, so reading it before or after gives one value.
+__global__ void k_run_apply(const u32* __restrict__ send_rev, const u32* __restrict__ sstart, const u8* __restrict__ rp,
+                            const u8* __restrict__ rcap, u64 na, const u32* __restrict__ tiles, u64 m,
+                            pos_t* __restrict__ rhi, pos_t* __restrict__ rlo) {
+    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const u64 t = run_elem_anchor(tiles, e);
+    if (t >= na || !rp[t]) return;
+    const u64 te = run_elem_anchor(tiles, send_rev[m - 1 - e]), ts = run_elem_anchor(tiles, sstart[e] - 1);
+    const pos_t hi = (rcap[te] & 1) ? (pos_t)0 : rhi[te];
+    const pos_t lo = (rcap[ts] & 2) ? (pos_t)RUN_LO_UNKNOWN : rlo[ts];
+    rhi[t] = hi;
+    rlo[t] = lo;
 }
 
 // ---------------------------------------------------------------------------
@@ -356,11 +389,18 @@ __global__ void k_run_finish(const u64* __restrict__ shi_rev, const u64* __restr
 //   output  i in S  <=>  m_i != INF and min(Phi'(i), Phi'(i+512)) == m_i
 //           (m_i <= both, so this is "either equals m_i"; the INF test folds into
 //           a clamp of the cross-lane minimum); decisions come out as 8 wave
-//           masks, emitted in position order by a scalar loop
-constexpr int SNB = 64;                       // decision blocks per stripe
-constexpr int SD = SNB * (int)TAU;            // decisions per stripe (32768)
+//           masks, compacted in position order by a wave scan of per-lane counts
+//
+// Two instantiations:
+//   PASS1  every stripe, Q assumed empty (Phi' = Phi), plus the periodicity filter
+//          of every block (sss_filter); a stripe with a confirmed filter hit stops
+//          computing S (it is re-run) and only filters its remaining blocks
+//   QSKIP  the exact re-run of the stripes listed by build_sss, with the Q
+//          intervals of k_q_anchors; blocks entirely inside Q skip their hashing
+//          and minima
 constexpr int SCAP = 1024;                    // sync positions per stripe before the fallback
 constexpr int SWAVES = 4;                     // independent waves per workgroup
+constexpr int FA_LANES = 22;                  // candidate lanes per filter anchor (4 shifts each)
 
 struct sss_pow32 {
     u32 pwb[8];    // b^e, e < 8
@@ -402,204 +442,401 @@ __device__ __forceinline__ u32 wave_suffix_min(u32 v, u32 lane) {  // inclusive,
     return min(v, lane < 16 ? a0 : lane < 32 ? a1 : lane < 48 ? r3 : INF32);
 }
 
-// QSKIP: the text has Q windows (k_q_anchors found one): blocks entirely inside Q
-// skip their hashing and minima (without Q the plain instantiation runs, whose code
-// is not burdened by the per-block test)
-template <bool QSKIP>
-__global__ __launch_bounds__(64 * SWAVES) void k_sss_stream(const u8* __restrict__ T, u64 n, u64 last_i,
+// Periodicity filter of one 512-block (PASS1), on the bytes the wave already holds
+// (lane L: bytes 8L..8L+7 as B).  Filter anchors A0 = block start and A1 = +256; bit
+// r of the (uniform) result is set when T[A_r .. A_r + 16) recurs at a shift in
+// [84, 171].  No false negatives: a tau-window with a period p <= 170 has the period
+// kp in (85, 170] (a multiple of p) and contains [A, A + 186) for its filter anchor A
+// in [j, j + 256), so T[A..A+16) recurs at A + kp.  Lane l < 22 of half h tests the 4
+// shifts 84 + 4l + k of A_h (its bytes gathered from 2-3 lanes by ds_bpermute); an
+// 8-byte repeat (about one block in 400 on ACGT text) is confirmed on bytes 8..15.
+__device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
+    const u32 lo = (u32)B, hi = (u32)(B >> 32);
+    const u32 li = lane & 31, grp = lane >> 5;
+    const u32 al = grp ? (u32)__builtin_amdgcn_readlane((int)lo, 32) : (u32)__builtin_amdgcn_readlane((int)lo, 0);
+    const u32 ah = grp ? (u32)__builtin_amdgcn_readlane((int)hi, 32) : (u32)__builtin_amdgcn_readlane((int)hi, 0);
+    // x0 = 84 + 4 li (+ 256 grp): the hi word of lane 10 + li/2 (li even) or the lo word of
+    // lane 11 + li/2 (li odd)
+    const bool ev = (li & 1) == 0;
+    const int l0 = (int)((grp << 5) + 10 + (li >> 1) + (li & 1));
+    const u32 s0l = (u32)__shfl((int)lo, l0, 64), s0h = (u32)__shfl((int)hi, l0, 64);
+    const u32 s1l = (u32)__shfl((int)lo, l0 + 1, 64), s1h = (u32)__shfl((int)hi, l0 + 1, 64);
+    const u32 d0 = ev ? s0h : s0l, d1 = ev ? s1l : s0h, d2 = ev ? s1h : s1l;
+    u32 hk = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        hk |= (__builtin_amdgcn_alignbyte(d1, d0, k) == al && __builtin_amdgcn_alignbyte(d2, d1, k) == ah ? 1u : 0u)
+              << k;
+    if (li >= (u32)FA_LANES) hk = 0;
+    if (!__ballot(hk != 0)) return 0;
+    const u32 cl = grp ? (u32)__builtin_amdgcn_readlane((int)lo, 33) : (u32)__builtin_amdgcn_readlane((int)lo, 1);
+    const u32 ch = grp ? (u32)__builtin_amdgcn_readlane((int)hi, 33) : (u32)__builtin_amdgcn_readlane((int)hi, 1);
+    const u32 s2l = (u32)__shfl((int)lo, l0 + 2, 64), s2h = (u32)__shfl((int)hi, l0 + 2, 64);
+    const u32 d3 = ev ? s2l : s1h, d4 = ev ? s2h : s2l;
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        hit |= ((hk >> k) & 1) && __builtin_amdgcn_alignbyte(d3, d2, k) == cl && __builtin_amdgcn_alignbyte(d4, d3, k) == ch;
+    const u64 hm = __ballot(hit);
+    return ((u32)hm ? 1u : 0u) | ((u32)(hm >> 32) ? 2u : 0u);
+}
+
+template <bool QSKIP, bool PASS1>
+__global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restrict__ T, u64 n, u64 last_i,
                                                            const u16* __restrict__ qinfo, u64 nstripes,
                                                            pos_t* __restrict__ s_out, u32* __restrict__ s_cnt,
-                                                           u32* __restrict__ s_flag, u32* __restrict__ any_flag,
-                                                           u32 b, sss_pow32 PW, u32 scap) {
+                                                           u32* __restrict__ s_flag, u32* __restrict__ ovf_ctr,
+                                                           u32 b, sss_pow32 PW, u32 scap, u64* __restrict__ hitw,
+                                                           u16* __restrict__ q_init, u8* __restrict__ rp_init,
+                                                           const u32* __restrict__ list,
+                                                           const u32* __restrict__ list_cnt) {
     const u32 lane = threadIdx.x & 63;
     // the stripe index is wave-uniform: keep it (and every address derived from it) in SGPRs
-    const u64 w = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (w >= nstripes) return;  // whole wave
+    const u64 wi = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    u64 w = wi;
+    if (list) {
+        if (wi >= *list_cnt) return;  // whole wave
+        w = list[wi];
+    } else if (wi >= nstripes) {
+        return;
+    }
     const u64 i0 = w * (u64)SD;
     const u64 jmax = n - TAU;                  // last position with a full window (n >= 2 tau here)
     const u64 ilim = min<u64>(last_i - i0, (u64)SD - 1);  // decisions i0 + u, u <= ilim
-    // per-lane powers: pwl = b^(8 lane), ibl = b^(-8 (lane + 1))
-    u32 pwl = 1, ibl = PW.ib8;
-    {
-        u32 f = PW.b8, g = PW.ib8;
-        for (int d = 0; d < 6; d++) {
-            if (lane & (1u << d)) {
-                pwl *= f;
-                ibl *= g;
-            }
-            f *= f;
-            g *= g;
-        }
-    }
-    const u32 nB = 0u - PW.B;
-    auto load8 = [&](u64 k) -> u64 { return *(const u64*)(T + i0 + k * TAU + 8 * lane); };
-    // Hp(s_k + 8 lane + e), e < 8, into h; carry = Hp(s_k) in, Hp(s_k+1) out (uniform)
-    auto block_prefix = [&](u64 bytes, u32& carry, u32* h) {
-        const u32 lo = (u32)bytes, hi = (u32)(bytes >> 32);
-        u32 c[8], loc[8];
-#pragma unroll
-        for (int e = 0; e < 8; e++) c[e] = ((e < 4 ? lo : hi) >> (8 * (e & 3))) & 255u;
-        loc[0] = 0;
-#pragma unroll
-        for (int e = 1; e < 8; e++) loc[e] = loc[e - 1] * b + c[e - 1];
-        const u32 h8 = loc[7] * b + c[7];
-        const u32 g = h8 * ibl;
-        const u32 G = wave_prefix_add(g);
-        const u32 hl = (carry + (G - g)) * pwl;  // Hp(s_k + 8 lane)
-        h[0] = hl;
-#pragma unroll
-        for (int e = 1; e < 8; e++) h[e] = hl * PW.pwb[e] + loc[e];
-        carry = (carry + (u32)__builtin_amdgcn_readlane((int)G, 63)) * PW.B;
-    };
-    // Phi'(s_k + 8 lane + e) from the prefix hashes of blocks k and k+1 (INF for Q
-    // windows and past the last full window).  q holds the Q intervals of the block's 5 anchors (s_k/128 + 0..4), loaded
-    // by the whole wave as one scalar load: the per-lane test runs only when one
-    // of them is non-empty
-    // block k lies entirely in Q (every window T[j..j+512) is periodic): its Phi' is
-    // INF at all 512 positions.  Uniform test on the anchors' intervals: anchor 0
-    // must cover rel 127 (offset 0), anchors 1-3 all of rel 0..127, anchor 4 rel 0..126
-    auto fullq = [&](uint4 q) -> bool {
-        const u32 a0 = q.x & 0xFFFFu, a4 = q.z & 0xFFFFu;
-        const bool m0 = (a0 >> 8) <= 127u && (a0 & 255u) >= 127u;
-        const bool m1 = (q.x >> 24) == 0u && ((q.x >> 16) & 255u) >= 127u;
-        const bool m2 = (q.y >> 8 & 255u) == 0u && (q.y & 255u) >= 127u;
-        const bool m3 = (q.y >> 24) == 0u && ((q.y >> 16) & 255u) >= 127u;
-        const bool m4 = (a4 >> 8) == 0u && (a4 & 255u) >= 126u;
-        return m0 && m1 && m2 && m3 && m4;
-    };
-    // all-Q test of a block (uniform; one per block, carried from step to step)
-    auto allq = [&](uint4 q) -> bool {
-        if constexpr (!QSKIP) return false;
-        const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
-        return __builtin_amdgcn_readfirstlane((int)anyq) && fullq(q);
-    };
-    auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
-        const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
-#pragma unroll
-        for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
-        const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
-        if (__builtin_amdgcn_readfirstlane((int)(anyq || endblk))) {
-            // anchor r (0..4) of the block covers offsets (128r - 128, 128r]; its Q interval
-            // [lo, hi] (rel = offset + 127 - 128r) is an offset interval, uniform per block:
-            // the lane ORs the part that meets its 8 positions into an INF mask
-            const int o = (int)(8 * lane);
-            const u32 qa[5] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu};
-            u32 bits = 0;
-#pragma unroll
-            for (int r = 0; r < 5; r++) {
-                const int lo = (int)(qa[r] >> 8), hi = min((int)(qa[r] & 255u), 127);
-                if (lo <= hi) {  // uniform
-                    const int l = max(128 * r - 127 + lo - o, 0), h = min(128 * r - 127 + hi - o, 7);
-                    if (l <= h) bits |= ((2u << h) - 1u) & ~((1u << l) - 1u);
-                }
-            }
-            if (endblk) {  // positions past the last full window
-                const u64 j0 = i0 + k * TAU + (u64)o;
-                const u64 keep = jmax >= j0 ? min<u64>(jmax - j0 + 1, 8) : 0;
-                bits |= 0xFFu & ~((1u << keep) - 1u);
-            }
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] |= 0u - ((bits >> e) & 1u);
-        }
-    };
-    auto phi_or_inf = [&](bool full, u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
-        if (full) {
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = INF32;
-        } else {
-            phi_block(k, h0, h1, q, v);
-        }
-    };
-    // Q intervals of the anchors of block k (uniform address: a scalar load)
-    auto loadq = [&](u64 k) -> uint4 { return *(const uint4*)(qinfo + ((i0 + k * TAU) >> 7)); };
-
-    // prologue: Hp for blocks 0 and 1, Phi'(block 0)
-    u32 carry = 0;
-    u64 Ba = load8(2), Bb = load8(3);
-    const uint4 qa = loadq(0);
-    uint4 qb = loadq(1);
-    u32 hA[8], hB[8], xA[8], xB[8];
-    block_prefix(load8(0), carry, hA);
-    block_prefix(load8(1), carry, hB);
-    bool fA = allq(qa), fB = false;
-    bool fq = allq(qb);  // all-Q flag of the block whose Phi' the next step computes
-    bool hvalid = true;  // the prefix hash carry continues the last computed block
-    phi_or_inf(fA, 0, hA, hB, qa, xA);
-    u32 nout = 0;       // outputs of this stripe so far (uniform)
-    pos_t* out = s_out + w * SCAP;
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
-    // one decision block: x = Phi'(block c) (in), y = Phi'(block c+1) (out),
-    // h0 = Hp(block c+1) (in), h1 <- Hp(block c+2); B = bytes of block c+2
-    // Phi(j) = Hp(j+512) - b^512 Hp(j) does not depend on where the prefix hash starts
-    // (the start's contribution cancels): the prefix hash of block k is needed only when
-    // block k-1 or k is not all Q, and restarts from 0 after skipped blocks
-    auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn, bool fx, bool& fy) {
-        const uint4 qc = loadq(c + 2);
-        const bool f1 = fq, f2 = allq(qc);
-        if (!(f1 && f2)) {
-            if (!hvalid) carry = 0;
-            block_prefix(B, carry, h1);
+    // PASS1 filter state: hit bits per filter anchor (block k < 64: bit k of hw[r]; blocks 64, 65
+    // of the last stripe: bits 2(k - 64) + r of hw2), confirmed hit in a decision block
+    u64 hw0 = 0, hw1 = 0, hw2 = 0;
+    bool dirty = false;
+    auto filt = [&](u32 k, u64 Bk) {
+        const u32 f = sss_filter(Bk, lane);
+        // branch-free (a conditional target makes the compiler spill the words to scratch)
+        const u64 lowk = k < 64 ? 1ull << (k & 63) : 0ull;
+        hw0 |= (f & 1) ? lowk : 0ull;
+        hw1 |= (f & 2) ? lowk : 0ull;
+        hw2 |= k >= 64 ? (u64)f << ((2 * k) & 63) : 0ull;  // blocks 64, 65: bits 0..3
+        if (f && k < nblk) dirty = true;
+    };
+    u32 nout = 0;  // outputs of this stripe so far (uniform)
+    {
+        // per-lane powers: pwl = b^(8 lane), ibl = b^(-8 (lane + 1))
+        u32 pwl = 1, ibl = PW.ib8;
+        {
+            u32 f = PW.b8, g = PW.ib8;
+            for (int d = 0; d < 6; d++) {
+                if (lane & (1u << d)) {
+                    pwl *= f;
+                    ibl *= g;
+                }
+                f *= f;
+                g *= g;
+            }
         }
-        hvalid = !(f1 && f2);
-        phi_or_inf(f1, c + 1, h0, h1, qn, y);
-        fy = f1;
-        fq = f2;
-        qn = qc;
-        // both blocks all INF: every window minimum is INF, no decision of block c is in S
-        if (fx && fy) return;
-        // window minima for decisions of block c
-        u32 sx[8], py[8];
-        sx[7] = x[7];
+        const u32 nB = 0u - PW.B;
+        auto load8 = [&](u64 k) -> u64 { return *(const u64*)(T + i0 + k * TAU + 8 * lane); };
+        // Hp(s_k + 8 lane + e), e < 8, into h; carry = Hp(s_k) in, Hp(s_k+1) out (uniform)
+        auto block_prefix = [&](u64 bytes, u32& carry, u32* h) {
+            const u32 lo = (u32)bytes, hi = (u32)(bytes >> 32);
+            u32 c[8], loc[8];
 #pragma unroll
-        for (int e = 6; e >= 0; e--) sx[e] = min(x[e], sx[e + 1]);
-        py[0] = y[0];
+            for (int e = 0; e < 8; e++) c[e] = ((e < 4 ? lo : hi) >> (8 * (e & 3))) & 255u;
+            loc[0] = 0;
 #pragma unroll
-        for (int e = 1; e < 8; e++) py[e] = min(py[e - 1], y[e]);
-        const u32 sufL = wave_suffix_min(sx[0], lane), preL = wave_prefix_min(py[7]);
-        const u32 suf_after = dpp<0x130>(INF32, sufL);   // wave_shl:1 -> lane + 1 (63: inf)
-        const u32 pre_before = dpp<0x138>(INF32, preL);  // wave_shr:1 -> lane - 1 (0: inf)
-        // clamped to INF-1: then min(x, y) == m' <=> (min(x, y) == m and m != INF), as m <= min(x, y)
-        const u32 g = min(min(suf_after, pre_before), INF32 - 1);
-        // decisions: M[e] = wave mask of lanes whose position 8 lane + e is in S
-        u64 M[8];
-        u64 U = 0;
+            for (int e = 1; e < 8; e++) loc[e] = loc[e - 1] * b + c[e - 1];
+            const u32 h8 = loc[7] * b + c[7];
+            const u32 g = h8 * ibl;
+            const u32 G = wave_prefix_add(g);
+            const u32 hl = (carry + (G - g)) * pwl;  // Hp(s_k + 8 lane)
+            h[0] = hl;
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-            M[e] = __ballot(min(x[e], y[e]) == min(min(sx[e], g), py[e]));
-            U |= M[e];
-        }
-        if (U) {
-            // ordered emission (lanes ascending, then e) by a scalar loop over the
-            // few emitting lanes (~2 per block)
-            const pos_t base = (pos_t)(i0 + c * TAU);
-            for (u64 u = U; u; u &= u - 1) {
-                const u32 L = (u32)__builtin_ctzll(u);
+            for (int e = 1; e < 8; e++) h[e] = hl * PW.pwb[e] + loc[e];
+            carry = (carry + (u32)__builtin_amdgcn_readlane((int)G, 63)) * PW.B;
+        };
+        // block k lies entirely in Q (every window T[j..j+512) is periodic): its Phi' is
+        // INF at all 512 positions.  Uniform test on the anchors' intervals: anchor 0
+        // must cover rel 127 (offset 0), anchors 1-3 all of rel 0..127, anchor 4 rel 0..126
+        auto fullq = [&](uint4 q) -> bool {
+            const u32 a0 = q.x & 0xFFFFu, a4 = q.z & 0xFFFFu;
+            const bool m0 = (a0 >> 8) <= 127u && (a0 & 255u) >= 127u;
+            const bool m1 = (q.x >> 24) == 0u && ((q.x >> 16) & 255u) >= 127u;
+            const bool m2 = (q.y >> 8 & 255u) == 0u && (q.y & 255u) >= 127u;
+            const bool m3 = (q.y >> 24) == 0u && ((q.y >> 16) & 255u) >= 127u;
+            const bool m4 = (a4 >> 8) == 0u && (a4 & 255u) >= 126u;
+            return m0 && m1 && m2 && m3 && m4;
+        };
+        // all-Q test of a block (uniform; one per block, carried from step to step)
+        auto allq = [&](uint4 q) -> bool {
+            if constexpr (!QSKIP) return false;
+            const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
+            return __builtin_amdgcn_readfirstlane((int)anyq) && fullq(q);
+        };
+        // Phi'(s_k + 8 lane + e) from the prefix hashes of blocks k and k+1 (INF for Q
+        // windows and past the last full window).  q holds the Q intervals of the block's
+        // 5 anchors (s_k/128 + 0..4), loaded by the whole wave as one scalar load: the
+        // per-lane test runs only when one of them is non-empty
+        auto phi_block = [&](u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
+            const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
 #pragma unroll
-                for (int e = 0; e < 8; e++) {
-                    if ((M[e] >> L) & 1) {
-                        const pos_t pos = base + 8 * L + e;
-                        if ((u64)pos - i0 <= ilim) {
-                            if (lane == 0 && nout < (u32)SCAP) out[nout] = pos;
-                            nout++;
-                        }
+            for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
+            const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
+            if (__builtin_amdgcn_readfirstlane((int)(anyq || endblk))) {
+                // anchor r (0..4) of the block covers offsets (128r - 128, 128r]; its Q interval
+                // [lo, hi] (rel = offset + 127 - 128r) is an offset interval, uniform per block:
+                // the lane ORs the part that meets its 8 positions into an INF mask
+                const int o = (int)(8 * lane);
+                const u32 qa[5] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu};
+                u32 bits = 0;
+#pragma unroll
+                for (int r = 0; r < 5; r++) {
+                    const int lo = (int)(qa[r] >> 8), hi = min((int)(qa[r] & 255u), 127);
+                    if (lo <= hi) {  // uniform
+                        const int l = max(128 * r - 127 + lo - o, 0), h = min(128 * r - 127 + hi - o, 7);
+                        if (l <= h) bits |= ((2u << h) - 1u) & ~((1u << l) - 1u);
                     }
                 }
+                if (endblk) {  // positions past the last full window
+                    const u64 j0 = i0 + k * TAU + (u64)o;
+                    const u64 keep = jmax >= j0 ? min<u64>(jmax - j0 + 1, 8) : 0;
+                    bits |= 0xFFu & ~((1u << keep) - 1u);
+                }
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] |= 0u - ((bits >> e) & 1u);
             }
+        };
+        auto phi_or_inf = [&](bool full, u64 k, const u32* h0, const u32* h1, uint4 q, u32* v) {
+            if (full) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = INF32;
+            } else {
+                phi_block(k, h0, h1, q, v);
+            }
+        };
+        // Q intervals of the anchors of block k (uniform address: a scalar load); PASS1
+        // assumes Q empty
+        auto loadq = [&](u64 k) -> uint4 {
+            if constexpr (PASS1) return make_uint4(0xFF00FF00u, 0xFF00FF00u, 0xFF00FF00u, 0xFF00FF00u);
+            return *(const uint4*)(qinfo + ((i0 + k * TAU) >> 7));
+        };
+
+        // prologue: Hp for blocks 0 and 1, Phi'(block 0)
+        u32 carry = 0;
+        const u64 B0 = load8(0), B1 = load8(1);
+        u64 Ba = load8(2), Bb = load8(3);
+        const uint4 qa = loadq(0);
+        uint4 qb = loadq(1);
+        u32 hA[8], hB[8], xA[8], xB[8];
+        if constexpr (PASS1) {
+            filt(0, B0);
+            filt(1, B1);
         }
-    };
-    for (u32 c = 0; c < nblk; c += 2) {
-        u64 Bn = load8(c + 4);  // prefetch (the text pad covers the stripe's end)
-        step(c, xA, xB, hB, hA, Ba, qb, fA, fB);
-        Ba = Bn;
-        if (c + 1 >= nblk) break;
-        Bn = load8(c + 5);
-        step(c + 1, xB, xA, hA, hB, Bb, qb, fB, fA);
-        Bb = Bn;
+        // a stripe with a hit in its decision blocks is re-run; it stops here and build_sss
+        // marks all of its anchors' tiles for the exact Q pass
+        if (dirty) goto stripe_done;
+        block_prefix(B0, carry, hA);
+        block_prefix(B1, carry, hB);
+        bool fA = allq(qa), fB = false;
+        bool fq = allq(qb);  // all-Q flag of the block whose Phi' the next step computes
+        bool hvalid = true;  // the prefix hash carry continues the last computed block
+        phi_or_inf(fA, 0, hA, hB, qa, xA);
+        pos_t* out = s_out + w * SCAP;
+        // one decision block: x = Phi'(block c) (in), y = Phi'(block c+1) (out),
+        // h0 = Hp(block c+1) (in), h1 <- Hp(block c+2); B = bytes of block c+2
+        // Phi(j) = Hp(j+512) - b^512 Hp(j) does not depend on where the prefix hash starts
+        // (the start's contribution cancels): the prefix hash of block k is needed only when
+        // block k-1 or k is not all Q, and restarts from 0 after skipped blocks
+        auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn, bool fx, bool& fy) {
+            const uint4 qc = loadq(c + 2);
+            const bool f1 = fq, f2 = allq(qc);
+            if (!(f1 && f2)) {
+                if (!hvalid) carry = 0;
+                block_prefix(B, carry, h1);
+            }
+            hvalid = !(f1 && f2);
+            phi_or_inf(f1, c + 1, h0, h1, qn, y);
+            fy = f1;
+            fq = f2;
+            qn = qc;
+            // both blocks all INF: every window minimum is INF, no decision of block c is in S
+            if (fx && fy) return;
+            // window minima for decisions of block c
+            u32 sx[8], py[8];
+            sx[7] = x[7];
+#pragma unroll
+            for (int e = 6; e >= 0; e--) sx[e] = min(x[e], sx[e + 1]);
+            py[0] = y[0];
+#pragma unroll
+            for (int e = 1; e < 8; e++) py[e] = min(py[e - 1], y[e]);
+            const u32 sufL = wave_suffix_min(sx[0], lane), preL = wave_prefix_min(py[7]);
+            const u32 suf_after = dpp<0x130>(INF32, sufL);   // wave_shl:1 -> lane + 1 (63: inf)
+            const u32 pre_before = dpp<0x138>(INF32, preL);  // wave_shr:1 -> lane - 1 (0: inf)
+            // clamped to INF-1: then min(x, y) == m' <=> (min(x, y) == m and m != INF), as m <= min(x, y)
+            const u32 g = min(min(suf_after, pre_before), INF32 - 1);
+            // decisions: M[e] = wave mask of lanes whose position 8 lane + e is in S
+            u64 M[8];
+            u64 U = 0;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                M[e] = __ballot(min(x[e], y[e]) == min(min(sx[e], g), py[e]));
+                U |= M[e];
+            }
+            if (U) {
+                // ordered emission: per-lane bit sets from the masks, a wave scan of their
+                // counts gives each lane its slot (positions ascend with lane, then e)
+                u32 mb = 0;
+#pragma unroll
+                for (int e = 0; e < 8; e++) mb |= __builtin_amdgcn_inverse_ballot_w64(M[e]) ? (1u << e) : 0u;
+                const u64 rem = ilim - (u64)c * TAU;  // decisions of this block: offsets <= rem
+                if (rem < (u64)TAU - 1) {
+                    const int lim = (int)rem - (int)(8 * lane);  // keep e <= lim
+                    mb = lim < 0 ? 0u : lim >= 7 ? mb : (mb & ((2u << lim) - 1u));
+                }
+                const u32 cnt = (u32)__popc(mb);
+                const u32 incl = wave_prefix_add(cnt);
+                u32 o = nout + incl - cnt;
+                const pos_t base = (pos_t)(i0 + c * TAU + 8 * lane);
+                for (u32 m = mb; m; m &= m - 1) {
+                    if (o < (u32)SCAP) out[o] = base + (pos_t)__builtin_ctz(m);
+                    o++;
+                }
+                nout += (u32)__builtin_amdgcn_readlane((int)incl, 63);
+            }
+        };
+        // PASS1 filters block c + 2 at step c (blocks 0 .. nblk + 1 in all: windows of the
+        // stripe's decisions reach two blocks past its end); once a decision block had a hit
+        // the stripe only filters (it is re-run)
+        for (u32 c = 0; c < nblk; c += 2) {
+            u64 Bn = load8(c + 4);  // prefetch (the text pad covers the stripe's end)
+            if constexpr (PASS1) {
+                filt(c + 2, Ba);
+                if (dirty) break;
+            }
+            step(c, xA, xB, hB, hA, Ba, qb, fA, fB);
+            Ba = Bn;
+            if (c + 1 >= nblk) break;
+            Bn = load8(c + 5);
+            if constexpr (PASS1) {
+                filt(c + 3, Bb);
+                if (dirty) break;
+            }
+            step(c + 1, xB, xA, hA, hB, Bb, qb, fB, fA);
+            Bb = Bn;
+        }
+    }
+stripe_done:
+    if constexpr (PASS1) {
+        if (lane == 0) {
+            hitw[3 * w] = hw0;
+            hitw[3 * w + 1] = hw1;
+            hitw[3 * w + 2] = hw2 | (dirty ? 1ull << 63 : 0ull);
+        }
+        // Q intervals and periods of the stripe's own anchors start out empty (k_q_anchors
+        // overwrites the tiles the filter marked)
+        if (lane < nblk) {
+            const u64 t = w * (u64)(SD / QA) + 4 * lane;
+            *(u64*)(q_init + t) = 0xFF00FF00FF00FF00ull;
+            *(u32*)(rp_init + t) = 0u;
+        }
+        if (dirty) nout = 0;  // re-run
     }
     if (lane == 0) {
+        const u32 fl = nout > scap ? 1u : 0u;
+        const u32 old = PASS1 ? 0u : s_flag[w];
         s_cnt[w] = nout;
-        s_flag[w] = nout > scap;
-        if (nout > scap) atomicOr(any_flag, 1u);
+        s_flag[w] = fl;
+        if (fl != old) atomicAdd(ovf_ctr, fl ? 1u : 0xFFFFFFFFu);
+    }
+}
+
+// Per stripe: the re-run list starts with the stripes whose own blocks had a confirmed
+// filter hit; per tile of 253 anchors: marked when a filter anchor A with A/128 in
+// [first anchor, last anchor + 1] was hit (a window in Q with exact anchor a has its
+// filter anchor in [a, a + 255]); the anchors past the last stripe's own ones (tail)
+// start out empty.
+__global__ void k_sss_marks(const u64* __restrict__ hitw, u64 nstripes, u64 ntiles, u64 tpad, u64 nanch,
+                            u8* __restrict__ tflag, u32* __restrict__ sflag, u32* __restrict__ slist,
+                            u32* __restrict__ scnt, u64 t_tail, u64 q_end, u16* __restrict__ qinfo,
+                            u8* __restrict__ run_p) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nstripes) {
+        const bool forced = (hitw[3 * i + 2] >> 63) != 0;
+        sflag[i] = forced ? 1u : 0u;
+        if (forced) slist[atomicAdd(scnt, 1u)] = (u32)i;
+    }
+    if (i < ntiles) {
+        // filter anchor f (position 256 f) of stripe f >> 7, block (f & 127) >> 1, half f & 1
+        const u64 flo = (QT_OWN * i + 1) / 2, fhi = (QT_OWN * i + QT_OWN) / 2;
+        bool d = false;
+        for (u64 w = flo >> 7; w <= (fhi >> 7) && !d; w++) {
+            const u64 ra = max<u64>(flo, w << 7) - (w << 7), rb = min<u64>(fhi, (w << 7) + 127) - (w << 7);
+            if (w < nstripes) {
+                // bits k with 2k + r in [ra, rb]
+                auto mask = [](u64 lo, u64 hi) -> u64 {  // bits lo..hi (empty if lo > hi)
+                    if (lo > hi) return 0;
+                    return (hi >= 63 ? ~0ull : ((2ull << hi) - 1)) & ~((1ull << lo) - 1);
+                };
+                const u64 m0 = mask((ra + 1) / 2, rb / 2);
+                const u64 m1 = rb >= 1 ? mask(ra / 2, (rb - 1) / 2) : 0;
+                d = ((hitw[3 * w] & m0) | (hitw[3 * w + 1] & m1)) != 0;
+            } else if (w == nstripes && nstripes) {
+                // blocks 64, 65 of the last stripe: bits f - 128 w of its third word
+                const u64 hi = min<u64>(rb, 3);
+                if (ra <= hi) {
+                    const u64 m = ((2ull << hi) - 1) & ~((1ull << ra) - 1);
+                    d = (hitw[3 * (nstripes - 1) + 2] & m) != 0;
+                }
+            }
+        }
+        // a forced stripe w stopped filtering at its first hit: every anchor whose Q windows
+        // its blocks 0..65 could hold, [256 w - 1, 256 w + 262) (to the end for the last)
+        const u64 t0 = QT_OWN * i, t1 = t0 + QT_OWN;
+        const u64 apw = SD / QA;
+        for (u64 w = t0 >= apw + 262 ? (t0 - 262) / apw : 0; !d && w < nstripes && w * apw <= t1; w++) {
+            if (!(hitw[3 * w + 2] >> 63)) continue;
+            const u64 lo = w ? w * apw - 1 : 0, hi = w + 1 == nstripes ? ~0ull : w * apw + apw + 6;
+            d = lo < t1 && t0 < hi;
+        }
+        tflag[i] = d ? 1 : 0;
+    } else if (i < tpad) {
+        tflag[i] = 0;
+    }
+    if (t_tail + i < q_end) {
+        qinfo[t_tail + i] = 0xFF00;
+        if (t_tail + i < nanch) run_p[t_tail + i] = 0;
+    }
+}
+
+// one workgroup: the sorted list of set flags (tiles to compute).  flag is padded with
+// zeros to a multiple of 16 * 1024 bytes; each thread owns a run of 16-byte words.
+__global__ __launch_bounds__(1024) void k_flag_list(const u8* __restrict__ flag, u64 m, u32* __restrict__ list,
+                                                    u32* __restrict__ cnt) {
+    __shared__ u32 s_w[16];
+    const u32 t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const u64 nw = (m + 16 * 1024 - 1) / (16 * 1024);  // 16-byte words per thread
+    const uint4* F = (const uint4*)flag + t * nw;
+    u32 c = 0;
+    for (u64 k = 0; k < nw; k++) {
+        const uint4 v = F[k];
+        c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // flags are 0/1 bytes
+    }
+    const u32 incl = wave_prefix_add(c);
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    if (t == 0) {
+        u32 tot = 0;
+        for (int k = 0; k < 16; k++) {
+            const u32 v = s_w[k];
+            s_w[k] = tot;
+            tot += v;
+        }
+        *cnt = tot;
+    }
+    __syncthreads();
+    u32 o = s_w[wv] + incl - c;
+    for (u64 k = 0; k < nw; k++) {
+        const uint4 v = F[k];
+        const u32 wd[4] = {v.x, v.y, v.z, v.w};
+        for (int q = 0; q < 4; q++)
+            for (u32 b = wd[q]; b; b &= b - 1) list[o++] = (u32)((t * nw + k) * 16 + 4 * q + (__builtin_ctz(b) >> 3));
     }
 }
 
@@ -713,89 +950,158 @@ static u32 pow32_host(u32 b, u64 e) {
     return r;
 }
 
-// Q anchors and the periodic-run table (the part of the SSS pass the LCE needs too);
-// returns whether some window is in Q
+// run chains of the anchors (all, or the anchors of a sorted tile list): exact run
+// ends/starts along chains by two last-marked scans
+void engine::run_chains(u64 nanch, const u32* tiles, u64 m) {
+    if (!m) {
+        runs_valid = true;
+        return;
+    }
+    if (m >= (1ull << 32) - 1) throw error(LZ77SSS_EINVAL, "too many anchors for the run-chain scans");
+    u32* ka = (u32*)run_scan_a.get(m);  // 2 x m u32
+    u32* kb = (u32*)run_scan_b.get(m);
+    k_run_keys<<<cdiv(m, 256), 256, 0, st>>>(run_p.p, run_hi.p, run_lo.p, nanch, tiles, m, ka, ka + m);
+    size_t tb = 0;
+    LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, ka, kb, hipcub::Min(), (int)m, st));
+    size_t tb2 = 0;
+    LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, ka + m, kb + m, hipcub::Max(), (int)m, st));
+    u8* t = scan_tmp.get(std::max(tb, tb2));
+    LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ka, kb, hipcub::Min(), (int)m, st));
+    LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb2, ka + m, kb + m, hipcub::Max(), (int)m, st));
+    k_run_apply<<<cdiv(m, 256), 256, 0, st>>>(kb, kb + m, run_p.p, tmp_bytes.p, nanch, tiles, m, run_hi.p, run_lo.p);
+    LZ_HIP(hipGetLastError());
+    runs_valid = true;
+}
+
+// Q anchors and the periodic-run table of every anchor (an externally built sync set
+// needs them for the LCE); returns whether some window is in Q
 bool engine::build_q_runs(const u8* T) {
     runs_valid = false;
     if (n < 2 * (u64)TAU) return false;
     const u64 nanch = (n - TAU) / QA + 2;
-    u16* qi = q_info.get(nanch + 64);  // k_sss_stream reads 8 anchors per block, up to 2 blocks past n
+    u16* qi = q_info.get(nanch + 64);
     u32* ctr = counters.get(16);
     LZ_HIP(hipMemsetAsync(ctr, 0, 16 * sizeof(u32), st));
     u8* rp = run_p.get(nanch);
     pos_t* rhi = run_hi.get(nanch);
     pos_t* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
-    k_q_anchors<<<cdiv(nanch, QT_OWN), QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap);
+    k_q_anchors<<<cdiv(nanch, QT_OWN), QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap, nullptr,
+                                                           nullptr, nullptr, nullptr, 0);
     LZ_HIP(hipGetLastError());
-    {
-        u64* ea = run_scan_a.get(2 * nanch);
-        u64* eb = run_scan_b.get(2 * nanch);
-        k_run_elems<<<cdiv(nanch, 256), 256, 0, st>>>(rp, rhi, rlo, rcap, nanch, ea, ea + nanch);
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, ea, eb, last_marked{}, (int)nanch, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ea, eb, last_marked{}, (int)nanch, st));
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ea + nanch, eb + nanch, last_marked{}, (int)nanch, st));
-        k_run_finish<<<cdiv(nanch, 256), 256, 0, st>>>(eb, eb + nanch, nanch, rhi, rlo);
-        LZ_HIP(hipGetLastError());
-        runs_valid = true;
-    }
-
+    run_chains(nanch, nullptr, nanch);
     return rd1(ctr, st) != 0;
 }
 
+// The sync set:
+//   1. k_sss_stream<PASS1> over every stripe with Q assumed empty + the periodicity filter
+//   2. k_sss_marks / k_flag_list: the tiles of anchors the filter hit (sorted), the stripes
+//      forced into the re-run; one host read of the tile count
+//   3. k_q_anchors on those tiles only (exact Q intervals + run table there; it appends the
+//      stripes whose decisions see a Q window), run chains over them
+//   4. k_sss_stream<QSKIP> re-runs the listed stripes exactly
+//   5. per-stripe counts -> offsets (one host read: |S|, overflow, any Q), fallback for
+//      overflowing stripes (rare), compaction
 void engine::build_sss(const u8* T) {
     s = 0;
     has_runs = false;
     sss_kernel_ms = 0;
     sss_kernel_bytes = 0;
-    const bool any_q = build_q_runs(T);  // picks the stream kernel's instantiation
+    runs_valid = false;
+    stats_fallback_lanes = 0;
+    stats_sss_tiles = 0;
     if (n < 2 * (u64)TAU) return;
     const u64 last_i = n - 2 * TAU;
     const u64 nanch = (n - TAU) / QA + 2;
-    const u16* qi = q_info.p;
-    u32* ctr = counters.p;
     const u64 nlanes = last_i / SD + 1;  // stripes
+    const u64 ntiles = cdiv(nanch, QT_OWN);
+    u16* qi = q_info.get(nanch + 64);  // k_sss_stream reads 8 anchors per block, up to 2 blocks past n
+    u8* rp = run_p.get(nanch);
+    pos_t* rhi = run_hi.get(nanch);
+    pos_t* rlo = run_lo.get(nanch);
+    u8* rcap = tmp_bytes.get(nanch);
+    u32* ctr = counters.get(16);
+    LZ_HIP(hipMemsetAsync(ctr, 0, 8 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes
     pos_t* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
+    u64* hw = sss_hitw.get(3 * nlanes);
+    const u64 tpad = (ntiles + 16 * 1024 - 1) / (16 * 1024) * (16 * 1024);  // k_flag_list reads 16-byte words
+    u8* tfl = sss_tflag.get(tpad);
+    u32* tl = sss_tiles.get(ntiles);
+    u32* sfl = sss_sflag.get(nlanes);
+    u32* sl = sss_slist.get(nlanes);
     sss_pow32 PW;
     for (int e = 0; e < 8; e++) PW.pwb[e] = pow32_host(SSS_BASE, e);
     PW.b8 = pow32_host(SSS_BASE, 8);
     PW.ib8 = pow32_host(PW.b8, (1ull << 31) - 1);  // b8^(2^31 - 1) = b8^-1 (odd units mod 2^32 have order | 2^30)
     PW.B = pow32_host(SSS_BASE, TAU);
     const u32 bpow = PW.B;
+    // test knob: a lower overflow threshold sends more stripes down the exact fallback
+    const char* scap_env = std::getenv("LZ77SSS_TEST_SCAP");
+    const u32 scap = scap_env ? (u32)std::min<long>(SCAP, std::max<long>(0, std::atol(scap_env))) : (u32)SCAP;
     hipEvent_t e0, e1;
     LZ_HIP(hipEventCreate(&e0));
     LZ_HIP(hipEventCreate(&e1));
     LZ_HIP(hipEventRecord(e0, st));
-    // test knob: a lower overflow threshold sends more stripes down the exact fallback
-    const char* scap_env = std::getenv("LZ77SSS_TEST_SCAP");
-    const u32 scap = scap_env ? (u32)std::min<long>(SCAP, std::max<long>(0, std::atol(scap_env))) : (u32)SCAP;
-    if (any_q)
-        k_sss_stream<true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
-                                                                       (u32)SSS_BASE, PW, scap);
-    else
-        k_sss_stream<false><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1,
-                                                                        (u32)SSS_BASE, PW, scap);
+    k_sss_stream<false, true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(
+        T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, hw, qi, rp, nullptr, nullptr);
     LZ_HIP(hipGetLastError());
+    // tiles the filter marked; anchors past the last stripe's own start out empty
+    const u64 nblk_last = std::min<u64>(SNB, (last_i - (nlanes - 1) * SD) / TAU + 1);
+    const u64 t_tail = (nlanes - 1) * (SD / QA) + 4 * nblk_last, q_end = nanch + 64;
+    const u64 nthr = std::max<u64>(std::max<u64>(nlanes, tpad), q_end - t_tail);
+    k_sss_marks<<<cdiv(nthr, 256), 256, 0, st>>>(hw, nlanes, ntiles, tpad, nanch, tfl, sfl, sl, ctr + 3, t_tail, q_end,
+                                                qi, rp);
+    k_flag_list<<<1, 1024, 0, st>>>(tfl, ntiles, tl, ctr + 2);
+    LZ_HIP(hipGetLastError());
+    u32* hp = h_pin + 32;
+    LZ_HIP(hipMemcpyAsync(hp, ctr + 2, sizeof(u32), hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    const u32 ndirty = hp[0];
+    stats_sss_tiles = ndirty;
+    if (ndirty) {
+        k_q_anchors<<<ndirty, QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap, tl, sfl, sl, ctr + 3,
+                                                   nlanes);
+        LZ_HIP(hipGetLastError());
+        run_chains(nanch, tl, (u64)ndirty * QT_OWN);
+        // a marked tile spans at most 3 stripes' decision ranges (its anchors' Q windows reach
+        // 639 decisions back); the forced stripes each meet a marked tile
+        const u64 maxw = std::min<u64>(nlanes, 4ull * ndirty + 4);
+        k_sss_stream<true, false><<<cdiv(maxw, SWAVES), 64 * SWAVES, 0, st>>>(
+            T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, nullptr, nullptr, nullptr, sl,
+            ctr + 3);
+        LZ_HIP(hipGetLastError());
+    }
+    runs_valid = true;  // period 0 outside the marked tiles
+    // sss_kernel_ms: pass 1 through the re-run (the phase's kernels and its one host read)
     LZ_HIP(hipEventRecord(e1, st));
 
-    u32 h_ctr[2];
-    LZ_HIP(hipMemcpyAsync(h_ctr, ctr, 2 * sizeof(u32), hipMemcpyDeviceToHost, st));
+    // exclusive scan of stripe counts -> offsets; total = |S|
+    u32* off = u32a.get(nlanes + 1);
+    auto scan_counts = [&]() {
+        size_t tb = 0;
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lc, off, (int)(nlanes + 1), st));
+        u8* tmp = scan_tmp.get(tb);
+        LZ_HIP(hipMemsetAsync(lc + nlanes, 0, sizeof(u32), st));
+        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, lc, off, (int)(nlanes + 1), st));
+    };
+    scan_counts();
+    LZ_HIP(hipMemcpyAsync(hp, ctr, 2 * sizeof(u32), hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipMemcpyAsync(hp + 2, off + nlanes, sizeof(u32), hipMemcpyDeviceToHost, st));
     LZ_HIP(hipStreamSynchronize(st));
+    has_runs = hp[0] != 0;
+    u32 total = hp[2];
     float ms = 0;
     LZ_HIP(hipEventElapsedTime(&ms, e0, e1));
     sss_kernel_ms = ms;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    has_runs = h_ctr[0] != 0;
 
-    // overflowing tiles -> exact slow path
+    // overflowing stripes -> exact workgroup-parallel path
     u32* ovf_slot = u32c.get(nlanes);
-    pos_t* ovf_out = nullptr;
-    if (h_ctr[1]) {
+    pos_t* ovf_out = lo;  // unused unless some stripe overflowed
+    if (hp[1]) {
         std::vector<u32> hf(nlanes);
         LZ_HIP(hipMemcpy(hf.data(), lf, nlanes * sizeof(u32), hipMemcpyDeviceToHost));
         std::vector<u32> lanes, slot(nlanes, 0);
@@ -810,19 +1116,10 @@ void engine::build_sss(const u8* T) {
                                                                 (u32)SSS_BASE, bpow);
         LZ_HIP(hipGetLastError());
         stats_fallback_lanes = lanes.size();
-    } else {
-        ovf_out = lo;  // unused
-        stats_fallback_lanes = 0;
+        scan_counts();
+        total = rd1(off + nlanes, st);
     }
-
-    // exclusive scan of lane counts -> offsets; total = |S|
-    u32* off = u32a.get(nlanes + 1);
-    size_t tb = 0;
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lc, off, (int)(nlanes + 1), st));
-    u8* tmp = tmp_bytes.get(std::max<size_t>(tb, tmp_bytes.cap));
-    LZ_HIP(hipMemsetAsync(lc + nlanes, 0, sizeof(u32), st));
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, lc, off, (int)(nlanes + 1), st));
-    s = rd1(off + nlanes, st);
+    s = total;
     sss_kernel_bytes = n + sizeof(pos_t) * (u64)s;
     pos_t* dS = S.get((u64)s + 1);
     k_sss_compact<<<cdiv(nlanes, 256), 256, 0, st>>>(lo, lc, off, lf, ovf_slot, ovf_out, nlanes, dS);

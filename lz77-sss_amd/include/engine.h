@@ -72,6 +72,11 @@ struct engine {
     u64 s64 = 0;
     bool has_runs64 = false;
     u64 stats_sss_windows = 0;
+    // filter pass of build_sss: hit words per stripe, marked tiles, re-run stripes
+    dbuf<u64> sss_hitw;
+    dbuf<u8> sss_tflag;
+    dbuf<u32> sss_tiles, sss_sflag, sss_slist;
+    u64 stats_sss_tiles = 0;
     run_tab runs() const {
         run_tab R;
         if (runs_valid) { R.p = run_p.p; R.hi = run_hi.p; R.lo = run_lo.p; }
@@ -159,7 +164,7 @@ struct engine {
 
     phase_timer timer;
 
-    // pinned read-back slots + events: a host decision overlaps the next launches
+    // pinned read-back slots (64 x u32; sa_s uses the first, build_sss 32..) + events
     u32* h_pin = nullptr;
     hipEvent_t ev_pin[2] = {nullptr, nullptr};
 
@@ -170,6 +175,7 @@ struct engine {
     // pipeline phases (each enqueues on `st`)
     void build_sss(const u8* T);
     bool build_q_runs(const u8* T);     // Q anchors + periodic-run table only
+    void run_chains(u64 nanch, const u32* tiles, u64 m);  // exact run ends along anchor chains
     void set_sss(const pos_t* S_any, u64 count, bool runs);  // an externally built (sharded) sync set
     void build_sss_range(u64 first, u64 end, u64 base, u64 window);  // csrc/sss.hip
     void build_sa_s(const u8* T);

@@ -34,7 +34,8 @@ __device__ inline u64 dev_lce_fwd(const u8* T, const run_tab& R, u64 i, u64 j, u
         const u64 step = min<u64>(lim - k, 512);
         const u64 c = dev_naive_lce(T, i + k, j + k, step);
         k += c;
-        if (c < step || k >= lim || !R.p || k < 512) return min(k, lim);
+        if (c < step || k >= lim) return min(k, lim);
+        if (!R.p || k < 512) continue;  // no run table: plain comparison of the next 512 bytes
         const u64 x = i + k, y = j + k;  // T[x-512..x) == T[y-512..y)
         const u64 ax = (x - 340) >> 7, by = (y - 340) >> 7;
         const u32 pp = R.p[ax];
@@ -69,7 +70,8 @@ __device__ inline u64 wave_lce_fwd(const u8* T, const run_tab& R, u64 i, u64 j, 
             return fo + (__builtin_ctzll(x ^ y) >> 3);
         }
         k += step;
-        if (k >= lim || !R.p || k < 512) return min(k, lim);
+        if (k >= lim) return min(k, lim);
+        if (!R.p || k < 512) continue;
         const u64 xi = i + k, yj = j + k;
         const u64 ax = (xi - 340) >> 7, by = (yj - 340) >> 7;
         const u32 pp = R.p[ax];
@@ -100,7 +102,8 @@ __device__ inline u64 dev_lce_bwd(const u8* T, const run_tab& R, u64 i, u64 j, u
         const u64 step = min<u64>(lim - k, 512);
         const u64 c = dev_naive_lce_left(T, i - k, j - k, step);
         k += c;
-        if (c < step || k >= lim || !R.p || k < 512) return min(k, lim);
+        if (c < step || k >= lim) return min(k, lim);
+        if (!R.p || k < 512) continue;  // no run table: plain comparison of the next 512 bytes
         const u64 x = i - k + 1, y = j - k + 1;  // T[x..x+512) == T[y..y+512)
         const u64 ax = (x + 127) >> 7, by = (y + 127) >> 7;
         const u32 pp = R.p[ax];

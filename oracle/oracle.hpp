@@ -381,16 +381,17 @@ static inline void build_pgv_ngv(const lce_structure<P>& L, std::vector<u32>& PG
 // ===========================================================================
 //  build_LPF_opt for p = 1: restates lpf_opt.cpp:33-157
 // ===========================================================================
+// One partition [b, e) of build_LPF_opt (lpf_opt.cpp:46-146): the sync positions in
+// [b, e), max_end starting at b.  p = 1 is the single partition [0, n).
 template <class P>
-static inline std::vector<lpf_t<P>> build_lpf_opt(const u8* T, u64 n, const lce_structure<P>& L) {
+static inline void lpf_opt_part(const u8* T, const lce_structure<P>& L, const std::vector<u32>& PSV,
+                                const std::vector<u32>& NSV, P b, P e, std::vector<lpf_t<P>>& out) {
     using lpf = lpf_t<P>;
-    std::vector<u32> PSV, NSV;
-    build_psv_nsv(L, PSV, NSV);
-    std::vector<lpf> out;
     const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
     const u32 s = L.s();
-    P max_end = 0;
-    const u32 i_min = 0, i_max = s;  // p = 1: b = 0, e = n (lpf_opt.cpp:50-56)
+    P max_end = b;
+    const u32 i_min = (u32)(std::lower_bound(S.begin(), S.end(), b) - S.begin());  // lpf_opt.cpp:50-53
+    const u32 i_max = (u32)(std::lower_bound(S.begin(), S.end(), e) - S.begin());
     for (u32 i = i_min; i < i_max; i++) {
         while (i + 1 < i_max && S[i + 1] <= max_end) i++;
         P lst_end = max_end;
@@ -425,7 +426,31 @@ static inline std::vector<lpf_t<P>> build_lpf_opt(const u8* T, u64 n, const lce_
             if (phr.end - phr.beg > 1) out.push_back(phr);  // quirk: push only in NSV branch (lpf_opt.cpp:138-140)
         }
     }
-    (void)n;
+}
+template <class P>
+static inline std::vector<lpf_t<P>> build_lpf_opt(const u8* T, u64 n, const lce_structure<P>& L) {
+    std::vector<u32> PSV, NSV;
+    build_psv_nsv(L, PSV, NSV);
+    std::vector<lpf_t<P>> out;
+    lpf_opt_part<P>(T, L, PSV, NSV, 0, (P)n, out);  // p = 1: b = 0, e = n (lpf_opt.cpp:50-56)
+    return out;
+}
+// build_LPF_opt at p threads (lpf_opt.cpp:46-56: thread i_p takes [i_p n/p, (i_p+1) n/p),
+// the last one up to n; the per-thread lists are concatenated in thread order).  The
+// phrases differ from p = 1 at partition boundaries: the CPU baseline's p = nproc leg
+// times this, parity is always against p = 1.
+template <class P>
+static inline std::vector<lpf_t<P>> build_lpf_opt_par(const u8* T, u64 n, const lce_structure<P>& L, int p) {
+    std::vector<u32> PSV, NSV;
+    build_psv_nsv(L, PSV, NSV);
+    std::vector<std::vector<lpf_t<P>>> parts(p);
+#pragma omp parallel for num_threads(p) schedule(static, 1)
+    for (int i = 0; i < p; i++) {
+        const P b = (P)((u64)i * (n / p)), e = i == p - 1 ? (P)n : (P)((u64)(i + 1) * (n / p));
+        lpf_opt_part<P>(T, L, PSV, NSV, b, e, parts[i]);
+    }
+    std::vector<lpf_t<P>> out;
+    for (auto& v : parts) out.insert(out.end(), v.begin(), v.end());
     return out;
 }
 
@@ -721,7 +746,7 @@ struct approx_stats {
 
 template <class Q = u32, typename OUT>
 static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, OUT&& output,
-                                         approx_stats* st = nullptr, int fact_mode = 1) {
+                                         approx_stats* st = nullptr, int fact_mode = 1, int lpf_parts = 1) {
     using lpf = lpf_t<Q>;
     using factor = factor_t<Q>;
     if (n == 0) return;
@@ -729,7 +754,7 @@ static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, 
     lce_structure<Q> L;
     if (phr_mode == lpf_opt) {
         L.build(T, n);
-        P = build_lpf_opt(T, n, L);
+        P = lpf_parts > 1 ? build_lpf_opt_par(T, n, L, lpf_parts) : build_lpf_opt(T, n, L);
     } else if (phr_mode == lpf_naive) {
         L.build(T, n);
         P = build_lpf_naive(T, n, L);

@@ -42,6 +42,9 @@ def lib():
         L.oracle_factorize_timed.restype = ctypes.c_int64
         L.oracle_factorize_timed.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(_U64)]
+        L.oracle_factorize_timed_p.restype = ctypes.c_int64
+        L.oracle_factorize_timed_p.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
         L.oracle_sss.restype = ctypes.c_int64
         L.oracle_sss.argtypes = [_P, _U64, _P, _U64, ctypes.POINTER(ctypes.c_int)]
         L.oracle_q_bruteforce.restype = None
@@ -179,6 +182,18 @@ def factorize_timed(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):
     n = _u8(T).size
     sec, h = ctypes.c_double(), _U64()
     z = lib().oracle_factorize_timed(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, ctypes.byref(sec), ctypes.byref(h))
+    return int(z), sec.value, h.value
+
+
+def factorize_timed_p(T, threads: int, phr_mode: int = LPF_OPT, rk_seed: int = 42):
+    """CPU baseline at `threads` threads (every OpenMP stage; LPF in per-thread partitions as
+    lpf_opt.cpp:46-56 when threads > 1) -> (z, seconds, hash).  Timing only: at threads > 1
+    the phrases (and so the stream) may differ from the p = 1 parity stream."""
+    buf = _padded(T)
+    n = _u8(T).size
+    sec, h = ctypes.c_double(), _U64()
+    z = lib().oracle_factorize_timed_p(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, threads, ctypes.byref(sec),
+                                       ctypes.byref(h))
     return int(z), sec.value, h.value
 
 

@@ -167,6 +167,29 @@ int64_t oracle_factorize_timed(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk
     return (int64_t)k;
 }
 
+// The CPU baseline at p threads: every OpenMP stage of the
+// restatement on p threads, and for p > 1 the LPF phrases in p partitions
+// (lpf_opt.cpp:46-56).  The greedy emitter stays sequential: the reference's parallel
+// gap index (lz77_sss.hpp:470-474, run-free texts only) is not restated.  Timing only.
+int64_t oracle_factorize_timed_p(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed, int p,
+                                 double* seconds, uint64_t* stream_hash) {
+    const int prev = omp_get_max_threads();
+    omp_set_num_threads(std::max(1, p));
+    uint64_t k = 0, h = 1469598103934665603ull;
+    auto t0 = std::chrono::steady_clock::now();
+    factorize_approximate(T, (u32)n, phr_mode, rk_seed, [&](factor f) {
+        k++;
+        uint32_t w[2] = {f.src, f.len};
+        const uint8_t* q = (const uint8_t*)w;
+        for (int i = 0; i < 8; i++) { h ^= q[i]; h *= 1099511628211ull; }
+    }, nullptr, 1, std::max(1, p));
+    auto t1 = std::chrono::steady_clock::now();
+    omp_set_num_threads(prev);
+    if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+    if (stream_hash) *stream_hash = h;
+    return (int64_t)k;
+}
+
 // SSS only.  Returns |S| (or -1 if cap too small); *has_runs set.
 int64_t oracle_sss(const uint8_t* T, uint64_t n, uint32_t* out, uint64_t cap, int* has_runs) {
     bool hr = false;
