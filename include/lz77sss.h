@@ -114,10 +114,11 @@ int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_
  * reference's exact modes produce at p = 1; the sources follow a fixed rule
  * (the longer of the PSV/NSV candidates in suffix-array order, the earlier one
  * on ties) instead of the reference's sample/range-structure visit order.
- * transf_mode (naive / with_samples / without_samples) and the range structure
- * of the reference select different ways to the same lengths; all are
- * accepted and computed by the one device algorithm (csrc/exact.hip).
- * Requires n < 2^31. */
+ * transf_mode naive and without_samples (and the reference's range structure)
+ * select different ways to the same lengths; both are computed by the one device
+ * algorithm (csrc/exact.hip).  with_samples (transform_to_exact/with_samples.cpp,
+ * the sample index of config exact-smpl) returns LZ77SSS_EINVAL: its structures
+ * are not built.  Requires n < 2^31. */
 int lz77sss_factorize_exact_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm, int transf_mode,
                                 lz77sss_emit_fn emit, void* user);
 /* pos_t = uint64_t form of the exact factorization (same algorithm and limit n < 2^31). */

@@ -350,6 +350,12 @@ static void check_exact_params(const lz77sss_params* prm, int transf_mode) {
         throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
     if (transf_mode < LZ77SSS_TRANSF_NAIVE || transf_mode > LZ77SSS_TRANSF_WITHOUT_SAMPLES)
         throw lz::error(LZ77SSS_EINVAL, "unsupported transf_mode");
+    // with_samples names the sample index + range structures of
+    // transform_to_exact/with_samples.cpp, which the device path does not build
+    if (transf_mode == LZ77SSS_TRANSF_WITH_SAMPLES)
+        throw lz::error(LZ77SSS_EINVAL,
+                        "transf_mode with_samples is not supported (no sample-index structures on the device); "
+                        "naive and without_samples give the canonical greedy lengths");
 }
 
 LZ77SSS_API int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out) {

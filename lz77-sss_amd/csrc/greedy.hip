@@ -2109,6 +2109,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     pos_t* d_tins = tail_ins_buf.p;
                     k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], off, bmI2);
                 }
+                if (dbg) {  // (before the scan below: k_bmb_write reads its offsets from g_bincl)
+                    const u64 c1 = bmb_scan(bm_bits{bmI, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
+                    const u64 c2 = bmb_scan(bm_bits{bmI2, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
+                    std::fprintf(stderr, "[lz77sss-debug] greedy |I|=%llu |I'|=%llu base=%llu chain=%u\n",
+                                 (unsigned long long)c1, (unsigned long long)c2, (unsigned long long)nb, nchain);
+                }
                 k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
                 const u64 ny = bmb_scan(bm_bits{bmT, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
                 lap("insert set");

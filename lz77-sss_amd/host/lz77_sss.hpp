@@ -4,7 +4,7 @@
 //
 // A caller of
 //     lz77_sss<pos_t>::factorize_approximate<greedy, lpf_opt, 512>(T, n, out, {.num_threads = p});
-//     lz77_sss<uint32_t>::factorize_exact<greedy, lpf_opt, with_samples>(T, n, out);
+//     lz77_sss<uint32_t>::factorize_exact<greedy, lpf_opt, without_samples>(T, n, out);
 //     lz77_sss<uint32_t>::decode(fact_it, out_it, n);
 // keeps its code and links against the HIP library instead.  Differences:
 //   * the factorization runs on an MI355X (device `parameters::device`) with the
@@ -144,6 +144,9 @@ class lz77_sss {
     static void factorize_exact(char_t* input, pos_t input_size, output_fnc_t output, parameters params = {}) {
         static_assert(sizeof(char_t) == 1, "byte alphabet only (lz77_sss.hpp:287)");
         static_assert(fact_mode != skip_phrases, "lz77_sss.hpp:333");
+        static_assert(transf_mode != with_samples,
+                      "with_samples needs the reference's sample index, which the device path does not build "
+                      "(the C-ABI returns LZ77SSS_EINVAL); naive / without_samples give the same lengths");
         lz77sss_params p;
         lz77sss_default_params(&p);
         p.phr_mode = static_cast<int32_t>(phr_mode);

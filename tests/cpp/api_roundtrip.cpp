@@ -33,7 +33,7 @@ static int run(int nseeds) {
         }
         // exact mode, as tests/test_lz77_sss.cpp:95-133 of the reference (round trip only)
         std::vector<typename lz::factor> FX;
-        lz::template factorize_exact<greedy, lpf_opt, with_samples, decomposed_semi_dynamic_square_grid>(
+        lz::template factorize_exact<greedy, lpf_opt, without_samples, decomposed_semi_dynamic_square_grid>(
             T.data(), (pos_t)n, [&](typename lz::factor f) { FX.push_back(f); });
         std::string DX;
         lz::decode(FX.begin(), std::back_inserter(DX), (pos_t)n);

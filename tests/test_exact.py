@@ -94,11 +94,22 @@ def test_gpu_exact_c1_seeds(session, orc, lz, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transf_mode", [0, 1, 2])
+@pytest.mark.parametrize("transf_mode", [0, 2])
 def test_gpu_exact_transform_modes_agree(session, orc, lz, transf_mode):
     T = lz.gen_random_repetitive(50000, 120000, 77)
     _, F = run_exact(session, T, transf_mode=transf_mode)
     assert np.array_equal(F, orc.factorize_exact(T))
+
+
+@pytest.mark.gpu
+def test_gpu_exact_with_samples_rejected(session, lz):
+    """with_samples needs the reference's sample index (not built on the device): EINVAL, not a silent
+    substitute."""
+    T = lz.gen_random_repetitive(20000, 20000, 3)
+    s = session(T.size)
+    s.load(T)
+    with pytest.raises(lz.Lz77SssError, match="with_samples"):
+        s.factorize_exact(transf_mode=lz.WITH_SAMPLES)
 
 
 @pytest.mark.gpu
