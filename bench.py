@@ -105,9 +105,10 @@ def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2, runs: in
     res = {}
     for threads in (p, 1):
         secs, z = [], 0
-        for _ in range(runs):
+        for r in range(runs):
             z, sec, _ = oracle.factorize_timed_p(T, threads, phr_mode=phr_mode)
             secs.append(sec)
+            print(f"cpu_baseline {workload} p={threads} run {r + 1}/{runs}: {sec:.2f} s", file=sys.stderr, flush=True)
         res[threads] = (statistics.median(secs), z, secs)
     sec_p, z_p, _ = res[p]
     sec_1, z_1, _ = res[1]
