@@ -1221,8 +1221,13 @@ __global__ void k_rem_from_bm(const pos_t* __restrict__ ipos, u64 nb, const u32*
 }
 
 // walks over a list of segment ids (outputs in the table; WRITE: factors at offs)
+// waves per SIMD the walk kernel is compiled for (its loads are dependent chains:
+// occupancy hides their latency; fewer registers cost a few spilled bytes)
+#ifndef LZ_WALK_WAVES
+#define LZ_WALK_WAVES 8
+#endif
 template <bool WRITE>
-__global__ void k_walk(walk_ctx W, seg_tab S, const u32* __restrict__ ids, u32 cnt, const u64* __restrict__ offs,
+__global__ __launch_bounds__(64, LZ_WALK_WAVES) void k_walk(walk_ctx W, seg_tab S, const u32* __restrict__ ids, u32 cnt, const u64* __restrict__ offs,
                        pos_t* __restrict__ fact) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;

@@ -644,8 +644,8 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
         // Phi(j) = Hp(j+512) - b^512 Hp(j) does not depend on where the prefix hash starts
         // (the start's contribution cancels): the prefix hash of block k is needed only when
         // block k-1 or k is not all Q, and restarts from 0 after skipped blocks
-        auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn, bool fx, bool& fy) {
-            const uint4 qc = loadq(c + 2);
+        auto step = [&](u32 c, const u32* x, u32* y, const u32* h0, u32* h1, u64 B, uint4& qn, bool fx, bool& fy,
+                        uint4 qc /* Q intervals of block c + 2 */) {
             const bool f1 = fq, f2 = allq(qc);
             if (!(f1 && f2)) {
                 if (!hvalid) carry = 0;
@@ -702,15 +702,15 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
             }
         };
         // PASS1 filters block c + 2 at step c (blocks 0 .. nblk + 1 in all: windows of the
-        // stripe's decisions reach two blocks past its end); once a decision block had a hit
-        // the stripe only filters (it is re-run)
+        // stripe's decisions reach two blocks past its end); a hit in a decision block ends
+        // the stripe (it is re-run)
         for (u32 c = 0; c < nblk; c += 2) {
             u64 Bn = load8(c + 4);  // prefetch (the text pad covers the stripe's end)
             if constexpr (PASS1) {
                 filt(c + 2, Ba);
                 if (dirty) break;
             }
-            step(c, xA, xB, hB, hA, Ba, qb, fA, fB);
+            step(c, xA, xB, hB, hA, Ba, qb, fA, fB, loadq(c + 2));
             Ba = Bn;
             if (c + 1 >= nblk) break;
             Bn = load8(c + 5);
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
                 filt(c + 3, Bb);
                 if (dirty) break;
             }
-            step(c + 1, xB, xA, hA, hB, Bb, qb, fB, fA);
+            step(c + 1, xB, xA, hA, hB, Bb, qb, fB, fA, loadq(c + 3));
             Bb = Bn;
         }
     }

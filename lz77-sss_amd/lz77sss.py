@@ -101,7 +101,7 @@ def load_library(path: Path | str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("LZ77SSS_LIB", LIB_PATH))  # LZ77SSS_LIB: build variants (tools)
     if not p.exists():
         raise Lz77SssError(f"HIP library not built: {p} (run `make -C lz77-sss_amd`)")
     lib = ctypes.CDLL(str(p))
