@@ -126,12 +126,31 @@ __device__ __forceinline__ u64 mix64(u64 z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
-// h(key) = mix(len) + sum over its 8-byte words w of mix(word_w + w*C).  The sum is
-// order-free, so a key is cut into KH_CHUNK-byte pieces hashed by different waves
-// and added atomically: long keys (gaps of MBs inside periodic runs) no longer
-// serialize on one wave.  k_key_prep sets H = mix(len) and the piece counts.
+// h(key) = mix(len) + sum over its 8-byte words w of mix(word_w) * R^w (mod 2^64, R odd).
+// The sum splits over pieces, so a key is cut into KH_CHUNK-byte pieces hashed by
+// different waves and added atomically: long keys (gaps of MBs inside periodic runs)
+// do not serialize on one wave.  A piece inside a p-periodic run (run table, lce_dev.h)
+// has a word sequence of period L = p / gcd(p, 8): its sum is the first L terms times
+// geometric series in R^L, so run-heavy text is hashed without reading the runs.
+// k_key_prep sets H = mix(len) and the piece counts.
 constexpr u32 KH_CHUNK = 16384;
 constexpr u32 KH_WAVES = 16384;
+constexpr u64 KH_R = 0x9e3779b97f4a7c15ull;  // odd
+constexpr u64 kh_pow_host(u64 e) {
+    u64 r = 1, b = KH_R;
+    while (e) { if (e & 1) r *= b; b *= b; e >>= 1; }
+    return r;
+}
+constexpr u64 KH_R64 = kh_pow_host(64);
+__device__ __forceinline__ u64 kh_pow(u64 e) {  // R^e mod 2^64
+    u64 r = 1, b = KH_R;
+    while (e) {
+        if (e & 1) r *= b;
+        b *= b;
+        e >>= 1;
+    }
+    return r;
+}
 __global__ void k_key_prep(const pos_t* __restrict__ KL, u32 s, u64* __restrict__ H, u32* __restrict__ CC) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s) return;
@@ -142,7 +161,7 @@ __global__ void k_key_prep(const pos_t* __restrict__ KL, u32 s, u64* __restrict_
 // OFF = inclusive scan of the piece counts; wave w hashes pieces [w*per, (w+1)*per)
 __global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, const pos_t* __restrict__ S,
                                                   const pos_t* __restrict__ KL, const u32* __restrict__ OFF, u32 s,
-                                                  u64* __restrict__ H) {
+                                                  run_tab R, u64* __restrict__ H) {
     const u32 wave = (u32)(((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const u32 lane = threadIdx.x & 63;
     const u32 total = OFF[s - 1];
@@ -163,11 +182,43 @@ __global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, cons
         const u64 beg = S[k], len = KL[k];
         const u64 b0 = (u64)(c - first) * KH_CHUNK, b1 = min<u64>(len, b0 + KH_CHUNK);
         u64 h = 0;
-        for (u64 w = b0 / 8 + lane; 8 * w < b1; w += 64) {
-            u64 x = ldu64(T + beg + 8 * w);
-            const u64 rem = len - 8 * w;
-            if (rem < 8) x &= (1ull << (8 * rem)) - 1;
-            h += mix64(x + w * 0x9e3779b97f4a7c15ull);
+        u32 pp = 0;  // period of a run holding the whole piece (and the word after it), else 0
+        if (R.p && b1 == b0 + KH_CHUNK && b1 + 8 <= len) {
+            const u64 x0 = beg + b0, t = (x0 + 127) >> 7;
+            const u32 p = R.p[t];
+            if (p && (u64)R.lo[t] <= x0 && (u64)R.hi[t] >= x0 + KH_CHUNK + 8) pp = p;
+        }
+        if (pp) {
+            const u32 L = pp / min(pp & (0u - pp), 8u), NW = KH_CHUNK / 8;
+            const u64 RL = kh_pow(L), Rw0 = kh_pow(b0 / 8);
+            const u32 K = NW / L, rem = NW % L;  // words j < rem recur K + 1 times, the others K
+            u64 g0 = 0, q = 1;  // g0 = sum_{i<K} RL^i, q = RL^K
+            {
+                u64 base = RL, e = K, acc = 0, pw = 1;  // geometric sum by binary doubling
+                u64 sb = 1;                            // sum_{i<2^b} base^i for the current bit block
+                while (e) {
+                    if (e & 1) { acc += sb * pw; pw *= base; }
+                    sb += sb * base;
+                    base *= base;
+                    e >>= 1;
+                }
+                g0 = acc;
+                q = pw;
+            }
+            const u64 g1 = g0 + q;
+            for (u32 j = lane; j < L; j += 64) {
+                const u64 x = ldu64(T + beg + b0 + 8ull * j);
+                h += mix64(x) * Rw0 * kh_pow(j) * (j < rem ? g1 : g0);
+            }
+        } else {
+            u64 pw = kh_pow(b0 / 8 + lane);
+            for (u64 w = b0 / 8 + lane; 8 * w < b1; w += 64) {
+                u64 x = ldu64(T + beg + 8 * w);
+                const u64 rem = len - 8 * w;
+                if (rem < 8) x &= (1ull << (8 * rem)) - 1;
+                h += mix64(x) * pw;
+                pw *= KH_R64;
+            }
         }
         for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o);
         if (lane == 0 && b0 < b1) atomicAdd((unsigned long long*)&H[k], (unsigned long long)h);
@@ -426,7 +477,7 @@ void engine::build_sa_s(const u8* T) {
         u32* CC = u32e.get(s);
         k_key_prep<<<g, 256, 0, st>>>(KL, s, H, CC);
         scan_incl(CC, CC, s, scan_tmp, st);
-        k_key_hash<<<KH_WAVES * 64 / 256, 256, 0, st>>>(T, dS, KL, CC, s, H);
+        k_key_hash<<<KH_WAVES * 64 / 256, 256, 0, st>>>(T, dS, KL, CC, s, runs(), H);
         SA_DBG("key hash");
         k_iota<<<g, 256, 0, st>>>(idx_in, s);
         size_t tb = 0;

@@ -139,6 +139,7 @@ struct engine {
     dbuf<u32> g_pbm, g_pwp, g_pcnt, g_sdk, g_dstart, g_pflag;  // dense slot ids of the base set  // per-block bitmap counts and their inclusive scan
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32;
     dbuf<pos_t> g_xpos;
+    dbuf<pos_t> g_stash;  // per segment: factors of its last speculative walk (csrc/greedy.hip STASH_CAP)
     dbuf<pos_t> g_H;    // materialized gap-index table of the sequential completion
     dbuf<pos_t> g_Hs;   // greedy windows: last insert per slot before the window (pos + 1)
     dbuf<pos_t> fact_acc;  // greedy windows: the stream so far

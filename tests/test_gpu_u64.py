@@ -142,7 +142,7 @@ def test_u64_one_shot_callback_and_device_decode(lz, orc):
     # exact mode through the 64-bit entry point (n < 2^31): the 32-bit stream, widened
     got.clear()
     rc = lz.load_library().lz77sss_factorize_exact_u64(T.ctypes.data_as(ctypes.c_void_p), T.size, ctypes.byref(p),
-                                                       1, cb, None)
+                                                       lz.WITHOUT_SAMPLES, cb, None)
     assert rc == 0
     assert np.array_equal(np.concatenate(got), orc.factorize_exact(T).astype(np.uint64))
 

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread -k "greedy or window or completion or golden or medium or one_gib or parity or u64 or shard" > gpurun_out/pytest_sel.log 2>&1 || { tail -40 gpurun_out/pytest_sel.log; exit 1; }
+tail -2 gpurun_out/pytest_sel.log
+for wl in rr genome; do timeout -k 10 200 python3 tools/prof_step.py $wl 2 > gpurun_out/st_$wl.log 2>&1 || exit 1; grep "^step 2" gpurun_out/st_$wl.log | cut -c1-140; done
