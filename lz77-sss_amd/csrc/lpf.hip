@@ -286,7 +286,10 @@ void engine::build_lpf_naive(const u8* T) {
         u8* t = scan_tmp.get(tb);
         LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, push, off, (int)s, st));
     }
-    num_phr = rd1(off + s - 1, st) + rd1(push + s - 1, st);
+    {
+        const auto [lo, lp] = rd2(off + s - 1, push + s - 1, st);
+        num_phr = lo + lp;
+    }
     pos_t* out = lpf.get((u64)(num_phr + 1) * 3);
     k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);
     LZ_HIP(hipGetLastError());
@@ -355,7 +358,7 @@ void engine::build_lpf_opt(const u8* T) {
         u8* t = scan_tmp.get(tb);
         LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, push, off, (int)s, st));
     }
-    const u32 last_off = rd1(off + s - 1, st), last_push = rd1(push + s - 1, st);
+    const auto [last_off, last_push] = rd2(off + s - 1, push + s - 1, st);
     num_phr = last_off + last_push;
     pos_t* out = lpf.get((u64)(num_phr + 1) * 3);
     k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);

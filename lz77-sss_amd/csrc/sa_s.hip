@@ -489,10 +489,9 @@ void engine::build_sa_s(const u8* T) {
         SA_DBG("hash sort");
         k_group_verify<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, Hs, idx, s, flag, ctr + 2);
         scan_incl(flag, rank, s, scan_tmp, st);  // rank[t] = group id + 1
-        const u32 collide = rd1(ctr + 2, st);
+        const auto [collide, d] = rd2(ctr + 2, rank + s - 1, st);
         if (debug_enabled()) fprintf(stderr, "[sa_s] s=%u collide=%u\n", s, collide);
         if (!collide) {
-            const u32 d = rd1(rank + s - 1, st);
             u32* rep = sa_tmp1.get(d);
             k_reps<<<g, 256, 0, st>>>(flag, rank, idx, s, rep);
             // 2. sort distinct keys: bounded comparison, then exact wave sort of bounded ties

@@ -209,6 +209,15 @@ static inline T rd1(const T* dptr, hipStream_t st) {
     LZ_HIP(hipStreamSynchronize(st));
     return v;
 }
+// two device values with one synchronization
+template <class T>
+static inline std::pair<T, T> rd2(const T* a, const T* b, hipStream_t st) {
+    T v[2];
+    LZ_HIP(hipMemcpyAsync(&v[0], a, sizeof(T), hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipMemcpyAsync(&v[1], b, sizeof(T), hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    return {v[0], v[1]};
+}
 static inline unsigned cdiv(u64 a, u64 b) { return (unsigned)((a + b - 1) / b); }
 
 }  // namespace LZ_NS
