@@ -2171,6 +2171,33 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
                 const u64 ny = bmb_scan(bm_bits{bmT, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
                 lap("insert set");
+                if (ny == 0 && dbg && std::getenv("LZ77SSS_DEBUG_JUMP")) {
+                    // which phrases the converged chain rolled over (interior in I), by log2 length
+                    std::vector<u32> hb(nw);
+                    std::vector<pos_t> hp(3 * ((u64)m + 1));
+                    LZ_HIP(hipStreamSynchronize(st));
+                    LZ_HIP(hipMemcpy(hb.data(), bmI, nw * 4, hipMemcpyDeviceToHost));
+                    LZ_HIP(hipMemcpy(hp.data(), P, hp.size() * sizeof(pos_t), hipMemcpyDeviceToHost));
+                    u64 tot[2][40] = {}, jmp[2][40] = {}, jpos[2][40] = {};
+                    pos_t prev_end = 0;
+                    for (u32 k = 0; k < m; k++) {
+                        const pos_t b0 = hp[3 * k], b1 = hp[3 * k + 1];
+                        const int g = b0 > prev_end ? 1 : 0;
+                        prev_end = b1;
+                        if (b0 < a || b1 >= hi_ins || b1 - b0 < 4) continue;
+                        int lg = 0;
+                        while (((pos_t)2 << lg) <= b1 - b0) lg++;
+                        const pos_t q = b0 + (b1 - b0) / 2 - off;
+                        tot[g][lg]++;
+                        if ((hb[q >> 5] >> (q & 31)) & 1) { jmp[g][lg]++; jpos[g][lg] += b1 - b0; }
+                    }
+                    for (int g = 0; g < 2; g++)
+                        for (int lg = 0; lg < 40; lg++)
+                            if (tot[g][lg])
+                                std::fprintf(stderr, "[lz77sss-debug] jump %s len 2^%d: phrases=%llu rolled=%llu pos=%llu\n",
+                                             g ? "after-gap" : "adjacent", lg, (unsigned long long)tot[g][lg],
+                                             (unsigned long long)jmp[g][lg], (unsigned long long)jpos[g][lg]);
+                }
                 if (ny == 0) {
                     // every lookup of the chain was exact: emit the factors
                     if (nchain) {
