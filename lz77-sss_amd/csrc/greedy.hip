@@ -2016,7 +2016,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             if (nb) k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem);
             rebuild_added(true);
         };
-        W.use_pred = std::getenv("LZ77SSS_NO_PRED") ? 0 : 1;
+        // same-slot predecessors (pred5) pay for their scatter when the walks make many
+        // lookups: short gaps (many factors per gap position).  Texts with few, long gaps
+        // (long factors, few lookups) search the buckets instead.  LZ77SSS_PRED /
+        // LZ77SSS_NO_PRED force either path (tests).
+        W.use_pred = std::getenv("LZ77SSS_PRED") ? 1
+                     : std::getenv("LZ77SSS_NO_PRED") ? 0
+                     : ((u64)(N - len_lpf_phr) < 4096ull * (u64)std::max<u64>(1, num_gaps)) ? 1 : 0;
 
         // ---- walk + link until the chain from the window entry is complete, then check I
         u32 nseg = nseg_init;

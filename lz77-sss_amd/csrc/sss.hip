@@ -398,6 +398,9 @@ __global__ void k_run_apply(const u32* __restrict__ send_rev, const u32* __restr
 //   QSKIP  the exact re-run of the stripes listed by build_sss, with the Q
 //          intervals of k_q_anchors; blocks entirely inside Q skip their hashing
 //          and minima
+#ifndef SSS_VAR
+#define SSS_VAR 0  // timing experiments only (tools/sss_variants.sh); 0 = the product kernel
+#endif
 constexpr int SCAP = 1024;                    // sync positions per stripe before the fallback
 constexpr int SWAVES = 4;                     // independent waves per workgroup
 constexpr int FA_LANES = 22;                  // candidate lanes per filter anchor (4 shifts each)
@@ -442,6 +445,13 @@ __device__ __forceinline__ u32 wave_suffix_min(u32 v, u32 lane) {  // inclusive,
     return min(v, lane < 16 ? a0 : lane < 32 ? a1 : lane < 48 ? r3 : INF32);
 }
 
+// one v_min3_u32 (the compiler otherwise re-associates the clamp into every decision)
+__device__ __forceinline__ u32 min3u(u32 a, u32 b, u32 c) {
+    u32 r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // Periodicity filter of one 512-block (PASS1), on the bytes the wave already holds
 // (lane L: bytes 8L..8L+7 as B).  Filter anchors A0 = block start and A1 = +256; bit
 // r of the (uniform) result is set when T[A_r .. A_r + 16) recurs at a shift in
@@ -453,8 +463,9 @@ __device__ __forceinline__ u32 wave_suffix_min(u32 v, u32 lane) {  // inclusive,
 __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
     const u32 lo = (u32)B, hi = (u32)(B >> 32);
     const u32 li = lane & 31, grp = lane >> 5;
-    const u32 al = grp ? (u32)__builtin_amdgcn_readlane((int)lo, 32) : (u32)__builtin_amdgcn_readlane((int)lo, 0);
-    const u32 ah = grp ? (u32)__builtin_amdgcn_readlane((int)hi, 32) : (u32)__builtin_amdgcn_readlane((int)hi, 0);
+    // anchor bytes of the lane's half (lane 0 or 32)
+    const int la = (int)(lane & 32u);
+    const u64 A = (u64)(u32)__shfl((int)hi, la, 64) << 32 | (u32)__shfl((int)lo, la, 64);
     // x0 = 84 + 4 li (+ 256 grp): the hi word of lane 10 + li/2 (li even) or the lo word of
     // lane 11 + li/2 (li odd)
     const bool ev = (li & 1) == 0;
@@ -462,13 +473,16 @@ __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
     const u32 s0l = (u32)__shfl((int)lo, l0, 64), s0h = (u32)__shfl((int)hi, l0, 64);
     const u32 s1l = (u32)__shfl((int)lo, l0 + 1, 64), s1h = (u32)__shfl((int)hi, l0 + 1, 64);
     const u32 d0 = ev ? s0h : s0l, d1 = ev ? s1l : s0h, d2 = ev ? s1h : s1l;
-    u32 hk = 0;
+    // any 8-byte repeat among the 4 shifts of the candidate lanes (wave masks, no per-lane bits)
+    u64 any = 0;
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-        hk |= (__builtin_amdgcn_alignbyte(d1, d0, k) == al && __builtin_amdgcn_alignbyte(d2, d1, k) == ah ? 1u : 0u)
-              << k;
-    if (li >= (u32)FA_LANES) hk = 0;
-    if (!__ballot(hk != 0)) return 0;
+    for (int k = 0; k < 4; k++) {
+        const u64 w = (u64)__builtin_amdgcn_alignbyte(d2, d1, k) << 32 | __builtin_amdgcn_alignbyte(d1, d0, k);
+        any |= __ballot(w == A);
+    }
+    if (!(any & 0x003FFFFF003FFFFFull)) return 0;  // candidate lanes li < FA_LANES (22)
+    static_assert(FA_LANES == 22, "candidate lane mask");
+    // rare: confirm on bytes 8..15
     const u32 cl = grp ? (u32)__builtin_amdgcn_readlane((int)lo, 33) : (u32)__builtin_amdgcn_readlane((int)lo, 1);
     const u32 ch = grp ? (u32)__builtin_amdgcn_readlane((int)hi, 33) : (u32)__builtin_amdgcn_readlane((int)hi, 1);
     const u32 s2l = (u32)__shfl((int)lo, l0 + 2, 64), s2h = (u32)__shfl((int)hi, l0 + 2, 64);
@@ -476,7 +490,9 @@ __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
     bool hit = false;
 #pragma unroll
     for (int k = 0; k < 4; k++)
-        hit |= ((hk >> k) & 1) && __builtin_amdgcn_alignbyte(d3, d2, k) == cl && __builtin_amdgcn_alignbyte(d4, d3, k) == ch;
+        hit |= __builtin_amdgcn_alignbyte(d1, d0, k) == (u32)A && __builtin_amdgcn_alignbyte(d2, d1, k) == (u32)(A >> 32) &&
+               __builtin_amdgcn_alignbyte(d3, d2, k) == cl && __builtin_amdgcn_alignbyte(d4, d3, k) == ch;
+    if (li >= (u32)FA_LANES) hit = false;
     const u64 hm = __ballot(hit);
     return ((u32)hm ? 1u : 0u) | ((u32)(hm >> 32) ? 2u : 0u);
 }
@@ -504,11 +520,16 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
     const u64 jmax = n - TAU;                  // last position with a full window (n >= 2 tau here)
     const u64 ilim = min<u64>(last_i - i0, (u64)SD - 1);  // decisions i0 + u, u <= ilim
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
+    // blocks k >= kend hold positions past the last full window (jmax): k TAU + TAU - 1 > jmax - i0
+    const u32 kend = (u32)min<u64>((jmax + 1 - i0) / TAU, 0xFFFFFFFFull);
     // PASS1 filter state: hit bits per filter anchor (block k < 64: bit k of hw[r]; blocks 64, 65
     // of the last stripe: bits 2(k - 64) + r of hw2), confirmed hit in a decision block
     u64 hw0 = 0, hw1 = 0, hw2 = 0;
     bool dirty = false;
     auto filt = [&](u32 k, u64 Bk) {
+#if SSS_VAR == 1
+        return;
+#endif
         const u32 f = sss_filter(Bk, lane);
         // branch-free (a conditional target makes the compiler spill the words to scratch)
         const u64 lowk = k < 64 ? 1ull << (k & 63) : 0ull;
@@ -518,6 +539,9 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
         if (f && k < nblk) dirty = true;
     };
     u32 nout = 0;  // outputs of this stripe so far (uniform)
+#if SSS_VAR == 2
+    u32 vacc = 0;
+#endif
     {
         // per-lane powers: pwl = b^(8 lane), ibl = b^(-8 (lane + 1))
         u32 pwl = 1, ibl = PW.ib8;
@@ -537,6 +561,11 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
         // Hp(s_k + 8 lane + e), e < 8, into h; carry = Hp(s_k) in, Hp(s_k+1) out (uniform)
         auto block_prefix = [&](u64 bytes, u32& carry, u32* h) {
             const u32 lo = (u32)bytes, hi = (u32)(bytes >> 32);
+#if SSS_VAR == 3
+            for (int e = 0; e < 8; e++) h[e] = (e < 4 ? lo : hi) + carry + e;
+            carry += lo;
+            return;
+#endif
             u32 c[8], loc[8];
 #pragma unroll
             for (int e = 0; e < 8; e++) c[e] = ((e < 4 ? lo : hi) >> (8 * (e & 3))) & 255u;
@@ -578,7 +607,7 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
             const bool anyq = (q.x != 0xFF00FF00u) || (q.y != 0xFF00FF00u) || ((q.z & 0xFFFFu) != 0xFF00u);
 #pragma unroll
             for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
-            const bool endblk = i0 + k * TAU + TAU - 1 > jmax;
+            const bool endblk = (u32)k >= kend;
             if (__builtin_amdgcn_readfirstlane((int)(anyq || endblk))) {
                 // anchor r (0..4) of the block covers offsets (128r - 128, 128r]; its Q interval
                 // [lo, hi] (rel = offset + 127 - 128r) is an offset interval, uniform per block:
@@ -658,6 +687,10 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
             qn = qc;
             // both blocks all INF: every window minimum is INF, no decision of block c is in S
             if (fx && fy) return;
+#if SSS_VAR == 2
+            for (int e = 0; e < 8; e++) vacc ^= x[e] + y[e];
+            return;
+#endif
             // window minima for decisions of block c
             u32 sx[8], py[8];
             sx[7] = x[7];
@@ -676,7 +709,7 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
             u64 U = 0;
 #pragma unroll
             for (int e = 0; e < 8; e++) {
-                M[e] = __ballot(min(x[e], y[e]) == min(min(sx[e], g), py[e]));
+                M[e] = __ballot(min(x[e], y[e]) == min3u(sx[e], g, py[e]));
                 U |= M[e];
             }
             if (U) {
@@ -691,14 +724,23 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
                     mb = lim < 0 ? 0u : lim >= 7 ? mb : (mb & ((2u << lim) - 1u));
                 }
                 const u32 cnt = (u32)__popc(mb);
-                const u32 incl = wave_prefix_add(cnt);
-                u32 o = nout + incl - cnt;
                 const pos_t base = (pos_t)(i0 + c * TAU + 8 * lane);
-                for (u32 m = mb; m; m &= m - 1) {
-                    if (o < (u32)SCAP) out[o] = base + (pos_t)__builtin_ctz(m);
-                    o++;
+                if (!__ballot(cnt > 1)) {
+                    // usual case (sparse S): at most one output per lane, slot = lanes below with one
+                    const u64 has = __ballot(cnt != 0);
+                    const u32 o = nout + (u32)__builtin_amdgcn_mbcnt_hi((u32)(has >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((u32)has, 0u));
+                    if (cnt && o < (u32)SCAP) out[o] = base + (pos_t)__builtin_ctz(mb);
+                    nout += (u32)__popcll(has);
+                } else {
+                    const u32 incl = wave_prefix_add(cnt);
+                    u32 o = nout + incl - cnt;
+                    for (u32 m = mb; m; m &= m - 1) {
+                        if (o < (u32)SCAP) out[o] = base + (pos_t)__builtin_ctz(m);
+                        o++;
+                    }
+                    nout += (u32)__builtin_amdgcn_readlane((int)incl, 63);
                 }
-                nout += (u32)__builtin_amdgcn_readlane((int)incl, 63);
             }
         };
         // PASS1 filters block c + 2 at step c (blocks 0 .. nblk + 1 in all: windows of the
@@ -723,6 +765,9 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
         }
     }
 stripe_done:
+#if SSS_VAR == 2
+    if (vacc == 0x9e3779b9u) nout++;
+#endif
     if constexpr (PASS1) {
         if (lane == 0) {
             hitw[3 * w] = hw0;

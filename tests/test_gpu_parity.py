@@ -315,6 +315,23 @@ def test_sorted_predecessor_paths_vs_oracle(session, orc, lz, kind, mib, monkeyp
     assert np.array_equal(F2, F_ref)
 
 
+@pytest.mark.parametrize("kind,mib", [("genome", 16), ("rr", 32)])
+def test_pred_and_bucket_search_paths_vs_oracle(session, orc, lz, kind, mib, monkeypatch):
+    """Base lookups through the same-slot predecessors (LZ77SSS_PRED) and through bucket
+    searches (LZ77SSS_NO_PRED; chosen by default for texts with few long gaps) both equal
+    the oracle stream."""
+    n = mib << 20
+    T = lz.gen_genome(n, 2 << 20, 0.001, 17) if kind == "genome" else lz.gen_random_repetitive(n, n, 9, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    monkeypatch.setenv("LZ77SSS_PRED", "1")
+    _, F1 = run(session, T)
+    assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    monkeypatch.delenv("LZ77SSS_PRED")
+    monkeypatch.setenv("LZ77SSS_NO_PRED", "1")
+    _, F2 = run(session, T)
+    assert np.array_equal(F2, F_ref)
+
+
 # ---- bounded greedy completion (k_seq_walk): the exact sequential walk from the confirmed chain prefix
 
 @pytest.mark.parametrize("max_outer", [0, 1, 2])

@@ -1,0 +1,7 @@
+# SSS + greedy path checks and timings after kernel changes
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "sss or pred or hash_adversarial or fallback or thue or fib" --timeout 300 --timeout-method thread > gpurun_out/pytest_sel.log 2>&1 || { tail -30 gpurun_out/pytest_sel.log; exit 1; }
+tail -2 gpurun_out/pytest_sel.log
+for wl in genome rr; do timeout -k 10 200 python3 tools/sss_time.py $wl || exit 1; done
+for wl in rr genome; do timeout -k 10 200 python3 tools/prof_step.py $wl 2 > gpurun_out/st_$wl.log 2>&1 || exit 1; grep "^step 2" gpurun_out/st_$wl.log | cut -c1-140; done
