@@ -144,19 +144,42 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
     const u64 a = (u64)t * QA;
     const bool probe_ok = t >= 0 && (u64)t < nanch && a + QM <= n;
     u32 cm[6] = {0, 0, 0, 0, 0, 0};  // bit pp-1
-    if (probe_ok) {
+    // candidates of the words k >= kbeg (fully unrolled; the guard is uniform or a lane mask)
+    auto filt_words = [&](int kbeg) {
         const u32 w0 = word(oa >> 2);
-        u32 dprev = w0;
 #pragma unroll
         for (int k = 0; k <= (int)(QL / 4); k++) {
-            const u32 dnext = word((oa >> 2) + k + 1);
+            if (k < kbeg) continue;
+            const u32 dprev = word((oa >> 2) + k), dnext = word((oa >> 2) + k + 1);
 #pragma unroll
             for (int r = 0; r < 4; r++) {
                 const u32 pp = 4 * k + r;
                 if (pp >= 1 && pp <= QL && __builtin_amdgcn_alignbyte(dnext, dprev, r) == w0)
                     cm[(pp - 1) >> 5] |= 1u << ((pp - 1) & 31);
             }
-            dprev = dnext;
+        }
+    };
+    // the smallest candidate first: groups of 4 words until every probe of the wave has one
+    // (inside runs of small period after a few words); the rest only where p1 fails
+    int kdone = (int)(QL / 4) + 1;
+    if (probe_ok) {
+        const u32 w0 = word(oa >> 2);
+#pragma unroll
+        for (int g = 0; g <= (int)(QL / 4); g += 4) {
+#pragma unroll
+            for (int k = g; k < g + 4 && k <= (int)(QL / 4); k++) {
+                const u32 dprev = word((oa >> 2) + k), dnext = word((oa >> 2) + k + 1);
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const u32 pp = 4 * k + r;
+                    if (pp >= 1 && pp <= QL && __builtin_amdgcn_alignbyte(dnext, dprev, r) == w0)
+                        cm[(pp - 1) >> 5] |= 1u << ((pp - 1) & 31);
+                }
+            }
+            if (g + 4 <= (int)(QL / 4) && !__ballot((cm[0] | cm[1] | cm[2] | cm[3] | cm[4] | cm[5]) == 0)) {
+                kdone = g + 4;
+                break;
+            }
         }
     }
     u32 p1 = 0;
@@ -227,6 +250,7 @@ __global__ __launch_bounds__(QT_THREADS) void k_q_anchors(const u8* __restrict__
             // Fine-Wilf a period pp <= f of the probe would share gcd(p1, pp) = p1
             // with it, and every multiple of p1 up to f disagrees at f - pp + p1:
             // only candidates pp > f remain (at run ends this skips ~85 full checks)
+            if (kdone <= (int)(QL / 4)) filt_words(kdone);  // the candidates past the early stop
             cm[(p1 - 1) >> 5] &= ~(1u << ((p1 - 1) & 31));
             for (int wi = 0; wi < 6; wi++) {
                 const int lo = 32 * wi + 1;  // candidate of bit 0
