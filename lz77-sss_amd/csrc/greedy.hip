@@ -100,7 +100,8 @@ struct ichunk { pos_t q0, q1; u32 rank0; };
 // lanes (5x the threads of a chunk-per-thread walk for latency hiding, and the 5
 // entries of a position are written by adjacent lanes)
 __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __restrict__ chunks, u32 nch,
-                        u32* __restrict__ keys, u32* __restrict__ vals, pos_t* __restrict__ ipos) {
+                        u32* __restrict__ keys, u32* __restrict__ vals, pos_t* __restrict__ ipos,
+                        u8* __restrict__ pf = nullptr) {
     const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= 5ull * nch) return;
     const u64 c = g / 5;
@@ -114,7 +115,9 @@ __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __res
         const u32 rank = ch.rank0 + (q - ch.q0);
         if (ipos && x == 4) ipos[rank] = q;
         const u32 e = 5 * rank + (4 - x);
-        keys[e] = (u32)((u64)fp & G.mask);
+        const u32 key = (u32)((u64)fp & G.mask);
+        keys[e] = key;
+        if (pf && !pf[key]) pf[key] = 1;  // slot presence (dense ids): plain stores, a hot slot is read far more often
         if (vals) vals[e] = e;
         if (q + 1 < ch.q1) fp = kr_roll(fp, b, np[T[q]], T[q + len]);
     }
@@ -123,13 +126,6 @@ __global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __res
 // (rr 1 GiB: 6 091 of 2^25), so sorting dense ids needs 2 radix passes instead of 4.
 // Presence as one byte per slot written with plain stores (idempotent: hot slots cost
 // no atomics), packed into a bitmap with per-word popcounts; id = rank of the slot.
-__global__ void k_slot_presence(const u32* __restrict__ keys, u64 m, u8* __restrict__ pf) {
-    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < m) {
-        const u32 k = keys[e];
-        if (!pf[k]) pf[k] = 1;  // a hot slot's byte is read (cached) far more often than written
-    }
-}
 __global__ void k_presence_pack(const u8* __restrict__ pf, u64 nw, u32* __restrict__ pbm, u32* __restrict__ c) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nw) return;
@@ -1880,16 +1876,16 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             u32* pbm = g_pbm.get(npw + 1);
             u32* pwp = g_pwp.get(npw + 1);
             if (nch) {
-                k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos);
-                lap("base slots");
                 // distinct slots -> dense ids when that saves radix passes
                 // (tried below 2^28 entries: a base set that large comes from a non-repetitive
-                // text, whose slots are all in use)
-                if (ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE")) {
+                // text, whose slots are all in use); k_slots marks the present slots
+                const bool try_dense = ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE");
+                u8* pf = try_dense ? (u8*)g_pflag.get(npw * 8) : nullptr;
+                if (pf) LZ_HIP(hipMemsetAsync(pf, 0, npw * 32, st));
+                k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos, pf);
+                lap("base slots");
+                if (try_dense) {
                     u32* pcnt = g_pcnt.get(npw + 1);
-                    u8* pf = (u8*)g_pflag.get(npw * 8);
-                    LZ_HIP(hipMemsetAsync(pf, 0, npw * 32, st));
-                    k_slot_presence<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pf);
                     k_presence_pack<<<cdiv(npw, 256), 256, 0, st>>>(pf, npw, pbm, pcnt);
                     D = excl_scan(pcnt, pwp, npw, scan_tmp, st);
                     u32 dbits = 1;
@@ -1900,6 +1896,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 u32* sk_in = keys;
                 u32 sbits = gp.log2_size_h;
                 if (dense) {
+                    // (a transform iterator mapping the ids inside the sort was slower: rr sort
+                    // passes +234 us against this pass's 211 us)
                     k_dense_keys<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pbm, pwp, skeys);
                     sk_in = skeys;
                     skeys = g_sdk.get(ne5 + 1);
