@@ -1188,6 +1188,9 @@ void engine::build_sss(const u8* T) {
         scan_counts();
         total = rd1(off + nlanes, st);
     }
+    // |S| feeds hipcub/rocprim item counts (int) in SA_S and LPF: a sync set this large would
+    // need > 2^31 entries (about 2^39 text bytes of random-like text, past one GPU's HBM)
+    if (total >= 0x7FFFFFFFu) throw error(LZ77SSS_EINVAL, "sync set of 2^31 or more positions (split the text)");
     s = total;
     sss_kernel_bytes = n + sizeof(pos_t) * (u64)s;
     pos_t* dS = S.get((u64)s + 1);
