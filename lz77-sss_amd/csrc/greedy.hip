@@ -307,7 +307,15 @@ struct walk_ctx {
 };
 
 __device__ __forceinline__ u32 base_rank(const walk_ctx& W, pos_t q, int& hint) {
-    if (hint >= 0 && q >= W.istart[hint] && q < W.iend[hint]) return W.irank[hint] + (u32)(q - W.istart[hint]);
+    if (hint >= 0) {
+        if (q >= W.istart[hint] && q < W.iend[hint]) return W.irank[hint] + (u32)(q - W.istart[hint]);
+        // a walk moves forward: the query after an LPF phrase is usually in the next interval
+        const int h1 = hint + 1;
+        if ((u32)h1 < W.nint && q >= W.istart[h1] && q < W.iend[h1]) {
+            hint = h1;
+            return W.irank[h1] + (u32)(q - W.istart[h1]);
+        }
+    }
     u32 lo = 0, hi = W.nint;
     while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
