@@ -285,6 +285,7 @@ struct walk_ctx {
     const u32* svals;    // entry ids in sorted order
     const u32* pred5;    // predecessor entry in the same slot
     const pos_t* ipos;   // rank -> position
+    const pos_t* iposr;  // ipos | POS_RFLAG when the rank is removed (one load per pred step), or null
     u64 nentries;
     const u32* bstart;   // slot -> first sorted base entry (nslots + 1)
     // delta
@@ -306,6 +307,7 @@ struct walk_ctx {
     lce_view L;
 };
 
+constexpr pos_t POS_RFLAG = (pos_t)1 << (8 * sizeof(pos_t) - 1);  // iposr: removed (texts below 2^31 / 2^63)
 __device__ __forceinline__ u32 base_rank(const walk_ctx& W, pos_t q, int& hint) {
     if (hint >= 0) {
         if (q >= W.istart[hint] && q < W.iend[hint]) return W.irank[hint] + (u32)(q - W.istart[hint]);
@@ -413,7 +415,15 @@ __device__ pos_t lookup(const walk_ctx& W, pos_t q, int x, int& hint) {
     if (rk != NONE) {
         const u32 e = 5 * rk + ord;
         slot = W.keys[e];
-        if (W.use_pred) {
+        if (W.use_pred && W.iposr) {
+            u32 p = W.pred5[e];
+            pos_t v = p == NONE ? 0 : W.iposr[p / 5];
+            while (p != NONE && (v & POS_RFLAG) && (v & ~POS_RFLAG) != q) {
+                p = W.pred5[p];
+                if (p != NONE) v = W.iposr[p / 5];
+            }
+            cb = p == NONE ? POS_NONE : (v & ~POS_RFLAG);
+        } else if (W.use_pred) {
             u32 p = W.pred5[e];
             while (p != NONE && W.rem[p / 5] && W.ipos[p / 5] != q) p = W.pred5[p];
             cb = p == NONE ? POS_NONE : W.ipos[p / 5];
@@ -592,7 +602,10 @@ __global__ void k_flip(walk_ctx W, const pos_t* __restrict__ ys, const u8* __res
     int hint = -1;
     const u32 rk = base_rank(W, ys[k], hint);
     in_base[k] = rk != NONE;
-    if (rk != NONE) rem[rk] = joined[k] ? 0 : 1;
+    if (rk != NONE) {
+        rem[rk] = joined[k] ? 0 : 1;
+        if (W.iposr) ((pos_t*)W.iposr)[rk] = W.ipos[rk] | (joined[k] ? (pos_t)0 : POS_RFLAG);
+    }
 }
 // ---------------------------------------------------------------------------
 // exact single-thread walk from a segment start to the end of the text, with
@@ -1224,11 +1237,13 @@ __global__ void k_iv_chunks(const pos_t* __restrict__ st, const pos_t* __restric
 }
 // rem[r] = base position r not in I
 __global__ void k_rem_from_bm(const pos_t* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, pos_t off,
-                              u8* __restrict__ rem) {
+                              u8* __restrict__ rem, pos_t* __restrict__ iposr) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nb) return;
-    const pos_t q = ipos[r] - off;
-    rem[r] = ((bmI[q >> 5] >> (q & 31)) & 1) ? 0 : 1;
+    const pos_t p = ipos[r], q = p - off;
+    const bool in = (bmI[q >> 5] >> (q & 31)) & 1;
+    rem[r] = in ? 0 : 1;
+    if (iposr) iposr[r] = p | (in ? (pos_t)0 : POS_RFLAG);
 }
 
 // walks over a list of segment ids (outputs in the table; WRITE: factors at offs)
@@ -1966,6 +1981,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             W.keys = keys; W.skeys = skeys; W.svals = svals; W.pred5 = pred5; W.ipos = ipos; W.nentries = ne5;
             W.bstart = g_bstart.p;
             W.rem = rem; W.akeys = nullptr; W.nadd = 0; W.akeys2 = nullptr; W.nadd2 = 0;
+            // removed flags packed into the positions (the flag bit is above every position)
+            W.iposr = (W.use_pred && (u64)N < (u64)POS_RFLAG && !std::getenv("LZ77SSS_NO_IPOSR"))
+                          ? iposr_buf.get(nb + 1) : nullptr;
             lap("base buckets");
         };
         // added entries: positions of I outside the base set.  The main list is
@@ -2019,7 +2037,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         };
         auto set_state = [&]() {  // rem + added for the current I
             W.bmI = bmI;
-            if (nb) k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem);
+            if (nb)
+                k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem, (pos_t*)W.iposr);
             rebuild_added(true);
         };
         // same-slot predecessors (pred5) pay for their scatter when the walks make many

@@ -115,7 +115,7 @@ struct engine {
     dbuf<seg_in> seg_in_buf;
     dbuf<seg_out> seg_out_buf;
     dbuf<u32> seg_ids, irank, ekeys, evals, ekeys2, evals2, occ_buf;
-    dbuf<pos_t> ist, iend, ipos_buf, tail_ins_buf;
+    dbuf<pos_t> ist, iend, ipos_buf, iposr_buf, tail_ins_buf;
     dbuf<u64> seg_offs, counters64;
     // device-resident greedy orchestration (csrc/greedy.hip)
     dbuf<seg_in> g_sin;

@@ -326,6 +326,10 @@ def test_pred_and_bucket_search_paths_vs_oracle(session, orc, lz, kind, mib, mon
     monkeypatch.setenv("LZ77SSS_PRED", "1")
     _, F1 = run(session, T)
     assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    monkeypatch.setenv("LZ77SSS_NO_IPOSR", "1")  # removed flags in their own array, not in the positions
+    _, F3 = run(session, T)
+    assert np.array_equal(F3, F_ref)
+    monkeypatch.delenv("LZ77SSS_NO_IPOSR")
     monkeypatch.delenv("LZ77SSS_PRED")
     monkeypatch.setenv("LZ77SSS_NO_PRED", "1")
     _, F2 = run(session, T)
