@@ -153,7 +153,11 @@ __global__ void k_dense_keys(const u32* __restrict__ keys, u64 m, const u32* __r
 // pass 1 moves (e, pv) pairs into their buckets (per tile: an LDS histogram, one global
 // atomic per non-empty bucket, LDS cursors), pass 2 scatters each bucket's pairs inside
 // its own 1 MiB window of pred5 (L2-local writes)
-constexpr u32 PB_SH = 18;
+#ifndef LZ_PB_SH
+#define LZ_PB_SH 18
+#endif
+constexpr u32 PB_SH = LZ_PB_SH;
+static_assert(((1ull << 32) >> PB_SH) <= (1u << 14), "k_pb_move's LDS histogram holds 2^14 buckets");
 constexpr int PB_T = 1024;
 __global__ void k_pb_init(u32* __restrict__ cursor, u32 nb) {
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
