@@ -143,10 +143,18 @@ __global__ void k_presence_pack(const u8* __restrict__ pf, u64 nw, u32* __restri
 __device__ __forceinline__ u32 slot_rank(const u32* pbm, const u32* pwp, u32 k) {
     return pwp[k >> 5] + __popc(pbm[k >> 5] & ((1u << (k & 31)) - 1u));
 }
+// four keys per thread (16-byte load and store, eight independent table reads in
+// flight): one key per thread left the pass latency-bound (rr: 1.9 TB/s)
 __global__ void k_dense_keys(const u32* __restrict__ keys, u64 m, const u32* __restrict__ pbm,
                              const u32* __restrict__ pwp, u32* __restrict__ dk) {
-    const u64 e = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < m) dk[e] = slot_rank(pbm, pwp, keys[e]);
+    const u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // quad
+    if (4 * q + 3 < m) {
+        const uint4 k = *(const uint4*)(keys + 4 * q);
+        *(uint4*)(dk + 4 * q) = make_uint4(slot_rank(pbm, pwp, k.x), slot_rank(pbm, pwp, k.y),
+                                           slot_rank(pbm, pwp, k.z), slot_rank(pbm, pwp, k.w));
+    } else {
+        for (u64 e = 4 * q; e < m; e++) dk[e] = slot_rank(pbm, pwp, keys[e]);
+    }
 }
 // pred5[e] = pv[t] for the permutation e = svals[t] without a radix sort by e: bucket
 // b holds the 2^PB_SH consecutive ids [b << PB_SH, (b+1) << PB_SH), so its size is known;
@@ -205,11 +213,19 @@ __global__ void k_dense_heads(const u32* __restrict__ sdk, u64 m, u32 D, u32* __
     if (t == 0 || sdk[t - 1] != sdk[t]) dstart[sdk[t]] = (u32)t;
 }
 // slot -> first sorted index with slot >= s: the start of the next present slot's id
+// four slots per thread (one presence word, a 16-byte store)
 __global__ void k_bstart_rank(const u32* __restrict__ pbm, const u32* __restrict__ pwp,
                               const u32* __restrict__ dstart, u32 nslots, u32 D, u32* __restrict__ bstart) {
-    const u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (x > nslots) return;
-    bstart[x] = dstart[x < nslots ? slot_rank(pbm, pwp, (u32)x) : D];
+    const u64 x = 4 * ((u64)blockIdx.x * blockDim.x + threadIdx.x);
+    if (x + 3 < nslots) {
+        const u32 w = pbm[x >> 5], r0 = pwp[x >> 5], sh = (u32)x & 31;  // x, x + 3 share the word
+        const u32 below = w & ((1u << sh) - 1u);
+        const u32 r = r0 + __popc(below);
+        const u32 b0 = (w >> sh) & 1u, b1 = (w >> (sh + 1)) & 1u, b2 = (w >> (sh + 2)) & 1u;
+        *(uint4*)(bstart + x) = make_uint4(dstart[r], dstart[r + b0], dstart[r + b0 + b1], dstart[r + b0 + b1 + b2]);
+    } else {
+        for (u64 y = x; y <= nslots; y++) bstart[y] = dstart[y < nslots ? slot_rank(pbm, pwp, (u32)y) : D];
+    }
 }
 // predecessor entry within the same slot (base set)
 __global__ void k_pred(const u32* __restrict__ skeys, const u32* __restrict__ svals, u64 m, u32* __restrict__ pred5) {
@@ -1023,31 +1039,38 @@ __global__ void k_gap_counts(const pos_t* __restrict__ P, u32 m, u32 CH, pos_t l
     nsegs[k] = (a < b) ? 1 + K : 0;
     ncbs[k] = K;
 }
-__global__ void k_gap_cbv(const pos_t* __restrict__ P, u32 m, u32 CH, pos_t lo, pos_t hi, const u32* __restrict__ cb_off,
-                          pos_t* __restrict__ cbv) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k > m) return;
-    pos_t a, b;
-    gap_in(P, (u32)k, lo, hi, a, b);
-    const u32 K = gap_chunks(a, b, CH);
-    for (u32 t = 1; t <= K; t++) cbv[cb_off[k] + t - 1] = a + (pos_t)t * CH;
-}
-__global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off) {
-    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per gap
-    const u32 lane = threadIdx.x & 63;
-    if (k > S.m) return;
-    pos_t a, b;
-    gap_in(S.P, (u32)k, S.segoff, S.N, a, b);
-    if (a >= b) return;
-    const u32 K = gap_chunks(a, b, CH);
-    for (u32 t = lane; t <= K; t += 64) {
-        const pos_t x = a + (pos_t)t * CH;
-        const u32 id = seg_off[k] + t;
-        S.sin[id] = seg_in{x, (u32)k, x, S.zmask0, upper_cb(S, x)};
-        S.valid[id] = 0;
-        S.succ[id] = NONE;
-        S.seg_at[x - S.segoff] = id;
+// item id (a chunk boundary or a segment) -> its gap: the k with off[k] <= id < off[k+1]
+// (off = exclusive scan over the m + 1 gaps; a gap without items repeats its offset).
+// One thread per item: a long gap (repetitive text: 10^5 chunks in one gap) is spread
+// over the grid instead of being walked by one thread or wave
+__device__ __forceinline__ u32 item_gap(const u32* __restrict__ off, u32 m, u32 id) {
+    u32 lo = 0, hi = m + 1;
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (off[mid] <= id) lo = mid; else hi = mid;
     }
+    return lo;
+}
+__global__ void k_gap_cbv(const pos_t* __restrict__ P, u32 m, u32 CH, pos_t lo, pos_t hi, const u32* __restrict__ cb_off,
+                          u32 ncb, pos_t* __restrict__ cbv) {
+    const u64 id = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= ncb) return;
+    const u32 k = item_gap(cb_off, m, (u32)id);
+    pos_t a, b;
+    gap_in(P, k, lo, hi, a, b);
+    cbv[id] = a + (pos_t)((u32)id - cb_off[k] + 1) * CH;
+}
+__global__ void k_gap_segs(seg_tab S, u32 CH, const u32* __restrict__ seg_off, u32 nseg) {
+    const u64 id = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= nseg) return;
+    const u32 k = item_gap(seg_off, S.m, (u32)id);
+    pos_t a, b;
+    gap_in(S.P, k, S.segoff, S.N, a, b);
+    const pos_t x = a + (pos_t)((u32)id - seg_off[k]) * CH;
+    S.sin[id] = seg_in{x, k, x, S.zmask0, upper_cb(S, x)};
+    S.valid[id] = 0;
+    S.succ[id] = NONE;
+    S.seg_at[x - S.segoff] = (u32)id;
 }
 // bitmaps over text positions (bit q of word q >> 5)
 __device__ __forceinline__ void bm_set_range(u32* bm, pos_t a, pos_t b) {  // [a, b)
@@ -1070,24 +1093,40 @@ __device__ __forceinline__ void bm_set_range_wave(u32* bm, pos_t a, pos_t b, u32
         atomicOr(&bm[w], mask);
     }
 }
-// positions of the window [lo, hi) only, relative to off
-__global__ void k_gap_bitmaps(const pos_t* __restrict__ P, u32 m, pos_t N, pos_t nt, pos_t lo, pos_t hi, pos_t off,
-                              u32* __restrict__ bmI, u32* __restrict__ bmSup) {
-    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per phrase
+// I_0 and the base superset over the window [lo, hi) (relative to off): every gap
+// [a_k, b_k) plus its LPF-start query position b_k, and the interiors of phrases of at
+// most 48 bytes.  The gap parts are set per default segment (one wave each: at most 2 CH
+// positions), the rest per phrase (one thread: at most 48 positions)
+__global__ void k_gap_bitmaps(seg_tab S, u32 CH, const u32* __restrict__ seg_off, u32 nseg, pos_t N, pos_t nt,
+                              pos_t hi, pos_t off, u32* __restrict__ bmI, u32* __restrict__ bmSup) {
+    const u64 id = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per segment
     const u32 lane = threadIdx.x & 63;
+    if (id >= nseg) return;
+    const u32 k = item_gap(seg_off, S.m, (u32)id);  // uniform
+    pos_t a, b;
+    gap_in(S.P, k, S.segoff, S.N, a, b);
+    const u32 t = (u32)id - seg_off[k], K = gap_chunks(a, b, CH);
+    const pos_t x0 = a + (pos_t)t * CH;
+    const pos_t x1 = min(t < K ? x0 + (pos_t)CH : b, min(min(N, nt), hi));
+    if (x0 < x1) {
+        bm_set_range_wave(bmI, x0 - off, x1 - off, lane);
+        bm_set_range_wave(bmSup, x0 - off, x1 - off, lane);
+    }
+}
+__global__ void k_gap_bitmaps_phr(const pos_t* __restrict__ P, u32 m, pos_t N, pos_t nt, pos_t lo, pos_t hi, pos_t off,
+                                  u32* __restrict__ bmI, u32* __restrict__ bmSup) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
     pos_t a, b;
     gap_of(P, (u32)k, a, b);
-    if (a < b) {
-        const pos_t s0 = max(a, lo), e = min(min(min((pos_t)(b + 1), N), nt), hi);
-        if (s0 < e) {
-            bm_set_range_wave(bmI, s0 - off, e - off, lane);
-            bm_set_range_wave(bmSup, s0 - off, e - off, lane);
-        }
+    if (a < b && b >= lo && b < min(min(N, nt), hi)) {  // the query position past the gap
+        const pos_t q = b - off;
+        atomicOr(&bmI[q >> 5], 1u << (q & 31));
+        atomicOr(&bmSup[q >> 5], 1u << (q & 31));
     }
     if (k < m) {
         const pos_t pb = max(P[3 * k], lo), pe = min(min(P[3 * k + 1], nt), hi);
-        if (P[3 * k + 1] - P[3 * k] <= 48 && pb < pe) bm_set_range_wave(bmSup, pb - off, pe - off, lane);
+        if (P[3 * k + 1] - P[3 * k] <= 48 && pb < pe) bm_set_range(bmSup, pb - off, pe - off);
     }
 }
 __global__ void k_bm_xor(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
@@ -1156,6 +1195,9 @@ __global__ __launch_bounds__(BMB_T) void k_bmb_write(M mk, u64 nw, const u64* __
     __shared__ u64 wsum[BMB_T / 64];
     const u32 l = threadIdx.x, lane = l & 63, wv = l >> 6;
     u64 base = blockIdx.x ? bincl[blockIdx.x - 1] : 0ull;
+    // a block without marked bits writes nothing (uniform exit; sparse bitmaps of
+    // repetitive text skip almost every block instead of 8 scan rounds each)
+    if (bincl[blockIdx.x] == base) return;
     for (u32 r = 0; r < BMB_W; r++) {
         const u64 w = (u64)blockIdx.x * BMB + (u64)r * BMB_T + l;
         u32 a = 0, b = 0;
@@ -1717,7 +1759,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         LZ_HIP(hipMemcpyAsync(&ncb, off_cb + m + 1, 4, hipMemcpyDeviceToHost, st));
         LZ_HIP(hipStreamSynchronize(st));
         pos_t* cbv = g_cbv.get(ncb + 1);
-        k_gap_cbv<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, a, bw, off_cb, cbv);
+        if (ncb) k_gap_cbv<<<cdiv(ncb, 256), 256, 0, st>>>(P, m, CH, a, bw, off_cb, ncb, cbv);
         u32 cap = nseg0 + nseg0 / 2 + (1u << 16);
         seg_tab S{};
         auto bind_tab = [&]() {
@@ -1745,7 +1787,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         LZ_HIP(hipMemsetAsync(S.nseg, 0, 8, st));
         LZ_HIP(hipMemcpyAsync(S.nseg, &nseg0, 4, hipMemcpyHostToDevice, st));
         S.cbv = cbv; S.ncb = ncb; S.P = P; S.m = m; S.N = bw; S.zmask0 = zmask0;
-        k_gap_segs<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(S, CH, off_seg);
+        if (nseg0) k_gap_segs<<<cdiv(nseg0, 256), 256, 0, st>>>(S, CH, off_seg, nseg0);
         u32* d_c0 = (u32*)(counters64.p + 1);
         static_assert(sizeof(seg_in) <= 12 * sizeof(u64), "entry slot");
         seg_in* d_entry = (seg_in*)(counters64.p + 4);
@@ -1757,7 +1799,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         u32* bmT = g_bmT.get(nw);
         LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
         LZ_HIP(hipMemsetAsync(bmT, 0, nw * 4, st));
-        k_gap_bitmaps<<<cdiv((u64)(m + 1) * 64, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmT);
+        if (nseg0)
+            k_gap_bitmaps<<<cdiv((u64)nseg0 * 64, 256), 256, 0, st>>>(S, CH, off_seg, nseg0, N, G.nt, hi_ins, off, bmI, bmT);
+        k_gap_bitmaps_phr<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmT);
         u32 hn[2];
         LZ_HIP(hipMemcpyAsync(hn, S.nseg, 8, hipMemcpyDeviceToHost, st));
         u32 c0 = 0;
@@ -1925,7 +1969,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 if (dense) {
                     // (a transform iterator mapping the ids inside the sort was slower: rr sort
                     // passes +234 us against this pass's 211 us)
-                    k_dense_keys<<<cdiv(ne5, 256), 256, 0, st>>>(keys, ne5, pbm, pwp, skeys);
+                    k_dense_keys<<<cdiv(cdiv(ne5, 4), 256), 256, 0, st>>>(keys, ne5, pbm, pwp, skeys);
                     sk_in = skeys;
                     skeys = g_sdk.get(ne5 + 1);
                     sbits = dense_bits;
@@ -1976,7 +2020,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             if (dense) {
                 u32* dstart = g_dstart.get((u64)D + 1);
                 if (ne5 >= pred_sorted_min) k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
-                k_bstart_rank<<<cdiv((u64)nslots + 1, 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
+                k_bstart_rank<<<cdiv(cdiv((u64)nslots + 1, 4), 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
                                                                           g_bstart.get((u64)nslots + 1));
             } else {
                 build_buckets(key_u32{skeys}, ne5, g_bstart);

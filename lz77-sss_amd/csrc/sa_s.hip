@@ -53,12 +53,15 @@ __global__ void k_scatter_rank(const u32* __restrict__ idx, const u32* __restric
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < s) R[idx[t]] = rank[t];
 }
-__global__ void k_pack_pairs(const u32* __restrict__ R, u32 s, u32 h, u32 bits, u64* __restrict__ kv,
+// the q ranks R[k], R[k+h], .., R[k+(q-1)h] (0 past the end) as one radix key: the
+// next level ranks rank-string prefixes q times as long (q = 64 / bits, at most 4)
+__global__ void k_pack_pairs(const u32* __restrict__ R, u32 s, u64 h, u32 bits, u32 q, u64* __restrict__ kv,
                              u32* __restrict__ idx) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s) return;
-    const u64 r2 = (k + h < s) ? R[k + h] : 0;
-    kv[k] = ((u64)R[k] << bits) | r2;
+    u64 key = R[k];
+    for (u32 j = 1; j < q; j++) key = (key << bits) | ((k + j * h < s) ? R[k + j * h] : 0u);
+    kv[k] = key;
     idx[k] = (u32)k;
 }
 __global__ void k_pair_diff(const u64* __restrict__ kv, u32 s, u32* __restrict__ flag) {
@@ -75,7 +78,7 @@ __global__ void k_sa_from_rank(const u32* __restrict__ R, u32 s, u32* __restrict
 }
 
 struct rank_levels {
-    u32 nlev;
+    u32 nlev, step;  // level lv ranks prefixes of step^lv key ranks
     const u32* R[MAX_LV];
 };
 
@@ -87,9 +90,15 @@ __global__ void k_lcp(const u8* __restrict__ T, u64 n, const pos_t* __restrict__
     if (r == 0) { LCP[0] = 0; return; }
     const u32 a = SA[r - 1], b = SA[r];
     u64 c = 0;
-    for (int lv = (int)RL.nlev - 1; lv >= 0; lv--) {
-        const u64 w = 1ull << lv;
-        if (a + c < s && b + c < s && RL.R[lv][a + c] == RL.R[lv][b + c]) c += w;
+    u64 w = 1;  // span of the top level
+    for (u32 lv = 1; lv < RL.nlev; lv++) w *= RL.step;
+    // the top level ranks are all distinct; below level lv + 1 the common prefix left is
+    // shorter than step * w: at most step - 1 steps of w per level
+    for (int lv = (int)RL.nlev - 1; lv >= 0; lv--, w /= RL.step) {
+        for (u32 t = 1; t < RL.step; t++) {
+            if (a + c < s && b + c < s && RL.R[lv][a + c] == RL.R[lv][b + c]) c += w;
+            else break;
+        }
     }
     u64 v;
     if (a + c >= s) v = n - S[a];
@@ -602,6 +611,10 @@ void engine::build_sa_s(const u8* T) {
     // ---- prefix doubling over the sequence of key ranks
     u32 bits = 1;
     while (bits < 32 && (1ull << bits) <= s) bits++;
+    // ranks per radix key: a small sync set (repetitive text) packs 3-4 ranks into the
+    // 64-bit key and needs half the rounds, each a chain of small sort launches
+    const u32 q = std::min<u32>(4, 64 / bits);
+    rank_step = q;
     u64* kv = u64a.get(s);
     u64* kv2 = u64b.get(s);
     // every round's max rank goes to pinned memory behind its launches, and is read
@@ -611,13 +624,14 @@ void engine::build_sa_s(const u8* T) {
     int pending = -1;  // slot of the last round whose max rank is in flight
     while (maxr < s) {
         if (nlev_rank >= MAX_LV) throw error(-6, "prefix doubling did not converge");
-        const u32 h = 1u << (nlev_rank - 1);
+        u64 h = 1;
+        for (u32 l = 1; l < nlev_rank; l++) h *= q;
         const u32* R = rank_lv[nlev_rank - 1].p;
-        k_pack_pairs<<<g, 256, 0, st>>>(R, s, h, bits, kv, idx_in);
+        k_pack_pairs<<<g, 256, 0, st>>>(R, s, h, bits, q, kv, idx_in);
         size_t tb = 0;
-        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kv, kv2, idx_in, idx, (int)s, 0, (int)(2 * bits), st));
+        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kv, kv2, idx_in, idx, (int)s, 0, (int)(q * bits), st));
         u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, kv, kv2, idx_in, idx, (int)s, 0, (int)(2 * bits), st));
+        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, kv, kv2, idx_in, idx, (int)s, 0, (int)(q * bits), st));
         k_pair_diff<<<g, 256, 0, st>>>(kv2, s, flag);
         scan_incl(flag, rank, s, scan_tmp, st);
         u32* Rn = rank_lv[nlev_rank].get(s);
@@ -647,6 +661,7 @@ void engine::build_lcp_rmq(const u8* T) {
     const unsigned g = cdiv(s, 256);
     rank_levels RL{};
     RL.nlev = nlev_rank;
+    RL.step = rank_step;
     for (u32 i = 0; i < nlev_rank; i++) RL.R[i] = rank_lv[i].p;
     u32* L0 = lcp_rmq[0].get(s);
     k_lcp<<<g, 256, 0, st>>>(T, n, S.p, key_len.p, SA.p, s, RL, runs(), L0);

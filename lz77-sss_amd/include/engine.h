@@ -89,6 +89,7 @@ struct engine {
     dbuf<u32> rank_lv[MAX_LV];       // R_h per doubling level (for LCP binary lifting)
     dbuf<u32> lcp_rmq[MAX_LV];       // sparse table levels over LCP
     u32 nlev_rank = 0, nlev_rmq = 0;
+    u32 rank_step = 2;  // SA_S prefix doubling: ranks per radix key (level lv spans rank_step^lv)
     dbuf<u32> succ_tab;              // bucket -> first sync index with S >= bucket*512
     dbuf<u8> tmp_bytes, tmp_bytes2, tmp_bytes3, scan_tmp;
     dbuf<u64> u64a, u64b;
