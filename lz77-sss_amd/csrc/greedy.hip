@@ -1797,11 +1797,13 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         u32* bmI2 = g_bmI2.get(nw);
         u32* bmIb = g_bmIb.get(nw);
         u32* bmT = g_bmT.get(nw);
+        // the superset goes straight into Ib (the first base set); the scratch bitmap is
+        // always fully overwritten before it is read
         LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
-        LZ_HIP(hipMemsetAsync(bmT, 0, nw * 4, st));
+        LZ_HIP(hipMemsetAsync(bmIb, 0, nw * 4, st));
         if (nseg0)
-            k_gap_bitmaps<<<cdiv((u64)nseg0 * 64, 256), 256, 0, st>>>(S, CH, off_seg, nseg0, N, G.nt, hi_ins, off, bmI, bmT);
-        k_gap_bitmaps_phr<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmT);
+            k_gap_bitmaps<<<cdiv((u64)nseg0 * 64, 256), 256, 0, st>>>(S, CH, off_seg, nseg0, N, G.nt, hi_ins, off, bmI, bmIb);
+        k_gap_bitmaps_phr<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmIb);
         u32 hn[2];
         LZ_HIP(hipMemcpyAsync(hn, S.nseg, 8, hipMemcpyDeviceToHost, st));
         u32 c0 = 0;
@@ -2109,7 +2111,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         if (max_outer == 0) {
             wfact = seq_complete(nullptr, 0, nullptr, nullptr, true);
         } else {
-            build_base(bmT);  // superset: gaps + short phrase interiors
+            build_base(bmIb);  // superset: gaps + short phrase interiors
             set_state();
             bool restart_seq = false;  // a walk overflowed or linking ran away: complete from the entry
             for (;; outer++) {

@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B of the SSS-phase knobs on rr (kernel traces of the last step's SSS phase):
-#   base: this build; g0: LZ77SSS_QT_GRID=0 (one workgroup per tile); nsl: LZ77SSS_SSS_NOSKIPLOAD=1
+# A/B of SSS-phase variants on rr (kernel traces of the last step's SSS phase).  The knobs
+# (LZ77SSS_QT_GRID, LZ77SSS_SSS_NOSKIPLOAD) belonged to the reverted round-2c experiment.
 set -eo pipefail
 REPO=$(pwd); OUT=$REPO/gpurun_out; mkdir -p "$OUT"
 WL=${1:-rr}
