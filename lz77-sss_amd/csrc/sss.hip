@@ -37,7 +37,10 @@ namespace LZ_NS {
 // staged in LDS.
 constexpr int SNB = 64;                       // decision blocks per stripe (k_sss_stream)
 constexpr int SD = SNB * (int)TAU;            // decisions per stripe (32768)
-constexpr int QT_THREADS = 256;
+#ifndef LZ_QT_THREADS
+#define LZ_QT_THREADS 128  // k_q_anchors workgroup (anchors per tile + 3 halo); rr: 256 -> 623 us, 128 -> 576 us, 64 -> 580 us
+#endif
+constexpr int QT_THREADS = LZ_QT_THREADS;
 constexpr int QT_OWN = QT_THREADS - 3;                  // owned anchors per workgroup
 constexpr int QT_LDS = QT_THREADS * (int)QA + 256 + 1024;
 constexpr u32 RUN_HCAP = 640;                           // local run extension: [a-256, a+640)
