@@ -171,7 +171,9 @@ __global__ void k_pb_init(u32* __restrict__ cursor, u32 nb) {
     const u32 b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < nb) cursor[b] = b << PB_SH;
 }
-__global__ __launch_bounds__(PB_T) void k_pb_move(const u32* __restrict__ svals, const u32* __restrict__ pv, u64 m,
+// (the sorted-order predecessor of entry svals[t] is svals[t-1] when skeys[t-1] == skeys[t],
+// computed here instead of in a pass of its own)
+__global__ __launch_bounds__(PB_T) void k_pb_move(const u32* __restrict__ svals, const u32* __restrict__ skeys, u64 m,
                                                   u64 tile, u32 nb, u32* __restrict__ cursor, u64* __restrict__ tmp) {
     __shared__ u32 h[1u << 14];  // nb <= 2^32 >> PB_SH
     const int tid = (int)threadIdx.x;
@@ -185,8 +187,9 @@ __global__ __launch_bounds__(PB_T) void k_pb_move(const u32* __restrict__ svals,
     __syncthreads();
     for (u64 t = t0 + tid; t < t1; t += PB_T) {
         const u32 e = svals[t];
+        const u32 pv = (t > 0 && skeys[t - 1] == skeys[t]) ? svals[t - 1] : NONE;
         const u32 p = atomicAdd(&h[e >> PB_SH], 1u);
-        tmp[p] = ((u64)e << 32) | pv[t];
+        tmp[p] = ((u64)e << 32) | pv;
     }
 }
 __global__ void k_pb_apply(const u64* __restrict__ tmp, u64 m, u32* __restrict__ pred5) {
@@ -1097,17 +1100,20 @@ __device__ __forceinline__ void bm_set_range_wave(u32* bm, pos_t a, pos_t b, u32
 // [a_k, b_k) plus its LPF-start query position b_k, and the interiors of phrases of at
 // most 48 bytes.  The gap parts are set per default segment (one wave each: at most 2 CH
 // positions), the rest per phrase (one thread: at most 48 positions)
-__global__ void k_gap_bitmaps(seg_tab S, u32 CH, const u32* __restrict__ seg_off, u32 nseg, pos_t N, pos_t nt,
-                              pos_t hi, pos_t off, u32* __restrict__ bmI, u32* __restrict__ bmSup) {
+__global__ void k_gap_bitmaps(seg_tab S, u32 nseg, pos_t N, pos_t nt, pos_t hi, pos_t off, u32* __restrict__ bmI,
+                              u32* __restrict__ bmSup) {
     const u64 id = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per segment
     const u32 lane = threadIdx.x & 63;
     if (id >= nseg) return;
-    const u32 k = item_gap(seg_off, S.m, (u32)id);  // uniform
+    // the segment table (k_gap_segs) holds each segment's start and gap; a segment ends
+    // where the next one of its gap starts, the last one at the (clipped) gap end
+    const seg_in g = S.sin[id];
+    const u32 k = g.p;
     pos_t a, b;
     gap_in(S.P, k, S.segoff, S.N, a, b);
-    const u32 t = (u32)id - seg_off[k], K = gap_chunks(a, b, CH);
-    const pos_t x0 = a + (pos_t)t * CH;
-    const pos_t x1 = min(t < K ? x0 + (pos_t)CH : b, min(min(N, nt), hi));
+    const pos_t x0 = g.start;
+    const bool more = id + 1 < nseg && S.sin[id + 1].p == k;
+    const pos_t x1 = min(more ? S.sin[id + 1].start : b, min(min(N, nt), hi));
     if (x0 < x1) {
         bm_set_range_wave(bmI, x0 - off, x1 - off, lane);
         bm_set_range_wave(bmSup, x0 - off, x1 - off, lane);
@@ -1802,7 +1808,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
         LZ_HIP(hipMemsetAsync(bmIb, 0, nw * 4, st));
         if (nseg0)
-            k_gap_bitmaps<<<cdiv((u64)nseg0 * 64, 256), 256, 0, st>>>(S, CH, off_seg, nseg0, N, G.nt, hi_ins, off, bmI, bmIb);
+            k_gap_bitmaps<<<cdiv((u64)nseg0 * 64, 256), 256, 0, st>>>(S, nseg0, N, G.nt, hi_ins, off, bmI, bmIb);
         k_gap_bitmaps_phr<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmIb);
         u32 hn[2];
         LZ_HIP(hipMemcpyAsync(hn, S.nseg, 8, hipMemcpyDeviceToHost, st));
@@ -1994,9 +2000,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 } else if (W.use_pred) {
                     // pred5[e] = predecessor of entry e in its slot: the sorted-order predecessors
                     // moved back to entry order (a random scatter of 4-byte writes is ~3x slower)
-                    u32* pv = vals;  // the unsorted values are no longer needed
-                    k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
                     if (std::getenv("LZ77SSS_PRED_RADIX")) {  // reference path: radix sort by entry id
+                        u32* pv = vals;  // the unsorted values are no longer needed
+                        k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
                         u32* kdump = g_predk.get(ne5 + 1);
                         int eb = 1;
                         while (eb < 32 && (1ull << eb) < ne5) eb++;
@@ -2013,7 +2019,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                         const u32 ntile = (u32)std::min<u64>(1024, cdiv(ne5, PB_T));
                         const u64 tile = (ne5 + ntile - 1) / ntile;
                         k_pb_init<<<cdiv(nbk, 256), 256, 0, st>>>(cursor, nbk);
-                        k_pb_move<<<ntile, PB_T, 0, st>>>(svals, pv, ne5, tile, nbk, cursor, tmp);
+                        k_pb_move<<<ntile, PB_T, 0, st>>>(svals, skeys, ne5, tile, nbk, cursor, tmp);
                         k_pb_apply<<<cdiv(ne5, 256), 256, 0, st>>>(tmp, ne5, pred5);
                     }
                 }
