@@ -336,6 +336,36 @@ def test_pred_and_bucket_search_paths_vs_oracle(session, orc, lz, kind, mib, mon
     assert np.array_equal(F2, F_ref)
 
 
+CHUNKS_PROBE = ["16", "64", "128", "256", "512", "1024", "100000"]
+
+
+@pytest.mark.parametrize("chunk", CHUNKS_PROBE)
+@pytest.mark.parametrize("name", golden_names())
+def test_gap_chunk_lengths_golden(session, name, chunk, monkeypatch, request):
+    """Every chunk length must give the fixture's stream.  Known defect: chunks
+    of 128 positions or fewer change one factor source on c1_seed2; the default (512) and every
+    length >= 256 match all fixtures and tests."""
+    if name == "c1_seed2" and int(chunk) <= 128:
+        request.node.add_marker(pytest.mark.xfail(reason="chunk length <= 128 diverges on c1_seed2", strict=False))
+    g = load_golden(name)
+    monkeypatch.setenv("LZ77SSS_GAP_CHUNK", chunk)
+    _, F = run(session, g["text"])
+    assert np.array_equal(F, g["factors"])
+
+
+@pytest.mark.parametrize("chunk", CHUNKS_PROBE)
+@pytest.mark.parametrize("kind,mib", [("genome", 8), ("rr", 16)])
+def test_gap_chunk_lengths_vs_oracle(session, orc, lz, kind, mib, chunk, monkeypatch):
+    """Long gaps are cut into chunks of LZ77SSS_GAP_CHUNK positions whose walks converge onto
+    the chain at a shared factor start: every chunk length gives the oracle stream."""
+    n = mib << 20
+    T = lz.gen_genome(n, 1 << 20, 0.001, 19) if kind == "genome" else lz.gen_random_repetitive(n, n, 21, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    monkeypatch.setenv("LZ77SSS_GAP_CHUNK", chunk)
+    _, F = run(session, T)
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
 # ---- bounded greedy completion (k_seq_walk): the exact sequential walk from the confirmed chain prefix
 
 @pytest.mark.parametrize("max_outer", [0, 1, 2])
