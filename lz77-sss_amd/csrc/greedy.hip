@@ -1032,13 +1032,16 @@ __device__ __forceinline__ void gap_in(const pos_t* P, u32 k, pos_t lo, pos_t hi
     a = max(a, lo);
     b = min(b, hi);
 }
-__global__ void k_gap_counts(const pos_t* __restrict__ P, u32 m, u32 CH, pos_t lo, pos_t hi, u32* __restrict__ nsegs,
-                             u32* __restrict__ ncbs) {
+// chunk boundaries stay below the tail region (cmax = nt): a chunk walk starting inside
+// it would walk tail positions without the tail model's stale-fingerprint semantics
+__global__ void k_gap_counts(const pos_t* __restrict__ P, u32 m, u32 CH, pos_t lo, pos_t hi, pos_t cmax,
+                             u32* __restrict__ nsegs, u32* __restrict__ ncbs) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;
     pos_t a, b;
     gap_in(P, (u32)k, lo, hi, a, b);
-    const u32 K = gap_chunks(a, b, CH);
+    u32 K = gap_chunks(a, b, CH);
+    if (K) K = min(K, a < cmax ? (u32)((cmax - a - 1) / CH) : 0u);  // boundaries a + t CH < cmax
     nsegs[k] = (a < b) ? 1 + K : 0;
     ncbs[k] = K;
 }
@@ -1757,7 +1760,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         u32* cnt_cb = g_tmp2.get(m + 2);
         u32* off_seg = g_tmp3.get(m + 2);
         u32* off_cb = g_tmp4.get(m + 2);
-        k_gap_counts<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, a, bw, cnt_seg, cnt_cb);
+        k_gap_counts<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, CH, a, bw, G.nt, cnt_seg, cnt_cb);
         excl_scan_nr(cnt_seg, off_seg, m + 1, scan_tmp, st);
         excl_scan_nr(cnt_cb, off_cb, m + 1, scan_tmp, st);
         u32 nseg0, ncb;
