@@ -75,7 +75,7 @@ struct engine {
     // filter pass of build_sss: hit words per stripe, marked tiles, re-run stripes
     dbuf<u64> sss_hitw;
     dbuf<u8> sss_tflag;
-    dbuf<u32> sss_tiles, sss_sflag, sss_slist;
+    dbuf<u32> sss_tiles, sss_sflag, sss_slist, sss_fcnt;
     u64 stats_sss_tiles = 0;
     run_tab runs() const {
         run_tab R;
