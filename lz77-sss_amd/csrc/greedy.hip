@@ -2229,6 +2229,10 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                         tin.idxpos = entry_in.idxpos;
                         tin.zmask = entry_in.zmask;
                     }
+                    if (dbg)
+                        std::fprintf(stderr, "[lz77sss-debug] greedy tail entry: start=%llu p=%u idxpos=%llu zmask=%u lim=%llu nall=%u\n",
+                                     (unsigned long long)tin.start, tin.p, (unsigned long long)tin.idxpos, tin.zmask,
+                                     (unsigned long long)tin.lim, nall);
                     tail_bound = (u64)N - tin.start + 1;
                     pos_t* fo = fact.get(2 * (chain_fact + tail_bound) + 2);
                     u64* d_tc = (u64*)g_tailc.get(4 * sizeof(u64));
