@@ -141,7 +141,8 @@ void engine::prepare_phrases(int phr_mode, bool external_sss) {
 
 void engine::set_sss(const pos_t* S_any, u64 count, bool runs) {
     LZ_HIP(hipSetDevice(device));
-    if (count >= (1ull << 32)) throw error(LZ77SSS_EINVAL, "sync set too large");
+    // the same bound as build_sss: SA_S / LPF pass item counts to hipcub / rocprim as int
+    if (count >= 0x7FFFFFFFull) throw error(LZ77SSS_EINVAL, "sync set too large");
     pos_t* d = S.get(count + 1);
     if (count) LZ_HIP(hipMemcpyAsync(d, S_any, count * sizeof(pos_t), hipMemcpyDefault, st));
     LZ_HIP(hipStreamSynchronize(st));
@@ -262,6 +263,7 @@ struct engine64_impl final : lz::engine_if {
         return block_prepare(E, phr_mode, external_sss, log2_override);
     }
     void* carried_table() override { return E.g_Hs.p; }
+    u64 carried_bytes() const override { return E.g_Hs.cap * sizeof(pos_t); }
     u64 greedy_block(u32 rk_seed, int log2_override, u64* st) override { return block_run(E, rk_seed, log2_override, st); }
 };
 }  // namespace lz64
@@ -790,9 +792,9 @@ LZ77SSS_API int lz77sss_session_carried_copy(lz77sss_session* s, void* buf, uint
     if (!s || (!buf && bytes)) return LZ77SSS_EINVAL;
     return guarded([&] {
         void* tab = s->E64 ? s->E64->carried_table() : (void*)s->E.g_Hs.p;
-        const uint64_t cap = s->E64 ? 0 : s->E.g_Hs.cap * sizeof(lz::pos_t);
+        const uint64_t cap = s->E64 ? s->E64->carried_bytes() : s->E.g_Hs.cap * sizeof(lz::pos_t);
         if (!tab) throw lz::error(LZ77SSS_EINVAL, "no carried table: call lz77sss_session_prepare first");
-        if (!s->E64 && bytes > cap) throw lz::error(LZ77SSS_EINVAL, "carried table smaller than the copy");
+        if (bytes > cap) throw lz::error(LZ77SSS_EINVAL, "carried table smaller than the copy");
         const int dev = s->E64 ? s->E64->device() : s->E.device;
         hipStream_t st = s->E64 ? s->E64->stream() : s->E.st;
         LZ_HIP(hipSetDevice(dev));

@@ -526,13 +526,17 @@ __device__ void walk_segment(const walk_ctx& W, seg_in in, seg_out* __restrict__
                 idx = i;
             }
             do {
+                // the tail test comes first: a chunk walk that stopped at its boundary on a
+                // factor start >= nt would hand the tail walk a start past the positions its
+                // last factor advanced over in the tail region (conditional inserts,
+                // rolling_hash_index_107.hpp:121-127), which the tail model then never sees
+                if (i >= nt) { flags |= 1; finish(); return; }
                 if (i >= in.lim) {  // chunk boundary reached: stop at the next factor start
                     next = i;
                     e = i;
                     finish();
                     return;
                 }
-                if (i >= nt) { flags |= 1; finish(); return; }
                 if (++guard > guard_max || i > n) { flags |= 4; finish(); return; }
                 if (!WRITE && first_gap && nb < SEG_NBND) og->bnd[nb++] = i;
                 pos_t fsrc, flen;
@@ -1742,13 +1746,18 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
     int outer_all = 0, rounds_all = 0, nwin = 0;
     u32 nseg_last = 0, nseg0_all = 0;
     lce_view Lv = view(T);
+    // a non-last window (or block) whose chain reaches the tail region (a gap factor
+    // longer than the >= 4096 positions left after the window end) is walked again as the
+    // last window: the tail model needs every insert in the tail region before its start
+    bool force_last = false;
 
     for (;;) {
         const pos_t a = entry.start;
         // the window [a, bw): non-last windows end below the tail region (nt) and leave >= 4096 positions
-        pos_t bw = target_end;
-        if (WS < (u64)(target_end - a) && (u64)a + WS + 4096 <= (u64)G.nt) bw = (pos_t)(a + WS);
+        pos_t bw = force_last ? N : target_end;
+        if (!force_last && WS < (u64)(target_end - a) && (u64)a + WS + 4096 <= (u64)G.nt) bw = (pos_t)(a + WS);
         const bool last = bw == N;
+        bool redo = false;
         const pos_t off = a & ~(pos_t)31;  // bitmap origin (word aligned)
         const u64 nw = (u64)(bw - off) / 32 + 2;  // bitmap words (a zero word past the end)
         const unsigned gw = cdiv(nw, 256);
@@ -1864,6 +1873,10 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             LZ_HIP(hipMemcpyAsync(hc, d_sq, 32, hipMemcpyDeviceToHost, st));
             LZ_HIP(hipStreamSynchronize(st));
             if (hc[1]) throw error(-6, "greedy: sequential completion guard tripped (internal error)");
+            if (!last && hc[2] >= (u64)G.nt) {
+                redo = true;  // the hand-over point lies in the tail region
+                return 0;
+            }
             if (!last) {
                 exit_in.start = (pos_t)hc[2];
                 exit_in.idxpos = (pos_t)hc[3];
@@ -2198,6 +2211,10 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 }
                 // ---- the chain, its factor offsets, the tail
                 const bool tail = cs.flags & 1;
+                if (tail && !last) {
+                    redo = true;
+                    break;
+                }
                 const u32 nall = cs.hops + 1, nchain = nall - (tail ? 1u : 0u);
                 u32* chain = g_chain.get(nall + 1);
                 k_chain_expand<<<cdiv(nall, 256), 256, 0, st>>>(JL, nall, c0, chain);
@@ -2377,6 +2394,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         }
         k_seg_at_clear<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
         seg_at_clean = true;
+        if (redo) {
+            if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy window %d reaches the tail region: walked again as the last\n", nwin);
+            force_last = true;
+            stats[19] = 0;
+            continue;
+        }
         outer_all += max_outer == 0 ? 0 : outer + 1;
         rounds_all += rounds_total;
         walked_all += walked_total;

@@ -881,8 +881,8 @@ __global__ void k_sss_marks(const u64* __restrict__ hitw, u64 nstripes, u64 ntil
 // zeros to a multiple of 16 * 1024 bytes; each thread owns a run of 16-byte words.
 // Flag bytes (0/1) -> the sorted list of flagged indices.  Block b owns the 16-byte
 // words [1024 b, 1024 b + 1024) (16 Ki flags; one word per thread): k_flag_count
-// writes the block's count, k_flag_list adds the counts of the blocks before it (at
-// most a few dozen) and writes its indices in order.  (One workgroup over all the
+// writes the block's count, k_flag_list adds the counts of the blocks before it (a
+// workgroup-parallel sum) and writes its indices in order.  (One workgroup over all the
 // flags took 43 us for the 67 K tiles of a 1 GiB run-heavy text.)
 constexpr u32 FL_T = 1024;
 __device__ __forceinline__ u32 flag_word_count(const u8* __restrict__ flag, u64 nwords, u64 w, uint4& v) {
@@ -906,14 +906,24 @@ __global__ __launch_bounds__(FL_T) void k_flag_count(const u8* __restrict__ flag
 __global__ __launch_bounds__(FL_T) void k_flag_list(const u8* __restrict__ flag, u64 nwords, const u32* __restrict__ bcnt,
                                                     u32* __restrict__ list, u32* __restrict__ cnt) {
     __shared__ u32 s_w[FL_T / 64];
+    __shared__ u32 s_part[FL_T / 64];
     __shared__ u32 s_base;
     const u32 t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const u64 w = (u64)blockIdx.x * FL_T + t;
-    if (t == 0) {
+    {
+        // the counts of the blocks before this one, summed by the whole workgroup (a 2^40-byte
+        // text has ~4 K blocks: a one-thread sum per block would be quadratic in total)
         u32 b = 0;
-        for (u32 k = 0; k < blockIdx.x; k++) b += bcnt[k];
-        s_base = b;
-        if (blockIdx.x + 1 == gridDim.x) *cnt = b + bcnt[blockIdx.x];
+        for (u32 k = t; k < blockIdx.x; k += FL_T) b += bcnt[k];
+        for (int o = 32; o >= 1; o >>= 1) b += __shfl_xor(b, o);
+        if (lane == 0) s_part[wv] = b;
+        __syncthreads();
+        if (t == 0) {
+            u32 tot = 0;
+            for (u32 k = 0; k < FL_T / 64; k++) tot += s_part[k];
+            s_base = tot;
+            if (blockIdx.x + 1 == gridDim.x) *cnt = tot + bcnt[blockIdx.x];
+        }
     }
     uint4 v;
     const u32 c = flag_word_count(flag, nwords, w, v);

@@ -40,6 +40,7 @@ struct engine_if {
     virtual void set_sss(const u64* S_any, u64 count, bool runs) = 0;
     virtual u64 prepare(int phr_mode, bool external_sss, int log2_override) = 0;  // returns carried-table bytes
     virtual void* carried_table() = 0;
+    virtual u64 carried_bytes() const = 0;   // capacity of the carried table
     virtual u64 greedy_block(u32 rk_seed, int log2_override, u64* state /* start, idxpos, zmask, carried, end,
                                                                         exit_start, exit_idxpos, exit_zmask */) = 0;
 };

@@ -4,13 +4,13 @@
 #   2. PMC passes FETCH_SIZE, WRITE_SIZE over the SSS-phase kernels (separate runs)
 # tools/summarize_profile2.py turns gpurun_out/ into profiles/<tag>_<wl>_*.
 set -eo pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 WL=${2:-rr}
 REPO=$(pwd)
 OUT=$REPO/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-KR='k_sss_stream|k_sss_marks|k_flag_list|k_q_anchors|k_run_keys|k_run_apply|k_sss_compact'
+KR='k_sss_stream|k_sss_marks|k_flag_count|k_flag_list|k_q_anchors|k_run_keys|k_run_apply|k_sss_compact'
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_${TAG}_${WL}" -o run -- \
     python3 "$REPO/tools/prof_step.py" "$WL" 3 > "$OUT/prof_${TAG}_${WL}.log" 2>&1
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -f csv -d "$OUT/pmc_${TAG}_${WL}_fetch" -o run -- \
