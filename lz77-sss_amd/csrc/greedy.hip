@@ -2398,6 +2398,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy window %d reaches the tail region: walked again as the last\n", nwin);
             force_last = true;
             stats[19] = 0;
+            stats[23]++;
             continue;
         }
         outer_all += max_outer == 0 ? 0 : outer + 1;

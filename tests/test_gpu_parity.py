@@ -460,12 +460,24 @@ def _run_into_tail_text(n_rand=20000, run_len=19960, n_end=40, seed=5):
 
 @pytest.mark.parametrize("max_outer", [256, 0])
 @pytest.mark.parametrize("window", [4096, 8192])
-@pytest.mark.parametrize("n_end", [40, 60, 63, 64, 65, 100])
-def test_greedy_window_chain_reaches_tail(session, orc, window, max_outer, n_end, monkeypatch):
-    """A non-last window whose chain reaches the tail region (one gap factor crossing the window
-    end and n - 64) is walked again as the last window; the stream equals the oracle's."""
-    T = _run_into_tail_text(n_end=n_end)
+@pytest.mark.parametrize("run_len", [19960, 19995])
+@pytest.mark.parametrize("n_end", [1, 2, 5, 20])
+def test_greedy_window_chain_reaches_tail(session, orc, window, max_outer, run_len, n_end, monkeypatch):
+    """A non-last window whose chain reaches the tail region is walked again as the last window;
+    the stream equals the oracle's.  With 1-2 trailing bytes the run has no sync position near
+    its end, so the gap factor from 20 001 runs through every window end into the last 64
+    positions (checked on the oracle stream); with more, an LPF phrase truncates it first."""
+    T = _run_into_tail_text(run_len=run_len, n_end=n_end)
+    n = T.size
+    F_ref = orc.factorize(T)[0]
+    L = np.maximum(F_ref[:, 1].astype(np.int64), 1)
+    ends = np.cumsum(L)
+    crosses = bool(np.any((L > 4096) & (ends >= n - 64) & (ends < n)))
+    assert crosses == (n_end <= 2)
     monkeypatch.setenv("LZ77SSS_GREEDY_WINDOW", str(window))
     monkeypatch.setenv("LZ77SSS_GREEDY_MAX_OUTER", str(max_outer))
-    _, F = run(session, T)
-    assert np.array_equal(F, orc.factorize(T)[0])
+    s, F = run(session, T)
+    assert np.array_equal(F, F_ref)
+    # stats[23]: windows walked again as the last one (the sequential completion also re-walks
+    # a window whose hand-over point an LPF factor carried past n - 64)
+    assert s.stats()[23] >= 1 if crosses else (max_outer == 0 or s.stats()[23] == 0)
