@@ -39,6 +39,8 @@ void engine::load(const u8* h_text, u64 n_) {
     if (n_ > max_n) throw error(LZ77SSS_EINVAL, "text larger than the session capacity");
     LZ_HIP(hipSetDevice(device));
     n = n_;
+    runs_valid = false;
+    brk_valid = false;
     if (n) LZ_HIP(hipMemcpyAsync(d_text, h_text, n, hipMemcpyHostToDevice, st));
     LZ_HIP(hipMemsetAsync(d_text + n, 0, TEXT_PAD, st));
     LZ_HIP(hipStreamSynchronize(st));
@@ -105,10 +107,21 @@ u64 engine::emit_skip_phrases() {
 
 void engine::prepare_phrases(int phr_mode, bool external_sss) {
     const bool dbg = debug_enabled();
+    if (std::getenv("LZ77SSS_LCE_DEBUG") && !lce_dbg) {
+        LZ_HIP(hipMalloc(&lce_dbg, 8 * sizeof(unsigned long long)));
+        LZ_HIP(hipMemset(lce_dbg, 0, 8 * sizeof(unsigned long long)));
+    }
     auto trace = [&](const char* what) {
         if (!dbg) return;
         LZ_HIP(hipStreamSynchronize(st));
         std::fprintf(stderr, "[lz77sss-debug] done %s (|S|=%u phrases=%u)\n", what, s, num_phr);
+        if (lce_dbg) {
+            unsigned long long c[8];
+            LZ_HIP(hipMemcpy(c, lce_dbg, sizeof(c), hipMemcpyDeviceToHost));
+            LZ_HIP(hipMemset(lce_dbg, 0, sizeof(c)));
+            std::fprintf(stderr, "[lz77sss-debug]   lce fwd calls=%llu steps=%llu skips=%llu exact=%llu max_steps=%llu | bwd calls=%llu steps=%llu skips=%llu\n",
+                         c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7]);
+        }
     };
     if (phr_mode == LZ77SSS_LPF_OPT || phr_mode == LZ77SSS_LPF_NAIVE) {
         if (external_sss) {

@@ -192,10 +192,19 @@ __global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, cons
         const u64 b0 = (u64)(c - first) * KH_CHUNK, b1 = min<u64>(len, b0 + KH_CHUNK);
         u64 h = 0;
         u32 pp = 0;  // period of a run holding the whole piece (and the word after it), else 0
-        if (R.p && b1 == b0 + KH_CHUNK && b1 + 8 <= len) {
-            const u64 x0 = beg + b0, t = (x0 + 127) >> 7;
-            const u32 p = R.p[t];
-            if (p && (u64)R.lo[t] <= x0 && (u64)R.hi[t] >= x0 + KH_CHUNK + 8) pp = p;
+        if (b1 == b0 + KH_CHUNK && b1 + 8 <= len) {
+            const u64 x0 = beg + b0;
+            // a piece inside a p-periodic stretch of the block run records
+            if (R.re) {
+                const u64 bb = (x0 + 511) >> 9;
+                const u64 v = R.re[bb], u = R.rs[bb];
+                if ((v & 255) && (u >> 16) <= x0 && (v >> 16) >= x0 + KH_CHUNK + 8) pp = (u32)(v & 255);
+            }
+            if (!pp && R.p) {
+                const u64 t = (x0 + 127) >> 7;
+                const u32 p = R.p[t];
+                if (p && (u64)R.lo[t] <= x0 && (u64)R.hi[t] >= x0 + KH_CHUNK + 8) pp = p;
+            }
         }
         if (pp) {
             const u32 L = pp / min(pp & (0u - pp), 8u), NW = KH_CHUNK / 8;

@@ -27,6 +27,9 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+#include <vector>
+
 
 namespace LZ_NS {
 
@@ -819,6 +822,517 @@ stripe_done:
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_sss_runs: the exact sync set of the stripes pass 1 stopped (a confirmed filter hit in a
+// decision block), in one pass over the stripe when its periodic windows lie in runs.
+//
+// For a period p, a p-break is a position z with T[z] != T[z+p]; a window T[j..j+512) is
+// p-periodic iff it holds no p-break in [j, j+511-p].  A window in Q (period q <= 170) that is
+// not p-periodic holds no p-periodic stretch of p + 170 bytes: such a stretch has the periods p
+// and q and is longer than p + q - gcd(p, q), so gcd(p, q) is one of its periods (Fine-Wilf);
+// as it covers q consecutive bytes of the window, the window has the period gcd(p, q) | p and
+// would be p-periodic.  With the period p of the current run every window of a block is
+//   p-periodic                       -> in Q
+//   holding a p-periodic stretch of p + 170 bytes -> not in Q
+//   without a hit of its filter anchor (sss_filter has no false negatives) -> not in Q
+// and the windows none of this settles (at a change of period) are classified again with the
+// smallest period of the first of them.  A stripe that still has unsettled windows is left to
+// the exact Q-anchor path (k_q_anchors + the QSKIP re-run).  Run-heavy text (rr: nearly every
+// window periodic, periods 1..170) is thereby settled in this one pass.  The kernel also writes
+// the per-block run records of the LCE (lce_dev.h run_tab::bp).
+
+// bit e <=> byte e of d is nonzero
+__device__ __forceinline__ u32 byte_mask8(u64 d) {
+    auto m4 = [](u32 x) -> u32 {
+        u32 t = x | (x >> 4);
+        t |= t >> 2;
+        t |= t >> 1;
+        t &= 0x01010101u;
+        return ((t * 0x00204081u) >> 21) & 0xFu;  // bytes 0..3 -> bits 21..24
+    };
+    return m4((u32)d) | (m4((u32)(d >> 32)) << 4);
+}
+__device__ __forceinline__ u32 mask_le(int t) { return t < 0 ? 0u : t >= 7 ? 0xFFu : ((2u << t) - 1u); }        // e <= t
+__device__ __forceinline__ u32 mask_ge(int t) { return t <= 0 ? 0xFFu : t > 7 ? 0u : ((0xFFu << t) & 0xFFu); }  // e >= t
+
+// Classification of the windows j = 8 lane + e of a block k with the period p, from the
+// p-differences T[z] ^ T[z+p] of the lane's positions in blocks k (pd0) and k + 1 (pd1).
+// Returns the lane's mask of p-periodic windows; *u = the windows it does not settle.
+// Positions are block-relative; a window's p-breaks lie in [j, j + 511 - p].
+__device__ u32 q_classify(u64 pd0, u64 pd1, u32 p, u32 lane, u32& u) {
+    constexpr u32 NB = 1u << 12;  // no p-break
+    const u32 m0 = byte_mask8(pd0), m1 = byte_mask8(pd1);
+    const u32 b0 = 8 * lane, b1 = 512 + 8 * lane;
+    const int hb0 = m0 ? 31 - __builtin_clz(m0) : -1, hb1 = m1 ? 31 - __builtin_clz(m1) : -1;
+    const u32 f0 = m0 ? b0 + __builtin_ctz(m0) : NB, f1 = m1 ? b1 + __builtin_ctz(m1) : NB;
+    const u32 S1 = wave_suffix_min(f1, lane);
+    const u32 S0n = dpp<0x130>(NB, wave_suffix_min(f0, lane)), S1n = dpp<0x130>(NB, S1);
+    const u32 F1 = (u32)__builtin_amdgcn_readlane((int)S1, 0);
+    const u32 nx0 = min(S0n, F1), nx1 = S1n;  // first p-break past the lane's positions in block k / k+1
+    // a p-break followed by 170 positions without one (a p-periodic stretch of p + 170 bytes
+    // after it): only a lane's highest p-break can be one
+    const u32 la0 = (m0 && nx0 >= b0 + (u32)hb0 + 171u) ? b0 + (u32)hb0 : NB;
+    const u32 la1 = (m1 && nx1 >= b1 + (u32)hb1 + 171u) ? b1 + (u32)hb1 : NB;
+    const u32 SL0n = dpp<0x130>(NB, wave_suffix_min(la0, lane));
+    const u32 L1 = (u32)__builtin_amdgcn_readlane((int)wave_suffix_min(la1, lane), 0);
+    const u32 R = min(SL0n, L1);  // the first such p-break past the lane's positions
+    const int ip = (int)p, rb = (int)b0;
+    const u32 above = hb0 < 0 ? 0xFFu : ((0xFFu << (hb0 + 1)) & 0xFFu);   // no p-break of the lane in [e, 8)
+    const u32 per = above & mask_le((int)nx0 - rb - 512 + ip);             // none in [j, j + 511 - p]
+    const u32 longA = above & mask_le((int)nx0 - rb - 170);                // none in [j, j + 169]
+    const u32 longB = (la0 != NB ? mask_le(hb0) : 0u) | mask_ge((int)R - rb - 341 + ip);  // one at z <= j + 341 - p
+    u = ~per & ~(longA | longB) & 0xFFu;
+    return per;
+}
+// the smallest period q <= 170 of T[j..j+512) (0: none).  Lane l tests q = base + l; wrong
+// candidates fail at their first differing word
+__device__ u32 find_period(const u8* __restrict__ T, u64 j, u32 lane) {
+    for (u32 base = 1; base <= QL; base += 64) {
+        const u32 q = base + lane;
+        bool ok = q <= QL;
+        if (ok) {
+            const u32 len = TAU - q;
+            for (u32 o = 0; o < len; o += 8) {
+                u64 a = ldu64(T + j + o), c = ldu64(T + j + q + o);
+                const u32 r = len - o;
+                if (r < 8) {
+                    const u64 m = (1ull << (8 * r)) - 1;
+                    a &= m;
+                    c &= m;
+                }
+                if (a != c) {
+                    ok = false;
+                    break;
+                }
+            }
+        }
+        const u64 bal = __ballot(ok);
+        if (bal) return base + (u32)__builtin_ctzll(bal);
+    }
+    return 0;
+}
+// 8 bytes at byte offset 8 lane + p of the 1024-byte concatenation [Bx, By] of two blocks in
+// registers (p <= 170): the lane's words lane + p/8 and lane + p/8 + 1, by cross-lane moves
+__device__ __forceinline__ u64 shfl64(u64 v, u32 src) {
+    return ((u64)(u32)__shfl((int)(u32)(v >> 32), (int)src, 64) << 32) | (u32)__shfl((int)(u32)v, (int)src, 64);
+}
+__device__ __forceinline__ u64 shifted8(u64 Bx, u64 By, u32 p, u32 lane) {
+    const u32 q = p >> 3, sh = 8 * (p & 7);
+    const u32 src = (lane + q) & 63;
+    const u64 a = shfl64(Bx, src), c = shfl64(By, src);
+    const u64 w0 = lane + q >= 64 ? c : a;
+    if (!sh) return w0;
+    // word lane + q + 1: lane + 1's w0; for lane 63 word 64 + q, i.e. By's lane q
+    u64 w1 = ((u64)dpp<0x130>(0u, (u32)(w0 >> 32)) << 32) | dpp<0x130>(0u, (u32)w0);
+    if (lane == 63)
+        w1 = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(By >> 32), (int)q) << 32) |
+             (u32)__builtin_amdgcn_readlane((int)(u32)By, (int)q);
+    return (w0 >> sh) | (w1 << (64 - sh));
+}
+// first / last nonzero byte of a wave's 512 p-differences (block offsets), -1 if none
+__device__ __forceinline__ int first_diff(u64 d) {
+    const u64 b = __ballot(d != 0);
+    if (!b) return -1;
+    const u32 L = (u32)__builtin_ctzll(b);
+    const u64 v = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(d >> 32), (int)L) << 32) |
+                  (u32)__builtin_amdgcn_readlane((int)(u32)d, (int)L);
+    return (int)(8 * L + (__builtin_ctzll(v) >> 3));
+}
+__device__ __forceinline__ int last_diff(u64 d) {
+    const u64 b = __ballot(d != 0);
+    if (!b) return -1;
+    const u32 L = 63u - (u32)__builtin_clzll(b);
+    const u64 v = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(d >> 32), (int)L) << 32) |
+                  (u32)__builtin_amdgcn_readlane((int)(u32)d, (int)L);
+    return (int)(8 * L + ((63 - __builtin_clzll(v)) >> 3));
+}
+
+__global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__ T, u64 n, u64 last_i, u64 nstripes,
+                                                        pos_t* __restrict__ s_out, u32* __restrict__ s_cnt,
+                                                        u32* __restrict__ s_flag, u32* __restrict__ ovf_ctr, u32 b,
+                                                        sss_pow32 PW, u32 scap, u64* __restrict__ hitw,
+                                                        u8* __restrict__ blk_p, u16* __restrict__ blk_fo,
+                                                        u16* __restrict__ blk_lo, u64 nbk, u32* __restrict__ any_q,
+                                                        u32* __restrict__ dbg) {
+    // a ring of 4 blocks per wave in LDS: the bytes at offset p of a block are two aligned word
+    // reads (the block after it follows in the ring)
+    __shared__ u64 s_ring[SWAVES][256];
+    const u32 lane = threadIdx.x & 63;
+    u64* ring = s_ring[threadIdx.x >> 6];
+    const u64 w = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (w >= nstripes) return;
+    if (!(hitw[3 * w + 2] >> 63)) return;  // settled by pass 1
+    const u64 i0 = w * (u64)SD;
+    const u64 jmax = n - TAU;
+    const u64 ilim = min<u64>(last_i - i0, (u64)SD - 1);
+    const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
+    const u32 kend = (u32)min<u64>((jmax + 1 - i0) / TAU, 0xFFFFFFFFull);
+    const u64 gk0 = i0 / TAU;
+    u32 pwl = 1, ibl = PW.ib8;
+    {
+        u32 f = PW.b8, g = PW.ib8;
+        for (int d = 0; d < 6; d++) {
+            if (lane & (1u << d)) {
+                pwl *= f;
+                ibl *= g;
+            }
+            f *= f;
+            g *= g;
+        }
+    }
+    const u32 nB = 0u - PW.B;
+    auto load8 = [&](u64 k) -> u64 { return *(const u64*)(T + i0 + k * TAU + 8 * lane); };
+    // (other lanes read the words: a wavefront fence orders the write before their reads)
+    auto put_ring = [&](u32 k, u64 B) {
+        ring[(k & 3) * 64 + lane] = B;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // bytes at offset 8 lane + p of block k (blocks k, k + 1 in the ring)
+    auto ring_shift = [&](u32 k, u32 p) -> u64 {
+        const u32 o = (k & 3) * 64 + lane + (p >> 3), sh = 8 * (p & 7);
+        const u64 lo = ring[o & 255];
+        if (!sh) return lo;
+        const u64 hi = ring[(o + 1) & 255];
+        return (lo >> sh) | (hi << (64 - sh));
+    };
+    auto block_prefix = [&](u64 bytes, u32& carry, u32* h) {
+        const u32 lo = (u32)bytes, hi = (u32)(bytes >> 32);
+        u32 c[8], loc[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) c[e] = ((e < 4 ? lo : hi) >> (8 * (e & 3))) & 255u;
+        loc[0] = 0;
+#pragma unroll
+        for (int e = 1; e < 8; e++) loc[e] = loc[e - 1] * b + c[e - 1];
+        const u32 h8 = loc[7] * b + c[7];
+        const u32 g = h8 * ibl;
+        const u32 G = wave_prefix_add(g);
+        const u32 hl = (carry + (G - g)) * pwl;
+        h[0] = hl;
+#pragma unroll
+        for (int e = 1; e < 8; e++) h[e] = hl * PW.pwb[e] + loc[e];
+        carry = (carry + (u32)__builtin_amdgcn_readlane((int)G, 63)) * PW.B;
+    };
+    auto valid_mask = [&](u32 k) -> u32 {
+        if (k < kend) return 0xFFu;
+        const u64 j0 = i0 + (u64)k * TAU + 8 * lane;
+        return jmax >= j0 ? mask_le((int)min<u64>(jmax - j0, 7)) : 0u;
+    };
+    // filter anchor hits of window j = 8 lane + e of a block: A0, A1 of the block (bits 0, 1),
+    // A0 of the next (bit 2)
+    auto hit_mask = [&](u32 hits) -> u32 {
+        if (lane == 0) return ((hits & 1) ? 1u : 0u) | ((hits & 2) ? 0xFEu : 0u);
+        if (lane < 32) return (hits & 2) ? 0xFFu : 0u;
+        if (lane == 32) return ((hits & 2) ? 1u : 0u) | ((hits & 4) ? 0xFEu : 0u);
+        return (hits & 4) ? 0xFFu : 0u;
+    };
+    // the smallest p <= 170 with T[z] == T[z+p] for every z of ring block k (bytes Bx), 0 if none
+    auto block_period = [&](u32 k, u64 Bx) -> u32 {
+        for (u32 q = 1; q <= QL; q++)
+            if (!__ballot(ring_shift(k, q) != Bx)) return q;
+        return 0;
+    };
+
+    u32 p = 1;  // the period of the current run
+    bool fail = false, anyq = false;
+    u32 nout = 0;
+    u32 n_cls = 0, n_find = 0;  // slow classifications, period searches (debug counters)
+    pos_t* out = s_out + w * SCAP;
+    // run records of the stripe's blocks, lane k holding block k's (stored together at the end):
+    // the period when the block is p-extendable (rp), the first break in it of the period in
+    // effect before it (rf: the exact end of the previous block's run), at a segment start the
+    // last break of its period in the block before (rl: the exact start of its run).  Offsets + 1;
+    // 0 = unknown, 0xFFFF = no such break (lce_dev.h run_tab)
+    u32 rp = 0, rf = 0, rl = 0, prev_rec = 0;
+    auto put_rec = [&](u32 k, bool ext, int fo, int lo) {
+        const u32 rec = ext ? p : 0u;
+        const u32 f = fo == -2 ? 0u : fo < 0 ? 0xFFFFu : (u32)(fo + 1);
+        if (lane == k) {
+            rp = rec;
+            rf = f;
+            if (lo >= -1) rl = lo < 0 ? 0xFFFFu : (u32)(lo + 1);
+        }
+        prev_rec = rec;
+    };
+    // last break of period p in ring block k - 1 (block k follows): the exact start of a new run
+    auto seg_lo = [&](u32 k, u64 Bprev) -> int { return last_diff(Bprev ^ ring_shift(k - 1, p)); };
+
+    // Q mask of block k (bytes B0k, B1k of blocks k, k + 1; ring holds k .. k + 2; p-differences
+    // pd0, pd1 of blocks k, k + 1 for the current period, updated when it changes), slow path
+    auto classify = [&](u32 k, u64 B0k, u64 B1k, u64& pd0, u64& pd1) -> u32 {
+        const u32 vm = valid_mask(k);
+        u32 u;
+        n_cls++;
+        u32 q = q_classify(pd0, pd1, p, lane, u);
+        u &= vm;
+        if (__ballot(u != 0)) {
+            const u32 h = sss_filter(B0k, lane) | ((sss_filter(B1k, lane) & 1u) << 2);
+            u &= hit_mask(h);
+            // a change of period: classify again with the smallest period of block k + 1 (where
+            // the windows of block k end), then of block k, then of the first unsettled window;
+            // the period that settles them is kept for the blocks after
+            for (int t = 0; t < 3 && __ballot(u != 0); t++) {
+                u32 p2;
+                if (t == 0) {
+                    p2 = block_period(k + 1, B1k);
+                } else if (t == 1) {
+                    p2 = block_period(k, B0k);
+                } else {
+                    const u64 ub = __ballot(u != 0);
+                    const u32 L = (u32)__builtin_ctzll(ub);
+                    const u32 e = (u32)__builtin_ctz((u32)__builtin_amdgcn_readlane((int)u, (int)L));
+                    p2 = find_period(T, i0 + (u64)k * TAU + 8 * L + e, lane);
+                }
+                n_find++;
+                if (!p2 || p2 == p) continue;
+                const u64 qd0 = B0k ^ ring_shift(k, p2), qd1 = B1k ^ ring_shift(k + 1, p2);
+                u32 u2;
+                q |= q_classify(qd0, qd1, p2, lane, u2);
+                u &= u2;
+                p = p2;
+                pd0 = qd0;
+                pd1 = qd1;
+            }
+            if (__ballot(u != 0)) fail = true;
+        }
+        q &= vm;
+        if (__ballot(q != 0)) anyq = true;
+        return q;
+    };
+    auto phi = [&](u32 k, const u32* h0, const u32* h1, u32 q, u32* v) {
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = h0[e] * nB + h1[e];
+        u32 bits = q;
+        if (k >= kend) {
+            const u64 j0 = i0 + (u64)k * TAU + 8 * lane;
+            const u64 keep = jmax >= j0 ? min<u64>(jmax - j0 + 1, 8) : 0;
+            bits |= 0xFFu & ~((1u << keep) - 1u);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] |= 0u - ((bits >> e) & 1u);
+    };
+
+    // prologue: blocks 0 .. 2 in the ring, up to 6 in flight; block 0 classified, Phi'(0)
+    u64 Bp = 0, Bk = load8(0), Bk1 = load8(1), B3 = load8(2), B4 = load8(3), B5 = load8(4), B6 = load8(5),
+        B7 = load8(6);
+    put_ring(0, Bk);
+    put_ring(1, Bk1);
+    put_ring(2, B3);
+    u64 pdk = Bk ^ ring_shift(0, 1), pdk1 = Bk1 ^ ring_shift(1, 1);
+    bool z1 = __ballot(pdk1 != 0) != 0;
+    u32 hc[8], hn[8], x[8], y[8];  // Hp of block c+1 (hc), of block c+2 (hn); Phi' of blocks c, c+1
+    u32 carry = 0;
+    int hk = -1;  // the block whose Hp is in hc (prefix hashes continue from carry after it)
+    bool fx;
+    {
+        const bool z0 = __ballot(pdk != 0) != 0;
+        u32 q0 = 0xFFu;
+        fx = !z0 && !z1;
+        if (!fx) {
+            q0 = classify(0, Bk, Bk1, pdk, pdk1);
+            z1 = __ballot(pdk1 != 0) != 0;
+        } else if (i0 <= jmax) {
+            anyq = true;
+        }
+        put_rec(0, __ballot(pdk != 0) == 0, -2, -2);
+        if (!fx) {
+            block_prefix(Bk, carry, hc);
+            block_prefix(Bk1, carry, hn);
+            phi(0, hc, hn, q0, x);
+#pragma unroll
+            for (int e = 0; e < 8; e++) hc[e] = hn[e];
+            hk = 1;
+        }
+    }
+    const bool fail_pro = fail;  // block 0 unsettled
+    u32 c = 0;
+    for (; c < nblk && !fail; c++) {
+        // blocks c .. c + 6 in registers (Bp .. B6), c + 7 in flight; the ring gets block c + 3
+        Bp = Bk;
+        Bk = Bk1;
+        Bk1 = B3;
+        B3 = B4;
+        B4 = B5;
+        B5 = B6;
+        B6 = B7;
+        B7 = load8(c + 7);  // six blocks ahead (the text pad covers the stripe's end)
+        put_ring(c + 3, B3);
+        const u32 k = c + 1;
+        pdk = pdk1;
+        const bool z0 = z1;
+        pdk1 = Bk1 ^ ring_shift(k + 1, p);
+        z1 = __ballot(pdk1 != 0) != 0;
+        const int fok = z0 ? first_diff(pdk) : -1;  // before a change of period: the end of the last run
+        bool allk = !z0 && !z1;  // no p-break in blocks k, k + 1: every window of block k is p-periodic
+        u32 qk = 0xFFu;
+        if (!allk) {
+            qk = classify(k, Bk, Bk1, pdk, pdk1);
+            z1 = __ballot(pdk1 != 0) != 0;
+        } else if (i0 + (u64)k * TAU <= jmax) {
+            anyq = true;
+        }
+        if (fail) break;
+        const bool ext = __ballot(pdk != 0) == 0;
+        put_rec(k, ext, fok, (ext && p != prev_rec) ? seg_lo(k, Bp) : -2);
+        // Phi'(block k)
+        if (!allk) {
+            if (hk != (int)k) {  // restart the prefix hash at block k (Phi is origin-free)
+                carry = 0;
+                block_prefix(Bk, carry, hc);
+            }
+            block_prefix(Bk1, carry, hn);
+            phi(k, hc, hn, qk, y);
+#pragma unroll
+            for (int e = 0; e < 8; e++) hc[e] = hn[e];
+            hk = (int)k + 1;
+        }
+        // decisions of block c from Phi'(c) = x and Phi'(c+1) = y
+        if (!(fx && allk)) {
+            u32 xx[8], yy[8];
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                xx[e] = fx ? INF32 : x[e];
+                yy[e] = allk ? INF32 : y[e];
+            }
+            u32 sx[8], py[8];
+            sx[7] = xx[7];
+#pragma unroll
+            for (int e = 6; e >= 0; e--) sx[e] = min(xx[e], sx[e + 1]);
+            py[0] = yy[0];
+#pragma unroll
+            for (int e = 1; e < 8; e++) py[e] = min(py[e - 1], yy[e]);
+            const u32 sufL = wave_suffix_min(sx[0], lane), preL = wave_prefix_min(py[7]);
+            const u32 suf_after = dpp<0x130>(INF32, sufL);
+            const u32 pre_before = dpp<0x138>(INF32, preL);
+            const u32 g = min(min(suf_after, pre_before), INF32 - 1);
+            u64 M[8];
+            u64 U = 0;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                M[e] = __ballot(min(xx[e], yy[e]) == min3u(sx[e], g, py[e]));
+                U |= M[e];
+            }
+            if (U) {
+                u32 mb = 0;
+#pragma unroll
+                for (int e = 0; e < 8; e++) mb |= __builtin_amdgcn_inverse_ballot_w64(M[e]) ? (1u << e) : 0u;
+                const u64 rem = ilim - (u64)c * TAU;
+                if (rem < (u64)TAU - 1) {
+                    const int lim = (int)rem - (int)(8 * lane);
+                    mb = lim < 0 ? 0u : lim >= 7 ? mb : (mb & ((2u << lim) - 1u));
+                }
+                const u32 cnt = (u32)__popc(mb);
+                const pos_t base = (pos_t)(i0 + (u64)c * TAU + 8 * lane);
+                const u32 incl = wave_prefix_add(cnt);
+                u32 o = nout + incl - cnt;
+                for (u32 m = mb; m; m &= m - 1) {
+                    if (o < (u32)SCAP) out[o] = base + (pos_t)__builtin_ctz(m);
+                    o++;
+                }
+                nout += (u32)__builtin_amdgcn_readlane((int)incl, 63);
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) x[e] = y[e];
+        fx = allk;
+    }
+    if (fail) {
+        // the exact Q-anchor path takes the stripe; its remaining blocks still get their run
+        // records (the LCE consults them on both sides of a comparison)
+        const u32 k0 = fail_pro ? 1u : c + 1;
+        u64 Bq = fail_pro ? Bk : Bp, B0x = fail_pro ? Bk1 : Bk, B1x = fail_pro ? B3 : Bk1;
+        for (u32 kk = k0; kk < (u32)SNB; kk++) {
+            if (kk > k0) {
+                Bq = B0x;
+                B0x = B1x;
+                B1x = load8(kk + 1);
+            }
+            u64 pd = B0x ^ shifted8(B0x, B1x, p, lane);
+            const int fo = first_diff(pd);
+            if (__ballot(pd != 0)) {
+                u32 p2 = 0;
+                for (u32 q = 1; q <= QL && !p2; q++)
+                    if (!__ballot(shifted8(B0x, B1x, q, lane) != B0x)) p2 = q;
+                if (p2) {
+                    p = p2;
+                    pd = 0;
+                }
+            }
+            const bool ext = __ballot(pd != 0) == 0;
+            put_rec(kk, ext, fo, (ext && p != prev_rec) ? last_diff(Bq ^ shifted8(Bq, B0x, p, lane)) : -2);
+        }
+    }
+    // the stripe's run records, one store per lane
+    if (gk0 + lane < nbk) {
+        blk_p[gk0 + lane] = (u8)rp;
+        blk_fo[gk0 + lane] = (u16)rf;
+        blk_lo[gk0 + lane] = (u16)rl;
+    }
+    // a stripe whose sync set overflows goes to the exact path too (k_sss_fallback reads the Q
+    // intervals of k_q_anchors)
+    if (nout > scap) fail = true;
+    if (lane == 0) {
+        if (dbg) {  // (same-address atomics from every wave serialize: debug runs only)
+            atomicAdd(dbg + 0, n_cls);
+            atomicAdd(dbg + 1, n_find);
+            atomicAdd(dbg + 2, fail ? 1u : 0u);
+        }
+        if (fail) return;  // left to the Q-anchor path (still forced)
+        hitw[3 * w] = 0;
+        hitw[3 * w + 1] = 0;
+        hitw[3 * w + 2] = 1ull << 62;  // settled here
+        // one flag for the whole text: no atomic once it is visible
+        if (anyq && __hip_atomic_load(any_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(any_q, 1u);
+        const u32 fl = nout > scap ? 1u : 0u;
+        const u32 old = s_flag[w];
+        s_cnt[w] = nout;
+        s_flag[w] = fl;
+        if (fl != old) atomicAdd(ovf_ctr, fl ? 1u : 0xFFFFFFFFu);
+    }
+}
+// per-block run end / start packed for one-load lookups (lce_dev.h run_tab::re / rs): the
+// segment's end made exact by the first break of its period in the block after it (fo), its
+// start by the last break in the block before it (lo); offsets + 1, 0 = unknown, 0xFFFF = none
+// in that block (a bound one block further)
+__global__ void k_blk_runinfo(const u8* __restrict__ bp, const u16* __restrict__ fo, const u16* __restrict__ lo,
+                              const pos_t* __restrict__ ser, const pos_t* __restrict__ ss, u64 nbk,
+                              u64* __restrict__ re, u64* __restrict__ rs) {
+    const u64 b = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nbk) return;
+    const u64 p = bp[b];
+    if (!p) {
+        re[b] = 0;
+        rs[b] = 0;
+        return;
+    }
+    const u64 se = ser[nbk - 1 - b], eb = se >> 9;
+    u64 e = se + p, xe = 0;
+    if (eb < nbk) {
+        const u32 f = fo[eb];
+        if (f == 0xFFFFu) e = se + TAU + p;
+        else if (f) { e = se + (f - 1) + p; xe = 1; }
+    }
+    const u64 s0 = ss[b], sb = s0 >> 9;
+    u64 st = s0, xs = 0;
+    if (sb) {
+        const u32 l = lo[sb];
+        if (l == 0xFFFFu) st = s0 - TAU;
+        else if (l) { st = s0 - TAU + l; xs = 1; }
+    }
+    re[b] = (e << 16) | (xe << 8) | p;
+    rs[b] = (st << 16) | (xs << 8) | p;
+}
+// run-record segment markers: ends (stored reversed, for a min-scan) and starts (max-scan)
+__global__ void k_blk_marks(const u8* __restrict__ bp, u64 nbk, pos_t* __restrict__ end_rev, pos_t* __restrict__ beg) {
+    const u64 b = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nbk) return;
+    const u32 p = bp[b];
+    const bool cont_f = p && b + 1 < nbk && bp[b + 1] == p, cont_b = p && b > 0 && bp[b - 1] == p;
+    end_rev[nbk - 1 - b] = cont_f ? (pos_t)~(pos_t)0 : (pos_t)((b + 1) * TAU);
+    beg[b] = cont_b ? (pos_t)0 : (pos_t)(b * TAU);
+}
+
 // Per stripe: the re-run list starts with the stripes whose own blocks had a confirmed
 // filter hit; per tile of 253 anchors: marked when a filter anchor A with A/128 in
 // [first anchor, last anchor + 1] was hit (a window in Q with exact anchor a has its
@@ -830,8 +1344,10 @@ __global__ void k_sss_marks(const u64* __restrict__ hitw, u64 nstripes, u64 ntil
                             u8* __restrict__ run_p) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < nstripes) {
-        const bool forced = (hitw[3 * i + 2] >> 63) != 0;
-        sflag[i] = forced ? 1u : 0u;
+        // forced: pass 1 stopped the stripe and k_sss_runs could not settle it (bit 63); settled by
+        // k_sss_runs (bit 62): exact already, never appended to the re-run by k_q_anchors
+        const bool forced = (hitw[3 * i + 2] >> 63) != 0, settled = ((hitw[3 * i + 2] >> 62) & 1) != 0;
+        sflag[i] = (forced || settled) ? 1u : 0u;
         if (forced) slist[atomicAdd(scnt, 1u)] = (u32)i;
     }
     if (i < ntiles) {
@@ -1082,6 +1598,7 @@ void engine::run_chains(u64 nanch, const u32* tiles, u64 m) {
 // needs them for the LCE); returns whether some window is in Q
 bool engine::build_q_runs(const u8* T) {
     runs_valid = false;
+    brk_valid = false;
     if (n < 2 * (u64)TAU) return false;
     const u64 nanch = (n - TAU) / QA + 2;
     u16* qi = q_info.get(nanch + 64);
@@ -1115,6 +1632,7 @@ void engine::build_sss(const u8* T) {
     runs_valid = false;
     stats_fallback_lanes = 0;
     stats_sss_tiles = 0;
+    brk_valid = false;
     if (n < 2 * (u64)TAU) return;
     const u64 last_i = n - 2 * TAU;
     const u64 nanch = (n - TAU) / QA + 2;
@@ -1126,7 +1644,7 @@ void engine::build_sss(const u8* T) {
     pos_t* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
     u32* ctr = counters.get(16);
-    LZ_HIP(hipMemsetAsync(ctr, 0, 8 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes
+    LZ_HIP(hipMemsetAsync(ctr, 0, 12 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes; 8..10: k_sss_runs counters
     pos_t* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
@@ -1152,6 +1670,20 @@ void engine::build_sss(const u8* T) {
     k_sss_stream<false, true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(
         T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, hw, qi, rp, nullptr, nullptr);
     LZ_HIP(hipGetLastError());
+    // the stripes pass 1 stopped: settled in one pass where their periodic windows are runs
+    // (k_sss_runs), which also writes the per-block run records of the LCE
+    const u64 nbk = (n + TAU - 1) / TAU;
+    u8* bp = blk_p.get(nbk + 1);
+    LZ_HIP(hipMemsetAsync(bp, 0, nbk + 1, st));
+    u16* bfo = blk_fo.get(nbk + 1);
+    u16* blo = blk_lo.get(nbk + 1);
+    LZ_HIP(hipMemsetAsync(bfo, 0, 2 * (nbk + 1), st));  // 0: unknown
+    LZ_HIP(hipMemsetAsync(blo, 0, 2 * (nbk + 1), st));
+    if (!std::getenv("LZ77SSS_NO_RUNS_KERNEL"))  // test knob: every stopped stripe through the Q-anchor path
+        k_sss_runs<<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, nlanes, lo, lc, lf, ctr + 1,
+                                                                (u32)SSS_BASE, PW, scap, hw, bp, bfo, blo, nbk, ctr + 0,
+                                                                debug_enabled() ? ctr + 8 : nullptr);
+    LZ_HIP(hipGetLastError());
     // tiles the filter marked; anchors past the last stripe's own start out empty
     const u64 nblk_last = std::min<u64>(SNB, (last_i - (nlanes - 1) * SD) / TAU + 1);
     const u64 t_tail = (nlanes - 1) * (SD / QA) + 4 * nblk_last, q_end = nanch + 64;
@@ -1171,6 +1703,12 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipStreamSynchronize(st));
     const u32 ndirty = hp[0];
     stats_sss_tiles = ndirty;
+    if (debug_enabled()) {
+        u32 dc[3];
+        LZ_HIP(hipMemcpy(dc, ctr + 8, 12, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[lz77sss-debug] sss: k_sss_runs slow classifications=%u period searches=%u unsettled stripes=%u tiles=%u\n",
+                     dc[0], dc[1], dc[2], ndirty);
+    }
     if (ndirty) {
         k_q_anchors<<<ndirty, QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap, tl, sfl, sl, ctr + 3,
                                                    nlanes);
@@ -1185,6 +1723,47 @@ void engine::build_sss(const u8* T) {
         LZ_HIP(hipGetLastError());
     }
     runs_valid = true;  // period 0 outside the marked tiles
+    if (nbk < 0x7FFFFFFFull) {  // (hipcub item counts are int: texts below 2^40 bytes)
+        // run-record segments: ends by a min-scan over the reversed markers, starts by a max-scan
+        pos_t* mk = blk_mk.get(2 * nbk);
+        pos_t* ser = blk_ser.get(nbk);
+        pos_t* bss = blk_ss.get(nbk);
+        k_blk_marks<<<cdiv(nbk, 256), 256, 0, st>>>(bp, nbk, mk, mk + nbk);
+        size_t tb = 0, tb2 = 0;
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, mk, ser, hipcub::Min(), (int)nbk, st));
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
+        u8* t = scan_tmp.get(std::max(tb, tb2));
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, mk, ser, hipcub::Min(), (int)nbk, st));
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
+        k_blk_runinfo<<<cdiv(nbk, 256), 256, 0, st>>>(bp, bfo, blo, ser, bss, nbk, blk_re.get(nbk), blk_rs.get(nbk));
+        LZ_HIP(hipGetLastError());
+        brk_nbk = nbk;
+        brk_valid = true;
+        if (debug_enabled()) {
+            std::vector<u8> hb(nbk);
+            LZ_HIP(hipMemcpy(hb.data(), bp, nbk, hipMemcpyDeviceToHost));
+            u64 cnt[4] = {0, 0, 0, 0}, seg = 0;
+            for (u64 i = 0; i < nbk; i++) {
+                cnt[hb[i] == 0 ? 0 : hb[i] == 1 ? 1 : hb[i] <= 16 ? 2 : 3]++;
+                if (hb[i] && (i == 0 || hb[i - 1] != hb[i])) seg++;
+            }
+            std::fprintf(stderr, "[lz77sss-debug] sss: run records: blocks=%llu none=%llu p1=%llu p2-16=%llu p17+=%llu segments=%llu\n",
+                         (unsigned long long)nbk, (unsigned long long)cnt[0], (unsigned long long)cnt[1],
+                         (unsigned long long)cnt[2], (unsigned long long)cnt[3], (unsigned long long)seg);
+            if (nbk <= 64) {
+                std::vector<u16> hf(nbk), hl(nbk);
+                std::vector<pos_t> hse(nbk), hss(nbk);
+                LZ_HIP(hipMemcpy(hf.data(), bfo, 2 * nbk, hipMemcpyDeviceToHost));
+                LZ_HIP(hipMemcpy(hl.data(), blo, 2 * nbk, hipMemcpyDeviceToHost));
+                LZ_HIP(hipMemcpy(hse.data(), ser, sizeof(pos_t) * nbk, hipMemcpyDeviceToHost));
+                LZ_HIP(hipMemcpy(hss.data(), bss, sizeof(pos_t) * nbk, hipMemcpyDeviceToHost));
+                for (u64 i = 0; i < nbk; i++)
+                    std::fprintf(stderr, "[lz77sss-debug]   block %llu: p=%u fo=%u lo=%u se=%llu ss=%llu\n",
+                                 (unsigned long long)i, hb[i], hf[i], hl[i], (unsigned long long)hse[nbk - 1 - i],
+                                 (unsigned long long)hss[i]);
+            }
+        }
+    }
     // sss_kernel_ms: pass 1 through the re-run (the phase's kernels and its one host read)
     LZ_HIP(hipEventRecord(e1, st));
 
@@ -1310,6 +1889,7 @@ void engine::build_sss_range(u64 first, u64 end, u64 base, u64 window) {
     // the u32 structures now describe the last view, not the text
     s = 0;
     runs_valid = false;
+    brk_valid = false;
     LZ_HIP(hipStreamSynchronize(st));
 }
 

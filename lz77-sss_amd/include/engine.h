@@ -6,6 +6,7 @@
 #include "timer.h"
 
 #include <array>
+#include <cstdlib>
 #include <string>
 #include <utility>
 #include <vector>
@@ -77,9 +78,25 @@ struct engine {
     dbuf<u8> sss_tflag;
     dbuf<u32> sss_tiles, sss_sflag, sss_slist, sss_fcnt;
     u64 stats_sss_tiles = 0;
+    // per-block run records (lce_dev.h run_tab::bp / ser / ss): the period of every
+    // p-extendable 512-byte block (k_sss_runs), segment ends / starts by two scans
+    dbuf<u8> blk_p;
+    dbuf<u16> blk_fo, blk_lo;
+    dbuf<pos_t> blk_mk, blk_ser, blk_ss;
+    dbuf<u64> blk_re, blk_rs;  // packed per-block run end / start (lce_dev.h run_tab::re / rs)
+    u64 brk_nbk = 0;
+    bool brk_valid = false;
+    bool no_blkrec = std::getenv("LZ77SSS_NO_BLKREC") != nullptr;  // test knob: LCE without the block records
+    unsigned long long* lce_dbg = nullptr;  // LZ77SSS_LCE_DEBUG: device counters of dev_lce_fwd / bwd
     run_tab runs() const {
         run_tab R;
         if (runs_valid) { R.p = run_p.p; R.hi = run_hi.p; R.lo = run_lo.p; }
+        if (brk_valid && !no_blkrec) {
+            R.re = blk_re.p;
+            R.rs = blk_rs.p;
+            R.nbk = brk_nbk;
+        }
+        R.dbg = lce_dbg;
         return R;
     }
 

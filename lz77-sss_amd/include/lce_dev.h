@@ -25,27 +25,125 @@ struct run_tab {
     const u8* p = nullptr;
     const pos_t* hi = nullptr;
     const pos_t* lo = nullptr;
+    // Per-block run records from the SSS pass (csrc/sss.hip k_sss_runs + k_blk_runinfo): for a
+    // 512-byte block b that is p-extendable (T[z] == T[z+p] for z in [512b, 512b+512)),
+    //   re[b] = end << 16 | exact << 8 | p,  rs[b] = start << 16 | exact << 8 | p
+    // where [start, end) is the p-periodic run holding it (the end exact or a lower bound, the
+    // start exact or an upper bound); 0 for other blocks.  One load per side of a skip.
+    const u64* re = nullptr;
+    const u64* rs = nullptr;
+    u64 nbk = 0;
+    unsigned long long* dbg = nullptr;  // LZ77SSS_LCE_DEBUG: step / skip counters (engine::lce_dbg)
 };
+__device__ __forceinline__ void lce_count(const run_tab& R, int c) {
+    if (R.dbg) atomicAdd(R.dbg + c, 1ull);
+}
+// One side of a run skip.  Forward: T[x-512..x) matched; the run around x - 1 must hold
+// [x - 340, x) -- from the block records (the block holding x - 1, or the one before it whose
+// run may end inside x - 1's block) or else from the Q-anchor table (the anchor of x - 340,
+// whose probe [a, a + 340) lies inside the matched bytes; its end is exact when known).
+// Output: e = the run's end, exact or a lower bound.  Backward: T[x..x+512) matched, the run
+// around x holds [x, x + 340); output its start (exact or an upper bound).
+__device__ __forceinline__ bool run_side_fwd(const run_tab& R, u64 x, u64& e, bool& xe) {
+    if (R.re) {
+        const u64 b = (x - 1) >> 9;
+        const u64 v0 = R.re[b], u0 = R.rs[b], v1 = b ? R.re[b - 1] : 0, u1 = b ? R.rs[b - 1] : 0;
+        if ((v0 & 255) && (u0 >> 16) + 340 <= x && (v0 >> 16) >= x) {
+            e = v0 >> 16;
+            xe = (v0 >> 8) & 1;
+            return true;
+        }
+        if ((v1 & 255) && (u1 >> 16) + 340 <= x && (v1 >> 16) >= x) {
+            e = v1 >> 16;
+            xe = (v1 >> 8) & 1;
+            return true;
+        }
+    }
+    if (R.p) {
+        const u64 a = (x - 340) >> 7;
+        if (R.p[a]) {
+            const u64 hi = R.hi[a];  // 0: unknown
+            if (hi >= x) {
+                e = hi;
+                xe = true;
+                return true;
+            }
+        }
+    }
+    return false;
+}
+__device__ __forceinline__ bool run_side_bwd(const run_tab& R, u64 x, u64& s0, bool& xs) {
+    if (R.re) {
+        const u64 b = x >> 9;
+        const bool nx = b + 1 < R.nbk;
+        const u64 v0 = R.re[b], u0 = R.rs[b], v1 = nx ? R.re[b + 1] : 0, u1 = nx ? R.rs[b + 1] : 0;
+        if ((u0 & 255) && (u0 >> 16) <= x && (v0 >> 16) >= x + 340) {
+            s0 = u0 >> 16;
+            xs = (u0 >> 8) & 1;
+            return true;
+        }
+        if ((u1 & 255) && (u1 >> 16) <= x && (v1 >> 16) >= x + 340) {
+            s0 = u1 >> 16;
+            xs = (u1 >> 8) & 1;
+            return true;
+        }
+    }
+    if (R.p) {
+        const u64 a = (x + 127) >> 7;
+        if (R.p[a]) {
+            const u64 lo = R.lo[a];  // RUN_LO_UNKNOWN: larger than every position
+            if (lo <= x) {
+                s0 = lo;
+                xs = true;
+                return true;
+            }
+        }
+    }
+    return false;
+}
+// T[x-512..x) == T[y-512..y), both inside periodic runs (run_side_fwd).  The two periods px,
+// py may differ: the runs share [x - 340, x) ~ [y - 340, y), 340 >= px + py bytes, so both
+// have the period gcd(px, py) there and, being px- resp. py-periodic, everywhere (Fine-Wilf).
+// Returns 0: no skip; 1: equal for *d more bytes (go on comparing from there); 2: they differ
+// exactly at *d (the run that ends first ends exactly there, the other goes on)
+__device__ __forceinline__ int run_skip_fwd(const run_tab& R, u64 x, u64 y, u64& d) {
+    u64 ex, ey;
+    bool xx, xy;
+    if (!run_side_fwd(R, x, ex, xx) || !run_side_fwd(R, y, ey, xy)) return 0;
+    const u64 dx = ex - x, dy = ey - y;
+    d = min(dx, dy);
+    return (dx != dy && (dx < dy ? xx : xy)) ? 2 : 1;
+}
+// T[x..x+512) == T[y..y+512): the same going left
+__device__ __forceinline__ int run_skip_bwd(const run_tab& R, u64 x, u64 y, u64& d) {
+    u64 sx, sy;
+    bool xx, xy;
+    if (!run_side_bwd(R, x, sx, xx) || !run_side_bwd(R, y, sy, xy)) return 0;
+    const u64 dx = x - sx, dy = y - sy;
+    d = min(dx, dy);
+    return (dx != dy && (dx < dy ? xx : xy)) ? 2 : 1;
+}
 
 // exact LCE of T[i..] and T[j..], at most lim (caller guarantees i+lim, j+lim <= n)
 __device__ inline u64 dev_lce_fwd(const u8* T, const run_tab& R, u64 i, u64 j, u64 lim) {
     u64 k = 0;
+    lce_count(R, 0);
+    u64 nst = 0;
     while (k < lim) {
         const u64 step = min<u64>(lim - k, 512);
+        lce_count(R, 1);
+        if (R.dbg && ++nst > R.dbg[4]) atomicMax(R.dbg + 4, nst);
         const u64 c = dev_naive_lce(T, i + k, j + k, step);
         k += c;
         if (c < step || k >= lim) return min(k, lim);
-        if (!R.p || k < 512) continue;  // no run table: plain comparison of the next 512 bytes
-        const u64 x = i + k, y = j + k;  // T[x-512..x) == T[y-512..y)
-        const u64 ax = (x - 340) >> 7, by = (y - 340) >> 7;
-        const u32 pp = R.p[ax];
-        if (pp == 0 || R.p[by] != pp) continue;
-        const u64 hx = R.hi[ax], hy = R.hi[by];
-        if (hx < x || hy < y) continue;
-        const u64 dx = hx - x, dy = hy - y, d = min(dx, dy);
-        if (k + d >= lim) return lim;
-        k += d;
-        if (dx != dy) return k;
+        if (!(R.p || R.re) || k < 512) continue;  // no run table: plain comparison of the next 512 bytes
+        u64 dj;
+        if (const int sk = run_skip_fwd(R, i + k, j + k, dj)) {  // T[x-512..x) == T[y-512..y)
+            lce_count(R, sk == 2 ? 3 : 2);
+            if (k + dj >= lim) return lim;
+            k += dj;
+            if (sk == 2) return k;
+        }
     }
     return lim;
 }
@@ -71,23 +169,31 @@ __device__ inline u64 wave_lce_fwd(const u8* T, const run_tab& R, u64 i, u64 j, 
         }
         k += step;
         if (k >= lim) return min(k, lim);
-        if (!R.p || k < 512) continue;
-        const u64 xi = i + k, yj = j + k;
-        const u64 ax = (xi - 340) >> 7, by = (yj - 340) >> 7;
-        const u32 pp = R.p[ax];
-        if (pp == 0 || R.p[by] != pp) continue;
-        const u64 hx = R.hi[ax], hy = R.hi[by];
-        if (hx < xi || hy < yj) continue;
-        const u64 dx = hx - xi, dy = hy - yj, d = min(dx, dy);
-        if (k + d >= lim) return lim;
-        k += d;
-        if (dx != dy) return k;
+        if (!(R.p || R.re) || k < 512) continue;
+        u64 dj;
+        if (const int sk = run_skip_fwd(R, i + k, j + k, dj)) {
+            if (k + dj >= lim) return lim;
+            k += dj;
+            if (sk == 2) return k;
+        }
     }
     return lim;
 }
 // #equal chars going left from i and j (T[i-t] == T[j-t]), at most lim <= min(i,j)+1
 __device__ __forceinline__ u64 dev_naive_lce_left(const u8* T, u64 i, u64 j, u64 lim) {
     u64 k = 0;
+    while (k + 32 <= lim) {  // 32 bytes per memory round trip (dev_naive_lce)
+        u64 x[4], y[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            x[t] = ldu64(T + (i - k - 8 * t - 7));
+            y[t] = ldu64(T + (j - k - 8 * t - 7));
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            if (x[t] != y[t]) return k + 8 * t + (__builtin_clzll(x[t] ^ y[t]) >> 3);
+        k += 32;
+    }
     while (k + 8 <= lim) {
         const u64 x = ldu64(T + (i - k - 7)), y = ldu64(T + (j - k - 7));
         if (x != y) return k + (__builtin_clzll(x ^ y) >> 3);
@@ -98,22 +204,21 @@ __device__ __forceinline__ u64 dev_naive_lce_left(const u8* T, u64 i, u64 j, u64
 }
 __device__ inline u64 dev_lce_bwd(const u8* T, const run_tab& R, u64 i, u64 j, u64 lim) {
     u64 k = 0;
+    lce_count(R, 5);
     while (k < lim) {
         const u64 step = min<u64>(lim - k, 512);
+        lce_count(R, 6);
         const u64 c = dev_naive_lce_left(T, i - k, j - k, step);
         k += c;
         if (c < step || k >= lim) return min(k, lim);
-        if (!R.p || k < 512) continue;  // no run table: plain comparison of the next 512 bytes
-        const u64 x = i - k + 1, y = j - k + 1;  // T[x..x+512) == T[y..y+512)
-        const u64 ax = (x + 127) >> 7, by = (y + 127) >> 7;
-        const u32 pp = R.p[ax];
-        if (pp == 0 || R.p[by] != pp) continue;
-        const u64 lx = R.lo[ax], ly = R.lo[by];
-        if (lx > x || ly > y) continue;
-        const u64 dx = x - lx, dy = y - ly, d = min(dx, dy);
-        if (k + d >= lim) return lim;
-        k += d;
-        if (dx != dy) return k;
+        if (!(R.p || R.re) || k < 512) continue;  // no run table: plain comparison of the next 512 bytes
+        u64 dj;
+        if (const int sk = run_skip_bwd(R, i - k + 1, j - k + 1, dj)) {  // T[x..x+512) == T[y..y+512)
+            lce_count(R, 7);
+            if (k + dj >= lim) return lim;
+            k += dj;
+            if (sk == 2) return k;
+        }
     }
     return lim;
 }

@@ -194,6 +194,20 @@ __device__ __forceinline__ u64 ldu64(const u8* p) {
 // a+lim, b+lim <= n + TEXT_PAD)
 __device__ __forceinline__ u64 dev_naive_lce(const u8* T, u64 a, u64 b, u64 lim) {
     u64 k = 0;
+    // 32 bytes per round: the eight loads of a round are issued before any compare (one memory
+    // round trip instead of four; a long comparison is latency-bound)
+    while (k + 32 <= lim) {
+        u64 x[4], y[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            x[t] = ldu64(T + a + k + 8 * t);
+            y[t] = ldu64(T + b + k + 8 * t);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            if (x[t] != y[t]) return k + 8 * t + (__builtin_ctzll(x[t] ^ y[t]) >> 3);
+        k += 32;
+    }
     while (k + 8 <= lim) {
         u64 x = ldu64(T + a + k), y = ldu64(T + b + k);
         if (x != y) return k + (__builtin_ctzll(x ^ y) >> 3);
