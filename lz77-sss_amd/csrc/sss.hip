@@ -954,9 +954,12 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
                                                         u8* __restrict__ blk_p, u16* __restrict__ blk_fo,
                                                         u16* __restrict__ blk_lo, u64 nbk, u32* __restrict__ any_q,
                                                         u32* __restrict__ dbg) {
-    // a ring of 4 blocks per wave in LDS: the bytes at offset p of a block are two aligned word
-    // reads (the block after it follows in the ring)
-    __shared__ u64 s_ring[SWAVES][256];
+    // a ring of RSL blocks per wave in LDS: the bytes at offset p of a block are two aligned word
+    // reads (the block after it follows in the ring).  The text arrives RCH blocks at a time in
+    // registers, loaded one chunk ahead (a register rotation per block would make every load
+    // wait for the one before: one load in flight)
+    constexpr u32 RSL = 16, RCH = 8;
+    __shared__ u64 s_ring[SWAVES][RSL * 64];
     const u32 lane = threadIdx.x & 63;
     u64* ring = s_ring[threadIdx.x >> 6];
     const u64 w = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -982,19 +985,18 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
     }
     const u32 nB = 0u - PW.B;
     auto load8 = [&](u64 k) -> u64 { return *(const u64*)(T + i0 + k * TAU + 8 * lane); };
-    // (other lanes read the words: a wavefront fence orders the write before their reads)
-    auto put_ring = [&](u32 k, u64 B) {
-        ring[(k & 3) * 64 + lane] = B;
+    // (other lanes read the words: a wavefront fence orders the writes before their reads)
+    auto ring_sync = [&]() {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     // bytes at offset 8 lane + p of block k (blocks k, k + 1 in the ring)
     auto ring_shift = [&](u32 k, u32 p) -> u64 {
-        const u32 o = (k & 3) * 64 + lane + (p >> 3), sh = 8 * (p & 7);
-        const u64 lo = ring[o & 255];
+        const u32 o = (k % RSL) * 64 + lane + (p >> 3), sh = 8 * (p & 7);
+        const u64 lo = ring[o % (RSL * 64)];
         if (!sh) return lo;
-        const u64 hi = ring[(o + 1) & 255];
+        const u64 hi = ring[(o + 1) % (RSL * 64)];
         return (lo >> sh) | (hi << (64 - sh));
     };
     auto block_prefix = [&](u64 bytes, u32& carry, u32* h) {
@@ -1113,31 +1115,47 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         for (int e = 0; e < 8; e++) v[e] |= 0u - ((bits >> e) & 1u);
     };
 
-    // prologue: blocks 0 .. 2 in the ring, up to 6 in flight; block 0 classified, Phi'(0)
-    u64 Bp = 0, Bk = load8(0), Bk1 = load8(1), B3 = load8(2), B4 = load8(3), B5 = load8(4), B6 = load8(5),
-        B7 = load8(6);
-    put_ring(0, Bk);
-    put_ring(1, Bk1);
-    put_ring(2, B3);
-    u64 pdk = Bk ^ ring_shift(0, 1), pdk1 = Bk1 ^ ring_shift(1, 1);
+    // prologue: blocks 0 .. RSL - 1 in the ring, the chunk after them loading (blocks past
+    // nblk + 4 are never read: the text pad covers up to there); block 0 classified, Phi'(0).
+    // Iteration c reads ring blocks c .. c + 3
+    const u32 lend = nblk + 5;
+    u64 R[RCH];
+    auto load_chunk = [&](u32 k0) {
+#pragma unroll
+        for (u32 e = 0; e < RCH; e++) R[e] = k0 + e < lend ? load8(k0 + e) : 0ull;
+    };
+    auto store_chunk = [&](u32 k0) {
+#pragma unroll
+        for (u32 e = 0; e < RCH; e++) ring[((k0 + e) % RSL) * 64 + lane] = R[e];
+    };
+    load_chunk(0);
+    store_chunk(0);
+    load_chunk(RCH);
+    store_chunk(RCH);
+    load_chunk(RSL);
+    ring_sync();
+    auto ring_blk = [&](u32 k) -> u64 { return ring[(k % RSL) * 64 + lane]; };
+    u64 Bk1 = ring_blk(1);
+    u64 pdk = ring_blk(0) ^ ring_shift(0, 1), pdk1 = Bk1 ^ ring_shift(1, 1);
     bool z1 = __ballot(pdk1 != 0) != 0;
     u32 hc[8], hn[8], x[8], y[8];  // Hp of block c+1 (hc), of block c+2 (hn); Phi' of blocks c, c+1
     u32 carry = 0;
     int hk = -1;  // the block whose Hp is in hc (prefix hashes continue from carry after it)
     bool fx;
     {
+        const u64 B0 = ring_blk(0);
         const bool z0 = __ballot(pdk != 0) != 0;
         u32 q0 = 0xFFu;
         fx = !z0 && !z1;
         if (!fx) {
-            q0 = classify(0, Bk, Bk1, pdk, pdk1);
+            q0 = classify(0, B0, Bk1, pdk, pdk1);
             z1 = __ballot(pdk1 != 0) != 0;
         } else if (i0 <= jmax) {
             anyq = true;
         }
         put_rec(0, __ballot(pdk != 0) == 0, -2, -2);
         if (!fx) {
-            block_prefix(Bk, carry, hc);
+            block_prefix(B0, carry, hc);
             block_prefix(Bk1, carry, hn);
             phi(0, hc, hn, q0, x);
 #pragma unroll
@@ -1146,23 +1164,48 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         }
     }
     const bool fail_pro = fail;  // block 0 unsettled
+    // blocks of a run continuing with the period p (lanes [fa, fb)): recorded together
+    u32 fa = 0, fb = 0, fp = 0;
+    auto flush_fast = [&]() {
+        if (fb > fa) {
+            if (lane >= fa && lane < fb) {
+                rp = fp;
+                rf = 0xFFFFu;
+            }
+            fa = fb = 0;
+        }
+    };
     u32 c = 0;
     for (; c < nblk && !fail; c++) {
-        // blocks c .. c + 6 in registers (Bp .. B6), c + 7 in flight; the ring gets block c + 3
-        Bp = Bk;
-        Bk = Bk1;
-        Bk1 = B3;
-        B3 = B4;
-        B4 = B5;
-        B5 = B6;
-        B6 = B7;
-        B7 = load8(c + 7);  // six blocks ahead (the text pad covers the stripe's end)
-        put_ring(c + 3, B3);
+        if (c % RCH == 0 && c) {
+            // blocks c + RCH .. c + 2 RCH - 1 replace c - RCH .. c - 1 (read no more); the next
+            // chunk loads for RCH iterations
+            store_chunk(c + RCH);
+            if (c + 2 * RCH < lend) load_chunk(c + 2 * RCH);
+            ring_sync();
+        }
         const u32 k = c + 1;
+        Bk1 = ring_blk(k + 1);
         pdk = pdk1;
         const bool z0 = z1;
         pdk1 = Bk1 ^ ring_shift(k + 1, p);
         z1 = __ballot(pdk1 != 0) != 0;
+        if (fx && !z0 && !z1) {
+            // the run goes on: every window of block k p-periodic, no decision of block c in S
+            // (Phi'(c) and Phi'(k) all INF); block k recorded with the run's period
+            if (fb != k || fp != p) {
+                flush_fast();
+                fa = k;
+                fp = p;
+                if (i0 + (u64)k * TAU <= jmax) anyq = true;
+            }
+            fb = k + 1;
+            prev_rec = p;
+            hk = -1;
+            continue;
+        }
+        flush_fast();
+        const u64 Bk = ring_blk(k);
         const int fok = z0 ? first_diff(pdk) : -1;  // before a change of period: the end of the last run
         bool allk = !z0 && !z1;  // no p-break in blocks k, k + 1: every window of block k is p-periodic
         u32 qk = 0xFFu;
@@ -1174,7 +1217,7 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         }
         if (fail) break;
         const bool ext = __ballot(pdk != 0) == 0;
-        put_rec(k, ext, fok, (ext && p != prev_rec) ? seg_lo(k, Bp) : -2);
+        put_rec(k, ext, fok, (ext && p != prev_rec) ? seg_lo(k, ring_blk(c)) : -2);
         // Phi'(block k)
         if (!allk) {
             if (hk != (int)k) {  // restart the prefix hash at block k (Phi is origin-free)
@@ -1237,11 +1280,12 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         for (int e = 0; e < 8; e++) x[e] = y[e];
         fx = allk;
     }
+    flush_fast();
     if (fail) {
         // the exact Q-anchor path takes the stripe; its remaining blocks still get their run
         // records (the LCE consults them on both sides of a comparison)
         const u32 k0 = fail_pro ? 1u : c + 1;
-        u64 Bq = fail_pro ? Bk : Bp, B0x = fail_pro ? Bk1 : Bk, B1x = fail_pro ? B3 : Bk1;
+        u64 Bq = ring_blk(k0 - 1), B0x = ring_blk(k0), B1x = ring_blk(k0 + 1);
         for (u32 kk = k0; kk < (u32)SNB; kk++) {
             if (kk > k0) {
                 Bq = B0x;
