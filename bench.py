@@ -140,14 +140,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="rr", choices=["rr", "genome"])
+    ap.add_argument("--workload", default="rr", choices=["rr", "genome", "chr19"],
+                    help="chr19 (--shard only): configs[3]'s chr19-style text of --size-gib GiB generated in "
+                         "HBM (59 MiB ACGT base block, 0.1%% mutations per copy), pos_t = uint64_t")
     ap.add_argument("--size-mib", type=int, default=1024)
     ap.add_argument("--phr-mode", default="lpf_opt", choices=["lpf_opt", "lpf_lnf_opt"],
                     help="lpf_opt = configs[1]; lpf_lnf_opt = configs[2] (LPF/LNF phrases)")
     ap.add_argument("--mode", default="approx", choices=["approx", "exact", "sss"],
                     help="approx = configs[1]/[2] (3-aprx); exact = configs[4] (exact factorization); "
                          "sss = the sharded pos_t=uint64 sync-set pass of configs[3] (chr19-style text)")
-    ap.add_argument("--size-gib", type=float, default=50.0, help="--mode sss: text size in GiB (configs[3]: 50)")
+    ap.add_argument("--size-gib", type=float, default=50.0,
+                    help="--mode sss / --workload chr19: text size in GiB (configs[3]: 50)")
     ap.add_argument("--cpu-sample-mib", type=int, default=-1,
                     help="oracle sample size in MiB (default: the full workload text, 2-30 s of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -178,6 +181,8 @@ def main():
         if args.mode != "approx" or args.phr_mode != "lpf_opt":
             raise SystemExit("--shard runs the 3-aprx with lpf_opt (configs[1])")
         return main_shard(args, lz, torch, dist, world, rank, local_rank)
+    if args.workload == "chr19":
+        raise SystemExit("--workload chr19 runs with --shard (configs[3])")
 
     n = args.size_mib << 20
     T = make_text(lz, args.workload, n, rank)
@@ -318,19 +323,28 @@ def main():
 
 
 def main_shard(args, lz, torch, dist, world, rank, local_rank):
-    """One text (seed 42, the rank-0 text of the default mode) factorized by all ranks
-    together: one step = sharded.factorize_sharded_resident (collectives (1)-(4) of
-    SURVEY.md 8e).  The greedy chain is walked block by block in rank order, so the
-    phases that shard are the sync set and the emission; total work is fixed (strong
-    scaling).  After the timed region rank 0 checks the stream against a one-GPU
-    factorize of the same text in the same session."""
+    """One text factorized by all ranks together: one step = sharded.factorize_sharded_resident
+    (collectives (1)-(4) of SURVEY.md 8e).  rr / genome: the seed-42 text of the default mode
+    (--size-mib); chr19: configs[3]'s chr19-style text of --size-gib GiB generated in HBM with
+    pos_t = uint64_t (every rank holds the whole text: the phrases are replicated).  The greedy
+    chain is walked block by block in rank order, so the phases that shard are the sync set and
+    the emission; total work is fixed (strong scaling).  After the timed region rank 0 checks
+    the stream against a one-GPU factorize of the same text in the same session."""
     import sharded
 
-    n = args.size_mib << 20
-    T = make_text(lz, args.workload, n, 0)
-    sess = lz.Session(n, device=local_rank)
-    sess.load(T)
-    del T
+    chr19 = args.workload == "chr19"
+    n = int(args.size_gib * GIB) if chr19 else args.size_mib << 20
+    pos64 = chr19 or n > (1 << 32) - 16
+    sess = lz.Session(n, device=local_rank, pos64=pos64)
+    t_gen0 = time.perf_counter()
+    if chr19:
+        sess.gen_genome(n, 59 << 20, 0.001, 7)
+    else:
+        T = make_text(lz, args.workload, n, 0)
+        sess.load(T)
+        del T
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t_gen0
     tm = {}
 
     def step():
@@ -356,26 +370,34 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
     phases = {k: round(v * 1e3, 3) for k, v in tm.items()}
     z = int(F.shape[0])
     same = None
+    st = sess.stats()
     if rank == 0:
         z1 = sess.factorize(device=local_rank)
-        ref = torch.empty(max(z1, 1) * 2, dtype=torch.int32, device=f"cuda:{local_rank}")
+        ref = torch.empty(max(z1, 1) * 2, dtype=torch.int64 if pos64 else torch.int32, device=f"cuda:{local_rank}")
         if z1:
-            sess.copy_factors(ref.data_ptr(), z1 * 8)
+            sess.copy_factors(ref.data_ptr(), z1 * (16 if pos64 else 8))
         same = bool(z1 == z and torch.equal(ref[: 2 * z1].view(-1, 2), F))
     if rank == 0:
+        if chr19:
+            data = "synthetic chr19-style (59 MiB ACGT base block, 0.1% mutations per copy), generated in HBM"
+        elif args.workload == "rr":
+            data = "synthetic (seeded restatement of the reference's random_repetitive_string)"
+        else:
+            data = "synthetic (genome-like: 64 MiB ACGT base block, 0.1% mutations)"
         out = {
             "metric": "factorization MB/s (3-aprx LZ77, greedy + lpf_opt, tau=512)",
             "value": round(n / dt / 1e6, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (seeded restatement of the reference's random_repetitive_string)"
-            if args.workload == "rr" else "synthetic (genome-like: 64 MiB ACGT base block, 0.1% mutations)",
-            "config": {"workload": f"{args.workload} n={n} ({args.size_mib} MiB), ONE text split over {world} rank(s)",
+            "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": data,
+            "config": {"workload": (f"chr19 n={n} ({args.size_gib} GiB)" if chr19 else
+                                    f"{args.workload} n={n} ({args.size_mib} MiB)") +
+                       f", ONE text split over {world} rank(s), pos_t={'uint64' if pos64 else 'uint32'}",
                        "n": n, "tau": 512, "phr_mode": "lpf_opt", "fact_mode": "greedy",
                        "parallelism": f"sharded x{world}: S by block + all-gather, replicated phrases, "
                                       f"rank-ordered greedy blocks, gathered emission",
                        "factors": z, "equals_one_gpu_stream": same,
-                       "rank0_phase_ms": phases},
+                       "sss_size": int(st[0]) if st else None, "lpf_phrases": int(st[2]) if st else None,
+                       "text_gen_s": round(t_gen, 3), "rank0_phase_ms": phases},
             "roofline": None, "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)

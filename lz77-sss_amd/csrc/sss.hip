@@ -1164,19 +1164,7 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         }
     }
     const bool fail_pro = fail;  // block 0 unsettled
-    // blocks of a run continuing with the period p (lanes [fa, fb)): recorded together
-    u32 fa = 0, fb = 0, fp = 0;
-    auto flush_fast = [&]() {
-        if (fb > fa) {
-            if (lane >= fa && lane < fb) {
-                rp = fp;
-                rf = 0xFFFFu;
-            }
-            fa = fb = 0;
-        }
-    };
-    u32 c = 0;
-    for (; c < nblk && !fail; c++) {
+    auto refill = [&](u32 c) {
         if (c % RCH == 0 && c) {
             // blocks c + RCH .. c + 2 RCH - 1 replace c - RCH .. c - 1 (read no more); the next
             // chunk loads for RCH iterations
@@ -1184,27 +1172,51 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
             if (c + 2 * RCH < lend) load_chunk(c + 2 * RCH);
             ring_sync();
         }
-        const u32 k = c + 1;
-        Bk1 = ring_blk(k + 1);
-        pdk = pdk1;
-        const bool z0 = z1;
-        pdk1 = Bk1 ^ ring_shift(k + 1, p);
-        z1 = __ballot(pdk1 != 0) != 0;
-        if (fx && !z0 && !z1) {
-            // the run goes on: every window of block k p-periodic, no decision of block c in S
-            // (Phi'(c) and Phi'(k) all INF); block k recorded with the run's period
-            if (fb != k || fp != p) {
-                flush_fast();
-                fa = k;
-                fp = p;
-                if (i0 + (u64)k * TAU <= jmax) anyq = true;
+    };
+    u32 c = 0;
+    for (; c < nblk && !fail; c++) {
+        refill(c);
+        u32 k = c + 1;
+        bool z0;
+        if (fx && !z1) {
+            // the run goes on while block c + 2 has no p-break: every window of block c + 1
+            // p-periodic, no decision of block c in S (Phi'(c), Phi'(c + 1) all INF); those
+            // blocks are recorded together with the run's period (a tight loop: one p-difference
+            // per block)
+            const u32 cs = c;
+            const u32 ol = lane + (p >> 3), sh = 8 * (p & 7);
+            u64 d;
+            for (;;) {
+                const u32 o = ((c + 2) % RSL) * 64;
+                const u64 lo = ring[(o + ol) % (RSL * 64)], hi = ring[(o + ol + 1) % (RSL * 64)];
+                d = ring[o + lane] ^ (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo);
+                if (__ballot(d != 0)) break;
+                if (++c >= nblk) break;
+                refill(c);
             }
-            fb = k + 1;
-            prev_rec = p;
-            hk = -1;
-            continue;
+            if (c > cs) {
+                if (lane > cs && lane <= c) {
+                    rp = p;
+                    rf = 0xFFFFu;
+                }
+                prev_rec = p;
+                hk = -1;
+                if (i0 + (u64)(cs + 1) * TAU <= jmax) anyq = true;
+            }
+            if (c >= nblk) break;
+            k = c + 1;
+            Bk1 = ring_blk(k + 1);
+            pdk = 0;  // block k: clean
+            z0 = false;
+            pdk1 = d;
+            z1 = true;
+        } else {
+            Bk1 = ring_blk(k + 1);
+            pdk = pdk1;
+            z0 = z1;
+            pdk1 = Bk1 ^ ring_shift(k + 1, p);
+            z1 = __ballot(pdk1 != 0) != 0;
         }
-        flush_fast();
         const u64 Bk = ring_blk(k);
         const int fok = z0 ? first_diff(pdk) : -1;  // before a change of period: the end of the last run
         bool allk = !z0 && !z1;  // no p-break in blocks k, k + 1: every window of block k is p-periodic
@@ -1280,7 +1292,6 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         for (int e = 0; e < 8; e++) x[e] = y[e];
         fx = allk;
     }
-    flush_fast();
     if (fail) {
         // the exact Q-anchor path takes the stripe; its remaining blocks still get their run
         // records (the LCE consults them on both sides of a comparison)

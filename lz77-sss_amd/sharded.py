@@ -282,9 +282,11 @@ def factorize_sharded(text, n: int, rank: int, world: int, device: int | None = 
 
 def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int, group=None,
                                timings: dict | None = None, **params):
-    """Collectives (1)-(4) with everything in HBM: `sess` is a 32-bit Session on `device`
-    holding the whole text (every rank loads it; phrases are replicated).  Returns the
-    factors as an int32 (z, 2) torch tensor on `device`, identical on every rank.
+    """Collectives (1)-(4) with everything in HBM: `sess` is a Session on `device` holding the
+    whole text (every rank loads it; phrases are replicated), pos_t = uint32_t or, for texts
+    past 4 GiB (configs[3]), uint64_t (Session(pos64=True); the reference's choice at
+    cli/lz77_sss_3_aprx.cpp:73-83).  Returns the factors as an int32 (uint32 session) or int64
+    (uint64 session) (z, 2) torch tensor on `device`, identical on every rank.
 
     With backend "nccl" the sync-set blocks, the chain state, the carried table and the
     factor blocks move GPU to GPU (RCCL over xGMI); with "gloo" they go through host
@@ -363,4 +365,6 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
         F = gather_blocks(F.to(cdev), group).to(dev)
     if timings is not None:
         timings.update(sss=t1 - t0, prepare=t2 - t1, greedy_chain=t3 - t2, emit=time.perf_counter() - t3)
+    if getattr(sess, "pos64", False):
+        return F.view(-1, 2)  # (src, len) as uint64 pairs; positions < 2^63
     return F.view(torch.int32).view(-1, 2)

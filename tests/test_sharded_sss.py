@@ -326,7 +326,9 @@ def test_greedy_blocks_one_session(lz, orc, bounds_kind):
     assert np.array_equal(np.concatenate(parts), F_ref)
 
 
-def _resident_worker(rank, world, port, q, T):
+def _resident_worker(rank, world, port, q, T, wide=False, gen=None):
+    import hashlib
+
     import torch
     import torch.distributed as dist
 
@@ -337,35 +339,64 @@ def _resident_worker(rank, world, port, q, T):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        with L.Session(T.size, 0) as s:
-            s.load(T)
+        n = T.size if gen is None else gen["n"]
+        with L.Session(n, 0, pos64=wide) as s:
+            if gen is None:
+                s.load(T)
+            else:  # generated in HBM (the seeded chr19-style generator)
+                s.gen_genome(n, gen["base_len"], gen["mut"], gen["seed"])
             tm = {}
-            F = SH.factorize_sharded_resident(s, T.size, rank, world, 0, timings=tm)
-            F2 = SH.factorize_sharded_resident(s, T.size, rank, world, 0)  # a second step on the same session
-            q.put((rank, F.cpu().numpy().astype(np.uint64), bool(torch.equal(F, F2)), sorted(tm)))
+            F = SH.factorize_sharded_resident(s, n, rank, world, 0, timings=tm)
+            if gen is None:
+                F2 = SH.factorize_sharded_resident(s, n, rank, world, 0)  # a second step on the same session
+                q.put((rank, F.cpu().numpy().astype(np.uint64), bool(torch.equal(F, F2)), sorted(tm)))
+            else:  # the stream's SHA-256 in the fixture layout (little-endian uint64 pairs)
+                h = hashlib.sha256(F.cpu().numpy().astype("<u8").view(np.uint8)).hexdigest()
+                q.put((rank, int(F.shape[0]), h, sorted(tm)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_sharded_resident_ranks_on_gpu(lz, orc, world):
-    """factorize_sharded_resident (the bench's --shard step: every buffer stays in HBM, handed
-    over through the process group) == the one-process stream, on every rank, twice."""
+def _run_resident(world, T, wide=False, gen=None):
     import torch.multiprocessing as mp
 
-    T = lz.gen_genome(3 << 20, 1 << 20, 0.001, 23)
-    F_ref = orc.factorize(T)[0].astype(np.uint64)
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_resident_worker, args=(r, world, port, qq, T)) for r in range(world)]
+    procs = [ctx.Process(target=_resident_worker, args=(r, world, port, qq, T, wide, gen)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted((qq.get(timeout=300) for _ in procs), key=lambda x: x[0])
+    res = sorted((qq.get(timeout=900) for _ in procs), key=lambda x: x[0])
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for _, F, same, keys in res:
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,wide", [(1, False), (2, False), (3, False), (2, True)])
+def test_sharded_resident_ranks_on_gpu(lz, orc, world, wide):
+    """factorize_sharded_resident (the bench's --shard step: every buffer stays in HBM, handed
+    over through the process group) == the one-process stream, on every rank, twice; also on
+    pos_t = uint64_t sessions (configs[3])."""
+    T = lz.gen_genome(3 << 20, 1 << 20, 0.001, 23)
+    F_ref = orc.factorize64(T)[0] if wide else orc.factorize(T)[0].astype(np.uint64)
+    for _, F, same, keys in _run_resident(world, T, wide):
         assert same and keys == ["emit", "greedy_chain", "prepare", "sss"]
         assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_sharded_resident_u64_past_4gib_hash():
+    """configs[3] at C4's mutation rate past 2^32: a 4 GiB + 3 MiB chr19-style text (0.1 %
+    mutations, pos_t = uint64_t) factorized by 2 ranks (gloo, sharing the GPU) with
+    factorize_sharded_resident == the oracle's stream (SHA-256 fixture of
+    tests/golden/make_stream_hashes.py, entry chr19_4gib_u64) on both ranks."""
+    import json
+
+    e = json.loads((ROOT / "tests" / "golden" / "stream_hashes.json").read_text())["chr19_4gib_u64"]
+    gen = dict(n=e["n"], base_len=e["args"]["base_len"], mut=e["args"]["mut"], seed=e["args"]["seed"])
+    for _, z, h, keys in _run_resident(2, np.zeros(0, np.uint8), True, gen):
+        assert keys == ["emit", "greedy_chain", "prepare", "sss"]
+        assert z == e["z"] and h == e["stream_sha256"]
