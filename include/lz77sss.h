@@ -54,8 +54,10 @@ enum { LZ77SSS_LPF_NAIVE = 0, LZ77SSS_LPF_LNF_NAIVE = 1, LZ77SSS_LPF_OPT = 2, LZ
 /* enum factorize_mode, lz77_sss.hpp:55-59 (same numeric values) */
 enum { LZ77SSS_GREEDY_NAIVE = 0, LZ77SSS_GREEDY = 1, LZ77SSS_SKIP_PHRASES = 2 };
 
-/* enum transform_mode, lz77_sss.hpp:60-64 (same numeric values) */
-enum { LZ77SSS_TRANSF_NAIVE = 0, LZ77SSS_TRANSF_WITH_SAMPLES = 1, LZ77SSS_TRANSF_WITHOUT_SAMPLES = 2 };
+/* enum transform_mode, lz77_sss.hpp:60-64 (same numeric values); FULL_SA is a device
+ * extension (not a reference mode): the lengths from LPF over the full suffix array */
+enum { LZ77SSS_TRANSF_NAIVE = 0, LZ77SSS_TRANSF_WITH_SAMPLES = 1, LZ77SSS_TRANSF_WITHOUT_SAMPLES = 2,
+       LZ77SSS_TRANSF_FULL_SA = 3 };
 
 enum {
     LZ77SSS_OK = 0,
@@ -111,14 +113,14 @@ int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_
 /* One-shot exact factorization (greedy LZ77: every factor is a longest previous
  * factor; a copy {src, len >= 1} or the literal {char, 0} when the character is
  * new).  The factor lengths are the canonical greedy LZ77 ones, as the
- * reference's exact modes produce at p = 1; the sources follow a fixed rule
- * (the longer of the PSV/NSV candidates in suffix-array order, the earlier one
- * on ties) instead of the reference's sample/range-structure visit order.
- * transf_mode naive and without_samples (and the reference's range structure)
- * select different ways to the same lengths; both are computed by the one device
- * algorithm (csrc/exact.hip).  with_samples (transform_to_exact/with_samples.cpp,
- * the sample index of config exact-smpl) returns LZ77SSS_EINVAL: its structures
- * are not built.  Requires n < 2^31. */
+ * reference's exact modes produce at p = 1.  transf_mode naive, with_samples and
+ * without_samples run the reference's exact-smpl path on the device (csrc/smpl.hip:
+ * the 3-approximation, the sample index over its phrase ends and delta-samples, the
+ * decomposed weighted square grid; with_samples adds the RKS fingerprints and the
+ * interval samples; lz77_sss.hpp:558-709, transform_to_exact/{naive,with_samples,without_samples}.cpp); their sources are
+ * the lighter points the range queries find.  LZ77SSS_TRANSF_FULL_SA computes the
+ * same lengths from LPF over the full suffix array of the text (csrc/exact.hip; 44 B
+ * per character, n < 2^31) with the PSV/NSV source rule.  Requires n < 2^32 - 16. */
 int lz77sss_factorize_exact_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm, int transf_mode,
                                 lz77sss_emit_fn emit, void* user);
 /* pos_t = uint64_t form of the exact factorization (same algorithm and limit n < 2^31). */

@@ -262,6 +262,14 @@ struct engine64_impl final : lz::engine_if {
     }
     u64 sss_size() const override { return E.s; }
     const u64* sss_ptr() const override { return E.S.p; }
+    void sss_range(u64 first, u64 end, u64 base, u64 window, u64* size, int* has_runs) override {
+        LZ_HIP(hipSetDevice(E.device));
+        E.build_sss_range(first, end, base, window);
+        *size = E.s64;
+        *has_runs = E.has_runs64;
+    }
+    u64 range_size() const override { return E.s64; }
+    const u64* range_ptr() const override { return E.S64.p; }
     u64 num_phr() const override { return E.num_phr; }
     const u64* lpf_ptr() const override { return E.lpf.p; }
     const u32* sa_ptr() const override { return E.SA.p; }
@@ -299,6 +307,7 @@ engine_if* make_engine64(int dev, u64 maxn) {
 struct lz77sss_session {
     lz::engine E;                          // pos_t = uint32_t sessions
     std::unique_ptr<lz::engine_if> E64;    // pos_t = uint64_t sessions (lz77sss_session_create64)
+    bool range64 = false;                  // E64: the last sync set came from sss_range
 };
 
 static thread_local std::string g_err;
@@ -363,14 +372,8 @@ static void check_exact_params(const lz77sss_params* prm, int transf_mode) {
     if (prm->fact_mode != LZ77SSS_GREEDY) throw lz::error(LZ77SSS_EINVAL, "exact mode requires fact_mode = greedy");
     if (prm->phr_mode != LZ77SSS_LPF_OPT && prm->phr_mode != LZ77SSS_LPF_LNF_OPT)
         throw lz::error(LZ77SSS_EINVAL, "unsupported phr_mode");
-    if (transf_mode < LZ77SSS_TRANSF_NAIVE || transf_mode > LZ77SSS_TRANSF_WITHOUT_SAMPLES)
+    if (transf_mode < LZ77SSS_TRANSF_NAIVE || transf_mode > LZ77SSS_TRANSF_FULL_SA)
         throw lz::error(LZ77SSS_EINVAL, "unsupported transf_mode");
-    // with_samples names the sample index + range structures of
-    // transform_to_exact/with_samples.cpp, which the device path does not build
-    if (transf_mode == LZ77SSS_TRANSF_WITH_SAMPLES)
-        throw lz::error(LZ77SSS_EINVAL,
-                        "transf_mode with_samples is not supported (no sample-index structures on the device); "
-                        "naive and without_samples give the canonical greedy lengths");
 }
 
 LZ77SSS_API int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out) {
@@ -416,6 +419,7 @@ LZ77SSS_API int lz77sss_session_factorize(lz77sss_session* s, const lz77sss_para
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
         check_params(prm);
+        s->range64 = false;
         uint64_t z = s->E64 ? s->E64->factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0,
                                                  prm->fact_mode)
                             : s->E.factorize(prm->phr_mode, prm->rk_seed, prm->index_log2_size, prm->log != 0,
@@ -430,7 +434,12 @@ LZ77SSS_API int lz77sss_session_factorize_exact(lz77sss_session* s, const lz77ss
     return guarded([&] {
         need32(s, "session_factorize_exact");
         check_exact_params(prm, transf_mode);
-        uint64_t z = s->E.factorize_exact(prm->log != 0);
+        // the reference's transforms run the sample-index path (csrc/smpl.hip); FULL_SA the
+        // full suffix array (csrc/exact.hip)
+        uint64_t z = transf_mode == LZ77SSS_TRANSF_FULL_SA
+                         ? s->E.factorize_exact(prm->log != 0)
+                         : s->E.factorize_exact_smpl(transf_mode, prm->phr_mode, prm->rk_seed, prm->index_log2_size,
+                                                     prm->log != 0);
         if (num_factors) *num_factors = z;
     });
 }
@@ -504,6 +513,7 @@ LZ77SSS_API int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int*
             uint64_t sz = 0;
             int hr = 0;
             s->E64->sss(&sz, &hr);
+            s->range64 = false;
             if (size_sss) *size_sss = sz;
             if (has_runs) *has_runs = hr;
             return;
@@ -520,7 +530,15 @@ LZ77SSS_API int lz77sss_session_sss_range(lz77sss_session* s, uint64_t first, ui
                                           uint64_t window, uint64_t* size_sss, int* has_runs) {
     if (!s) return LZ77SSS_EINVAL;
     return guarded([&] {
-        need32(s, "sss_range");
+        if (s->E64) {
+            uint64_t cnt = 0;
+            int hr = 0;
+            s->E64->sss_range(first, end, base, window, &cnt, &hr);
+            s->range64 = true;
+            if (size_sss) *size_sss = cnt;
+            if (has_runs) *has_runs = hr;
+            return;
+        }
         LZ_HIP(hipSetDevice(s->E.device));
         s->E.build_sss_range(first, end, base, window);
         if (size_sss) *size_sss = s->E.s64;
@@ -531,7 +549,10 @@ LZ77SSS_API int lz77sss_session_sss_range(lz77sss_session* s, uint64_t first, ui
 // 64-bit sync set: of the last sss_range call (32-bit session) or of the last sss /
 // factorize call (64-bit session)
 static void sss64_src(lz77sss_session* s, const uint64_t*& p, uint64_t& cnt) {
-    if (s->E64) {
+    if (s->E64 && s->range64) {
+        p = s->E64->range_ptr();
+        cnt = s->E64->range_size();
+    } else if (s->E64) {
         p = s->E64->sss_ptr();
         cnt = s->E64->sss_size();
     } else {

@@ -1874,7 +1874,6 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipGetLastError());
 }
 
-#ifndef LZ_POS64  // the u32 engine's windowed 64-bit sync set (the u64 engine builds S directly)
 // ---------------------------------------------------------------------------
 // pos_t = uint64_t sync set of a decision range (lce_sss.hpp:53 instantiated with
 // pos_t = uint64_t, lz77_sss.hpp:72-75).  Phi and Q are functions of window contents
@@ -1884,7 +1883,7 @@ void engine::build_sss(const u8* T) {
 // 64 bits with the view offset plus `base` added.  The same halo is what a rank of a
 // sharded job holds: it loads T[b_r, e_r + 2tau - 1) and passes
 // base = b_r.
-__global__ void k_lower_bound_u32(const u32* __restrict__ S, u32 s, u32 x, u32* __restrict__ out) {
+__global__ void k_lower_bound_u32(const pos_t* __restrict__ S, u32 s, u32 x, u32* __restrict__ out) {
     u32 lo = 0, hi = s;
     while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
@@ -1892,7 +1891,7 @@ __global__ void k_lower_bound_u32(const u32* __restrict__ S, u32 s, u32 x, u32* 
     }
     *out = lo;
 }
-__global__ void k_sss_widen(const u32* __restrict__ S, u32 s, const u32* __restrict__ skip, u64 add,
+__global__ void k_sss_widen(const pos_t* __restrict__ S, u32 s, const u32* __restrict__ skip, u64 add,
                             u64* __restrict__ out) {
     const u32 k0 = *skip;
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x + k0;
@@ -1947,7 +1946,5 @@ void engine::build_sss_range(u64 first, u64 end, u64 base, u64 window) {
     brk_valid = false;
     LZ_HIP(hipStreamSynchronize(st));
 }
-
-#endif
 
 }  // namespace LZ_NS

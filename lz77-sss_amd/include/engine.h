@@ -14,6 +14,7 @@
 namespace LZ_NS {
 
 struct lpf3 { pos_t beg, end, src; };
+struct smpl_view;  // csrc/smpl.hip
 
 // greedy walk segments (csrc/greedy.hip)
 // walk segment input: start position, first phrase index, gap-index state, and
@@ -168,6 +169,12 @@ struct engine {
     dbuf<u32> x_idx, x_idx2, x_sa, x_rank, x_flag, x_tree, x_ltree, x_lcp, x_lpf, x_src, x_mark, x_chunk;
     const u32* sa_full = nullptr;    // suffix array of the text (x_sa) after build_sa_full
     u32 x_rounds = 0;
+    // exact-smpl mode (csrc/smpl.hip): approximate factors, samples, PA / SA, grid, RKS,
+    // interval samples, phrase tasks
+    dbuf<u32> e_afact, e_afst, e_tmp1, e_tmp2, e_C, e_PA, e_SA, e_PAR, e_SAR, e_Pi, e_Psi, e_CS;
+    dbuf<u32> e_gx, e_gy, e_gw, e_cell, e_rks, e_rkspw, e_adjL, e_adjR;
+    dbuf<u32> e_tpos, e_tlen, e_tsrc, e_thop, e_tkeys, e_tvals;
+    dbuf<u64> e_key, e_key2, e_key3, e_hkey, e_hval;
     // device decode (csrc/decode.hip)
     dbuf<u32> dec_fid, dec_fid2;
     dbuf<pos_t> dec_ref, dec_ref2;
@@ -214,7 +221,9 @@ struct engine {
     u64 ssszip_gapped();      // csrc/ssszip.hip
     u64 huffman_container();  // csrc/huffman.hip
     void build_sa_full(const u8* T);
-    u64 factorize_exact(bool log);  // csrc/exact.hip
+    u64 factorize_exact(bool log);  // csrc/exact.hip (full suffix array, LZ77SSS_TRANSF_FULL_SA)
+    u64 factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int log2_override, bool log);  // csrc/smpl.hip
+    void build_interval_samples(smpl_view& V, u64 nn, u64 za);                                         // csrc/smpl.hip
     u64 decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
     lce_view view(const u8* T) const;
 };

@@ -27,6 +27,10 @@ struct engine_if {
     virtual void sss(u64* size, int* has_runs) = 0;
     virtual u64 sss_size() const = 0;
     virtual const u64* sss_ptr() const = 0;
+    // sync set of a decision range (build_sss_range), kept apart from the text's own S
+    virtual void sss_range(u64 first, u64 end, u64 base, u64 window, u64* size, int* has_runs) = 0;
+    virtual u64 range_size() const = 0;
+    virtual const u64* range_ptr() const = 0;
     virtual u64 num_phr() const = 0;
     virtual const u64* lpf_ptr() const = 0;  // (beg, end, src) triples
     virtual const u32* sa_ptr() const = 0;

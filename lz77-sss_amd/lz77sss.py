@@ -23,6 +23,7 @@ import numpy as np
 LPF_NAIVE, LPF_LNF_NAIVE, LPF_OPT, LPF_LNF_OPT = 0, 1, 2, 3   # enum phrase_mode, lz77_sss.hpp:48-53
 GREEDY_NAIVE, GREEDY, SKIP_PHRASES = 0, 1, 2                 # enum factorize_mode, lz77_sss.hpp:55-59
 NAIVE, WITH_SAMPLES, WITHOUT_SAMPLES = 0, 1, 2               # enum transform_mode, lz77_sss.hpp:60-64
+FULL_SA = 3                                                    # device extension: LPF over the full suffix array
 DEFAULT_TAU = 512
 
 _HERE = Path(__file__).resolve().parent
@@ -186,7 +187,9 @@ class Session:
         return z.value
 
     def factorize_exact(self, transf_mode=WITHOUT_SAMPLES, **kw) -> int:
-        """factorize_exact<greedy, lpf_opt, transf_mode>: canonical greedy LZ77 lengths (csrc/exact.hip)."""
+        """factorize_exact<greedy, lpf_opt, transf_mode>: canonical greedy LZ77 lengths.  naive /
+        with_samples / without_samples: the sample-index path (csrc/smpl.hip); FULL_SA: LPF over
+        the full suffix array (csrc/exact.hip)."""
         p = params(**kw)
         z = _U64()
         _check(load_library().lz77sss_session_factorize_exact(self._h, ctypes.byref(p), transf_mode, ctypes.byref(z)))
@@ -332,8 +335,8 @@ class Session:
         return out[:c.value]
 
     def stats(self) -> list[int]:
-        out = np.zeros(24, np.uint64)
-        k = load_library().lz77sss_session_stats(self._h, out.ctypes.data_as(_P), 24)
+        out = np.zeros(28, np.uint64)
+        k = load_library().lz77sss_session_stats(self._h, out.ctypes.data_as(_P), 28)
         return [int(x) for x in out[:max(k, 0)]]
 
     def phase_times(self) -> dict[str, float]:

@@ -3,10 +3,12 @@
 The reference's own tests check its exact modes only by decode(factorize(T)) == T
 (tests/test_lz77_sss.cpp:95-133).  Here the lengths are pinned harder: the
 oracle's exact restatement is checked against a brute-force longest-previous-
-factor parse, and the device stream (lengths and the PSV/NSV source rule) is
-compared bit for bit with the oracle.  Sources are not the reference's (its
-sample/range-structure visit order is not restated): "parity unpinned" for
-sources, pinned by definition for lengths.
+factor parse; the sample-index path (transf_mode naive / with_samples /
+without_samples, csrc/smpl.hip) must give the oracle's lengths with valid sources,
+and FULL_SA (csrc/exact.hip) the oracle's stream bit for bit (lengths and the
+PSV/NSV source rule).  Sources are not the reference's (its PA / SA tie order comes
+from an unstable parallel sort): "parity unpinned" for sources, pinned by
+definition for lengths.
 """
 from __future__ import annotations
 
@@ -76,51 +78,92 @@ def run_exact(session, T, **kw):
     return s, s.factors(z)
 
 
+def check_exact(lz, T, F, F_ref):
+    """Exact-smpl stream: the canonical lengths (the oracle's), valid sources, decodes to T."""
+    assert F.shape == F_ref.shape
+    assert np.array_equal(F[:, 1], F_ref[:, 1])
+    check_valid(T, F)
+    if T.size:
+        ln = F[:, 1].astype(np.int64)
+        pos = np.concatenate([[0], np.cumsum(np.maximum(ln, 1))[:-1]])
+        cp = ln > 0
+        # every copy's source is an earlier occurrence (checked by decoding)
+        assert np.array_equal(lz.decode(F, T.size), T)
+        assert np.all(F[cp, 0].astype(np.int64) < pos[cp])
+
+
+SMPL_MODES = [0, 1, 2]  # naive, with_samples, without_samples (lz77_sss.hpp:60-64)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", golden_names())
 def test_gpu_exact_golden(session, name):
+    """FULL_SA (LPF over the full suffix array): bit-exact with the oracle, sources included."""
     g = load_golden(name)
-    _, F = run_exact(session, g["text"])
+    _, F = run_exact(session, g["text"], transf_mode=3)
     assert np.array_equal(F, g["factors_exact"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transf_mode", SMPL_MODES)
+@pytest.mark.parametrize("name", golden_names())
+def test_gpu_exact_smpl_golden(session, lz, name, transf_mode):
+    """The sample-index path (csrc/smpl.hip): the oracle's lengths on every fixture."""
+    g = load_golden(name)
+    _, F = run_exact(session, g["text"], transf_mode=transf_mode)
+    check_exact(lz, g["text"], F, g["factors_exact"])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(1, 17))
 def test_gpu_exact_c1_seeds(session, orc, lz, seed):
     T = lz.gen_random_repetitive(10000, 200000, seed)
-    _, F = run_exact(session, T)
-    assert np.array_equal(F, orc.factorize_exact(T))
-    assert np.array_equal(lz.decode(F, T.size), T)
+    F_ref = orc.factorize_exact(T)
+    _, F = run_exact(session, T, transf_mode=3)
+    assert np.array_equal(F, F_ref)
+    for tm in SMPL_MODES:
+        _, F = run_exact(session, T, transf_mode=tm)
+        check_exact(lz, T, F, F_ref)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transf_mode", [0, 2])
+@pytest.mark.parametrize("transf_mode", SMPL_MODES + [3])
 def test_gpu_exact_transform_modes_agree(session, orc, lz, transf_mode):
     T = lz.gen_random_repetitive(50000, 120000, 77)
     _, F = run_exact(session, T, transf_mode=transf_mode)
-    assert np.array_equal(F, orc.factorize_exact(T))
+    check_exact(lz, T, F, orc.factorize_exact(T))
 
 
 @pytest.mark.gpu
-def test_gpu_exact_with_samples_rejected(session, lz):
-    """with_samples needs the reference's sample index (not built on the device): EINVAL, not a silent
-    substitute."""
-    T = lz.gen_random_repetitive(20000, 20000, 3)
+def test_gpu_exact_smpl_structures(session, lz):
+    """The sample set of common.cpp:34-88: delta = min(n / z_approx, 256), samples every delta
+    characters at most (stats 24..27: samples, delta, phrase tasks, rounds << 32 | walks)."""
+    T = lz.gen_random_repetitive(200000, 200000, 5)
     s = session(T.size)
     s.load(T)
-    with pytest.raises(lz.Lz77SssError, match="with_samples"):
-        s.factorize_exact(transf_mode=lz.WITH_SAMPLES)
+    za = s.factorize()
+    for tm in SMPL_MODES:
+        z = s.factorize_exact(transf_mode=tm)
+        st = s.stats()
+        c, delta = st[24], st[25]
+        assert delta == min(T.size // za, 256)
+        assert T.size // delta <= c <= T.size // delta + za + 1
+        assert z > 0 and st[26] >= za
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("period", [1, 3, 170, 171, 600])
-def test_gpu_exact_runs(session, orc, period):
+def test_gpu_exact_runs(session, orc, lz, period):
     rng = np.random.Generator(np.random.PCG64(period))
     unit = rng.integers(0, 256, period, dtype=np.uint8)
     T = np.concatenate([rng.integers(0, 256, 3000, dtype=np.uint8), np.tile(unit, 40000 // period + 1)[:40000],
                         rng.integers(0, 256, 2000, dtype=np.uint8)])
-    _, F = run_exact(session, T)
-    assert np.array_equal(F, orc.factorize_exact(T))
+    F_ref = orc.factorize_exact(T)
+    _, F = run_exact(session, T, transf_mode=3)
+    assert np.array_equal(F, F_ref)
+    for tm in SMPL_MODES:
+        _, F = run_exact(session, T, transf_mode=tm)
+        check_exact(lz, T, F, F_ref)
 
 
 @pytest.mark.gpu
@@ -128,9 +171,40 @@ def test_gpu_exact_runs(session, orc, period):
 def test_gpu_exact_medium(session, orc, lz, kind, mib):
     n = mib << 20
     T = lz.gen_genome(n, 2 << 20, 0.001, 11) if kind == "genome" else lz.gen_random_repetitive(n, n, 5, 0.5, 0.05)
-    _, F = run_exact(session, T)
     F_ref = orc.factorize_exact(T)
+    _, F = run_exact(session, T, transf_mode=3)
     assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+    _, F = run_exact(session, T, transf_mode=2)
+    check_exact(lz, T, F, F_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transf_mode", [1, 2])
+def test_gpu_exact_smpl_64mib(session, lz, transf_mode):
+    """exact-smpl on a 64 MiB repetitive text: the canonical lengths of FULL_SA (which equals the
+    oracle bit for bit up to 16 MiB, test_gpu_exact_medium)."""
+    n = 64 << 20
+    T = lz.gen_random_repetitive(n, n, 9, 0.5, 0.05)
+    _, F_ref = run_exact(session, T, transf_mode=3)
+    _, F = run_exact(session, T, transf_mode=transf_mode)
+    check_exact(lz, T, F, F_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_gpu_exact_smpl_one_gib(session, lz):
+    """configs[4] at full size (1 GiB rr): exact-smpl lengths == FULL_SA lengths, decode == T."""
+    n = 1 << 30
+    T = lz.gen_random_repetitive(n, n, 42, 0.5, 0.05)
+    s = session(n)
+    s.load(T)
+    z = s.factorize_exact(transf_mode=3)
+    F_ref = s.factors(z)
+    z2 = s.factorize_exact(transf_mode=2)
+    F = s.factors(z2)
+    assert z2 == z and np.array_equal(F[:, 1], F_ref[:, 1])
+    _, mism = s.decode(out=False)
+    assert mism == 0
 
 
 @pytest.mark.gpu
@@ -145,10 +219,16 @@ def test_gpu_exact_one_shot_callback(lz, orc):
 
     cb = EMIT(emit)
     p = lz.params()
-    rc = lz.load_library().lz77sss_factorize_exact_u32(T.ctypes.data_as(ctypes.c_void_p), T.size, ctypes.byref(p),
-                                                       lz.WITHOUT_SAMPLES, cb, None)
-    assert rc == 0
-    assert np.array_equal(np.concatenate(got), orc.factorize_exact(T))
+    for tm, exact_sources in [(lz.WITHOUT_SAMPLES, False), (3, True)]:
+        got.clear()
+        rc = lz.load_library().lz77sss_factorize_exact_u32(T.ctypes.data_as(ctypes.c_void_p), T.size,
+                                                           ctypes.byref(p), tm, cb, None)
+        assert rc == 0
+        F = np.concatenate(got)
+        if exact_sources:
+            assert np.array_equal(F, orc.factorize_exact(T))
+        else:
+            check_exact(lz, T, F, orc.factorize_exact(T))
 
 
 @pytest.mark.gpu

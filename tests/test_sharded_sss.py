@@ -366,7 +366,20 @@ def _run_resident(world, T, wide=False, gen=None):
     procs = [ctx.Process(target=_resident_worker, args=(r, world, port, qq, T, wide, gen)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted((qq.get(timeout=900) for _ in procs), key=lambda x: x[0])
+    import queue
+    import time
+
+    got, t0 = [], time.time()
+    while len(got) < world:  # a rank that dies fails the test instead of leaving the others waiting
+        try:
+            got.append(qq.get(timeout=5))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() - t0 > 900:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f"rank failed (exit codes {[p.exitcode for p in procs]})")
+    res = sorted(got, key=lambda x: x[0])
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
