@@ -103,15 +103,19 @@ def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2, runs: in
     T = make_text(lz, workload, n, 0)
     p = oracle.num_threads()
     res = {}
+    par = False
     for threads in (p, 1):
         secs, z = [], 0
         for r in range(runs):
-            z, sec, _ = oracle.factorize_timed_p(T, threads, phr_mode=phr_mode)
+            z, sec, _, par_r = oracle.factorize_timed_p(T, threads, phr_mode=phr_mode)
+            par = par or (threads == p and par_r)
             secs.append(sec)
             print(f"cpu_baseline {workload} p={threads} run {r + 1}/{runs}: {sec:.2f} s", file=sys.stderr, flush=True)
         res[threads] = (statistics.median(secs), z, secs)
     sec_p, z_p, _ = res[p]
     sec_1, z_1, _ = res[1]
+    greedy = ("the reference's racy parallel greedy, greedy_parallel.cpp:31-285, selected as lz77_sss.hpp:467-474"
+              if par else "sequential greedy: lz77_sss.hpp:467-474 does not select the parallel one for this text")
     desc = ("full 1 GiB workload text" if n == GIB else f"{sample_mib} MiB instance of the same generator")
     return {"value": round(n / sec_p / 1e6, 2), "unit": "MB/s", "cores": p, "kind": "port",
             "cpu_model": cpu_model(), "runs": runs,
@@ -119,7 +123,8 @@ def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2, runs: in
             "sample": f"{workload}: {desc} (n={n}), oracle factorize_approximate<greedy,"
                       f"{'lpf_opt' if phr_mode == 2 else 'lpf_lnf_opt'}> median of {runs}: p={p} threads "
                       f"{sec_p:.2f} s (z={z_p}; OpenMP SSS/sort stages, LPF in {p} partitions as "
-                      f"lpf_opt.cpp:46-56, sequential greedy), p=1 {sec_1:.2f} s (z={z_1})"}
+                      f"lpf_opt.cpp:46-56, {greedy}), p=1 {sec_1:.2f} s (z={z_1})",
+            "greedy_parallel": par}
 
 
 def cpu_baseline_exact(lz, workload: str, sample_mib: int):

@@ -34,10 +34,10 @@
 namespace LZ_NS {
 
 // ---------------------------------------------------------------------------
-// Q anchors.  A workgroup of 256 lanes covers anchors tb-1 .. tb+254 (lane i ->
-// anchor tb-1+i) and owns tb .. tb+252; the three halo anchors give the owned
-// ones their neighbours' periods.  Text [a(tb-1) - 256, a(tb+254) + 1024) is
-// staged in LDS.
+// Q anchors.  A workgroup of QT_THREADS lanes (128 by default) covers anchors
+// tb-1 .. tb+QT_THREADS-2 (lane i -> anchor tb-1+i) and owns QT_OWN = QT_THREADS-3 of
+// them (tb .. tb+QT_OWN-1); the three halo anchors give the owned ones their
+// neighbours' periods.  Text [a(tb-1) - 256, a(tb+QT_THREADS-2) + 1024) is staged in LDS.
 constexpr int SNB = 64;                       // decision blocks per stripe (k_sss_stream)
 constexpr int SD = SNB * (int)TAU;            // decisions per stripe (32768)
 #ifndef LZ_QT_THREADS

@@ -449,8 +449,19 @@ static inline std::vector<lpf_t<P>> build_lpf_opt_par(const u8* T, u64 n, const 
         const P b = (P)((u64)i * (n / p)), e = i == p - 1 ? (P)n : (P)((u64)(i + 1) * (n / p));
         lpf_opt_part<P>(T, L, PSV, NSV, b, e, parts[i]);
     }
+    // concatenated as the reference's next_lpf walks them (factorize/common.cpp:74-104): entering
+    // partition k skips its phrases ending at or before the last phrase's end and trims the
+    // first one that overlaps it
     std::vector<lpf_t<P>> out;
-    for (auto& v : parts) out.insert(out.end(), v.begin(), v.end());
+    for (auto& v : parts) {
+        size_t i = 0;
+        if (!out.empty()) {
+            const P le = out.back().end;
+            while (i < v.size() && v[i].end <= le) i++;
+            if (i < v.size() && v[i].beg < le) { const P offs = le - v[i].beg; v[i].beg += offs; v[i].src += offs; }
+        }
+        out.insert(out.end(), v.begin() + i, v.end());
+    }
     return out;
 }
 
@@ -742,7 +753,170 @@ struct approx_stats {
     u64 num_lpf = 0, len_lpf_phr = 0, num_gaps = 0;
     std::array<u32, 5> patt_lens{};
     u32 roll_threshold = 0, log2_size_h = 0;
+    bool greedy_parallel = false;  // the p > 1 racy greedy ran (timing legs only)
 };
+
+// ===========================================================================
+//  The reference's p > 1 greedy, for the CPU baseline's timing only
+//  (factorize_greedy_parallel, approximate/factorize/greedy_parallel.cpp:31-285, with
+//  parallel_rolling_hash_index_107.hpp:33-178).  The gap positions are cut into blocks
+//  of max(4096, (n / p) / 512) gap bytes (greedy_parallel.cpp:196-230); the first p
+//  blocks are walked by one thread reading the table it writes, every later round
+//  walks p blocks at once, each reading the snapshot H_old taken at the round start
+//  and writing H_new unsynchronized (racy by design: the stream depends on the thread
+//  interleaving, so it is never a parity target).  Selected by the reference for
+//  greedy on run-free texts with |S| < 1.3 * 2n / tau, n > 500 000 and gaps covering
+//  more than 20 % of the text (lz77_sss.hpp:467-474).
+// ===========================================================================
+template <class Q>
+static inline bool use_greedy_parallel(Q n, const lce_structure<Q>& L, const gap_params& gp, int p) {
+    return !L.has_runs && (double)L.s() < 1.3 * ((2.0 * (double)n) / TAU) && (u64)n > 500000 &&
+           gp.rel_len_gaps > 0.2 && p > 1;
+}
+
+template <class Q, typename OUT>
+static inline void greedy_parallel(const u8* T, Q n, const lce_structure<Q>& L, const std::vector<lpf_t<Q>>& P,
+                                   const gap_params& gp, u32 rk_seed, int p, OUT&& output) {
+    using lpf = lpf_t<Q>;
+    using factor = factor_t<Q>;
+    const std::array<u64, 5> bases = gap_bases(rk_seed);
+    // par_gap_idx sizing: one entry less in log2 than the single table (two tables,
+    // parallel_rolling_hash_index_107.hpp:66-68)
+    const u32 lg = gp.log2_size_h > 1 ? gp.log2_size_h - 1 : 1;
+    const u64 mask = ((u64)1 << lg) - 1;
+    std::vector<Q> H_old((size_t)1 << lg), H_new((size_t)1 << lg, ~(Q)0);
+    rk107 rh[5];
+    for (int i = 0; i < 5; i++) rh[i].init(bases[i], gp.patt_lens[i]);
+    const auto& lens = gp.patt_lens;
+    const Q thr = gp.roll_threshold;
+    // next_lpf over the flat phrase list (the last element, the sentinel, repeats)
+    auto next_lpf = [&](size_t& li) -> lpf {
+        lpf phr = P[li++];
+        if (li == P.size()) li--;
+        return phr;
+    };
+    Q len_gaps = n;
+    for (size_t k = 0; k + 1 < P.size(); k++) len_gaps -= P[k].end - P[k].beg;
+    struct blk { size_t li; Q beg; };
+    const Q blk_size = std::max<Q>(4096, (Q)((n / (Q)p) / 512));
+    const Q num_blks = (len_gaps + blk_size - 1) / blk_size;
+    std::vector<blk> info;
+    info.reserve(num_blks + 1);
+    {
+        size_t cur = 0, lst = cur;
+        lpf lpf_lst = next_lpf(cur);
+        u64 cur_len_gaps = lpf_lst.beg, cur_blk_beg = 0;
+        for (Q b = 0; b < num_blks; b++) {
+            while (cur_len_gaps <= cur_blk_beg) {
+                const lpf lc = next_lpf(cur);
+                cur_len_gaps += lc.beg - lpf_lst.end;
+                lst = cur;
+                lpf_lst = lc;
+            }
+            info.push_back({lst, (Q)(lpf_lst.beg - (cur_len_gaps - cur_blk_beg))});
+            cur_blk_beg += blk_size;
+        }
+        info.push_back({0, n});
+    }
+    auto reinit = [&](std::array<u128, 5>& fps, Q pos) {
+        for (int i = 0; i < 5; i++) {
+            fps[i] = 0;
+            for (u32 j = 0; j < lens[i]; j++)
+                if ((u64)pos + lens[i] < n) fps[i] = mod107(fps[i] * rh[i].base + T[pos + j]);
+        }
+    };
+    auto roll_i = [&](std::array<u128, 5>& fps, int i, Q pos) {
+        fps[i] = mod107(fps[i] * rh[i].base + mod107((u128)T[pos + lens[i]] + rh[i].negpow[T[pos]]));
+    };
+    auto advance = [&](std::array<u128, 5>& fps, Q pos) {
+        for (int i = 0; i < 5; i++)
+            if ((u64)pos + lens[i] < n) { H_new[(u64)fps[i] & mask] = pos; roll_i(fps, i, pos); }
+    };
+    std::vector<std::vector<factor>> out(p);
+    auto factorize_block = [&](bool first, Q b0, Q b1, std::vector<factor>& fv) {
+        const Q beg = info[b0].beg, end = info[b1].beg;
+        std::array<u128, 5> fps;
+        size_t li = info[b0].li;
+        lpf phr = next_lpf(li);
+        Q pos_idx = beg;
+        reinit(fps, beg);
+        auto lpo = [&](Q pos) -> factor {  // longest_prev_occ_par (greedy_parallel.cpp:31-63)
+            factor f{T[pos], 0};
+            for (int x = 4; x >= 0; x--) {
+                if (f.len == 0) {
+                    const u64 h = (u64)fps[x] & mask;
+                    const Q occ = first ? H_new[h] : H_old[h];
+                    H_new[h] = pos;
+                    if ((u64)pos + lens[x] < n) roll_i(fps, x, pos);
+                    if (occ < pos && T[occ] == T[pos]) { f.len = (Q)L.lce(occ, pos); f.src = occ; }
+                } else if ((u64)pos + lens[x] < n) {
+                    H_new[(u64)fps[x] & mask] = pos;
+                    roll_i(fps, x, pos);
+                }
+            }
+            if (f.len > end - pos) f.len = end - pos;
+            return f;
+        };
+        for (Q i = beg; true;) {
+            Q gap_end = std::min<Q>(phr.beg, end);
+            if (i < gap_end) {
+                if (pos_idx < i) {
+                    if (i - pos_idx <= thr) {
+                        do {
+                            for (int x = 0; x < 5; x++)
+                                if ((u64)pos_idx + lens[x] < n) roll_i(fps, x, pos_idx);
+                            pos_idx++;
+                        } while (pos_idx < i);
+                    } else {
+                        reinit(fps, i);
+                        pos_idx = i;
+                    }
+                }
+                do {
+                    factor f = lpo(i);
+                    pos_idx++;
+                    i += std::max<Q>(1, f.len);
+                    if (i > gap_end) {
+                        if (i <= phr.end) { f.len -= i - gap_end; i = gap_end; }
+                        else {
+                            do { phr = next_lpf(li); } while (phr.end <= i);
+                            while (pos_idx < gap_end) advance(fps, pos_idx++);
+                            gap_end = std::min<Q>(phr.beg, end);
+                        }
+                    }
+                    fv.push_back(f);
+                    while (pos_idx < i) advance(fps, pos_idx++);
+                } while (i < gap_end);
+            }
+            if (i >= end) break;
+            const Q exc = i - gap_end;
+            factor lf{phr.src + exc, (phr.end - phr.beg) - exc};
+            if (pos_idx == i) {
+                factor f = lpo(i);
+                pos_idx++;
+                if (f.len > lf.len) lf = f;
+            }
+            fv.push_back(lf);
+            i += lf.len;
+            while (phr.end <= i) phr = next_lpf(li);
+        }
+    };
+    for (Q cur = 0; cur < num_blks;) {
+        const Q blks = std::min<Q>((Q)p, num_blks - cur);
+#pragma omp parallel for num_threads(p)
+        for (size_t k = 0; k < H_new.size(); k++) H_old[k] = H_new[k];  // overwrite(p)
+#pragma omp parallel num_threads(p)
+        {
+            const int ip = omp_get_thread_num();
+            if ((Q)ip < blks) {
+                if (cur == 0) { if (ip == 0) factorize_block(true, 0, blks, out[0]); }
+                else factorize_block(false, cur + ip, cur + ip + 1, out[ip]);
+            }
+        }
+        for (auto& v : out) { for (const factor& f : v) output(f); v.clear(); }
+        cur += blks;
+    }
+}
 
 template <class Q = u32, typename OUT>
 static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, OUT&& output,
@@ -798,6 +972,11 @@ static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, 
         st->size_sss = L.s(); st->has_runs = L.has_runs; st->num_lpf = pi.num_lpf;
         st->len_lpf_phr = pi.len_lpf_phr; st->num_gaps = pi.num_gaps; st->patt_lens = gp.patt_lens;
         st->roll_threshold = gp.roll_threshold; st->log2_size_h = gp.log2_size_h;
+    }
+    if (fact_mode == 1 && lpf_parts > 1 && use_greedy_parallel<Q>(n, L, gp, lpf_parts)) {
+        if (st) st->greedy_parallel = true;
+        greedy_parallel<Q>(T, n, L, P, gp, rk_seed, lpf_parts, output);
+        return;
     }
     gap_index<Q> G;
     G.create(T, n, gp.patt_lens, gp.log2_size_h, gap_bases(rk_seed));

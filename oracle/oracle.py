@@ -44,7 +44,11 @@ def lib():
                                              ctypes.POINTER(_U64)]
         L.oracle_factorize_timed_p.restype = ctypes.c_int64
         L.oracle_factorize_timed_p.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
-                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]
+                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64),
+                                               ctypes.POINTER(ctypes.c_int)]
+        L.oracle_factorize_p.restype = ctypes.c_int64
+        L.oracle_factorize_p.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, _P, _U64,
+                                         ctypes.POINTER(ctypes.c_int)]
         L.oracle_sss.restype = ctypes.c_int64
         L.oracle_sss.argtypes = [_P, _U64, _P, _U64, ctypes.POINTER(ctypes.c_int)]
         L.oracle_q_bruteforce.restype = None
@@ -187,14 +191,31 @@ def factorize_timed(T, phr_mode: int = LPF_OPT, rk_seed: int = 42):
 
 def factorize_timed_p(T, threads: int, phr_mode: int = LPF_OPT, rk_seed: int = 42):
     """CPU baseline at `threads` threads (every OpenMP stage; LPF in per-thread partitions as
-    lpf_opt.cpp:46-56 when threads > 1) -> (z, seconds, hash).  Timing only: at threads > 1
-    the phrases (and so the stream) may differ from the p = 1 parity stream."""
+    lpf_opt.cpp:46-56 when threads > 1, the reference's racy parallel greedy where
+    lz77_sss.hpp:467-474 selects it) -> (z, seconds, hash, parallel_greedy_ran).  Timing only: at
+    threads > 1 the phrases (and so the stream) may differ from the p = 1 parity stream."""
     buf = _padded(T)
     n = _u8(T).size
-    sec, h = ctypes.c_double(), _U64()
+    sec, h, par = ctypes.c_double(), _U64(), ctypes.c_int()
     z = lib().oracle_factorize_timed_p(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, threads, ctypes.byref(sec),
-                                       ctypes.byref(h))
-    return int(z), sec.value, h.value
+                                       ctypes.byref(h), ctypes.byref(par))
+    return int(z), sec.value, h.value, bool(par.value)
+
+
+def factorize_p(T, threads: int, rk_seed: int = 42):
+    """The CPU baseline's p-thread stream (LPF in `threads` partitions; the reference's racy parallel
+    greedy where lz77_sss.hpp:467-474 selects it) -> (factors (z,2) uint32, parallel_greedy_ran).
+    Validity tests of the timing leg only: it is not a parity stream."""
+    buf = _padded(T)
+    n = _u8(T).size
+    cap = n + 4
+    out = np.zeros((cap, 2), np.uint32)
+    par = ctypes.c_int()
+    z = lib().oracle_factorize_p(buf.ctypes.data_as(_P), n, threads, rk_seed, out.ctypes.data_as(_P), cap,
+                                 ctypes.byref(par))
+    if z < 0:
+        raise RuntimeError("oracle factorize_p failed")
+    return out[:z].copy(), bool(par.value)
 
 
 def factorize_skip(T, phr_mode: int = LPF_OPT):

@@ -39,6 +39,29 @@ int64_t oracle_factorize_approx(uint8_t* T, uint64_t n, int phr_mode, uint32_t r
     }
 }
 
+// The p-thread CPU-baseline leg's stream (LPF in p partitions, the reference's racy parallel
+// greedy where lz77_sss.hpp:467-474 selects it): for the validity tests of the timing leg only.
+// *par = 1 when the parallel greedy ran.  Returns the factor count, -1 on error / overflow.
+int64_t oracle_factorize_p(uint8_t* T, uint64_t n, int p, uint32_t rk_seed, uint32_t* out, uint64_t cap, int* par) {
+    try {
+        const int prev = omp_get_max_threads();
+        omp_set_num_threads(std::max(1, p));
+        uint64_t k = 0;
+        bool overflow = false;
+        approx_stats st;
+        factorize_approximate(T, (u32)n, lpf_opt, rk_seed, [&](factor f) {
+            if (k < cap) { out[2 * k] = f.src; out[2 * k + 1] = f.len; } else overflow = true;
+            k++;
+        }, &st, 1, std::max(1, p));
+        omp_set_num_threads(prev);
+        if (par) *par = st.greedy_parallel;
+        return overflow ? -1 : (int64_t)k;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -1;
+    }
+}
+
 // pos_t = uint64_t form (lz77_sss<uint64_t>): out 2*cap uint64 pairs, stats 12 x uint64.
 int64_t oracle_factorize_approx64(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed, int fact_mode,
                                   uint64_t* out, uint64_t cap, uint64_t* stats) {
@@ -172,19 +195,21 @@ int64_t oracle_factorize_timed(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk
 // (lpf_opt.cpp:46-56).  The greedy emitter stays sequential: the reference's parallel
 // gap index (lz77_sss.hpp:470-474, run-free texts only) is not restated.  Timing only.
 int64_t oracle_factorize_timed_p(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed, int p,
-                                 double* seconds, uint64_t* stream_hash) {
+                                 double* seconds, uint64_t* stream_hash, int* par) {
     const int prev = omp_get_max_threads();
     omp_set_num_threads(std::max(1, p));
     uint64_t k = 0, h = 1469598103934665603ull;
+    approx_stats st;
     auto t0 = std::chrono::steady_clock::now();
     factorize_approximate(T, (u32)n, phr_mode, rk_seed, [&](factor f) {
         k++;
         uint32_t w[2] = {f.src, f.len};
         const uint8_t* q = (const uint8_t*)w;
         for (int i = 0; i < 8; i++) { h ^= q[i]; h *= 1099511628211ull; }
-    }, nullptr, 1, std::max(1, p));
+    }, &st, 1, std::max(1, p));
     auto t1 = std::chrono::steady_clock::now();
     omp_set_num_threads(prev);
+    if (par) *par = st.greedy_parallel;
     if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
     if (stream_hash) *stream_hash = h;
     return (int64_t)k;

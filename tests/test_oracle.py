@@ -293,3 +293,22 @@ def test_gen_genome_pos_is_position_hashed(lz):
     a = lz.gen_genome_pos(300000, 70000, 0.01, 5)
     b = lz.gen_genome_pos(100000, 70000, 0.01, 5, offset=150000)
     assert np.array_equal(a[150000:250000], b)
+
+
+@pytest.mark.parametrize("threads", [2, 4])
+def test_cpu_baseline_parallel_greedy_leg(orc, lz, threads):
+    """The CPU baseline's p > 1 leg (bench.py cpu_baseline): on a run-free genome-like text the
+    reference selects its racy parallel greedy (lz77_sss.hpp:467-474, greedy_parallel.cpp:31-285);
+    the restated leg must take that path and still emit a valid stream (decode == T).  Timing
+    only: its stream depends on the thread interleaving and is no parity target."""
+    n = 4 << 20
+    T = lz.gen_genome(n, 1 << 20, 0.001, 7)
+    F, par = orc.factorize_p(T, threads)
+    assert par, "the parallel greedy was not selected on a run-free text with > 20 % gaps"
+    assert int(F[:, 1].astype(np.uint64).sum() + (F[:, 1] == 0).sum()) == n
+    assert np.array_equal(orc.decode(F, n), T)
+    # a text with runs keeps the sequential greedy (lz77_sss.hpp:467: !LCE.has_runs())
+    R = lz.gen_random_repetitive(1 << 20, 1 << 20, 3, 0.5, 0.05)
+    F2, par2 = orc.factorize_p(R, threads)
+    assert not par2
+    assert np.array_equal(orc.decode(F2, R.size), R)
