@@ -50,7 +50,10 @@ namespace LZ_NS {
 
 constexpr u32 SMPL_MAX_DELTA = 256;  // lz77_sss.hpp:81 max_delta
 constexpr u32 SCAN_T = 4096;         // lz77_sss.hpp:83 range_scan_threshold
-constexpr u32 SG_WIN = 2048;         // grid cell width in ranks (the reference: 16384 on a CPU core)
+#ifndef LZ_SG_WIN
+#define LZ_SG_WIN 2048
+#endif
+constexpr u32 SG_WIN = LZ_SG_WIN;    // grid cell width in ranks (the reference: 16384 on a CPU core)
 constexpr u32 RKS_RATE = 16;         // lz77_sss.hpp:82 rks_sample_rate
 constexpr u32 RKS_P = 0x7FFFFFFFu;   // Mersenne prime 2^31 - 1 (rabin_karp_substring<31>)
 constexpr u32 RKS_B = 0x2545F491u % RKS_P;  // fixed base (the reference draws one per run)

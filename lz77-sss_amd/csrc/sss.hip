@@ -535,7 +535,9 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
                                                            u32 b, sss_pow32 PW, u32 scap, u64* __restrict__ hitw,
                                                            u16* __restrict__ q_init, u8* __restrict__ rp_init,
                                                            const u32* __restrict__ list,
-                                                           const u32* __restrict__ list_cnt) {
+                                                           const u32* __restrict__ list_cnt,
+                                                           u8* __restrict__ blk_p, u16* __restrict__ blk_fo,
+                                                           u16* __restrict__ blk_lo, u64 nbk) {
     const u32 lane = threadIdx.x & 63;
     // the stripe index is wave-uniform: keep it (and every address derived from it) in SGPRs
     const u64 wi = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -811,6 +813,23 @@ stripe_done:
             *(u64*)(q_init + t) = 0xFF00FF00FF00FF00ull;
             *(u32*)(rp_init + t) = 0u;
         }
+        // the per-block run records start out unknown (k_sss_runs writes the stripes it settles);
+        // the last stripe also clears the blocks past its own, up to nbk inclusive
+        {
+            const u64 gk = w * (u64)SNB + lane;
+            if (gk <= nbk) {
+                blk_p[gk] = 0;
+                blk_fo[gk] = 0;
+                blk_lo[gk] = 0;
+            }
+            if (w + 1 == nstripes) {
+                for (u64 g2 = gk + 64; g2 <= nbk; g2 += 64) {
+                    blk_p[g2] = 0;
+                    blk_fo[g2] = 0;
+                    blk_lo[g2] = 0;
+                }
+            }
+        }
         if (dirty) nout = 0;  // re-run
     }
     if (lane == 0) {
@@ -947,6 +966,8 @@ __device__ __forceinline__ int last_diff(u64 d) {
     return (int)(8 * L + ((63 - __builtin_clzll(v)) >> 3));
 }
 
+// (113 VGPRs = 4 waves per SIMD; bounding it to the 5 its LDS allows spills 17 VGPRs and was
+// slower on rr: 0.518 vs 0.483 ms for the SSS kernels, tools/gpu_r03b.sh)
 __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__ T, u64 n, u64 last_i, u64 nstripes,
                                                         pos_t* __restrict__ s_out, u32* __restrict__ s_cnt,
                                                         u32* __restrict__ s_flag, u32* __restrict__ ovf_ctr, u32 b,
@@ -1378,6 +1399,151 @@ __global__ void k_blk_runinfo(const u8* __restrict__ bp, const u16* __restrict__
     re[b] = (e << 16) | (xe << 8) | p;
     rs[b] = (st << 16) | (xs << 8) | p;
 }
+// Run-record segments (maximal runs of consecutive blocks with the same nonzero period) in
+// two launches: k_blk_seg_tiles finds per tile of BT_TILE blocks its first segment end
+// (first block b with !cont_f(b)) and last segment start (last b with !cont_b(b)); then
+// k_blk_seg_info computes every block's segment end/start inside its tile by LDS scans,
+// resolves segments that cross tile boundaries through the tile table (a wave-parallel
+// search over 64 tiles per step) and writes the packed records.  Same values as the
+// marker + min/max-scan formulation (k_blk_marks + two device scans + k_blk_runinfo).
+constexpr u32 BT_T = 1024, BT_PER = 4, BT_TILE = BT_T * BT_PER;
+constexpr u64 BT_NONE = ~0ull;
+__device__ __forceinline__ bool blk_cont_f(const u8* __restrict__ bp, u64 nbk, u64 b) {
+    const u32 p = bp[b];
+    return p && b + 1 < nbk && bp[b + 1] == p;
+}
+__device__ __forceinline__ bool blk_cont_b(const u8* __restrict__ bp, u64 b) {
+    const u32 p = bp[b];
+    return p && b > 0 && bp[b - 1] == p;
+}
+__global__ __launch_bounds__(BT_T) void k_blk_seg_tiles(const u8* __restrict__ bp, u64 nbk, u64* __restrict__ tfe,
+                                                        u64* __restrict__ tls) {
+    __shared__ u64 s_e[BT_T / 64], s_s[BT_T / 64];
+    const u32 t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const u64 t0 = (u64)blockIdx.x * BT_TILE;
+    u64 fe = BT_NONE, ls = BT_NONE;
+    for (u32 k = 0; k < BT_PER; k++) {
+        const u64 b = t0 + (u64)k * BT_T + t;
+        if (b >= nbk) break;
+        if (fe == BT_NONE && !blk_cont_f(bp, nbk, b)) fe = b;
+        if (!blk_cont_b(bp, b)) ls = b;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        const u64 a = __shfl_xor(fe, o), c = __shfl_xor(ls, o);
+        fe = min(fe, a);
+        ls = (ls == BT_NONE) ? c : (c == BT_NONE ? ls : max(ls, c));
+    }
+    if (lane == 0) {
+        s_e[wv] = fe;
+        s_s[wv] = ls;
+    }
+    __syncthreads();
+    if (t == 0) {
+        u64 e = BT_NONE, l = BT_NONE;
+        for (u32 k = 0; k < BT_T / 64; k++) {
+            e = min(e, s_e[k]);
+            if (s_s[k] != BT_NONE) l = (l == BT_NONE) ? s_s[k] : max(l, s_s[k]);
+        }
+        tfe[blockIdx.x] = e;
+        tls[blockIdx.x] = l;
+    }
+}
+__global__ __launch_bounds__(BT_T) void k_blk_seg_info(const u8* __restrict__ bp, const u16* __restrict__ fo,
+                                                       const u16* __restrict__ lo, u64 nbk,
+                                                       const u64* __restrict__ tfe, const u64* __restrict__ tls,
+                                                       u64 ntile, u64* __restrict__ re, u64* __restrict__ rs) {
+    __shared__ u64 s_end[BT_TILE];  // per block: its segment's last block inside the tile, or BT_NONE
+    __shared__ u64 s_beg[BT_TILE];  // per block: its segment's first block inside the tile, or BT_NONE
+    __shared__ u64 s_after, s_before;
+    const u32 t = threadIdx.x, lane = t & 63;
+    const u64 tile = blockIdx.x, t0 = tile * BT_TILE;
+    const u64 tn = min<u64>(BT_TILE, nbk - t0);
+    for (u32 k = t; k < BT_TILE; k += BT_T) {
+        const u64 b = t0 + k;
+        s_end[k] = (k < tn && !blk_cont_f(bp, nbk, b)) ? b : BT_NONE;
+        s_beg[k] = (k < tn && !blk_cont_b(bp, b)) ? b : BT_NONE;
+    }
+    // the first segment end at or after the next tile, the last segment start before this
+    // tile (wave 0 / wave 1 search the tile table 64 tiles per step)
+    if (t < 64) {
+        u64 r = BT_NONE;
+        for (u64 base = tile + 1; base < ntile; base += 64) {
+            const u64 x = base + lane < ntile ? tfe[base + lane] : BT_NONE;
+            const u64 bal = __ballot(x != BT_NONE);
+            if (bal) {
+                const u32 L = (u32)__builtin_ctzll(bal);
+                r = __shfl(x, (int)L);
+                break;
+            }
+        }
+        if (lane == 0) s_after = r;
+    } else if (t < 128) {
+        u64 r = BT_NONE;
+        for (u64 top = tile; top > 0;) {
+            const u64 lo_t = top >= 64 ? top - 64 : 0;
+            const u64 idx = lo_t + lane;
+            const u64 x = idx < top ? tls[idx] : BT_NONE;
+            const u64 bal = __ballot(x != BT_NONE);
+            if (bal) {
+                const u32 L = 63u - (u32)__builtin_clzll(bal);
+                r = __shfl(x, (int)L);
+                break;
+            }
+            top = lo_t;
+        }
+        if (lane == 0) s_before = r;
+    }
+    __syncthreads();
+    // in-tile scans: s_end by a suffix minimum, s_beg by a prefix maximum (Hillis-Steele in LDS;
+    // BT_NONE acts as +inf for the minimum and is skipped by the maximum)
+    for (u32 d = 1; d < BT_TILE; d <<= 1) {
+        u64 ve[BT_PER], vb[BT_PER];
+        for (u32 k = 0; k < BT_PER; k++) {
+            const u32 i = k * BT_T + t;
+            const u64 e = s_end[i], e2 = i + d < BT_TILE ? s_end[i + d] : BT_NONE;
+            ve[k] = min(e, e2);
+            const u64 g = s_beg[i], g2 = i >= d ? s_beg[i - d] : BT_NONE;
+            vb[k] = g == BT_NONE ? g2 : (g2 == BT_NONE ? g : max(g, g2));
+        }
+        __syncthreads();
+        for (u32 k = 0; k < BT_PER; k++) {
+            s_end[k * BT_T + t] = ve[k];
+            s_beg[k * BT_T + t] = vb[k];
+        }
+        __syncthreads();
+    }
+    for (u32 k = 0; k < BT_PER; k++) {
+        const u32 i = k * BT_T + t;
+        if (i >= tn) break;
+        const u64 b = t0 + i;
+        const u64 p = bp[b];
+        if (!p) {
+            re[b] = 0;
+            rs[b] = 0;
+            continue;
+        }
+        u64 eb = s_end[i];
+        if (eb == BT_NONE) eb = s_after;     // always found: the last block ends every segment
+        u64 sb0 = s_beg[i];
+        if (sb0 == BT_NONE) sb0 = s_before;  // always found: block 0 starts every segment
+        const u64 se = (eb + 1) * TAU, ebn = eb + 1;
+        u64 e = se + p, xe = 0;
+        if (ebn < nbk) {
+            const u32 f = fo[ebn];
+            if (f == 0xFFFFu) e = se + TAU + p;
+            else if (f) { e = se + (f - 1) + p; xe = 1; }
+        }
+        const u64 s0 = sb0 * TAU, sb = sb0;
+        u64 st = s0, xs = 0;
+        if (sb) {
+            const u32 l = lo[sb];
+            if (l == 0xFFFFu) st = s0 - TAU;
+            else if (l) { st = s0 - TAU + l; xs = 1; }
+        }
+        re[b] = (e << 16) | (xe << 8) | p;
+        rs[b] = (st << 16) | (xs << 8) | p;
+    }
+}
 // run-record segment markers: ends (stored reversed, for a min-scan) and starts (max-scan)
 __global__ void k_blk_marks(const u8* __restrict__ bp, u64 nbk, pos_t* __restrict__ end_rev, pos_t* __restrict__ beg) {
     const u64 b = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1722,18 +1888,17 @@ void engine::build_sss(const u8* T) {
     LZ_HIP(hipEventCreate(&e0));
     LZ_HIP(hipEventCreate(&e1));
     LZ_HIP(hipEventRecord(e0, st));
+    // per-block run records (0: unknown), cleared by pass 1
+    const u64 nbk = (n + TAU - 1) / TAU;
+    u8* bp = blk_p.get(nbk + 1);
+    u16* bfo = blk_fo.get(nbk + 1);
+    u16* blo = blk_lo.get(nbk + 1);
     k_sss_stream<false, true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(
-        T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, hw, qi, rp, nullptr, nullptr);
+        T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, hw, qi, rp, nullptr, nullptr, bp, bfo,
+        blo, nbk);
     LZ_HIP(hipGetLastError());
     // the stripes pass 1 stopped: settled in one pass where their periodic windows are runs
     // (k_sss_runs), which also writes the per-block run records of the LCE
-    const u64 nbk = (n + TAU - 1) / TAU;
-    u8* bp = blk_p.get(nbk + 1);
-    LZ_HIP(hipMemsetAsync(bp, 0, nbk + 1, st));
-    u16* bfo = blk_fo.get(nbk + 1);
-    u16* blo = blk_lo.get(nbk + 1);
-    LZ_HIP(hipMemsetAsync(bfo, 0, 2 * (nbk + 1), st));  // 0: unknown
-    LZ_HIP(hipMemsetAsync(blo, 0, 2 * (nbk + 1), st));
     if (!std::getenv("LZ77SSS_NO_RUNS_KERNEL"))  // test knob: every stopped stripe through the Q-anchor path
         k_sss_runs<<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, nlanes, lo, lc, lf, ctr + 1,
                                                                 (u32)SSS_BASE, PW, scap, hw, bp, bfo, blo, nbk, ctr + 0,
@@ -1774,24 +1939,41 @@ void engine::build_sss(const u8* T) {
         const u64 maxw = std::min<u64>(nlanes, 4ull * ndirty + 4);
         k_sss_stream<true, false><<<cdiv(maxw, SWAVES), 64 * SWAVES, 0, st>>>(
             T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, nullptr, nullptr, nullptr, sl,
-            ctr + 3);
+            ctr + 3, nullptr, nullptr, nullptr, 0);
         LZ_HIP(hipGetLastError());
     }
     runs_valid = true;  // period 0 outside the marked tiles
-    if (nbk < 0x7FFFFFFFull) {  // (hipcub item counts are int: texts below 2^40 bytes)
-        // run-record segments: ends by a min-scan over the reversed markers, starts by a max-scan
-        pos_t* mk = blk_mk.get(2 * nbk);
-        pos_t* ser = blk_ser.get(nbk);
-        pos_t* bss = blk_ss.get(nbk);
-        k_blk_marks<<<cdiv(nbk, 256), 256, 0, st>>>(bp, nbk, mk, mk + nbk);
-        size_t tb = 0, tb2 = 0;
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, mk, ser, hipcub::Min(), (int)nbk, st));
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
-        u8* t = scan_tmp.get(std::max(tb, tb2));
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, mk, ser, hipcub::Min(), (int)nbk, st));
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
-        k_blk_runinfo<<<cdiv(nbk, 256), 256, 0, st>>>(bp, bfo, blo, ser, bss, nbk, blk_re.get(nbk), blk_rs.get(nbk));
+    {
+        // run-record segments -> packed per-block run end / start (two launches)
+        const u64 ntile = (nbk + BT_TILE - 1) / BT_TILE;
+        u64* tt = (u64*)blk_mk.get(4 * ntile + 4);  // 2 x ntile u64 (the buffer is pos_t-typed)
+        k_blk_seg_tiles<<<(unsigned)ntile, BT_T, 0, st>>>(bp, nbk, tt, tt + ntile);
+        k_blk_seg_info<<<(unsigned)ntile, BT_T, 0, st>>>(bp, bfo, blo, nbk, tt, tt + ntile, ntile, blk_re.get(nbk),
+                                                         blk_rs.get(nbk));
         LZ_HIP(hipGetLastError());
+        if (std::getenv("LZ77SSS_BLK_CHECK") && nbk < 0x7FFFFFFFull) {
+            // test knob: the marker + min/max-scan formulation, compared entry by entry
+            pos_t* mk = (pos_t*)u64a.get(2 * nbk + 2);
+            pos_t* ser = (pos_t*)u64b.get(nbk + 1);
+            pos_t* bss = (pos_t*)u32e.get(2 * nbk + 2);
+            k_blk_marks<<<cdiv(nbk, 256), 256, 0, st>>>(bp, nbk, mk, mk + nbk);
+            size_t tb = 0, tb2 = 0;
+            LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, mk, ser, hipcub::Min(), (int)nbk, st));
+            LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
+            u8* t = scan_tmp.get(std::max(tb, tb2));
+            LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, mk, ser, hipcub::Min(), (int)nbk, st));
+            LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
+            u64* re2 = (u64*)u32d.get(4 * nbk + 4);
+            u64* rs2 = re2 + nbk;
+            k_blk_runinfo<<<cdiv(nbk, 256), 256, 0, st>>>(bp, bfo, blo, ser, bss, nbk, re2, rs2);
+            std::vector<u64> a(2 * nbk), c(2 * nbk);
+            LZ_HIP(hipMemcpyAsync(a.data(), blk_re.p, 8 * nbk, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipMemcpyAsync(a.data() + nbk, blk_rs.p, 8 * nbk, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipMemcpyAsync(c.data(), re2, 16 * nbk, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));
+            for (u64 i = 0; i < 2 * nbk; i++)
+                if (a[i] != c[i]) throw error(LZ77SSS_EINTERNAL, "run-record check: tile kernels differ from the scan form");
+        }
         brk_nbk = nbk;
         brk_valid = true;
         if (debug_enabled()) {
@@ -1807,15 +1989,15 @@ void engine::build_sss(const u8* T) {
                          (unsigned long long)cnt[2], (unsigned long long)cnt[3], (unsigned long long)seg);
             if (nbk <= 64) {
                 std::vector<u16> hf(nbk), hl(nbk);
-                std::vector<pos_t> hse(nbk), hss(nbk);
+                std::vector<u64> hre(nbk), hrs(nbk);
                 LZ_HIP(hipMemcpy(hf.data(), bfo, 2 * nbk, hipMemcpyDeviceToHost));
                 LZ_HIP(hipMemcpy(hl.data(), blo, 2 * nbk, hipMemcpyDeviceToHost));
-                LZ_HIP(hipMemcpy(hse.data(), ser, sizeof(pos_t) * nbk, hipMemcpyDeviceToHost));
-                LZ_HIP(hipMemcpy(hss.data(), bss, sizeof(pos_t) * nbk, hipMemcpyDeviceToHost));
+                LZ_HIP(hipMemcpy(hre.data(), blk_re.p, 8 * nbk, hipMemcpyDeviceToHost));
+                LZ_HIP(hipMemcpy(hrs.data(), blk_rs.p, 8 * nbk, hipMemcpyDeviceToHost));
                 for (u64 i = 0; i < nbk; i++)
-                    std::fprintf(stderr, "[lz77sss-debug]   block %llu: p=%u fo=%u lo=%u se=%llu ss=%llu\n",
-                                 (unsigned long long)i, hb[i], hf[i], hl[i], (unsigned long long)hse[nbk - 1 - i],
-                                 (unsigned long long)hss[i]);
+                    std::fprintf(stderr, "[lz77sss-debug]   block %llu: p=%u fo=%u lo=%u run end=%llu start=%llu\n",
+                                 (unsigned long long)i, hb[i], hf[i], hl[i], (unsigned long long)(hre[i] >> 16),
+                                 (unsigned long long)(hrs[i] >> 16));
             }
         }
     }

@@ -139,12 +139,20 @@ def test_u64_one_shot_callback_and_device_decode(lz, orc):
     F = np.concatenate(got)
     assert np.array_equal(F, orc.factorize64(T)[0])
     assert np.array_equal(lz.decode_device(F, T.size), T)
-    # exact mode through the 64-bit entry point (n < 2^31): the 32-bit stream, widened
-    got.clear()
-    rc = lz.load_library().lz77sss_factorize_exact_u64(T.ctypes.data_as(ctypes.c_void_p), T.size, ctypes.byref(p),
-                                                       lz.WITHOUT_SAMPLES, cb, None)
-    assert rc == 0
-    assert np.array_equal(np.concatenate(got), orc.factorize_exact(T).astype(np.uint64))
+    # exact mode through the 64-bit entry point (n < 2^31): the 32-bit stream, widened.
+    # without_samples runs the sample-index path (csrc/smpl.hip): canonical lengths (the
+    # oracle's), sources the lighter sample points it finds; FULL_SA equals the oracle bit for bit
+    exp = orc.factorize_exact(T).astype(np.uint64)
+    for mode in (lz.WITHOUT_SAMPLES, lz.FULL_SA):
+        got.clear()
+        rc = lz.load_library().lz77sss_factorize_exact_u64(T.ctypes.data_as(ctypes.c_void_p), T.size,
+                                                           ctypes.byref(p), mode, cb, None)
+        assert rc == 0
+        FX = np.concatenate(got)
+        assert np.array_equal(FX[:, 1], exp[:, 1])
+        assert np.array_equal(lz.decode(FX, T.size), T)
+        if mode == lz.FULL_SA:
+            assert np.array_equal(FX, exp)
 
 
 def test_u64_session_rejects_32bit_accessors(session64, lz):
