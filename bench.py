@@ -350,10 +350,15 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
         del T
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen0
+    print(f"[bench --shard] rank {rank}: text of {n} bytes in HBM ({t_gen:.1f} s)", file=sys.stderr, flush=True)
     tm = {}
 
     def step():
-        return sharded.factorize_sharded_resident(sess, n, rank, world, local_rank, timings=tm)
+        t = time.perf_counter()
+        F = sharded.factorize_sharded_resident(sess, n, rank, world, local_rank, timings=tm)
+        print(f"[bench --shard] rank {rank}: step {time.perf_counter() - t:.2f} s, phases "
+              f"{ {k: round(v, 3) for k, v in tm.items()} }", file=sys.stderr, flush=True)
+        return F
 
     for _ in range(args.warmup):
         step()

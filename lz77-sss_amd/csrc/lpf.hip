@@ -24,6 +24,14 @@ __global__ void k_sa_min_level(const u32* __restrict__ prev, u32 cnt, u32 half, 
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < cnt) out[k] = min(prev[k], prev[k + half]);
 }
+__global__ void k_sa_min_level2(const u32* __restrict__ prev, u32 cnt1, u32 half, u32* __restrict__ out1, u32 cnt2,
+                                u32* __restrict__ out2) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= cnt1) return;
+    const u32 a = min(prev[k], prev[k + half]);
+    out1[k] = a;
+    if (k < cnt2) out2[k] = min(a, min(prev[k + 2 * half], prev[k + 3 * half]));
+}
 
 struct sa_min_levels {
     u32 nlev;
@@ -105,6 +113,14 @@ __global__ void k_jump(const u32* __restrict__ prev, u32 m, u32* __restrict__ ou
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) out[i] = prev[prev[i]];
 }
+// two doubling levels per launch: out1 = prev o prev, out2 = out1 o out1
+__global__ void k_jump2(const u32* __restrict__ prev, u32 m, u32* __restrict__ out1, u32* __restrict__ out2) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const u32 b = prev[prev[i]];
+    out1[i] = b;
+    out2[i] = prev[prev[b]];
+}
 // top-down path expansion: out[2m] = C[m], out[2m+1] = J[C[m]]
 __global__ void k_expand(const u32* __restrict__ C, u32 cnt, const u32* __restrict__ J, u32* __restrict__ out) {
     const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -112,6 +128,17 @@ __global__ void k_expand(const u32* __restrict__ C, u32 cnt, const u32* __restri
     const u32 c = C[m];
     out[2 * m] = c;
     out[2 * m + 1] = J[c];
+}
+// two expansion levels per launch (J = level t, J1 = level t - 1)
+__global__ void k_expand2l(const u32* __restrict__ C, u32 cnt, const u32* __restrict__ J, const u32* __restrict__ J1,
+                           u32* __restrict__ out) {
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= cnt) return;
+    const u32 c = C[m], d = J[c];
+    out[4 * m] = c;
+    out[4 * m + 1] = J1[c];
+    out[4 * m + 2] = d;
+    out[4 * m + 3] = J1[d];
 }
 __global__ void k_mark(const u32* __restrict__ C, u32 cnt, u32 s, u32* __restrict__ mark) {
     const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -230,20 +257,67 @@ __global__ void k_phrase_naive(const pos_t* __restrict__ S, u32 s, const pos_t* 
     push[i] = pu ? 1u : 0u;
 }
 
+// SA min levels 1.. (two per launch where both exist) into M.L; returns the level count
+static u32 sa_min_levels_build(hipStream_t st, const u32* SA, u32 s, dbuf<u32>* sa_min, sa_min_levels& M) {
+    M.L[0] = SA;
+    u32 nl = 1;
+    for (u32 lv = 1; (1ull << lv) <= s;) {
+        const u32 cnt = s - (1u << lv) + 1;
+        u32* out = sa_min[lv].get(cnt);
+        const u32* prev = lv == 1 ? SA : sa_min[lv - 1].p;
+        M.L[lv] = out;
+        if ((2ull << lv) <= s) {
+            const u32 cnt2 = s - (2u << lv) + 1;
+            u32* out2 = sa_min[lv + 1].get(cnt2);
+            k_sa_min_level2<<<cdiv(cnt, 256), 256, 0, st>>>(prev, cnt, 1u << (lv - 1), out, cnt2, out2);
+            M.L[lv + 1] = out2;
+            nl = lv + 2;
+            lv += 2;
+        } else {
+            k_sa_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(prev, cnt, 1u << (lv - 1), out);
+            nl = lv + 1;
+            lv += 1;
+        }
+    }
+    M.nlev = nl;
+    return nl;
+}
+// jump levels 1 .. T_lv - 1 over jump[0] (m nodes; level T_lv is never read by the expansion)
+static void jump_levels_build(hipStream_t st, u32 m, u32 T_lv, dbuf<u32>* jump) {
+    for (u32 t = 1; t < T_lv;) {
+        if (t + 1 < T_lv) {
+            k_jump2<<<cdiv(m, 256), 256, 0, st>>>(jump[t - 1].p, m, jump[t].get(m), jump[t + 1].get(m));
+            t += 2;
+        } else {
+            k_jump<<<cdiv(m, 256), 256, 0, st>>>(jump[t - 1].p, m, jump[t].get(m));
+            t += 1;
+        }
+    }
+}
+// top-down expansion of the path from node 0 over jump[0 .. T_lv - 1]: C (2^T_lv entries) in order
+static u32* path_expand(hipStream_t st, u32 T_lv, dbuf<u32>* jump, u32* C, u32* C2) {
+    u64 cnt = 1;
+    int t = (int)T_lv - 1;
+    while (t >= 0) {
+        if (t >= 1) {
+            k_expand2l<<<cdiv(cnt, 256), 256, 0, st>>>(C, (u32)cnt, jump[t].p, jump[t - 1].p, C2);
+            cnt *= 4;
+            t -= 2;
+        } else {
+            k_expand<<<cdiv(cnt, 256), 256, 0, st>>>(C, (u32)cnt, jump[t].p, C2);
+            cnt *= 2;
+            t -= 1;
+        }
+        std::swap(C, C2);
+    }
+    return C;
+}
+
 // PSV/NSV over SA_S into the engine's PSV / NSV buffers
 void engine::psv_nsv_s() {
     const unsigned g = cdiv(s, 256);
     sa_min_levels M{};
-    M.L[0] = SA.p;
-    u32 nl = 1;
-    for (u32 lv = 1; (1ull << lv) <= s; lv++) {
-        const u32 cnt = s - (1u << lv) + 1;
-        u32* out = sa_min[lv].get(cnt);
-        k_sa_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(lv == 1 ? SA.p : sa_min[lv - 1].p, cnt, 1u << (lv - 1), out);
-        M.L[lv] = out;
-        nl = lv + 1;
-    }
-    M.nlev = nl;
+    sa_min_levels_build(st, SA.p, s, sa_min, M);
     k_psv_nsv<<<g, 256, 0, st>>>(SA.p, s, M, PSV.get(s), NSV.get(s));
 }
 
@@ -252,16 +326,12 @@ void engine::mark_path(u32* mark) {
     const u32 m = s + 1;
     u32 T_lv = 0;
     while ((1ull << T_lv) < m) T_lv++;
-    for (u32 t = 1; t <= T_lv; t++) k_jump<<<cdiv(m, 256), 256, 0, st>>>(jump[t - 1].p, m, jump[t].get(m));
-    u32* C = u32a.get(2ull << T_lv);
-    u32* C2 = u32b.get(2ull << T_lv);
+    jump_levels_build(st, m, T_lv, jump);
+    u32* C = u32a.get(4ull << T_lv);
+    u32* C2 = u32b.get(4ull << T_lv);
     LZ_HIP(hipMemsetAsync(C, 0, 4, st));
-    u32 cnt = 1;
-    for (int t = (int)T_lv - 1; t >= 0; t--) {
-        k_expand<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, jump[t].p, C2);
-        std::swap(C, C2);
-        cnt *= 2;
-    }
+    C = path_expand(st, T_lv, jump, C, C2);
+    const u32 cnt = 1u << T_lv;
     LZ_HIP(hipMemsetAsync(mark, 0, (size_t)s * 4, st));
     k_mark<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, s, mark);
 }
@@ -300,19 +370,9 @@ void engine::build_lpf_opt(const u8* T) {
     if (s == 0) return;
     const unsigned g = cdiv(s, 256);
     // 1. PSV/NSV
-    u32 nl = 0;
     {
         sa_min_levels M{};
-        M.L[0] = SA.p;
-        nl = 1;
-        for (u32 lv = 1; (1ull << lv) <= s; lv++) {
-            const u32 cnt = s - (1u << lv) + 1;
-            u32* out = sa_min[lv].get(cnt);
-            k_sa_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(lv == 1 ? SA.p : sa_min[lv - 1].p, cnt, 1u << (lv - 1), out);
-            M.L[lv] = out;
-            nl = lv + 1;
-        }
-        M.nlev = nl;
+        sa_min_levels_build(st, SA.p, s, sa_min, M);
         k_psv_nsv<<<g, 256, 0, st>>>(SA.p, s, M, PSV.get(s), NSV.get(s));
     }
     // 2. candidates
@@ -323,17 +383,12 @@ void engine::build_lpf_opt(const u8* T) {
     u32 T_lv = 0;
     while ((1ull << T_lv) < m) T_lv++;
     k_next<<<cdiv(m, 256), 256, 0, st>>>(S.p, s, cd, jump[0].get(m));
-    for (u32 t = 1; t <= T_lv; t++) k_jump<<<cdiv(m, 256), 256, 0, st>>>(jump[t - 1].p, m, jump[t].get(m));
-    u32* C = u32a.get(2ull << T_lv);
-    u32* C2 = u32b.get(2ull << T_lv);
-    u32 zero = 0;
-    LZ_HIP(hipMemcpyAsync(C, &zero, 4, hipMemcpyHostToDevice, st));
-    u32 cnt = 1;
-    for (int t = (int)T_lv - 1; t >= 0; t--) {
-        k_expand<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, jump[t].p, C2);
-        std::swap(C, C2);
-        cnt *= 2;
-    }
+    jump_levels_build(st, m, T_lv, jump);
+    u32* C = u32a.get(4ull << T_lv);
+    u32* C2 = u32b.get(4ull << T_lv);
+    LZ_HIP(hipMemsetAsync(C, 0, 4, st));
+    C = path_expand(st, T_lv, jump, C, C2);
+    const u32 cnt = 1u << T_lv;
     u32* mark = u32c.get(s);
     LZ_HIP(hipMemsetAsync(mark, 0, (size_t)s * 4, st));
     k_mark<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, s, mark);

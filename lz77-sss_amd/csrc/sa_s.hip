@@ -116,6 +116,15 @@ __global__ void k_min_level(const u32* __restrict__ prev, u32 cnt, u32 half, u32
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < cnt) out[k] = min(prev[k], prev[k + half]);
 }
+// two sparse-table levels per launch (lv from lv - 1 and lv + 1 from lv - 1: half the launches)
+__global__ void k_min_level2(const u32* __restrict__ prev, u32 cnt1, u32 half, u32* __restrict__ out1, u32 cnt2,
+                             u32* __restrict__ out2) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= cnt1) return;
+    const u32 a = min(prev[k], prev[k + half]);
+    out1[k] = a;
+    if (k < cnt2) out2[k] = min(a, min(prev[k + 2 * half], prev[k + 3 * half]));
+}
 
 __global__ void k_succ_table(const pos_t* __restrict__ S, u32 s, u64 nb, u32* __restrict__ tab) {
     const u64 bkt = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -616,11 +625,20 @@ void engine::build_lcp_rmq(const u8* T) {
     u32* L0 = lcp_rmq[0].get(s);
     k_lcp<<<g, 256, 0, st>>>(T, n, S.p, key_len.p, SA.p, s, RL, runs(), L0);
     nlev_rmq = 1;
-    for (u32 lv = 1; (1ull << lv) <= s; lv++) {
+    for (u32 lv = 1; (1ull << lv) <= s;) {
         const u32 cnt = s - (1u << lv) + 1;
         u32* out = lcp_rmq[lv].get(cnt);
-        k_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(lcp_rmq[lv - 1].p, cnt, 1u << (lv - 1), out);
-        nlev_rmq = lv + 1;
+        if ((2ull << lv) <= s) {
+            const u32 cnt2 = s - (2u << lv) + 1;
+            k_min_level2<<<cdiv(cnt, 256), 256, 0, st>>>(lcp_rmq[lv - 1].p, cnt, 1u << (lv - 1), out, cnt2,
+                                                         lcp_rmq[lv + 1].get(cnt2));
+            nlev_rmq = lv + 2;
+            lv += 2;
+        } else {
+            k_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(lcp_rmq[lv - 1].p, cnt, 1u << (lv - 1), out);
+            nlev_rmq = lv + 1;
+            lv += 1;
+        }
     }
     LZ_HIP(hipGetLastError());
 }

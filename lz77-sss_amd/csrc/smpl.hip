@@ -28,9 +28,11 @@
 //            (exp/binary search over lce_r, intersect of common.cpp:258-358, decided for
 //            the whole wave one query at a time: the Pi / Psi scan below SCAN_T ranks,
 //            the grid above); the wave keeps the longest, the smallest j on ties
-//   chain    the greedy chain by speculation: every approximate phrase start is a task,
-//            every task's successor a task (up to HOPS hops); the true chain is then
-//            followed through the task table, missing stretches walked by one wave
+//   chain    chunk walks: one wave per chunk of ~32 approximate phrases walks the greedy
+//            chain from the chunk start (a task per phrase, in a hash table) until it meets
+//            another walk's task or passes its chunk end; bridges walk on from every chunk
+//            exit until they meet a task; the chain from position 0 is then marked in order
+//            by pointer doubling + top-down expansion over the successor tasks
 //
 // Lengths are the canonical greedy LZ77 lengths (every leftmost occurrence of a phrase
 // contains a sample within its first delta characters: DESIGN.md 4.8); sources are the
@@ -57,7 +59,6 @@ constexpr u32 SG_WIN = LZ_SG_WIN;    // grid cell width in ranks (the reference:
 constexpr u32 RKS_RATE = 16;         // lz77_sss.hpp:82 rks_sample_rate
 constexpr u32 RKS_P = 0x7FFFFFFFu;   // Mersenne prime 2^31 - 1 (rabin_karp_substring<31>)
 constexpr u32 RKS_B = 0x2545F491u % RKS_P;  // fixed base (the reference draws one per run)
-constexpr u32 HOPS = 3;              // successor tasks per approximate phrase start
 constexpr u32 SWPB = 4;              // waves per workgroup of the phrase kernels
 constexpr u32 NSMPL = 24;            // sampled pattern lengths per side at most (with_samples)
 
@@ -700,78 +701,87 @@ __device__ u32 task_find(const task_tab& Tt, u32 p) {
     }
     return NONE;
 }
-__global__ void k_seed_tasks(task_tab Tt, const u32* __restrict__ afst, u32 za) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < za) task_insert(Tt, afst[k], 0);
-}
-__global__ __launch_bounds__(64 * SWPB) void k_phrase_tasks(const smpl_view V, task_tab Tt, u32 t0, u32 t1) {
-    const u32 lane = threadIdx.x & 63;
-    const u32 t = t0 + blockIdx.x * SWPB + (threadIdx.x >> 6);
-    if (t >= t1) return;
-    u32 src, len;
-    wave_phrase(V, Tt.pos[t], src, len, lane);
-    if (lane == 0) {
-        Tt.src[t] = src;
-        Tt.len[t] = len;
-    }
-}
-__global__ void k_advance_tasks(task_tab Tt, u32 t0, u32 t1, u32 n) {
-    const u64 t = t0 + (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= t1) return;
-    const u32 h = Tt.hop[t];
-    if (h >= HOPS) return;
-    const u32 q = Tt.pos[t] + max(1u, Tt.len[t]);
-    if (q < n) task_insert(Tt, q, h + 1);
-}
-// follows the true chain from *cur; stops at the first position without a phrase
-// (cur = that position) or at n; counts the factors
-__global__ void k_chain_follow(task_tab Tt, u32 n, u32* __restrict__ cur, u64* __restrict__ z) {
-    if (threadIdx.x || blockIdx.x) return;
-    u32 p = *cur;
-    u64 cnt = *z;
-    while (p < n) {
-        const u32 t = task_find(Tt, p);
-        if (t == NONE || Tt.len[t] == NONE) break;
-        p += max(1u, Tt.len[t]);
-        cnt++;
-    }
-    *cur = p;
-    *z = cnt;
-}
-// one wave walks the true chain from *cur until it meets a known phrase (or n / maxsteps)
-__global__ __launch_bounds__(64) void k_chain_walk(const smpl_view V, task_tab Tt, const u32* __restrict__ cur,
-                                                   u32 maxsteps) {
-    const u32 lane = threadIdx.x;
-    const u32 n = (u32)V.L.n;
-    u32 p = *cur;
-    for (u32 s = 0; s < maxsteps && p < n; s++) {
-        const u32 t0 = task_find(Tt, p);
-        if (t0 != NONE && Tt.len[t0] != NONE) break;
+// ---- the chain by chunk walks + bridges (replaces one hop per launch) ----------------
+// Chunk k's wave walks the greedy chain from k * CS, inserting a task per phrase, until it
+// meets a task another walk inserted (merged) or passes its chunk end (its exit is kept).
+// A bridge walks from every exit until it meets a task.  Every task's successor position
+// then holds a task (a walk inserts it, finds it, or hands it to a bridge), so the chain
+// from position 0 lies in the table; it is marked by pointer doubling.
+__device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p, u64 stop, u32 lane, u32* __restrict__ full) {
+    const u64 n = V.L.n;
+    for (;;) {
+        if (p >= n) return NONE;
+        if (p >= stop) return (u32)p;
+        u32 t = NONE;
+        if (lane == 0) {
+            t = task_insert(Tt, (u32)p, 0);
+            if (t == NONE && task_find(Tt, (u32)p) == NONE) atomicOr(full, 1u);  // table full
+        }
+        t = (u32)__shfl((int)t, 0);
+        if (t == NONE) return NONE;  // merged (or out of room: reported)
         u32 src, len;
-        wave_phrase(V, p, src, len, lane);
-        if (lane == 0) {  // (a full table records nothing: the host reports the overflow)
-            u32 t = t0;
-            if (t == NONE) t = task_insert(Tt, p, HOPS);
-            if (t != NONE) {
-                Tt.src[t] = src;
-                Tt.len[t] = len;
-            }
+        wave_phrase(V, (u32)p, src, len, lane);
+        if (lane == 0) {
+            Tt.src[t] = src;
+            Tt.len[t] = len;
         }
         p += max(1u, len);
     }
 }
-__global__ void k_chain_emit(task_tab Tt, u32 n, u32* __restrict__ F) {
-    if (threadIdx.x || blockIdx.x) return;
-    u32 p = 0;
-    u64 k = 0;
-    while (p < n) {
-        const u32 t = task_find(Tt, p);
-        const u32 len = Tt.len[t];
-        F[2 * k] = Tt.src[t];
-        F[2 * k + 1] = len;
-        k++;
-        p += max(1u, len);
+__global__ __launch_bounds__(64 * SWPB) void k_chunk_walks(const smpl_view V, task_tab Tt, u64 CS, u32 nch,
+                                                          u32* __restrict__ ex, u32* __restrict__ full) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 k = blockIdx.x * SWPB + (threadIdx.x >> 6);
+    if (k >= nch) return;
+    const u32 e = wave_walk(V, Tt, (u64)k * CS, min<u64>(V.L.n, (u64)(k + 1) * CS), lane, full);
+    if (lane == 0) ex[k] = e;
+}
+__global__ __launch_bounds__(64 * SWPB) void k_bridge_walks(const smpl_view V, task_tab Tt, u32 nch,
+                                                           const u32* __restrict__ ex, u32* __restrict__ full) {
+    const u32 lane = threadIdx.x & 63;
+    const u32 k = blockIdx.x * SWPB + (threadIdx.x >> 6);
+    if (k >= nch || ex[k] == NONE) return;
+    wave_walk(V, Tt, ex[k], ~0ull, lane, full);
+}
+// successor task of every task (ntask = the end); a missing successor is reported
+__global__ void k_task_next(task_tab Tt, u32 ntask, u32 n, u32* __restrict__ nxt, u32* __restrict__ bad) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntask) return;
+    if (t == ntask) { nxt[t] = ntask; return; }
+    const u64 q = (u64)Tt.pos[t] + max(1u, Tt.len[t]);
+    u32 r = ntask;
+    if (q < n) {
+        r = task_find(Tt, (u32)q);
+        if (r == NONE || r >= ntask) { atomicOr(bad, 1u); r = ntask; }
     }
+    nxt[t] = r;
+}
+__global__ void k_tjump(const u32* __restrict__ prev, u32 m, u32* __restrict__ out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[i] = prev[prev[i]];
+}
+__global__ void k_texpand(const u32* __restrict__ C, u64 cnt, const u32* __restrict__ J, u32* __restrict__ out) {
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= cnt) return;
+    const u32 c = C[m];
+    out[2 * m] = c;
+    out[2 * m + 1] = J[c];
+}
+__global__ void k_troot(task_tab Tt, u32* __restrict__ C, u32 ntask) {
+    const u32 r = task_find(Tt, 0u);
+    C[0] = r == NONE ? ntask : r;
+}
+// the path from the root in order: its length (first end marker) and its factors
+__global__ void k_path_len(const u32* __restrict__ C, u64 cnt, u32 ntask, u32* __restrict__ z) {
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < cnt && C[m] == ntask && (m == 0 || C[m - 1] != ntask)) *z = (u32)m;
+}
+__global__ void k_path_emit(task_tab Tt, const u32* __restrict__ C, u32 z, u32* __restrict__ F) {
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= z) return;
+    const u32 t = C[m];
+    F[2 * m] = Tt.src[t];
+    F[2 * m + 1] = Tt.len[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -912,8 +922,12 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.mode = transf_mode;
     V.nlen[0] = V.nlen[1] = 0;
     if (transf_mode == LZ77SSS_TRANSF_WITH_SAMPLES) build_interval_samples(V, n, za64);
-    // the chain: speculative tasks from every approximate phrase start, then the true chain
-    const u32 tcap = (u32)std::min<u64>(0x7FFFFFFFull, (u64)za * (HOPS + 1) + 65536);
+    // the chain (chunk walks + bridges, then the path from position 0 by pointer doubling).
+    // Chunks hold about 32 approximate phrases each (the walks re-synchronise with the true
+    // chain within a few phrases).
+    const u64 CS = std::max<u64>(256, std::min<u64>(1ull << 26, 32 * (n / std::max<u64>(1, za64))));
+    const u32 nch = (u32)((n + CS - 1) / CS);
+    const u32 tcap = (u32)std::min<u64>(0x7FFFFFF0ull, 2 * (u64)za + n / 8 + 65536);
     u32 hsz = 1;
     while (hsz < 2ull * tcap) hsz <<= 1;
     task_tab Tt{};
@@ -927,47 +941,60 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     Tt.cap = tcap;
     u32* ctr = counters.get(16);
     Tt.ntask = ctr + 8;
+    u32* full = ctr + 9;
+    u32* bad = ctr + 10;
+    u32* zp = ctr + 11;
     LZ_HIP(hipMemsetAsync(Tt.keys, 0, (size_t)hsz * 4, st));
-    LZ_HIP(hipMemsetAsync(ctr + 8, 0, 8, st));
-    k_seed_tasks<<<cdiv(za, 256), 256, 0, st>>>(Tt, afst, za);
-    u32 t0 = 0, t1 = std::min(rd1(ctr + 8, st), tcap);
-    u32 rounds = 0;
-    while (t1 > t0) {
-        k_phrase_tasks<<<cdiv(t1 - t0, SWPB), 64 * SWPB, 0, st>>>(V, Tt, t0, t1);
-        k_advance_tasks<<<cdiv(t1 - t0, 256), 256, 0, st>>>(Tt, t0, t1, (u32)n);
-        t0 = t1;
-        t1 = std::min(rd1(ctr + 8, st), tcap);
-        rounds++;
-    }
+    LZ_HIP(hipMemsetAsync(ctr + 8, 0, 16, st));
+    u32* ex = e_tmp1.get((u64)nch + 1);
+    k_chunk_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, CS, nch, ex, full);
+    LZ_HIP(hipGetLastError());
     timer.mark("smpl_tasks");
-    u32* cur = ctr + 10;
-    u64* zc = (u64*)(ctr + 12);
-    LZ_HIP(hipMemsetAsync(cur, 0, 4, st));
-    LZ_HIP(hipMemsetAsync(zc, 0, 8, st));
-    u32 walks = 0;
-    for (;;) {
-        k_chain_follow<<<1, 64, 0, st>>>(Tt, (u32)n, cur, zc);
-        const u32 p = rd1(cur, st);
-        if (p >= n) break;
-        if (rd1(ctr + 8, st) >= tcap) throw error(LZ77SSS_EINTERNAL, "exact-smpl: task table full");
-        k_chain_walk<<<1, 64, 0, st>>>(V, Tt, cur, 1u << 16);
-        walks++;
+    k_bridge_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full);
+    LZ_HIP(hipGetLastError());
+    u32 hc[2];
+    LZ_HIP(hipMemcpyAsync(hc, ctr + 8, 8, hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    if (hc[1] || hc[0] >= tcap) throw error(LZ77SSS_EINTERNAL, "exact-smpl: task table full");
+    const u32 ntask = hc[0];
+    timer.mark("smpl_bridges");
+    // the path from the task at position 0: pointer doubling + top-down expansion (in order)
+    u32 T_lv = 0;
+    while ((1ull << T_lv) < (u64)ntask + 1) T_lv++;
+    if (T_lv >= MAX_LV) throw error(LZ77SSS_EINTERNAL, "exact-smpl: too many tasks");
+    k_task_next<<<cdiv((u64)ntask + 1, 256), 256, 0, st>>>(Tt, ntask, (u32)n, jump[0].get((u64)ntask + 1), bad);
+    for (u32 t = 1; t < T_lv; t++)
+        k_tjump<<<cdiv((u64)ntask + 1, 256), 256, 0, st>>>(jump[t - 1].p, ntask + 1, jump[t].get((u64)ntask + 1));
+    u32* PC = e_tmp2.get(2ull << T_lv);
+    u32* C2 = e_thop.get(2ull << T_lv);  // (task hops are not used by the chain)
+    k_troot<<<1, 1, 0, st>>>(Tt, PC, ntask);
+    u64 cnt = 1;
+    for (int t = (int)T_lv - 1; t >= 0; t--) {
+        k_texpand<<<cdiv(cnt, 256), 256, 0, st>>>(PC, cnt, jump[t].p, C2);
+        std::swap(PC, C2);
+        cnt *= 2;
     }
-    const u64 z = rd1(zc, st);
+    LZ_HIP(hipMemcpyAsync(zp, &cnt, 4, hipMemcpyHostToDevice, st));  // no end marker: the path fills C
+    k_path_len<<<cdiv(cnt, 256), 256, 0, st>>>(PC, cnt, ntask, zp);
+    LZ_HIP(hipMemcpyAsync(hc, bad, 8, hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    if (hc[0]) throw error(LZ77SSS_EINTERNAL, "exact-smpl: a task without its successor");
+    const u64 z = hc[1];
     u32* F = fact.get(2 * z + 2);
-    k_chain_emit<<<1, 64, 0, st>>>(Tt, (u32)n, F);
+    if (z) k_path_emit<<<cdiv(z, 256), 256, 0, st>>>(Tt, PC, (u32)z, F);
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipStreamSynchronize(st));
+    const u32 rounds = nch, walks = T_lv;
     timer.mark("smpl_chain");
     num_fact = z;
     stats.resize(28, 0);
     stats[24] = c;
     stats[25] = delta;
-    stats[26] = std::min(rd1(ctr + 8, st), tcap);
-    stats[27] = ((u64)rounds << 32) | walks;
+    stats[26] = ntask;
+    stats[27] = ((u64)rounds << 32) | walks;  // chunks, doubling levels
     if (log) {
         for (auto& [name, ms] : timer.read()) std::fprintf(stderr, "[lz77sss] %-12s %9.3f ms\n", name.c_str(), ms);
-        std::fprintf(stderr, "[lz77sss] exact-smpl: n=%llu approx=%u samples=%u delta=%u tasks=%llu rounds=%u walks=%u factors=%llu\n",
+        std::fprintf(stderr, "[lz77sss] exact-smpl: n=%llu approx=%u samples=%u delta=%u tasks=%llu chunks=%u levels=%u factors=%llu\n",
                      (unsigned long long)n, za, c, delta, (unsigned long long)stats[26], rounds, walks,
                      (unsigned long long)z);
     }

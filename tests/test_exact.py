@@ -137,7 +137,8 @@ def test_gpu_exact_transform_modes_agree(session, orc, lz, transf_mode):
 @pytest.mark.gpu
 def test_gpu_exact_smpl_structures(session, lz):
     """The sample set of common.cpp:34-88: delta = min(n / z_approx, 256), samples every delta
-    characters at most (stats 24..27: samples, delta, phrase tasks, rounds << 32 | walks)."""
+    characters at most (stats 24..27: samples, delta, phrase tasks, chunks << 32 | doubling levels);
+    the chain's phrases are all tasks."""
     T = lz.gen_random_repetitive(200000, 200000, 5)
     s = session(T.size)
     s.load(T)
@@ -148,7 +149,7 @@ def test_gpu_exact_smpl_structures(session, lz):
         c, delta = st[24], st[25]
         assert delta == min(T.size // za, 256)
         assert T.size // delta <= c <= T.size // delta + za + 1
-        assert z > 0 and st[26] >= za
+        assert z > 0 and st[26] >= z and (st[27] >> 32) >= 1
 
 
 @pytest.mark.gpu
