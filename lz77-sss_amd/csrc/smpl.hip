@@ -17,7 +17,7 @@
 //            57-bit key of 7 characters, then a comparison merge sort whose comparator
 //            falls back to the text (leftward LCE / the SSS-backed LCE of lce_dev.h)
 //   points   (x = PA rank, y = SA rank, weight = sample id); Pi, Psi (common.cpp:114-182)
-//   grid     per first character (decomposed_range.hpp:82-130) cells of SG_WIN x SG_WIN
+//   grid     per first character (decomposed_range.hpp:82-130) cells of >= SG_WIN ranks per side
 //            ranks, points sorted by (cell, weight) (static_weighted_square_grid.hpp:67-104)
 //   RKS      prefix fingerprints mod 2^31 - 1 every RKS_RATE characters
 //            (rabin_karp_substring.hpp:77-172); with_samples: hash tables of the PA / SA
@@ -55,7 +55,9 @@ constexpr u32 SCAN_T = 4096;         // lz77_sss.hpp:83 range_scan_threshold
 #ifndef LZ_SG_WIN
 #define LZ_SG_WIN 2048
 #endif
-constexpr u32 SG_WIN = LZ_SG_WIN;    // grid cell width in ranks (the reference: 16384 on a CPU core)
+constexpr u32 SG_WIN = LZ_SG_WIN;    // smallest grid cell width in ranks (the reference: 16384 on a CPU core)
+constexpr u32 SG_GMAX = 512;         // cells per side at most: wider blocks get wider cells
+constexpr u32 SG_LV = 10;            // row sparse-table levels (2^9 = SG_GMAX / 1)
 constexpr u32 RKS_RATE = 16;         // lz77_sss.hpp:82 rks_sample_rate
 constexpr u32 RKS_P = 0x7FFFFFFFu;   // Mersenne prime 2^31 - 1 (rabin_karp_substring<31>)
 constexpr u32 RKS_B = 0x2545F491u % RKS_P;  // fixed base (the reference draws one per run)
@@ -75,8 +77,10 @@ struct smpl_view {
     const u32* Psi;          // PA rank of SA rank y
     const u32* CS;           // [257] first rank per first character
     const u32* gcb;          // [257] first cell per character
-    const u32* gwd;          // [256] grid width per character
+    const u32* gwd;          // [256] grid width per character (cells per side)
+    const u32* gwin;         // [256] cell width in ranks per character
     const u32* cell;         // [ncells + 1] first point per cell
+    const u32* rst[SG_LV];   // per row of cells: min weight over cells [x, x + 2^k) of the row
     const u32* gx;           // points by (cell, weight): PA rank, SA rank, weight
     const u32* gy;
     const u32* gw;
@@ -286,59 +290,84 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
                 }
             }
         } else {
-            // the grid of character qch (static_weighted_square_grid.hpp:116-185)
-            const u32 r0 = V.CS[qch], gw = V.gwd[qch], cb = V.gcb[qch];
+            // the grid of character qch (static_weighted_square_grid.hpp:116-185): the contained
+            // cells through row sparse tables of their lightest weights (a lane per row), the
+            // border cells a lane each (their points in weight order up to the first heavy one)
+            const u32 r0 = V.CS[qch], gw = V.gwd[qch], cb = V.gcb[qch], win = V.gwin[qch];
             const u32 x1 = qxb - r0, x2 = qxe - r0, y1 = qyb - r0, y2 = qye - r0;
-            const u32 xw1 = x1 / SG_WIN, xw2 = x2 / SG_WIN, yw1 = y1 / SG_WIN, yw2 = y2 / SG_WIN;
-            const u32 xi1 = xw1 + (x1 % SG_WIN != 0), yi1 = yw1 + (y1 % SG_WIN != 0);
-            const u32 xi2 = xw2 + (x2 % SG_WIN == SG_WIN - 1), yi2 = yw2 + (y2 % SG_WIN == SG_WIN - 1);
+            const u32 xw1 = x1 / win, xw2 = x2 / win, yw1 = y1 / win, yw2 = y2 / win;
+            const u32 xi1 = xw1 + (x1 % win != 0), yi1 = yw1 + (y1 % win != 0);
+            const u32 xi2 = xw2 + (x2 % win == win - 1), yi2 = yw2 + (y2 % win == win - 1);
             const bool inner = xi1 < xi2 && yi1 < yi2;
             if (inner) {
-                // contained cells: their lightest point decides
-                const u32 wx = xi2 - xi1, ncell = wx * (yi2 - yi1);
-                for (u32 base = 0; base < ncell; base += 64) {
+                const u32 wx = xi2 - xi1, k = 31 - __builtin_clz(wx);
+                const u32* R = V.rst[k];
+                for (u32 base = yi1; base < yi2 && !f; base += 64) {
+                    const u32 row = base + lane;
+                    bool ok = false;
+                    if (row < yi2) {
+                        const u32 o = cb + row * gw;
+                        ok = min(R[o + xi1], R[o + xi2 - (1u << k)]) < qW;
+                    }
+                    const u64 bal = __ballot(ok);
+                    if (bal) {
+                        // the row's first cell with a lighter point: its lightest point
+                        const u32 row1 = base + (u32)__builtin_ctzll(bal), o = cb + row1 * gw;
+                        for (u32 xb = xi1; xb < xi2; xb += 64) {
+                            const u32 cx = xb + lane;
+                            const bool hit = cx < xi2 && V.rst[0][o + cx] < qW;
+                            const u64 hb = __ballot(hit);
+                            if (hb) {
+                                const u32 cid = o + xb + (u32)__builtin_ctzll(hb);
+                                y = V.gy[V.cell[cid]];
+                                f = true;
+                                break;
+                            }
+                        }
+                    }
+                }
+            }
+            if (!f) {
+                // border cells: full rows yw1 (< yi1) and yw2 (>= yi2) when not inner, and the
+                // columns xw1 (< xi1) and xw2 (>= xi2) of the inner rows (every cell when there
+                // is no inner part)
+                const u32 nx = xw2 - xw1 + 1, ny = yw2 - yw1 + 1;
+                const bool full = !inner;
+                const u32 top = full ? ny : (yw1 < yi1 ? 1u : 0u), bot = full ? 0u : (yw2 >= yi2 ? 1u : 0u);
+                const u32 lc = (!full && xw1 < xi1) ? 1u : 0u, rc = (!full && xw2 >= xi2) ? 1u : 0u;
+                const u32 nin = full ? 0u : yi2 - yi1;
+                const u32 nrow = (top + bot) * nx, ncol = (lc + rc) * nin, nb = nrow + ncol;
+                for (u32 base = 0; base < nb && !f; base += 64) {
                     const u32 t = base + lane;
                     bool ok = false;
                     u32 yy = 0;
-                    if (t < ncell) {
-                        const u32 cid = cb + (yi1 + t / wx) * gw + xi1 + t % wx;
-                        const u32 p0 = V.cell[cid];
-                        if (V.cell[cid + 1] > p0 && V.gw[p0] < qW) {
-                            ok = true;
-                            yy = V.gy[p0];
+                    if (t < nb) {
+                        u32 cx, cy;
+                        if (t < nrow) {
+                            const u32 r = t / nx;
+                            cy = r < top ? yw1 + r : yw2;
+                            cx = xw1 + t % nx;
+                        } else {
+                            const u32 u = t - nrow, side = lc ? u / nin : 1u;
+                            cy = yi1 + u % nin;
+                            cx = side == 0 ? xw1 : xw2;
+                        }
+                        const u32 cid = cb + cy * gw + cx;
+                        const u32 p1 = V.cell[cid + 1];
+                        for (u32 q = V.cell[cid]; q < p1; q++) {
+                            if (V.gw[q] >= qW) break;
+                            const u32 xx = V.gx[q], y3 = V.gy[q];
+                            if (xx >= qxb && xx <= qxe && y3 >= qyb && y3 <= qye) {
+                                ok = true;
+                                yy = y3;
+                                break;
+                            }
                         }
                     }
                     const u64 bal = __ballot(ok);
                     if (bal) {
                         f = true;
                         y = __builtin_amdgcn_readlane(yy, __builtin_ctzll(bal));
-                        break;
-                    }
-                }
-            }
-            // border cells: their points lighter than W, in weight order
-            for (u32 yw = yw1; yw <= yw2 && !f; yw++) {
-                for (u32 xw = xw1; xw <= xw2 && !f; xw++) {
-                    if (inner && yw >= yi1 && yw < yi2 && xw >= xi1 && xw < xi2) continue;
-                    const u32 cid = cb + yw * gw + xw;
-                    const u32 p0 = V.cell[cid], p1 = V.cell[cid + 1];
-                    for (u32 base = p0; base < p1; base += 64) {
-                        const u32 t = base + lane;
-                        bool ok = false, heavy = false;
-                        u32 yy = 0;
-                        if (t < p1) {
-                            heavy = V.gw[t] >= qW;
-                            yy = V.gy[t];
-                            const u32 xx = V.gx[t];
-                            ok = !heavy && xx >= qxb && xx <= qxe && yy >= qyb && yy <= qye;
-                        }
-                        const u64 bal = __ballot(ok);
-                        if (bal) {
-                            f = true;
-                            y = __builtin_amdgcn_readlane(yy, __builtin_ctzll(bal));
-                            break;
-                        }
-                        if (__ballot(heavy)) break;
                     }
                 }
             }
@@ -577,12 +606,13 @@ __global__ void k_char_hist(const u8* __restrict__ T, const u32* __restrict__ C,
 // grid cell of sample id k and its sort key (cell << 32 | weight)
 __global__ void k_grid_keys(const u8* __restrict__ T, const u32* __restrict__ C, u32 c, const u32* __restrict__ PAR,
                             const u32* __restrict__ SAR, const u32* __restrict__ CS, const u32* __restrict__ gcb,
-                            const u32* __restrict__ gwd, u64* __restrict__ key, u32* __restrict__ id) {
+                            const u32* __restrict__ gwd, const u32* __restrict__ gwin, u64* __restrict__ key,
+                            u32* __restrict__ id) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c) return;
     const u32 ch = T[C[k]];
     const u32 r0 = CS[ch];
-    const u32 cx = (PAR[k] - r0) / SG_WIN, cy = (SAR[k] - r0) / SG_WIN;
+    const u32 cx = (PAR[k] - r0) / gwin[ch], cy = (SAR[k] - r0) / gwin[ch];
     key[k] = ((u64)(gcb[ch] + cy * gwd[ch] + cx) << 32) | (u32)k;
     id[k] = (u32)k;
 }
@@ -603,6 +633,29 @@ __global__ void k_grid_points(const u64* __restrict__ skey, const u32* __restric
         gw[t] = k;
     }
 }
+// lightest weight per cell (cells sorted by weight inside; INF when empty) = row level 0
+__global__ void k_cell_min(const u32* __restrict__ cell, const u32* __restrict__ gw, u32 ncell, u32* __restrict__ out) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ncell) return;
+    const u32 p0 = cell[t];
+    out[t] = cell[t + 1] > p0 ? gw[p0] : 0xFFFFFFFFu;
+}
+// row level k from k - 1: cells x of a row with x + 2^k <= gw (the others are never read)
+__global__ void k_cell_rowmin(const u32* __restrict__ prev, const u32* __restrict__ cgw, const u32* __restrict__ cgcb,
+                              u32 ncell, u32 half, u32* __restrict__ out) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ncell) return;
+    // the character block of cell t (<= 256 blocks, binary search)
+    u32 lo = 0, hi = 256;
+    while (hi - lo > 1) {
+        const u32 m = (lo + hi) >> 1;
+        if (cgcb[m] <= t) lo = m; else hi = m;
+    }
+    const u32 gw = cgw[lo];
+    const u32 x = gw ? (u32)((t - cgcb[lo]) % gw) : 0u;
+    out[t] = x + half < gw ? min(prev[t], prev[t + half]) : prev[t];
+}
+
 // RKS block fingerprints: (fp(T[16k .. 16k + 16)), b^len) per block, then an inclusive scan
 // with the concatenation (fa, pa) . (fb, pb) = (fa pb + fb, pa pb) (rabin_karp_substring.hpp:205-208)
 __global__ void k_rks_blocks(const u8* __restrict__ T, u64 n, u64 nb, u64* __restrict__ out) {
@@ -862,8 +915,8 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     k_pi_psi<<<cdiv(c, 256), 256, 0, st>>>(PA, SA, PAR, SAR, c, Pi, Psi);
     timer.mark("smpl_index");
     // the decomposed grid (decomposed_range.hpp:82-130, static_weighted_square_grid.hpp:67-104)
-    u32 hCS[257], hgcb[257], hgwd[256];
-    u32* dCS = e_CS.get(257 + 257 + 256);
+    u32 hCS[257], hgcb[257], hgwd[256], hwin[256];
+    u32* dCS = e_CS.get(257 + 257 + 256 + 256);
     {
         u32* hist = e_tmp1.get(256);
         LZ_HIP(hipMemsetAsync(hist, 0, 1024, st));
@@ -875,12 +928,15 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         hgcb[0] = 0;
         for (int ch = 0; ch < 256; ch++) {
             hCS[ch + 1] = hCS[ch] + hh[ch];
-            hgwd[ch] = (hh[ch] + SG_WIN - 1) / SG_WIN;
+            // cells of at least SG_WIN ranks, at most SG_GMAX per side
+            hgwd[ch] = std::min<u32>((hh[ch] + SG_WIN - 1) / SG_WIN, SG_GMAX);
+            hwin[ch] = hgwd[ch] ? (hh[ch] + hgwd[ch] - 1) / hgwd[ch] : SG_WIN;
             hgcb[ch + 1] = hgcb[ch] + hgwd[ch] * hgwd[ch];
         }
         LZ_HIP(hipMemcpyAsync(dCS, hCS, 257 * 4, hipMemcpyHostToDevice, st));
         LZ_HIP(hipMemcpyAsync(dCS + 257, hgcb, 257 * 4, hipMemcpyHostToDevice, st));
         LZ_HIP(hipMemcpyAsync(dCS + 514, hgwd, 256 * 4, hipMemcpyHostToDevice, st));
+        LZ_HIP(hipMemcpyAsync(dCS + 770, hwin, 256 * 4, hipMemcpyHostToDevice, st));
     }
     const u32 ncell = hgcb[256];
     u32* gx = e_gx.get(c);
@@ -892,12 +948,27 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         u64* key2 = e_key2.get(c);
         u32* id = e_tmp1.get(c);
         u32* id2 = e_tmp2.get(c);
-        k_grid_keys<<<cdiv(c, 256), 256, 0, st>>>(d_text, C, c, PAR, SAR, dCS, dCS + 257, dCS + 514, key, id);
+        k_grid_keys<<<cdiv(c, 256), 256, 0, st>>>(d_text, C, c, PAR, SAR, dCS, dCS + 257, dCS + 514, dCS + 770, key,
+                                                  id);
         size_t tb = 0;
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, id, id2, (int)c, 0, 64, st));
         u8* t = scan_tmp.get(tb);
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key2, id, id2, (int)c, 0, 64, st));
         k_grid_points<<<cdiv((u64)c + 1, 256), 256, 0, st>>>(key2, PAR, SAR, c, gx, gy, gw, cell, ncell);
+    }
+    // row sparse tables over the cells' lightest weights (levels 0 .. SG_LV - 1)
+    const u32* rst[SG_LV];
+    {
+        u32* lv0 = e_rst[0].get((u64)ncell + 1);
+        if (ncell) k_cell_min<<<cdiv(ncell, 256), 256, 0, st>>>(cell, gw, ncell, lv0);
+        rst[0] = lv0;
+        for (u32 k = 1; k < SG_LV; k++) {
+            u32* out = e_rst[k].get((u64)ncell + 1);
+            if (ncell)
+                k_cell_rowmin<<<cdiv(ncell, 256), 256, 0, st>>>(e_rst[k - 1].p, dCS + 514, dCS + 257, ncell, 1u << (k - 1),
+                                                                 out);
+            rst[k] = out;
+        }
     }
     timer.mark("smpl_grid");
     smpl_view V{};
@@ -912,6 +983,8 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.CS = dCS;
     V.gcb = dCS + 257;
     V.gwd = dCS + 514;
+    V.gwin = dCS + 770;
+    for (u32 k = 0; k < SG_LV; k++) V.rst[k] = rst[k];
     V.cell = cell;
     V.gx = gx;
     V.gy = gy;
