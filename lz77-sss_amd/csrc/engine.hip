@@ -172,6 +172,9 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
     last_fact_mode = fact_mode;
     stats.assign(24, 0);
     if (n == 0) return 0;
+    const auto t_start = std::chrono::steady_clock::now();
+    const u64 peak0 = g_dev_bytes.load();
+    if (log) g_dev_peak.store(peak0);
     timer.begin(st);
     prepare_phrases(phr_mode, false);
     if (fact_mode == LZ77SSS_SKIP_PHRASES) {
@@ -188,8 +191,35 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         std::fprintf(stderr, "[lz77sss] n=%llu |S|=%u phrases=%u factors=%llu outer=%llu rounds=%llu\n",
                      (unsigned long long)n, s, num_phr, (unsigned long long)num_fact,
                      (unsigned long long)stats[12], (unsigned long long)stats[13]);
+        if (fact_mode != LZ77SSS_SKIP_PHRASES) log_summary(t_start);
     }
     return num_fact;
+}
+
+// the summary a logged factorization prints (lz77_sss.hpp:345-353, formats of
+// misc/utils.hpp:54-96); peak memory = the session's peak device bytes + n (the text)
+static std::string fmt_time(u64 ns) {
+    if (ns > 10000000000ull) return std::to_string(ns / 1000000000) + " s";
+    if (ns > 10000000ull) return std::to_string(ns / 1000000) + " ms";
+    if (ns > 10000ull) return std::to_string(ns / 1000) + " us";
+    return std::to_string(ns) + " ns";
+}
+static std::string fmt_size(u64 B) {
+    if (B > 10000000000ull) return std::to_string(B / 1000000000) + " GB";
+    if (B > 10000000ull) return std::to_string(B / 1000000) + " MB";
+    if (B > 10000ull) return std::to_string(B / 1000) + " KB";
+    return std::to_string(B) + " B";
+}
+void engine::log_summary(std::chrono::steady_clock::time_point t_start) const {
+    const u64 ns = (u64)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_start).count();
+    const double comp_ratio = n / (double)std::max<u64>(1, num_fact);
+    const double tp = 1000.0 * (double)n / (double)std::max<u64>(1, ns);
+    std::printf("num. of factors: %llu\n", (unsigned long long)num_fact);
+    std::printf("input length / num. of factors: %s\n", std::to_string(comp_ratio).c_str());
+    std::printf("total time: %s\n", fmt_time(ns).c_str());
+    std::printf("throughput: %s MB/s\n", std::to_string(tp).c_str());
+    std::printf("peak memory consumption: %s\n", fmt_size(g_dev_peak.load() + n).c_str());
+    std::fflush(stdout);
 }
 
 // the two halves of lz77sss_session_prepare / _greedy_block (a block of a sharded run)

@@ -852,6 +852,8 @@ static u32 pow31_host(u64 b, u64 e) {
 u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int log2_override, bool log) {
     LZ_HIP(hipSetDevice(device));
     if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
+    const auto t_start = std::chrono::steady_clock::now();
+    if (log) g_dev_peak.store(g_dev_bytes.load());
     // the 3-approximation (compute_approximation, lz77_sss.hpp:324)
     const u64 za64 = factorize(phr_mode, rk_seed, log2_override, false, LZ77SSS_GREEDY);
     num_fact = 0;
@@ -1000,35 +1002,42 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     // chain within a few phrases).
     const u64 CS = std::max<u64>(256, std::min<u64>(1ull << 26, 32 * (n / std::max<u64>(1, za64))));
     const u32 nch = (u32)((n + CS - 1) / CS);
-    const u32 tcap = (u32)std::min<u64>(0x7FFFFFF0ull, 2 * (u64)za + n / 8 + 65536);
-    u32 hsz = 1;
-    while (hsz < 2ull * tcap) hsz <<= 1;
+    // task capacity: the chain (z <= z_approx) plus the walks before they merge; a full
+    // table is detected and the walks rerun with four times the room
+    u64 tcap64 = std::min<u64>(0x7FFFFFF0ull, 3 * (u64)za + 64 * (u64)nch + 65536);
     task_tab Tt{};
-    Tt.pos = e_tpos.get(tcap);
-    Tt.len = e_tlen.get(tcap);
-    Tt.src = e_tsrc.get(tcap);
-    Tt.hop = e_thop.get(tcap);
-    Tt.keys = e_tkeys.get(hsz);
-    Tt.vals = e_tvals.get(hsz);
-    Tt.mask = hsz - 1;
-    Tt.cap = tcap;
     u32* ctr = counters.get(16);
-    Tt.ntask = ctr + 8;
     u32* full = ctr + 9;
     u32* bad = ctr + 10;
     u32* zp = ctr + 11;
-    LZ_HIP(hipMemsetAsync(Tt.keys, 0, (size_t)hsz * 4, st));
-    LZ_HIP(hipMemsetAsync(ctr + 8, 0, 16, st));
     u32* ex = e_tmp1.get((u64)nch + 1);
-    k_chunk_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, CS, nch, ex, full);
-    LZ_HIP(hipGetLastError());
-    timer.mark("smpl_tasks");
-    k_bridge_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full);
-    LZ_HIP(hipGetLastError());
     u32 hc[2];
-    LZ_HIP(hipMemcpyAsync(hc, ctr + 8, 8, hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipStreamSynchronize(st));
-    if (hc[1] || hc[0] >= tcap) throw error(LZ77SSS_EINTERNAL, "exact-smpl: task table full");
+    for (int attempt = 0;; attempt++) {
+        const u32 tcap = (u32)tcap64;
+        u32 hsz = 1;
+        while (hsz < 2ull * tcap) hsz <<= 1;
+        Tt.pos = e_tpos.get(tcap);
+        Tt.len = e_tlen.get(tcap);
+        Tt.src = e_tsrc.get(tcap);
+        Tt.hop = e_thop.get(tcap);
+        Tt.keys = e_tkeys.get(hsz);
+        Tt.vals = e_tvals.get(hsz);
+        Tt.mask = hsz - 1;
+        Tt.cap = tcap;
+        Tt.ntask = ctr + 8;
+        LZ_HIP(hipMemsetAsync(Tt.keys, 0, (size_t)hsz * 4, st));
+        LZ_HIP(hipMemsetAsync(ctr + 8, 0, 16, st));
+        k_chunk_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, CS, nch, ex, full);
+        LZ_HIP(hipGetLastError());
+        timer.mark("smpl_tasks");
+        k_bridge_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full);
+        LZ_HIP(hipGetLastError());
+        LZ_HIP(hipMemcpyAsync(hc, ctr + 8, 8, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        if (!hc[1] && hc[0] < tcap) break;
+        if (attempt >= 3 || tcap64 >= 0x7FFFFFF0ull) throw error(LZ77SSS_EINTERNAL, "exact-smpl: task table full");
+        tcap64 = std::min<u64>(0x7FFFFFF0ull, 4 * tcap64);
+    }
     const u32 ntask = hc[0];
     timer.mark("smpl_bridges");
     // the path from the task at position 0: pointer doubling + top-down expansion (in order)
@@ -1070,6 +1079,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         std::fprintf(stderr, "[lz77sss] exact-smpl: n=%llu approx=%u samples=%u delta=%u tasks=%llu chunks=%u levels=%u factors=%llu\n",
                      (unsigned long long)n, za, c, delta, (unsigned long long)stats[26], rounds, walks,
                      (unsigned long long)z);
+        log_summary(t_start);
     }
     return z;
 }

@@ -216,6 +216,7 @@ struct engine {
     void path_marks(u32 m, u32* nxt0, u32* marks);
     u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy_block* blk = nullptr);
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode = 1);
+    void log_summary(std::chrono::steady_clock::time_point t_start) const;  // lz77_sss.hpp:345-353
     void prepare_phrases(int phr_mode, bool external_sss);  // the phases before the emitter
     u64 carried_entries(int log2_override);                 // slots of the gap index (carried table size)
     u64 emit_skip_phrases();  // fact_mode = skip_phrases (csrc/engine.hip)

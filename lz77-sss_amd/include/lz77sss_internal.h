@@ -5,6 +5,7 @@
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <chrono>
@@ -133,6 +134,15 @@ struct error : std::runtime_error {
                                       + std::to_string(__LINE__));                                 \
     } while (0)
 
+// device bytes held by dbufs in this process, and their peak (the "peak memory consumption"
+// line of a logged factorization, lz77_sss.hpp:345-353)
+inline std::atomic<uint64_t> g_dev_bytes{0}, g_dev_peak{0};
+inline void dev_bytes_add(int64_t b) {
+    const uint64_t v = g_dev_bytes.fetch_add((uint64_t)b) + (uint64_t)b;
+    uint64_t pk = g_dev_peak.load();
+    while (b > 0 && v > pk && !g_dev_peak.compare_exchange_weak(pk, v)) {}
+}
+
 // grow-only device buffer
 template <class T>
 struct dbuf {
@@ -143,11 +153,16 @@ struct dbuf {
     dbuf& operator=(const dbuf&) = delete;
     T* get(size_t n) {
         if (n > cap) {
-            if (p) LZ_HIP(hipFree(p));
+            const size_t c = std::max<size_t>(n, cap + cap / 4);
+            if (p) {
+                LZ_HIP(hipFree(p));
+                dev_bytes_add(-(int64_t)(cap * sizeof(T)));
+            }
             p = nullptr;
-            size_t c = std::max<size_t>(n, cap + cap / 4);
+            cap = 0;
             LZ_HIP(hipMalloc(&p, std::max<size_t>(c, 1) * sizeof(T)));
             cap = c;
+            dev_bytes_add((int64_t)(cap * sizeof(T)));
         }
         return p;
     }
@@ -157,17 +172,22 @@ struct dbuf {
         T* q = nullptr;
         const size_t c = std::max<size_t>(n, cap + cap / 2);
         LZ_HIP(hipMalloc(&q, c * sizeof(T)));
+        dev_bytes_add((int64_t)(c * sizeof(T)));
         if (p && keep) LZ_HIP(hipMemcpyAsync(q, p, keep * sizeof(T), hipMemcpyDeviceToDevice, st));
         if (p) {
             LZ_HIP(hipStreamSynchronize(st));
             LZ_HIP(hipFree(p));
+            dev_bytes_add(-(int64_t)(cap * sizeof(T)));
         }
         p = q;
         cap = c;
         return p;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            dev_bytes_add(-(int64_t)(cap * sizeof(T)));
+        }
         p = nullptr;
         cap = 0;
     }

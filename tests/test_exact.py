@@ -197,15 +197,16 @@ def test_gpu_exact_smpl_one_gib(session, lz):
     """configs[4] at full size (1 GiB rr): exact-smpl lengths == FULL_SA lengths, decode == T."""
     n = 1 << 30
     T = lz.gen_random_repetitive(n, n, 42, 0.5, 0.05)
-    s = session(n)
-    s.load(T)
-    z = s.factorize_exact(transf_mode=3)
-    F_ref = s.factors(z)
-    z2 = s.factorize_exact(transf_mode=2)
-    F = s.factors(z2)
-    assert z2 == z and np.array_equal(F[:, 1], F_ref[:, 1])
-    _, mism = s.decode(out=False)
-    assert mism == 0
+    # its own session: FULL_SA's 44 B x n are released before the next tests
+    with lz.Session(n) as s:
+        s.load(T)
+        z = s.factorize_exact(transf_mode=3)
+        F_ref = s.factors(z)
+        z2 = s.factorize_exact(transf_mode=2)
+        F = s.factors(z2)
+        assert z2 == z and np.array_equal(F[:, 1], F_ref[:, 1])
+        _, mism = s.decode(out=False)
+        assert mism == 0
 
 
 @pytest.mark.gpu
