@@ -382,7 +382,20 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
     same = None
     st = sess.stats()
     if rank == 0:
+        # the one-GPU stream from a fresh session (the sharded session's buffers released first:
+        # at 50 GiB the two together do not fit, and the plain call is kept independent of it)
+        sess.close()
+        sess = lz.Session(n, device=local_rank, pos64=pos64)
+        if chr19:
+            sess.gen_genome(n, 59 << 20, 0.001, 7)
+        else:
+            T = make_text(lz, args.workload, n, 0)
+            sess.load(T)
+            del T
+        t_1 = time.perf_counter()
         z1 = sess.factorize(device=local_rank)
+        print(f"[bench --shard] one-GPU factorize {time.perf_counter() - t_1:.2f} s, z={z1}", file=sys.stderr,
+              flush=True)
         ref = torch.empty(max(z1, 1) * 2, dtype=torch.int64 if pos64 else torch.int32, device=f"cuda:{local_rank}")
         if z1:
             sess.copy_factors(ref.data_ptr(), z1 * (16 if pos64 else 8))

@@ -97,29 +97,71 @@ __device__ __forceinline__ u128 kr_direct(const u8* T, u64 q, u32 len, u64 b) {
 struct ichunk { pos_t q0, q1; u32 rank0; };
 
 // one thread per (chunk, x): the 5 fingerprint chains of a chunk run on 5 adjacent
-// lanes (5x the threads of a chunk-per-thread walk for latency hiding, and the 5
-// entries of a position are written by adjacent lanes)
-__global__ void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __restrict__ chunks, u32 nch,
-                        u32* __restrict__ keys, u32* __restrict__ vals, pos_t* __restrict__ ipos,
-                        u8* __restrict__ pf = nullptr) {
-    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= 5ull * nch) return;
-    const u64 c = g / 5;
-    const int x = 4 - (int)(g - 5 * c);  // lanes of a chunk: x = 4, 3, 2, 1, 0 (entry order)
-    const ichunk ch = chunks[c];
+// lanes (5x the threads of a chunk-per-thread walk for latency hiding).  A workgroup
+// holds SL_CH chunks; every SL_K positions the entries (and positions) go through LDS and
+// leave as runs of 5 SL_K contiguous entries per chunk: written straight from the lanes,
+// the 4-byte stores 5 chunk lengths apart wrote 4.4x the key bytes to HBM (PMC
+// WRITE_SIZE, rr: 1.2 GB for 0.27 GB).
+constexpr u32 SL_CH = 64, SL_K = 16, SL_T = 5 * SL_CH;
+__global__ __launch_bounds__(SL_T) void k_slots(const u8* __restrict__ T, gap_cfg G, const ichunk* __restrict__ chunks,
+                                                u32 nch, u32* __restrict__ keys, u32* __restrict__ vals,
+                                                pos_t* __restrict__ ipos, u8* __restrict__ pf = nullptr) {
+    __shared__ u32 s_key[SL_CH * SL_K * 5];
+    __shared__ pos_t s_pos[SL_CH * SL_K];
+    __shared__ ichunk s_ch[SL_CH];
+    __shared__ u32 s_maxlen;
+    const u32 tid = threadIdx.x;
+    const u64 c0 = (u64)blockIdx.x * SL_CH;
+    const u32 cl = tid / 5, ord = tid - 5 * cl;  // lanes of a chunk: x = 4, 3, 2, 1, 0 (entry order)
+    const int x = 4 - (int)ord;
+    if (tid == 0) s_maxlen = 0;
+    __syncthreads();
+    if (tid < SL_CH) {
+        ichunk c{0, 0, 0};
+        if (c0 + tid < nch) c = chunks[c0 + tid];
+        s_ch[tid] = c;
+        atomicMax(&s_maxlen, (u32)(c.q1 - c.q0));
+    }
+    __syncthreads();
+    const ichunk ch = s_ch[cl];
+    const bool act = c0 + cl < nch;
     const u32 len = G.lens[x];
     const u64 b = G.base[x];
     const u128* np = G.negpow + x * 256;
-    u128 fp = kr_direct(T, ch.q0, len, b);
-    for (pos_t q = ch.q0; q < ch.q1; q++) {
-        const u32 rank = ch.rank0 + (q - ch.q0);
-        if (ipos && x == 4) ipos[rank] = q;
-        const u32 e = 5 * rank + (4 - x);
-        const u32 key = (u32)((u64)fp & G.mask);
-        keys[e] = key;
-        if (pf && !pf[key]) pf[key] = 1;  // slot presence (dense ids): plain stores, a hot slot is read far more often
-        if (vals) vals[e] = e;
-        if (q + 1 < ch.q1) fp = kr_roll(fp, b, np[T[q]], T[q + len]);
+    u128 fp = act ? kr_direct(T, ch.q0, len, b) : (u128)0;
+    const u32 maxlen = s_maxlen;
+    for (u32 k0 = 0; k0 < maxlen; k0 += SL_K) {
+        // fingerprints of positions q0 + k0 .. + SL_K into LDS
+        for (u32 j = 0; j < SL_K; j++) {
+            const pos_t q = ch.q0 + k0 + j;
+            if (!act || q >= ch.q1) break;
+            const u32 key = (u32)((u64)fp & G.mask);
+            s_key[(cl * SL_K + j) * 5 + ord] = key;
+            if (x == 4) s_pos[cl * SL_K + j] = q;
+            if (pf && !pf[key]) pf[key] = 1;  // slot presence (dense ids): plain stores, a hot slot is read far more often
+            if (q + 1 < ch.q1) fp = kr_roll(fp, b, np[T[q]], T[q + len]);
+        }
+        __syncthreads();
+        // per chunk: entries 5 (rank0 + k0) .. + 5 min(SL_K, left), contiguous
+        for (u32 idx = tid; idx < SL_CH * SL_K * 5; idx += SL_T) {
+            const u32 c = idx / (SL_K * 5), r = idx - c * (SL_K * 5);
+            const ichunk cc = s_ch[c];
+            if (c0 + c >= nch) continue;
+            const u64 left = (u64)(cc.q1 - cc.q0);
+            if (k0 >= left || r >= 5 * min<u64>(SL_K, left - k0)) continue;
+            const u64 e = 5ull * (cc.rank0 + k0) + r;
+            keys[e] = s_key[idx];
+            if (vals) vals[e] = (u32)e;
+        }
+        if (ipos) {
+            for (u32 idx = tid; idx < SL_CH * SL_K; idx += SL_T) {
+                const u32 c = idx / SL_K, j = idx - c * SL_K;
+                const ichunk cc = s_ch[c];
+                if (c0 + c >= nch || (u64)k0 + j >= (u64)(cc.q1 - cc.q0)) continue;
+                ipos[cc.rank0 + k0 + j] = s_pos[idx];
+            }
+        }
+        __syncthreads();
     }
 }
 // dense slot ids: a repetitive text hashes its gap positions into few distinct slots
@@ -1977,7 +2019,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 const bool try_dense = ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE");
                 u8* pf = try_dense ? (u8*)g_pflag.get(npw * 8) : nullptr;
                 if (pf) LZ_HIP(hipMemsetAsync(pf, 0, npw * 32, st));
-                k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos, pf);
+                k_slots<<<cdiv(nch, SL_CH), SL_T, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos, pf);
                 lap("base slots");
                 if (try_dense) {
                     u32* pcnt = g_pcnt.get(npw + 1);
@@ -2078,7 +2120,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             pos_t* apos = kpos.get(na);
             apos_out = apos;
             napos_out = na;
-            k_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
+            k_slots<<<cdiv(nch, SL_CH), SL_T, 0, st>>>(T, G, ch, nch, akey32, nullptr, apos);
             u64* ak = ka.get(5 * na);
             u64* ak2 = kb.get(5 * na);
             k_pack_added<<<cdiv(5 * na, 256), 256, 0, st>>>(akey32, apos, 5 * na, ak);
