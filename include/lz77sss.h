@@ -257,6 +257,17 @@ int lz77sss_session_carried_copy(lz77sss_session* s, void* buf, uint64_t bytes, 
 /* The greedy chain of one block; its factors replace the session's factors. */
 int lz77sss_session_greedy_block(lz77sss_session* s, const lz77sss_params* prm, lz77sss_block* blk,
                                  uint64_t* num_factors);
+/* Speculative blocks (no reference counterpart: the reference's chain is one
+ * sequential loop, greedy.cpp:46-134).  spec_begin: the next greedy_block starts from the
+ * carried table now in the session (a speculated entry) and records which of its slots the
+ * block's lookups use.  spec_resolve: given the true entry table (host or device, `bytes` as
+ * lz77sss_session_prepare reported), *accepted = 1 when every used slot agrees -- the block's
+ * factors and exit state are then the true ones and the carried table becomes its exit table
+ * over the true entry table -- else *accepted = 0 and the carried table is the true entry
+ * table (re-walk the block from the true state).  The caller compares the chain states. */
+int lz77sss_session_spec_begin(lz77sss_session* s);
+int lz77sss_session_spec_resolve(lz77sss_session* s, const void* true_table, uint64_t bytes,
+                                 uint64_t block_start, int* accepted);
 
 /* Average duration (ms) of the dominant kernel (SSS main pass) over the
  * last call, measured with hipEvents on its own stream; bytes = algorithmic

@@ -231,6 +231,7 @@ static u64 block_prepare(engine& E, int phr_mode, bool external_sss, int log2_ov
     E.num_fact = 0;
     E.last_fact_mode = LZ77SSS_GREEDY;
     E.stats.assign(24, 0);
+    E.spec_track = false;
     E.timer.begin(E.st);
     E.prepare_phrases(phr_mode, external_sss);
     const u64 ent = E.n ? E.carried_entries(log2_override) : 1;
@@ -316,6 +317,10 @@ struct engine64_impl final : lz::engine_if {
     void* carried_table() override { return E.g_Hs.p; }
     u64 carried_bytes() const override { return E.g_Hs.cap * sizeof(pos_t); }
     u64 greedy_block(u32 rk_seed, int log2_override, u64* st) override { return block_run(E, rk_seed, log2_override, st); }
+    void spec_begin() override { E.spec_begin(); }
+    bool spec_resolve(const void* true_tab, u64 bytes, u64 blk_start) override {
+        return E.spec_resolve(true_tab, bytes, blk_start);
+    }
 };
 }  // namespace lz64
 namespace lz {
@@ -882,6 +887,24 @@ LZ77SSS_API int lz77sss_session_greedy_block(lz77sss_session* s, const lz77sss_p
         blk->exit_idxpos = st[6];
         blk->exit_zmask = (uint32_t)st[7];
         if (num_factors) *num_factors = z;
+    });
+}
+
+LZ77SSS_API int lz77sss_session_spec_begin(lz77sss_session* s) {
+    if (!s) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (s->E64) s->E64->spec_begin();
+        else s->E.spec_begin();
+    });
+}
+
+LZ77SSS_API int lz77sss_session_spec_resolve(lz77sss_session* s, const void* true_table, uint64_t bytes,
+                                             uint64_t block_start, int* accepted) {
+    if (!s || !true_table || !accepted) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        const bool ok = s->E64 ? s->E64->spec_resolve(true_table, bytes, block_start)
+                               : s->E.spec_resolve(true_table, bytes, block_start);
+        *accepted = ok ? 1 : 0;
     });
 }
 

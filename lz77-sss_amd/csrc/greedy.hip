@@ -368,6 +368,8 @@ struct walk_ctx {
     const u32* bmI;      // current insert set (membership of added positions)
     pos_t bmoff;         // text position of bit 0 of the window bitmaps (a multiple of 32)
     const pos_t* Hs;     // window mode: slot -> last insert before the window (POS_NONE), or null
+    u32* hs_used;        // speculative block: bitmap of the slots whose entry-table value a lookup used
+    pos_t blk_start;     //   (values below the block start come from the entry table)
     int use_pred;        // base lookups via pred5 (else bucket search)
     lce_view L;
 };
@@ -469,6 +471,7 @@ __device__ pos_t added_last_before(const walk_ctx& W, u32 slot, pos_t q, u32 ord
 // last insert into the slot before the window (the carried table holds pos + 1, 0 = none)
 __device__ __forceinline__ pos_t carried(const walk_ctx& W, u32 slot) {
     const pos_t h = W.Hs[slot];
+    if (W.hs_used && (h == 0 || h - 1 < W.blk_start)) atomicOr(&W.hs_used[slot >> 5], 1u << (slot & 31));
     return h ? h - 1 : POS_NONE;
 }
 // H[slot of (q,x)] just before longest_prev_occ's advance_and_get_occ<x> at q
@@ -850,7 +853,7 @@ __global__ void k_h_unfix(const pos_t* __restrict__ H, u64 m, pos_t* __restrict_
 // out: [0] factors, [1] guard tripped, [2] exit position (>= stop), [3] index position there
 __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __restrict__ P, lce_view L,
                            pos_t* __restrict__ H, seg_in in, pos_t stop, pos_t* __restrict__ fact, u64 off,
-                           u64* __restrict__ out) {
+                           u64* __restrict__ out, u32* __restrict__ hs_used, pos_t blk_start) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const pos_t n = G.n;
     u128 fp[5];
@@ -887,6 +890,7 @@ __global__ void k_seq_walk(const u8* __restrict__ T, gap_cfg G, const pos_t* __r
             if (flen == 0) {  // advance_and_get_occ<x>: always inserts
                 const u32 sl = slot_of(x);
                 const pos_t occ = H[sl];
+                if (hs_used && (occ == POS_NONE || occ < blk_start)) atomicOr(&hs_used[sl >> 5], 1u << (sl & 31));
                 H[sl] = cur;
                 roll1(x);
                 if (occ < pos && T[occ] == T[pos]) {
@@ -1575,6 +1579,21 @@ __global__ void k_h_export(const u8* __restrict__ T, gap_cfg G, seg_tab S, const
     for (pos_t q = a + lane; q < o.e; q += 64) put(q);
     if (lane < o.nsingle && lane < 4) put(o.single[lane]);
 }
+// speculative blocks: the used slots of the speculated entry table against the
+// true one; on agreement the exit table takes the true entry value where the block wrote none
+__global__ void k_spec_check(const u32* __restrict__ used, const pos_t* __restrict__ spec,
+                             const pos_t* __restrict__ tru, u64 nslots, u32* __restrict__ bad) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nslots) return;
+    if ((used[k >> 5] >> (k & 31)) & 1u)
+        if (spec[k] != tru[k]) atomicOr(bad, 1u);
+}
+__global__ void k_spec_merge(pos_t* __restrict__ Hs, const pos_t* __restrict__ tru, u64 nslots, pos_t blk_start) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nslots) return;
+    const pos_t h = Hs[k];
+    if (!(h != 0 && h - 1 >= blk_start)) Hs[k] = tru[k];
+}
 // completion start: the last chain node whose start is <= y0 (the first position where
 // the speculated insert set and the chain's differ): every lookup of its predecessors
 // happened below y0, so its start state is exact (index state from its predecessor)
@@ -1778,6 +1797,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         Hs = g_Hs.get(nslots_all);
         if (!(blk && blk->carried)) LZ_HIP(hipMemsetAsync(Hs, 0, nslots_all * sizeof(pos_t), st));
     }
+    if (blk && spec_track) {
+        // speculative block: the entry-table slots its lookups use
+        const u64 nw = nslots_all / 32 + 1;
+        LZ_HIP(hipMemsetAsync(g_hsused.get(nw), 0, nw * 4, st));
+    }
     seg_in entry{0, 0, 0, zmask0, N};
     if (blk) {
         entry.start = blk->start;
@@ -1882,6 +1906,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         W.L = Lv;
         W.bmoff = off;
         W.Hs = Hs;
+        W.hs_used = (blk && spec_track) ? g_hsused.p : nullptr;
+        W.blk_start = blk ? blk->start : 0;
 
         // window exit (the chain state at the first handover point >= bw) and the carried table
         seg_in exit_in{};
@@ -1909,7 +1935,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 k_h_fill<<<cdiv(((u64)(cut.in.start - off) + 31) / 32, 256), 256, 0, st>>>(T, G, ins_bm, off, cut.in.start,
                                                                                          H);
             k_h_fix<<<cdiv(nslots_all, 256), 256, 0, st>>>(H, nslots_all);
-            k_seq_walk<<<1, 64, 0, st>>>(T, G, P, Lv, H, cut.in, last ? N + 1 : bw, fo, offk, d_sq);
+            k_seq_walk<<<1, 64, 0, st>>>(T, G, P, Lv, H, cut.in, last ? N + 1 : bw, fo, offk, d_sq, W.hs_used,
+                                         W.blk_start);
             LZ_HIP(hipGetLastError());
             u64 hc[4];
             LZ_HIP(hipMemcpyAsync(hc, d_sq, 32, hipMemcpyDeviceToHost, st));
@@ -2485,6 +2512,42 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
     stats[21] = nwin;
     stats[22] = stats_sss_tiles;  // anchor tiles the SSS filter marked (exact Q pass)
     return total_fact;
+}
+
+// ---------------------------------------------------------------------------
+// speculative blocks of a sharded run.  spec_begin snapshots the carried
+// table the next greedy_block starts from and tracks the slots of it the block's lookups use;
+// spec_resolve compares those slots with the true entry table (host or device memory).  On
+// agreement every lookup of the block saw the value the true table holds, so its factors, exit
+// state and inserts are the true ones, and the exit table is the block's writes over the true
+// entry table; otherwise the true table becomes the carried table (the caller re-walks).
+void engine::spec_begin() {
+    LZ_HIP(hipSetDevice(device));
+    const u64 m = g_Hs.cap;
+    if (!m || !g_Hs.p) throw error(LZ77SSS_EINVAL, "speculative block: no carried table (prepare first)");
+    LZ_HIP(hipMemcpyAsync(g_hsave.get(m), g_Hs.p, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+    spec_track = true;
+}
+bool engine::spec_resolve(const void* true_tab, u64 bytes, u64 blk_start) {
+    LZ_HIP(hipSetDevice(device));
+    const bool tracked = spec_track;
+    spec_track = false;
+    const u64 m = bytes / sizeof(pos_t);
+    if (!true_tab || !m || m > g_Hs.cap) throw error(LZ77SSS_EINVAL, "speculative block: bad true table");
+    pos_t* tru = g_htrue.get(m);
+    LZ_HIP(hipMemcpyAsync(tru, true_tab, m * sizeof(pos_t), hipMemcpyDefault, st));
+    bool ok = false;
+    if (tracked && g_hsave.cap >= m && g_hsused.cap >= m / 32 + 1) {
+        u32* bad = g_specbad.get(4);
+        LZ_HIP(hipMemsetAsync(bad, 0, 4, st));
+        k_spec_check<<<cdiv(m, 256), 256, 0, st>>>(g_hsused.p, g_hsave.p, tru, m, bad);
+        ok = rd1(bad, st) == 0;
+    }
+    if (ok) k_spec_merge<<<cdiv(m, 256), 256, 0, st>>>(g_Hs.p, tru, m, (pos_t)blk_start);
+    else LZ_HIP(hipMemcpyAsync(g_Hs.p, tru, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+    LZ_HIP(hipGetLastError());
+    LZ_HIP(hipStreamSynchronize(st));
+    return ok;
 }
 
 }  // namespace LZ_NS

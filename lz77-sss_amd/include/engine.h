@@ -161,6 +161,14 @@ struct engine {
     dbuf<pos_t> g_stash;  // per segment: factors of its last speculative walk (csrc/greedy.hip STASH_CAP)
     dbuf<pos_t> g_H;    // materialized gap-index table of the sequential completion
     dbuf<pos_t> g_Hs;   // greedy windows: last insert per slot before the window (pos + 1)
+    // speculative blocks of a sharded run: the entry table the block started
+    // from, the slots of it its lookups used, the true entry table when it arrives
+    bool spec_track = false;
+    dbuf<u32> g_hsused;
+    dbuf<pos_t> g_hsave, g_htrue;
+    dbuf<u32> g_specbad;
+    void spec_begin();
+    bool spec_resolve(const void* true_tab, u64 bytes, u64 blk_start);
     dbuf<pos_t> fact_acc;  // greedy windows: the stream so far
     dbuf<u8> g_cut;     // chain_cut + completion counters
     dbuf<u64> g_xk, g_xk2;

@@ -280,8 +280,18 @@ def factorize_sharded(text, n: int, rank: int, world: int, device: int | None = 
     return allf
 
 
+def spec_lead(n: int, g: list[int], rank: int) -> int:
+    """Lead-in length of rank `rank`'s speculative block: a third of its block, at
+    least 64 MiB, at most everything before it (LZ77SSS_SPEC_LEAD overrides, for the tests)."""
+    import os
+
+    env = os.environ.get("LZ77SSS_SPEC_LEAD")
+    lead = int(env) if env else max(64 << 20, (g[rank + 1] - g[rank]) // 3)
+    return max(1, min(lead, g[rank]))
+
+
 def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int, group=None,
-                               timings: dict | None = None, **params):
+                               timings: dict | None = None, speculate: bool = True, **params):
     """Collectives (1)-(4) with everything in HBM: `sess` is a Session on `device` holding the
     whole text (every rank loads it; phrases are replicated), pos_t = uint32_t or, for texts
     past 4 GiB (configs[3]), uint64_t (Session(pos64=True); the reference's choice at
@@ -328,9 +338,29 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     # (2) replicated SA_S / LCP / LPF phrases
     tab_bytes = sess.prepare(external_sss=True, **params)
     t2 = time.perf_counter()
-    # (3) the greedy chain in rank order
+    # (3) the greedy chain.  With speculation (world > 1) every rank r > 0 first walks its block
+    # concurrently from a speculated entry: a lead-in walk of the text before g_r from an empty
+    # table gives the chain state at the first hand-over point >= g_r and the table of the
+    # inserts before it; the block then runs with the slots its lookups take from that table
+    # tracked.  In rank order, the true (state, table) from r - 1 either confirms it (equal
+    # state, every used slot equal: the factors stand, the exit table is merged) or the block
+    # is walked again from the true state, as without speculation.
     g = chain_bounds(n, world)
+    spec = speculate and multi and rank > 0 and g[rank] > 0
+    t_spec = 0.0
+    spec_state, spec_walked, z = None, False, 0
+    if spec:
+        ts = time.perf_counter()
+        lead0 = g[rank] - spec_lead(n, g, rank)
+        _, spec_state = sess.greedy_block(lead0, lead0, 0, False, g[rank], **params)
+        if spec_state[0] < g[rank + 1] or rank == world - 1:
+            sess.spec_begin()
+            z, spec_exit = sess.greedy_block(*spec_state, True, g[rank + 1], **params)
+            spec_walked = True
+        t_spec = time.perf_counter() - ts
+    t_wait = time.perf_counter()
     state, carried = (0, 0, 0), False
+    accepted = None
     if rank > 0:
         hdr = torch.zeros(4, dtype=torch.int64, device=cdev)
         dist.recv(hdr, rank - 1, group=group)
@@ -340,12 +370,28 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
             dist.recv(tab, rank - 1, group=group)
             if nccl:
                 ready()
-            sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
+            if spec and spec_walked:
+                ok = sess.spec_resolve(nbytes=tab_bytes, block_start=spec_state[0], device_ptr=tab.data_ptr())
+                accepted = ok and state == tuple(spec_state)
+                if ok and not accepted:  # the table agreed, the state did not: back to the true table
+                    sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
+            else:
+                sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
+                if spec:  # the block was covered by the speculated chain: nothing to walk
+                    accepted = state == tuple(spec_state)
             del tab
-    z = 0
-    if state[0] < g[rank + 1] or rank == world - 1:
-        z, state = sess.greedy_block(*state, carried, g[rank + 1], **params)
-        carried = True
+        elif spec:
+            accepted = False  # (no carried table: a text too short to speculate on)
+    if accepted:
+        if spec_walked:
+            state, carried = tuple(spec_exit), True
+        else:
+            state = tuple(spec_state)
+    else:
+        z = 0
+        if state[0] < g[rank + 1] or rank == world - 1:
+            z, state = sess.greedy_block(*state, carried, g[rank + 1], **params)
+            carried = True
     if multi and rank + 1 < world:
         hdr = torch.tensor([state[0], state[1], state[2], int(carried)], dtype=torch.int64, device=cdev)
         dist.send(hdr, rank + 1, group=group)
@@ -355,6 +401,8 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
             dist.send(tab, rank + 1, group=group)
             del tab
     t3 = time.perf_counter()
+    if timings is not None:
+        timings.update(spec_walk=t_spec, chain_wait=t3 - t_wait, spec_accepted=accepted)
     # (4) emission: the blocks' factors gathered in rank order
     fb = sess.factor_bytes() if z else 0
     F = torch.empty(max(fb // 8, 1), dtype=torch.int64, device=dev)
@@ -365,6 +413,8 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
         F = gather_blocks(F.to(cdev), group).to(dev)
     if timings is not None:
         timings.update(sss=t1 - t0, prepare=t2 - t1, greedy_chain=t3 - t2, emit=time.perf_counter() - t3)
+    # (a rejected or accepted speculation leaves the same factors: the session's buffer holds
+    # the block's walk either way; the spec walk of a rejected block was overwritten by the re-walk)
     if getattr(sess, "pos64", False):
         return F.view(-1, 2)  # (src, len) as uint64 pairs; positions < 2^63
     return F.view(torch.int32).view(-1, 2)
