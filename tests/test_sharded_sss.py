@@ -355,7 +355,8 @@ def _resident_worker(rank, world, port, q, T, wide=False, gen=None, env=None, sp
                        tm.get("spec_accepted")))
             else:  # the stream's SHA-256 in the fixture layout (little-endian uint64 pairs)
                 h = hashlib.sha256(F.cpu().numpy().astype("<u8").view(np.uint8)).hexdigest()
-                q.put((rank, int(F.shape[0]), h, sorted(tm)))
+                q.put((rank, int(F.shape[0]), h, sorted(tm), tm.get("spec_accepted"),
+                       {k: round(v, 3) for k, v in tm.items() if isinstance(v, float)}))
     finally:
         dist.destroy_process_group()
 
@@ -440,6 +441,7 @@ def test_sharded_resident_u64_past_4gib_hash():
 
     e = json.loads((ROOT / "tests" / "golden" / "stream_hashes.json").read_text())["chr19_4gib_u64"]
     gen = dict(n=e["n"], base_len=e["args"]["base_len"], mut=e["args"]["mut"], seed=e["args"]["seed"])
-    for _, z, h, keys in _run_resident(2, np.zeros(0, np.uint8), True, gen):
+    for rank, z, h, keys, acc, tm in _run_resident(2, np.zeros(0, np.uint8), True, gen):
+        print(f"rank {rank}: speculative block accepted={acc} times={tm}")
         assert {"emit", "greedy_chain", "prepare", "sss"} <= set(keys)
         assert z == e["z"] and h == e["stream_sha256"]
