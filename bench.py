@@ -331,10 +331,9 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
     """One text factorized by all ranks together: one step = sharded.factorize_sharded_resident
     (collectives (1)-(4) of SURVEY.md 8e).  rr / genome: the seed-42 text of the default mode
     (--size-mib); chr19: configs[3]'s chr19-style text of --size-gib GiB generated in HBM with
-    pos_t = uint64_t (every rank holds the whole text: the phrases are replicated).  Every rank
-    walks its greedy block concurrently from a speculated entry (a lead-in walk) and keeps it
-    when the true hand-over from the rank before confirms it (sharded.py); total
-    work is fixed (strong scaling).  After the timed region rank 0 checks the stream against a
+    pos_t = uint64_t (every rank holds the whole text: the phrases are replicated).  The greedy
+    chain is walked block by block in rank order (speculative concurrent blocks are opt-in,
+    LZ77SSS_SPECULATE=1: sharded.py); total work is fixed (strong scaling).  After the timed region rank 0 checks the stream against a
     one-GPU factorize of the same text in a fresh session."""
     import sharded
 
@@ -418,8 +417,8 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
                        f", ONE text split over {world} rank(s), pos_t={'uint64' if pos64 else 'uint32'}",
                        "n": n, "tau": 512, "phr_mode": "lpf_opt", "fact_mode": "greedy",
                        "parallelism": f"sharded x{world}: S by block + all-gather, replicated phrases, "
-                                      f"speculative greedy blocks (lead-in walks, checked in rank order), "
-                                      f"gathered emission",
+                                      f"rank-ordered greedy blocks (speculative blocks opt-in: "
+                                      f"LZ77SSS_SPECULATE=1), gathered emission",
                        "factors": z, "equals_one_gpu_stream": same,
                        "sss_size": int(st[0]) if st else None, "lpf_phrases": int(st[2]) if st else None,
                        "text_gen_s": round(t_gen, 3), "rank0_phase_ms": phases},

@@ -245,7 +245,8 @@ typedef struct {
     uint64_t exit_start;  /* out: the next block's start (the first hand-over point >= end) */
     uint64_t exit_idxpos; /* out */
     uint32_t exit_zmask;  /* out */
-    uint32_t reserved;
+    uint32_t reserved;    /* in: 1 (with carried = 0) = start from the table of the gap positions before
+                             start (the lead-in of a speculative block); else 0 */
 } lz77sss_block;
 /* Loads an externally computed sync set (host or device pointer, 64-bit positions). */
 int lz77sss_session_set_sss(lz77sss_session* s, const uint64_t* S, uint64_t count, int has_runs);

@@ -245,7 +245,8 @@ static u64 block_run(engine& E, u32 rk_seed, int log2_override, u64* st) {
     b.start = (pos_t)st[0];
     b.idxpos = (pos_t)st[1];
     b.zmask = (u32)st[2];
-    b.carried = st[3] != 0;
+    b.carried = (st[3] & 1) != 0;
+    b.seed = (st[3] & 2) != 0;
     b.end = (pos_t)st[4];
     E.timer.begin(E.st);
     E.num_fact = E.n ? E.factorize_greedy(E.d_text, rk_seed, log2_override, &b) : 0;
@@ -880,7 +881,10 @@ LZ77SSS_API int lz77sss_session_greedy_block(lz77sss_session* s, const lz77sss_p
     if (!s || !blk) return LZ77SSS_EINVAL;
     return guarded([&] {
         check_params(prm);
-        uint64_t st[8] = {blk->start, blk->idxpos, blk->zmask, (uint64_t)(blk->carried != 0), blk->end, 0, 0, 0};
+        // reserved = 1: seed the table from the gap positions before start (a speculative lead-in)
+        uint64_t st[8] = {blk->start, blk->idxpos, blk->zmask,
+                          (uint64_t)(blk->carried != 0) | (blk->reserved == 1 && !blk->carried ? 2u : 0u), blk->end, 0,
+                          0, 0};
         const uint64_t z = s->E64 ? s->E64->greedy_block(prm->rk_seed, prm->index_log2_size, st)
                                   : lz::block_run(s->E, prm->rk_seed, prm->index_log2_size, st);
         blk->exit_start = st[5];

@@ -234,8 +234,14 @@ __global__ __launch_bounds__(PB_T) void k_pb_move(const u32* __restrict__ svals,
         tmp[p] = ((u64)e << 32) | pv;
     }
 }
+// XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so consecutive logical
+// blocks (the same bucket's 1 MiB window of pred5) are given to workgroups of one XCD, whose L2
+// then merges the window's scattered 4-byte writes instead of eight L2s writing partial lines
+constexpr u32 N_XCD = 8;
 __global__ void k_pb_apply(const u64* __restrict__ tmp, u64 m, u32* __restrict__ pred5) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u32 per = gridDim.x / N_XCD;  // grid: a multiple of N_XCD
+    const u64 lb = (u64)(blockIdx.x % N_XCD) * per + blockIdx.x / N_XCD;
+    const u64 i = lb * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const u64 x = tmp[i];
     pred5[x >> 32] = (u32)x;
@@ -1496,6 +1502,16 @@ __global__ void k_jumpk(const u32* __restrict__ J, const u32* __restrict__ D, u3
     J2[g] = J[j];
     D2[g] = D[g] + D[j];
 }
+// two doubling levels per launch: J1 = J o J, J2 = J1 o J1, D2 = D + D o J + D o J1 + D o J o J1
+__global__ void k_jumpk2(const u32* __restrict__ J, const u32* __restrict__ D, u32 nseg, u32* __restrict__ J1,
+                         u32* __restrict__ J2, u32* __restrict__ D2) {
+    const u64 g = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nseg) return;
+    const u32 a = J[g], b = J[a], c = J[b], d = J[c];
+    J1[g] = b;
+    J2[g] = d;
+    D2[g] = D[g] + D[a] + D[b] + D[c];
+}
 struct chain_status { u32 term, hops, valid, flags; pos_t next; u32 err, nseg; };
 __global__ void k_chain_status(seg_tab S, const u32* __restrict__ J, const u32* __restrict__ D, u32 c0,
                                chain_status* out) {
@@ -1579,14 +1595,66 @@ __global__ void k_h_export(const u8* __restrict__ T, gap_cfg G, seg_tab S, const
     for (pos_t q = a + lane; q < o.e; q += 64) put(q);
     if (lane < o.nsingle && lane < 4) put(o.single[lane]);
 }
+// the lead-in table of a speculative block: the speculated insert set of
+// [0, upto) -- every gap position and the query position past each gap, as the first
+// speculation of the one-GPU engine -- as the last insert per slot (pos + 1)
+constexpr u32 SEED_CH = 128;
+__global__ void k_seed_counts(const pos_t* __restrict__ P, u32 m, pos_t upto, u32* __restrict__ cnt) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > m) return;
+    pos_t a, b;
+    gap_of(P, (u32)k, a, b);
+    b = min(b, upto);
+    cnt[k] = b > a ? (u32)((b - a + SEED_CH - 1) / SEED_CH) : 0u;
+}
+__global__ void k_seed_slots(const u8* __restrict__ T, gap_cfg G, const pos_t* __restrict__ P, u32 m, pos_t upto,
+                             const u32* __restrict__ off, u32 nch, pos_t* __restrict__ Hs) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 5ull * nch) return;
+    const u32 c = (u32)(t / 5);
+    const int x = (int)(t - 5ull * c);
+    u32 lo = 0, hi = m + 1;  // the gap holding chunk c: last k with off[k] <= c
+    while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (off[mid] <= c) lo = mid; else hi = mid;
+    }
+    pos_t a, b;
+    gap_of(P, lo, a, b);
+    b = min(b, upto);
+    const pos_t q0 = a + (pos_t)(c - off[lo]) * SEED_CH, q1 = min(b, q0 + SEED_CH);
+    const u32 len = G.lens[x];
+    const u64 base = G.base[x];
+    const u128* np = G.negpow + x * 256;
+    u128 fp = kr_direct(T, q0, len, base);
+    for (pos_t q = q0; q < q1; q++) {
+        if ((u64)q + len < (u64)G.n) atomic_max_pos(&Hs[(u32)((u64)fp & G.mask)], q + 1);
+        if (q + 1 < q1) fp = kr_roll(fp, base, np[T[q]], T[q + len]);
+    }
+}
+__global__ void k_seed_queries(const u8* __restrict__ T, gap_cfg G, const pos_t* __restrict__ P, u32 m, pos_t upto,
+                               pos_t* __restrict__ Hs) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 5ull * (m + 1)) return;
+    const u32 k = (u32)(t / 5);
+    const int x = (int)(t - 5ull * k);
+    pos_t a, b;
+    gap_of(P, k, a, b);
+    if (a < b && b < upto && (u64)b + G.lens[x] < (u64)G.n)
+        atomic_max_pos(&Hs[(u32)((u64)kr_direct(T, b, G.lens[x], G.base[x]) & G.mask)], b + 1);
+}
 // speculative blocks: the used slots of the speculated entry table against the
 // true one; on agreement the exit table takes the true entry value where the block wrote none
 __global__ void k_spec_check(const u32* __restrict__ used, const pos_t* __restrict__ spec,
                              const pos_t* __restrict__ tru, u64 nslots, u32* __restrict__ bad) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nslots) return;
-    if ((used[k >> 5] >> (k & 31)) & 1u)
+    if ((used[k >> 5] >> (k & 31)) & 1u) {
         if (spec[k] != tru[k]) atomicOr(bad, 1u);
+        if (bad[1] != 0xFFFFFFFFu) {  // debug counters (bad[1] = ~0: off): used slots, differing ones
+            atomicAdd(bad + 1, 1u);
+            if (spec[k] != tru[k]) atomicAdd(bad + 2, 1u);
+        }
+    }
 }
 __global__ void k_spec_merge(pos_t* __restrict__ Hs, const pos_t* __restrict__ tru, u64 nslots, pos_t blk_start) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1796,6 +1864,16 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             throw error(LZ77SSS_EINVAL, "greedy block: carried table not loaded (size it with carried_entries)");
         Hs = g_Hs.get(nslots_all);
         if (!(blk && blk->carried)) LZ_HIP(hipMemsetAsync(Hs, 0, nslots_all * sizeof(pos_t), st));
+    }
+    if (blk && !blk->carried && blk->seed && blk->start > 0) {
+        // a lead-in of a speculative block: the table seeded from the gap positions before it
+        u32* cnt = g_tmp1.get(m + 2);
+        u32* off = g_tmp2.get(m + 2);
+        k_seed_counts<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, blk->start, cnt);
+        const u32 nch = excl_scan(cnt, off, m + 1, scan_tmp, st);
+        if (nch) k_seed_slots<<<cdiv(5ull * nch, 256), 256, 0, st>>>(T, G, P, m, blk->start, off, nch, Hs);
+        k_seed_queries<<<cdiv(5ull * (m + 1), 256), 256, 0, st>>>(T, G, P, m, blk->start, Hs);
+        LZ_HIP(hipGetLastError());
     }
     if (blk && spec_track) {
         // speculative block: the entry-table slots its lookups use
@@ -2105,7 +2183,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                         const u64 tile = (ne5 + ntile - 1) / ntile;
                         k_pb_init<<<cdiv(nbk, 256), 256, 0, st>>>(cursor, nbk);
                         k_pb_move<<<ntile, PB_T, 0, st>>>(svals, skeys, ne5, tile, nbk, cursor, tmp);
-                        k_pb_apply<<<cdiv(ne5, 256), 256, 0, st>>>(tmp, ne5, pred5);
+                        k_pb_apply<<<cdiv(cdiv(ne5, 256), N_XCD) * N_XCD, 256, 0, st>>>(tmp, ne5, pred5);
                     }
                 }
             }
@@ -2255,10 +2333,17 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     k_jump0<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg, jump[0].get(nseg), D0);
                     u32 nlv = 1;
                     while ((1ull << (nlv - 1)) < nseg) {
-                        if (nlv >= (u32)MAX_LV) throw error(-6, "greedy: too many jump levels");
-                        k_jumpk<<<cdiv(nseg, 256), 256, 0, st>>>(jump[nlv - 1].p, D0, nseg, jump[nlv].get(nseg), D1);
+                        if (nlv + 1 >= (u32)MAX_LV) throw error(-6, "greedy: too many jump levels");
+                        if ((1ull << nlv) < nseg) {  // two levels in one launch
+                            k_jumpk2<<<cdiv(nseg, 256), 256, 0, st>>>(jump[nlv - 1].p, D0, nseg, jump[nlv].get(nseg),
+                                                                      jump[nlv + 1].get(nseg), D1);
+                            nlv += 2;
+                        } else {
+                            k_jumpk<<<cdiv(nseg, 256), 256, 0, st>>>(jump[nlv - 1].p, D0, nseg, jump[nlv].get(nseg),
+                                                                     D1);
+                            nlv++;
+                        }
                         std::swap(D0, D1);
-                        nlv++;
                     }
                     JL.nlv = nlv;
                     for (u32 l = 0; l < nlv; l++) JL.J[l] = jump[l].p;
@@ -2539,9 +2624,17 @@ bool engine::spec_resolve(const void* true_tab, u64 bytes, u64 blk_start) {
     bool ok = false;
     if (tracked && g_hsave.cap >= m && g_hsused.cap >= m / 32 + 1) {
         u32* bad = g_specbad.get(4);
-        LZ_HIP(hipMemsetAsync(bad, 0, 4, st));
+        const bool dbg = debug_enabled() || std::getenv("LZ77SSS_SPEC_DEBUG");
+        const u32 init[3] = {0, dbg ? 0u : 0xFFFFFFFFu, 0};
+        LZ_HIP(hipMemcpyAsync(bad, init, 12, hipMemcpyHostToDevice, st));
         k_spec_check<<<cdiv(m, 256), 256, 0, st>>>(g_hsused.p, g_hsave.p, tru, m, bad);
-        ok = rd1(bad, st) == 0;
+        u32 hb[3];
+        LZ_HIP(hipMemcpyAsync(hb, bad, 12, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        ok = hb[0] == 0;
+        if (dbg)
+            std::fprintf(stderr, "[lz77sss] speculative block at %llu: %u entry-table slots used, %u differ\n",
+                         (unsigned long long)blk_start, hb[1], hb[2]);
     }
     if (ok) k_spec_merge<<<cdiv(m, 256), 256, 0, st>>>(g_Hs.p, tru, m, (pos_t)blk_start);
     else LZ_HIP(hipMemcpyAsync(g_Hs.p, tru, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));

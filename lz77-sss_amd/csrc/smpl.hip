@@ -52,6 +52,7 @@ namespace LZ_NS {
 
 constexpr u32 SMPL_MAX_DELTA = 256;  // lz77_sss.hpp:81 max_delta
 constexpr u32 SCAN_T = 4096;         // lz77_sss.hpp:83 range_scan_threshold
+constexpr u32 SMALL_T = 32;          // intersect queries scanned by their own lane (no wave round trip)
 #ifndef LZ_SG_WIN
 #define LZ_SG_WIN 2048
 #endif
@@ -245,7 +246,35 @@ __device__ bool sampled_iv(const smpl_view& V, u32 k, u32 pp, u32 fp, u32& b, u3
 __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 yb, u32 ye, u32 W, u32 ch, bool& found,
                                u32& py, u32 lane) {
     found = false;
-    u64 pend = __ballot(q);
+    // queries with a small side (at most SMALL_T ranks) scan it on their own lane, in the order
+    // the cooperative scan below uses (ascending ranks of the smaller side: the same point)
+    bool qq = q;
+    if (q && V.mode != LZ77SSS_TRANSF_NAIVE) {
+        const u32 rx = xe - xb + 1, ry = ye - yb + 1;
+        if (min(rx, ry) <= SMALL_T) {
+            qq = false;
+            if (rx <= ry) {
+                for (u32 x = xb; x <= xe; x++) {
+                    const u32 yy = V.Pi[x];
+                    if (V.PA[x] < W && yy >= yb && yy <= ye) {
+                        found = true;
+                        py = yy;
+                        break;
+                    }
+                }
+            } else {
+                for (u32 yy = yb; yy <= ye; yy++) {
+                    const u32 xx = V.Psi[yy];
+                    if (V.SA[yy] < W && xx >= xb && xx <= xe) {
+                        found = true;
+                        py = yy;
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    u64 pend = __ballot(qq);
     while (pend) {
         const int L = __builtin_ctzll(pend);
         pend &= pend - 1;

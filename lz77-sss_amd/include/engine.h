@@ -41,6 +41,7 @@ struct greedy_block {
     pos_t start = 0, idxpos = 0;
     u32 zmask = 0;
     bool carried = false;  // g_Hs holds the inserts before start (else it is zeroed)
+    bool seed = false;     // (not carried) seed g_Hs from the gap positions before start (a lead-in)
     pos_t end = 0;
     pos_t exit_start = 0, exit_idxpos = 0;
     u32 exit_zmask = 0;

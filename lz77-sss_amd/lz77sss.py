@@ -228,10 +228,11 @@ class Session:
         a = np.ascontiguousarray(table, dtype=np.uint8)
         _check(load_library().lz77sss_session_carried_copy(self._h, a.ctypes.data_as(_P), a.size, 1))
 
-    def greedy_block(self, start: int, idxpos: int, zmask: int, carried: bool, end: int, **kw):
-        """The greedy chain of [start, end) -> (factor count, (exit_start, exit_idxpos, exit_zmask))."""
+    def greedy_block(self, start: int, idxpos: int, zmask: int, carried: bool, end: int, seed: bool = False, **kw):
+        """The greedy chain of [start, end) -> (factor count, (exit_start, exit_idxpos, exit_zmask)).
+        seed (not carried): the table starts as the gap positions before start (a speculative lead-in)."""
         p = params(**kw)
-        b = Block(start, idxpos, zmask, int(carried), end, 0, 0, 0, 0)
+        b = Block(start, idxpos, zmask, int(carried), end, 0, 0, 0, 1 if (seed and not carried) else 0)
         z = _U64()
         _check(load_library().lz77sss_session_greedy_block(self._h, ctypes.byref(p), ctypes.byref(b), ctypes.byref(z)))
         return z.value, (b.exit_start, b.exit_idxpos, b.exit_zmask)

@@ -291,7 +291,7 @@ def spec_lead(n: int, g: list[int], rank: int) -> int:
 
 
 def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int, group=None,
-                               timings: dict | None = None, speculate: bool = True, **params):
+                               timings: dict | None = None, speculate: bool | None = None, **params):
     """Collectives (1)-(4) with everything in HBM: `sess` is a Session on `device` holding the
     whole text (every rank loads it; phrases are replicated), pos_t = uint32_t or, for texts
     past 4 GiB (configs[3]), uint64_t (Session(pos64=True); the reference's choice at
@@ -346,13 +346,17 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     # state, every used slot equal: the factors stand, the exit table is merged) or the block
     # is walked again from the true state, as without speculation.
     g = chain_bounds(n, world)
+    if speculate is None:  # off by default: all-or-nothing acceptance rejects full-size blocks
+        import os
+
+        speculate = os.environ.get("LZ77SSS_SPECULATE", "0") == "1"
     spec = speculate and multi and rank > 0 and g[rank] > 0
     t_spec = 0.0
     spec_state, spec_walked, z = None, False, 0
     if spec:
         ts = time.perf_counter()
         lead0 = g[rank] - spec_lead(n, g, rank)
-        _, spec_state = sess.greedy_block(lead0, lead0, 0, False, g[rank], **params)
+        _, spec_state = sess.greedy_block(lead0, lead0, 0, False, g[rank], seed=True, **params)
         if spec_state[0] < g[rank + 1] or rank == world - 1:
             sess.spec_begin()
             z, spec_exit = sess.greedy_block(*spec_state, True, g[rank + 1], **params)
@@ -373,6 +377,8 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
             if spec and spec_walked:
                 ok = sess.spec_resolve(nbytes=tab_bytes, block_start=spec_state[0], device_ptr=tab.data_ptr())
                 accepted = ok and state == tuple(spec_state)
+                if timings is not None:
+                    timings.update(spec_table_ok=ok, spec_state_ok=state == tuple(spec_state))
                 if ok and not accepted:  # the table agreed, the state did not: back to the true table
                     sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
             else:

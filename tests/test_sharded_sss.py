@@ -356,7 +356,7 @@ def _resident_worker(rank, world, port, q, T, wide=False, gen=None, env=None, sp
             else:  # the stream's SHA-256 in the fixture layout (little-endian uint64 pairs)
                 h = hashlib.sha256(F.cpu().numpy().astype("<u8").view(np.uint8)).hexdigest()
                 q.put((rank, int(F.shape[0]), h, sorted(tm), tm.get("spec_accepted"),
-                       {k: round(v, 3) for k, v in tm.items() if isinstance(v, float)}))
+                       {k: (round(v, 3) if isinstance(v, float) else v) for k, v in tm.items()}))
     finally:
         dist.destroy_process_group()
 
