@@ -259,16 +259,22 @@ int lz77sss_session_carried_copy(lz77sss_session* s, void* buf, uint64_t bytes, 
 int lz77sss_session_greedy_block(lz77sss_session* s, const lz77sss_params* prm, lz77sss_block* blk,
                                  uint64_t* num_factors);
 /* Speculative blocks (no reference counterpart: the reference's chain is one
- * sequential loop, greedy.cpp:46-134).  spec_begin: the next greedy_block starts from the
- * carried table now in the session (a speculated entry) and records which of its slots the
- * block's lookups use.  spec_resolve: given the true entry table (host or device, `bytes` as
- * lz77sss_session_prepare reported), *accepted = 1 when every used slot agrees -- the block's
- * factors and exit state are then the true ones and the carried table becomes its exit table
- * over the true entry table -- else *accepted = 0 and the carried table is the true entry
- * table (re-walk the block from the true state).  The caller compares the chain states. */
-int lz77sss_session_spec_begin(lz77sss_session* s);
-int lz77sss_session_spec_resolve(lz77sss_session* s, const void* true_table, uint64_t bytes,
-                                 uint64_t block_start, int* accepted);
+ * sequential loop, greedy.cpp:46-134).  A speculative block starting at block_start is walked
+ * as consecutive parts 0, 1, ... (one greedy_block each, each from the previous one's exit
+ * state).  spec_begin(part): the next greedy_block is part `part`; part 0 starts from the
+ * carried table now in the session (a speculated entry table).  The session keeps the table
+ * each part started from and records which entry-table slots each part's lookups use.
+ * spec_resolve: given the true entry table (host or device, `bytes` as
+ * lz77sss_session_prepare reported), *accepted_parts = the number of leading parts all of whose
+ * used slots agree: those parts' factors and exit states are the true ones.  The carried table
+ * becomes the writes of the accepted parts over the true entry table -- the table to re-walk
+ * the rest of the block with, from the exit state of the last accepted part (or the true
+ * entry state), or the exit table when every part was accepted.  The caller compares the
+ * chain states (parts = 0 rejects everything: the carried table becomes the true one). */
+#define LZ77SSS_SPEC_MAX_PARTS 16
+int lz77sss_session_spec_begin(lz77sss_session* s, int part, uint64_t block_start);
+int lz77sss_session_spec_resolve(lz77sss_session* s, const void* true_table, uint64_t bytes, int parts,
+                                 int* accepted_parts);
 
 /* Average duration (ms) of the dominant kernel (SSS main pass) over the
  * last call, measured with hipEvents on its own stream; bytes = algorithmic

@@ -318,9 +318,9 @@ struct engine64_impl final : lz::engine_if {
     void* carried_table() override { return E.g_Hs.p; }
     u64 carried_bytes() const override { return E.g_Hs.cap * sizeof(pos_t); }
     u64 greedy_block(u32 rk_seed, int log2_override, u64* st) override { return block_run(E, rk_seed, log2_override, st); }
-    void spec_begin() override { E.spec_begin(); }
-    bool spec_resolve(const void* true_tab, u64 bytes, u64 blk_start) override {
-        return E.spec_resolve(true_tab, bytes, blk_start);
+    void spec_begin(int part, u64 base) override { E.spec_begin(part, base); }
+    int spec_resolve(const void* true_tab, u64 bytes, int parts) override {
+        return E.spec_resolve(true_tab, bytes, parts);
     }
 };
 }  // namespace lz64
@@ -894,21 +894,20 @@ LZ77SSS_API int lz77sss_session_greedy_block(lz77sss_session* s, const lz77sss_p
     });
 }
 
-LZ77SSS_API int lz77sss_session_spec_begin(lz77sss_session* s) {
-    if (!s) return LZ77SSS_EINVAL;
+LZ77SSS_API int lz77sss_session_spec_begin(lz77sss_session* s, int part, uint64_t block_start) {
+    if (!s || part < 0 || part >= LZ77SSS_SPEC_MAX_PARTS) return LZ77SSS_EINVAL;
     return guarded([&] {
-        if (s->E64) s->E64->spec_begin();
-        else s->E.spec_begin();
+        if (s->E64) s->E64->spec_begin(part, block_start);
+        else s->E.spec_begin(part, block_start);
     });
 }
 
-LZ77SSS_API int lz77sss_session_spec_resolve(lz77sss_session* s, const void* true_table, uint64_t bytes,
-                                             uint64_t block_start, int* accepted) {
-    if (!s || !true_table || !accepted) return LZ77SSS_EINVAL;
+LZ77SSS_API int lz77sss_session_spec_resolve(lz77sss_session* s, const void* true_table, uint64_t bytes, int parts,
+                                             int* accepted_parts) {
+    if (!s || !true_table || !accepted_parts || parts < 0 || parts > LZ77SSS_SPEC_MAX_PARTS) return LZ77SSS_EINVAL;
     return guarded([&] {
-        const bool ok = s->E64 ? s->E64->spec_resolve(true_table, bytes, block_start)
-                               : s->E.spec_resolve(true_table, bytes, block_start);
-        *accepted = ok ? 1 : 0;
+        *accepted_parts = s->E64 ? s->E64->spec_resolve(true_table, bytes, parts)
+                                 : s->E.spec_resolve(true_table, bytes, parts);
     });
 }
 

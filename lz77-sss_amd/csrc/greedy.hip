@@ -1642,20 +1642,26 @@ __global__ void k_seed_queries(const u8* __restrict__ T, gap_cfg G, const pos_t*
     if (a < b && b < upto && (u64)b + G.lens[x] < (u64)G.n)
         atomic_max_pos(&Hs[(u32)((u64)kr_direct(T, b, G.lens[x], G.base[x]) & G.mask)], b + 1);
 }
-// speculative blocks: the used slots of the speculated entry table against the
-// true one; on agreement the exit table takes the true entry value where the block wrote none
-__global__ void k_spec_check(const u32* __restrict__ used, const pos_t* __restrict__ spec,
+// speculative blocks: bad[0] = the first part whose lookups used a slot where the
+// speculated entry table and the true one differ (atomicMin; starts at the number of parts)
+__global__ void k_spec_check(const u32* __restrict__ used, int parts, u64 nw, const pos_t* __restrict__ spec,
                              const pos_t* __restrict__ tru, u64 nslots, u32* __restrict__ bad) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nslots) return;
-    if ((used[k >> 5] >> (k & 31)) & 1u) {
-        if (spec[k] != tru[k]) atomicOr(bad, 1u);
-        if (bad[1] != 0xFFFFFFFFu) {  // debug counters (bad[1] = ~0: off): used slots, differing ones
-            atomicAdd(bad + 1, 1u);
-            if (spec[k] != tru[k]) atomicAdd(bad + 2, 1u);
+    const bool differs = spec[k] != tru[k];
+    bool any = false;
+    for (int p = 0; p < parts; ++p)
+        if ((used[(u64)p * nw + (k >> 5)] >> (k & 31)) & 1u) {
+            if (differs) atomicMin(bad, (u32)p);
+            any = true;
+            break;
         }
+    if (any && bad[1] != 0xFFFFFFFFu) {  // debug counters (bad[1] = ~0: off): used slots, differing ones
+        atomicAdd(bad + 1, 1u);
+        if (differs) atomicAdd(bad + 2, 1u);
     }
 }
+// the carried table for the rest: the speculative block's writes (values > its start) over the true table
 __global__ void k_spec_merge(pos_t* __restrict__ Hs, const pos_t* __restrict__ tru, u64 nslots, pos_t blk_start) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nslots) return;
@@ -1875,11 +1881,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         k_seed_queries<<<cdiv(5ull * (m + 1), 256), 256, 0, st>>>(T, G, P, m, blk->start, Hs);
         LZ_HIP(hipGetLastError());
     }
-    if (blk && spec_track) {
-        // speculative block: the entry-table slots its lookups use
-        const u64 nw = nslots_all / 32 + 1;
-        LZ_HIP(hipMemsetAsync(g_hsused.get(nw), 0, nw * 4, st));
-    }
+    if (blk && spec_track && nslots_all > spec_m)
+        throw error(LZ77SSS_EINVAL, "speculative block: the carried table changed size since spec_begin");
     seg_in entry{0, 0, 0, zmask0, N};
     if (blk) {
         entry.start = blk->start;
@@ -1984,8 +1987,10 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         W.L = Lv;
         W.bmoff = off;
         W.Hs = Hs;
-        W.hs_used = (blk && spec_track) ? g_hsused.p : nullptr;
-        W.blk_start = blk ? blk->start : 0;
+        // speculative part: its bitmap of used entry-table slots; values below the
+        // speculative block's start come from that table (earlier parts' writes do not)
+        W.hs_used = (blk && spec_track) ? g_hsused.p + (u64)spec_part * (spec_m / 32 + 1) : nullptr;
+        W.blk_start = blk ? (spec_track ? (pos_t)spec_base : blk->start) : 0;
 
         // window exit (the chain state at the first handover point >= bw) and the carried table
         seg_in exit_in{};
@@ -2600,47 +2605,65 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
 }
 
 // ---------------------------------------------------------------------------
-// speculative blocks of a sharded run.  spec_begin snapshots the carried
-// table the next greedy_block starts from and tracks the slots of it the block's lookups use;
-// spec_resolve compares those slots with the true entry table (host or device memory).  On
-// agreement every lookup of the block saw the value the true table holds, so its factors, exit
-// state and inserts are the true ones, and the exit table is the block's writes over the true
-// entry table; otherwise the true table becomes the carried table (the caller re-walks).
-void engine::spec_begin() {
+// speculative blocks of a sharded run, walked as consecutive parts.  spec_begin
+// snapshots the carried table part `part` starts from (part 0: the speculated entry table) and
+// tracks the entry-table slots its lookups use; spec_resolve compares them, part by part, with the
+// true entry table (host or device memory).  A part all of whose used slots agree -- and whose
+// predecessors' did -- saw at every lookup the value the true table holds, so its factors, exit
+// state and inserts are the true ones.  The carried table becomes the writes of the accepted parts
+// over the true entry table: the table the caller re-walks the rest with (or passes on).
+void engine::spec_begin(int part, u64 base) {
     LZ_HIP(hipSetDevice(device));
     const u64 m = g_Hs.cap;
     if (!m || !g_Hs.p) throw error(LZ77SSS_EINVAL, "speculative block: no carried table (prepare first)");
-    LZ_HIP(hipMemcpyAsync(g_hsave.get(m), g_Hs.p, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+    if (part == 0) {
+        spec_m = m;
+        spec_base = base;
+    } else if (!spec_track || part != spec_part + 1 || base != spec_base || m != spec_m) {
+        throw error(LZ77SSS_EINVAL, "speculative block: parts must follow each other from part 0");
+    }
+    const u64 nw = m / 32 + 1;
+    pos_t* sv = g_hsave.grow_keep((u64)(part + 1) * m, (u64)part * m, st);
+    u32* used = g_hsused.grow_keep((u64)(part + 1) * nw, (u64)part * nw, st);
+    LZ_HIP(hipMemcpyAsync(sv + (u64)part * m, g_Hs.p, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+    LZ_HIP(hipMemsetAsync(used + (u64)part * nw, 0, nw * 4, st));
+    spec_part = part;
     spec_track = true;
 }
-bool engine::spec_resolve(const void* true_tab, u64 bytes, u64 blk_start) {
+int engine::spec_resolve(const void* true_tab, u64 bytes, int parts) {
     LZ_HIP(hipSetDevice(device));
-    const bool tracked = spec_track;
+    const bool tracked = spec_track && parts > 0;
     spec_track = false;
     const u64 m = bytes / sizeof(pos_t);
     if (!true_tab || !m || m > g_Hs.cap) throw error(LZ77SSS_EINVAL, "speculative block: bad true table");
+    if (tracked && (parts > spec_part + 1 || m > spec_m))
+        throw error(LZ77SSS_EINVAL, "speculative block: more parts than were walked");
     pos_t* tru = g_htrue.get(m);
     LZ_HIP(hipMemcpyAsync(tru, true_tab, m * sizeof(pos_t), hipMemcpyDefault, st));
-    bool ok = false;
-    if (tracked && g_hsave.cap >= m && g_hsused.cap >= m / 32 + 1) {
+    int acc = 0;
+    if (tracked) {
         u32* bad = g_specbad.get(4);
         const bool dbg = debug_enabled() || std::getenv("LZ77SSS_SPEC_DEBUG");
-        const u32 init[3] = {0, dbg ? 0u : 0xFFFFFFFFu, 0};
+        const u32 init[3] = {(u32)parts, dbg ? 0u : 0xFFFFFFFFu, 0};
         LZ_HIP(hipMemcpyAsync(bad, init, 12, hipMemcpyHostToDevice, st));
-        k_spec_check<<<cdiv(m, 256), 256, 0, st>>>(g_hsused.p, g_hsave.p, tru, m, bad);
+        k_spec_check<<<cdiv(m, 256), 256, 0, st>>>(g_hsused.p, parts, spec_m / 32 + 1, g_hsave.p, tru, m, bad);
         u32 hb[3];
         LZ_HIP(hipMemcpyAsync(hb, bad, 12, hipMemcpyDeviceToHost, st));
         LZ_HIP(hipStreamSynchronize(st));
-        ok = hb[0] == 0;
+        acc = (int)hb[0];
         if (dbg)
-            std::fprintf(stderr, "[lz77sss] speculative block at %llu: %u entry-table slots used, %u differ\n",
-                         (unsigned long long)blk_start, hb[1], hb[2]);
+            std::fprintf(stderr,
+                         "[lz77sss] speculative block at %llu: %u entry-table slots used, %u differ; %d of %d parts "
+                         "accepted\n",
+                         (unsigned long long)spec_base, hb[1], hb[2], acc, parts);
     }
-    if (ok) k_spec_merge<<<cdiv(m, 256), 256, 0, st>>>(g_Hs.p, tru, m, (pos_t)blk_start);
+    if (tracked && acc < parts)  // the table the first rejected part started from
+        LZ_HIP(hipMemcpyAsync(g_Hs.p, g_hsave.p + (u64)acc * spec_m, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
+    if (tracked && acc > 0) k_spec_merge<<<cdiv(m, 256), 256, 0, st>>>(g_Hs.p, tru, m, (pos_t)spec_base);
     else LZ_HIP(hipMemcpyAsync(g_Hs.p, tru, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipStreamSynchronize(st));
-    return ok;
+    return acc;
 }
 
 }  // namespace LZ_NS

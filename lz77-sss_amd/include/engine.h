@@ -162,14 +162,17 @@ struct engine {
     dbuf<pos_t> g_stash;  // per segment: factors of its last speculative walk (csrc/greedy.hip STASH_CAP)
     dbuf<pos_t> g_H;    // materialized gap-index table of the sequential completion
     dbuf<pos_t> g_Hs;   // greedy windows: last insert per slot before the window (pos + 1)
-    // speculative blocks of a sharded run: the entry table the block started
-    // from, the slots of it its lookups used, the true entry table when it arrives
+    // speculative blocks of a sharded run, walked as consecutive parts: the
+    // table each part started from (part 0: the speculated entry table), per part the
+    // entry-table slots its lookups used, the true entry table when it arrives
     bool spec_track = false;
+    int spec_part = 0;
+    u64 spec_base = 0, spec_m = 0;  // block start; table slots
     dbuf<u32> g_hsused;
     dbuf<pos_t> g_hsave, g_htrue;
     dbuf<u32> g_specbad;
-    void spec_begin();
-    bool spec_resolve(const void* true_tab, u64 bytes, u64 blk_start);
+    void spec_begin(int part, u64 base);
+    int spec_resolve(const void* true_tab, u64 bytes, int parts);
     dbuf<pos_t> fact_acc;  // greedy windows: the stream so far
     dbuf<u8> g_cut;     // chain_cut + completion counters
     dbuf<u64> g_xk, g_xk2;

@@ -47,8 +47,8 @@ struct engine_if {
     virtual u64 carried_bytes() const = 0;   // capacity of the carried table
     virtual u64 greedy_block(u32 rk_seed, int log2_override, u64* state /* start, idxpos, zmask, carried, end,
                                                                         exit_start, exit_idxpos, exit_zmask */) = 0;
-    virtual void spec_begin() = 0;
-    virtual bool spec_resolve(const void* true_tab, u64 bytes, u64 blk_start) = 0;
+    virtual void spec_begin(int part, u64 base) = 0;
+    virtual int spec_resolve(const void* true_tab, u64 bytes, int parts) = 0;
 };
 
 // defined in the LZ_POS64 compilation of csrc/engine.hip; throws lz::error

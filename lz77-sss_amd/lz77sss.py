@@ -61,8 +61,8 @@ _SYMBOLS = {
     "lz77sss_session_prepare": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.c_int, ctypes.POINTER(_U64)]),
     "lz77sss_session_carried_copy": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int]),
     "lz77sss_session_greedy_block": (ctypes.c_int, [_P, ctypes.POINTER(Params), _P, ctypes.POINTER(_U64)]),
-    "lz77sss_session_spec_begin": (ctypes.c_int, [_P]),
-    "lz77sss_session_spec_resolve": (ctypes.c_int, [_P, _P, _U64, _U64, ctypes.POINTER(ctypes.c_int)]),
+    "lz77sss_session_spec_begin": (ctypes.c_int, [_P, ctypes.c_int, _U64]),
+    "lz77sss_session_spec_resolve": (ctypes.c_int, [_P, _P, _U64, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "lz77sss_session_factorize_exact": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.c_int,
                                                        ctypes.POINTER(_U64)]),
     "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
@@ -237,23 +237,25 @@ class Session:
         _check(load_library().lz77sss_session_greedy_block(self._h, ctypes.byref(p), ctypes.byref(b), ctypes.byref(z)))
         return z.value, (b.exit_start, b.exit_idxpos, b.exit_zmask)
 
-    def spec_begin(self):
-        """The next greedy_block starts from a speculated carried table."""
-        _check(load_library().lz77sss_session_spec_begin(self._h))
+    def spec_begin(self, part: int = 0, block_start: int = 0):
+        """The next greedy_block is part `part` of a speculative block starting at `block_start`
+        (part 0: from the speculated carried table now in the session)."""
+        _check(load_library().lz77sss_session_spec_begin(self._h, part, block_start))
 
-    def spec_resolve(self, table=None, nbytes: int = 0, block_start: int = 0, device_ptr: int | None = None) -> bool:
-        """Checks the speculated block against the true entry table (host array or device pointer):
-        True = its factors / exit state stand (carried table = its exit table over the true one),
-        False = re-walk it (carried table = the true entry table)."""
+    def spec_resolve(self, table=None, nbytes: int = 0, parts: int = 1, device_ptr: int | None = None) -> int:
+        """Checks the speculative block's parts against the true entry table (host array or device
+        pointer) and returns how many leading parts stand (their factors / exit states are the
+        true ones).  The carried table becomes their writes over the true entry table: the exit
+        table when all stand, else the table to re-walk the rest with (parts=0: the true table)."""
         acc = ctypes.c_int()
         if device_ptr is not None:
-            _check(load_library().lz77sss_session_spec_resolve(self._h, _P(device_ptr), nbytes, block_start,
+            _check(load_library().lz77sss_session_spec_resolve(self._h, _P(device_ptr), nbytes, parts,
                                                                 ctypes.byref(acc)))
         else:
             a = np.ascontiguousarray(table, dtype=np.uint8)
-            _check(load_library().lz77sss_session_spec_resolve(self._h, a.ctypes.data_as(_P), a.size, block_start,
+            _check(load_library().lz77sss_session_spec_resolve(self._h, a.ctypes.data_as(_P), a.size, parts,
                                                                 ctypes.byref(acc)))
-        return bool(acc.value)
+        return acc.value
 
     def factors(self, z: int) -> np.ndarray:
         if self.pos64:

@@ -280,6 +280,14 @@ def factorize_sharded(text, n: int, rank: int, world: int, device: int | None = 
     return allf
 
 
+def spec_parts() -> int:
+    """Parts of a speculative block (LZ77SSS_SPEC_PARTS, 1..16, default 8): each is
+    confirmed on its own, so a difference late in the block costs only the parts from there on."""
+    import os
+
+    return max(1, min(16, int(os.environ.get("LZ77SSS_SPEC_PARTS", "8"))))
+
+
 def spec_lead(n: int, g: list[int], rank: int) -> int:
     """Lead-in length of rank `rank`'s speculative block: a third of its block, at
     least 64 MiB, at most everything before it (LZ77SSS_SPEC_LEAD overrides, for the tests)."""
@@ -303,6 +311,7 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     memory (several ranks sharing a GPU in the tests).  The session's own stream is
     synchronized before any buffer changes hands, and torch's current stream before the
     session reads a received buffer."""
+    import os
     import time
 
     import torch
@@ -339,32 +348,44 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     tab_bytes = sess.prepare(external_sss=True, **params)
     t2 = time.perf_counter()
     # (3) the greedy chain.  With speculation (world > 1) every rank r > 0 first walks its block
-    # concurrently from a speculated entry: a lead-in walk of the text before g_r from an empty
-    # table gives the chain state at the first hand-over point >= g_r and the table of the
-    # inserts before it; the block then runs with the slots its lookups take from that table
-    # tracked.  In rank order, the true (state, table) from r - 1 either confirms it (equal
-    # state, every used slot equal: the factors stand, the exit table is merged) or the block
-    # is walked again from the true state, as without speculation.
+    # concurrently from a speculated entry: a lead-in walk of the text before g_r from a table
+    # of the gap positions before it gives the chain state at the first hand-over point >= g_r
+    # and the table of the inserts before it; the block then runs as consecutive parts, the
+    # slots each part's lookups take from that table tracked.  In rank order, the true (state,
+    # table) from r - 1 confirms the leading parts whose used slots all agree (given an equal
+    # state); the rest of the block is walked again from the exit state of the last confirmed
+    # part, with their writes over the true table, exactly as without speculation.
     g = chain_bounds(n, world)
-    if speculate is None:  # off by default: all-or-nothing acceptance rejects full-size blocks
-        import os
-
+    if speculate is None:  # off by default
         speculate = os.environ.get("LZ77SSS_SPECULATE", "0") == "1"
     spec = speculate and multi and rank > 0 and g[rank] > 0
     t_spec = 0.0
-    spec_state, spec_walked, z = None, False, 0
+    spec_state, parts = None, []  # parts: (entry state, exit state, factors)
+
+    def take():  # the session's last factors, as a device tensor
+        fb = sess.factor_bytes()
+        F = torch.empty(max(fb // 8, 1), dtype=torch.int64, device=dev)
+        if fb:
+            sess.copy_factors(F.data_ptr(), fb)
+        return F[: fb // 8]
+
     if spec:
         ts = time.perf_counter()
         lead0 = g[rank] - spec_lead(n, g, rank)
         _, spec_state = sess.greedy_block(lead0, lead0, 0, False, g[rank], seed=True, **params)
-        if spec_state[0] < g[rank + 1] or rank == world - 1:
-            sess.spec_begin()
-            z, spec_exit = sess.greedy_block(*spec_state, True, g[rank + 1], **params)
-            spec_walked = True
+        spec_state = st = tuple(spec_state)
+        npart = spec_parts()
+        for k in range(npart):
+            e_k = g[rank + 1] if k == npart - 1 else g[rank] + (g[rank + 1] - g[rank]) * (k + 1) // npart
+            if st[0] < e_k or (rank == world - 1 and k == npart - 1):
+                sess.spec_begin(len(parts), spec_state[0])
+                _, st2 = sess.greedy_block(*st, True, e_k, **params)
+                parts.append((st, tuple(st2), take()))
+                st = tuple(st2)
         t_spec = time.perf_counter() - ts
     t_wait = time.perf_counter()
     state, carried = (0, 0, 0), False
-    accepted = None
+    accepted = None  # speculation: the number of parts that stood
     if rank > 0:
         hdr = torch.zeros(4, dtype=torch.int64, device=cdev)
         dist.recv(hdr, rank - 1, group=group)
@@ -374,30 +395,23 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
             dist.recv(tab, rank - 1, group=group)
             if nccl:
                 ready()
-            if spec and spec_walked:
-                ok = sess.spec_resolve(nbytes=tab_bytes, block_start=spec_state[0], device_ptr=tab.data_ptr())
-                accepted = ok and state == tuple(spec_state)
+            if parts:
+                same = state == spec_state
+                accepted = sess.spec_resolve(nbytes=tab_bytes, parts=len(parts) if same else 0,
+                                             device_ptr=tab.data_ptr())
                 if timings is not None:
-                    timings.update(spec_table_ok=ok, spec_state_ok=state == tuple(spec_state))
-                if ok and not accepted:  # the table agreed, the state did not: back to the true table
-                    sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
+                    timings.update(spec_state_ok=same, spec_parts=len(parts))
+                if accepted:
+                    state = parts[accepted - 1][1]
             else:
                 sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
-                if spec:  # the block was covered by the speculated chain: nothing to walk
-                    accepted = state == tuple(spec_state)
             del tab
-        elif spec:
-            accepted = False  # (no carried table: a text too short to speculate on)
-    if accepted:
-        if spec_walked:
-            state, carried = tuple(spec_exit), True
-        else:
-            state = tuple(spec_state)
-    else:
-        z = 0
-        if state[0] < g[rank + 1] or rank == world - 1:
-            z, state = sess.greedy_block(*state, carried, g[rank + 1], **params)
-            carried = True
+    keep = [F for (_, _, F) in parts[: accepted or 0]]  # factors of the confirmed parts
+    F_rest = None
+    if not (parts and accepted == len(parts)) and (state[0] < g[rank + 1] or rank == world - 1):
+        _, state = sess.greedy_block(*state, carried, g[rank + 1], **params)
+        state, carried = tuple(state), True
+        F_rest = take()
     if multi and rank + 1 < world:
         hdr = torch.tensor([state[0], state[1], state[2], int(carried)], dtype=torch.int64, device=cdev)
         dist.send(hdr, rank + 1, group=group)
@@ -410,17 +424,12 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     if timings is not None:
         timings.update(spec_walk=t_spec, chain_wait=t3 - t_wait, spec_accepted=accepted)
     # (4) emission: the blocks' factors gathered in rank order
-    fb = sess.factor_bytes() if z else 0
-    F = torch.empty(max(fb // 8, 1), dtype=torch.int64, device=dev)
-    if fb:
-        sess.copy_factors(F.data_ptr(), fb)
-    F = F[: fb // 8]
+    blocks = keep + ([F_rest] if F_rest is not None else [])
+    F = torch.cat(blocks) if blocks else torch.empty(0, dtype=torch.int64, device=dev)
     if multi:
         F = gather_blocks(F.to(cdev), group).to(dev)
     if timings is not None:
         timings.update(sss=t1 - t0, prepare=t2 - t1, greedy_chain=t3 - t2, emit=time.perf_counter() - t3)
-    # (a rejected or accepted speculation leaves the same factors: the session's buffer holds
-    # the block's walk either way; the spec walk of a rejected block was overwritten by the re-walk)
     if getattr(sess, "pos64", False):
         return F.view(-1, 2)  # (src, len) as uint64 pairs; positions < 2^63
     return F.view(torch.int32).view(-1, 2)

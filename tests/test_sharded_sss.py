@@ -352,7 +352,7 @@ def _resident_worker(rank, world, port, q, T, wide=False, gen=None, env=None, sp
                 # a second step on the same session
                 F2 = SH.factorize_sharded_resident(s, n, rank, world, 0, speculate=speculate)
                 q.put((rank, F.cpu().numpy().astype(np.uint64), bool(torch.equal(F, F2)), sorted(tm),
-                       tm.get("spec_accepted")))
+                       (tm.get("spec_accepted"), tm.get("spec_parts"))))
             else:  # the stream's SHA-256 in the fixture layout (little-endian uint64 pairs)
                 h = hashlib.sha256(F.cpu().numpy().astype("<u8").view(np.uint8)).hexdigest()
                 q.put((rank, int(F.shape[0]), h, sorted(tm), tm.get("spec_accepted"),
@@ -405,27 +405,29 @@ def test_sharded_resident_ranks_on_gpu(lz, orc, world, wide):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,lead", [(2, None), (3, None), (2, 100000), (3, 4096), (2, 1)])
-def test_sharded_resident_speculative_blocks(lz, orc, world, lead):
-    """Speculative chain blocks: every rank > 0 walks its block from a lead-in's
-    exit state and table while the ranks before it work, and keeps it only when the true
-    state and every carried slot its lookups used agree.  The stream equals the one-process
-    stream whatever the lead-in (a lead-in from position 0 -- the default on a text this
-    short -- is the true chain, so those blocks must be accepted; short lead-ins may be
-    rejected and re-walked), and equals the non-speculative run."""
+@pytest.mark.parametrize("world,lead,parts", [(2, None, None), (3, None, None), (2, 100000, None), (3, 4096, 3),
+                                              (2, 1, None), (3, 30000, 1), (2, 200000, 16)])
+def test_sharded_resident_speculative_blocks(lz, orc, world, lead, parts):
+    """Speculative chain blocks: every rank > 0 walks its block, as consecutive
+    parts, from a lead-in's exit state and table while the ranks before it work, and keeps the
+    leading parts all of whose used carried slots agree with the true table (given the true
+    state); the rest is re-walked.  The stream equals the one-process stream whatever the
+    lead-in and the part count (a lead-in from position 0 -- the default on a text this short
+    -- is the true chain, so every part must be accepted; short lead-ins may lose parts), and
+    equals the non-speculative run."""
     T = lz.gen_genome(3 << 20, 1 << 20, 0.001, 29)
     F_ref = orc.factorize(T)[0].astype(np.uint64)
     env = {} if lead is None else {"LZ77SSS_SPEC_LEAD": str(lead)}
+    if parts is not None:
+        env["LZ77SSS_SPEC_PARTS"] = str(parts)
     res = _run_resident(world, T, False, env=env)
-    for rank, F, same, keys, acc in res:
+    for rank, F, same, keys, (acc, npart) in res:
         assert same and {"spec_walk", "chain_wait", "spec_accepted"} <= set(keys)
         assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
-        if rank > 0 and lead is None:
-            assert acc is True
-        if rank > 0 and lead == 1:
-            # a 1-byte lead-in starts from an empty table: the block's first lookups use slots whose
-            # true values it lacks, so the check must reject it (and the re-walk give the stream)
-            assert acc is False
+        if rank > 0:
+            assert npart is not None and 1 <= npart <= (parts or 8) and 0 <= acc <= npart
+            if lead is None:
+                assert acc == npart
     plain = _run_resident(world, T, False, speculate=False)
     assert all(np.array_equal(a[1], b[1]) for a, b in zip(res, plain))
 
