@@ -523,8 +523,14 @@ void engine::build_sa_s(const u8* T) {
                 u32* units = dsb + nseg + 1;
                 k_gather_u32<<<cdiv(mt, 256), 256, 0, st>>>(srt, dpos, mt, it_a);
                 u32* uoff = sa_tmp1.p == srt ? sa_tmp2.get(nseg + 1) : sa_tmp1.get(nseg + 1);
+                // output runs per wave: up to 16, fewer while that leaves under 16 Ki waves -- a
+                // latency chain of wave comparisons per run (rr, 54 K keys: sa_s 1.57 -> 1.34 ms at
+                // 4; genome, millions of tie members: 16, 4 costs +0.4 ms; LZ77SSS_SEGMERGE_OPW forces)
+                u64 opw_cap = 16;
+                while (opw_cap > 4 && mt / opw_cap < 16384) opw_cap /= 2;
+                if (const char* e = std::getenv("LZ77SSS_SEGMERGE_OPW")) opw_cap = std::max<u64>(1, std::strtoull(e, nullptr, 10));
                 for (u64 w = 1; w < maxl; w *= 2) {
-                    const u32 opw = (u32)std::min<u64>(16, 2 * w);  // short output runs: more waves on long segments
+                    const u32 opw = (u32)std::min<u64>(opw_cap, 2 * w);  // short output runs: more waves on long segments
                     // no host read-back: launch for the upper bound cdiv(members, opw) + segments
                     k_seg_units<<<cdiv(nseg + 1, 256), 256, 0, st>>>(dsb, nseg, opw, units);
                     {
