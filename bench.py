@@ -288,7 +288,7 @@ def main():
                 "huffman_container": {"bytes": hbytes, "ms_incl_d2h": round(t_h * 1e3, 3)},
             },
             "roofline": {
-                "kernel": "SSS kernels: k_sss_stream pass 1 .. k_sss_stream re-run (DESIGN.md 4.1)",
+                "kernel": "SSS kernels: k_sss_stream pass 1 .. k_sss_stream re-run + k_blk_seg_tiles/info (DESIGN.md 4.1)",
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
