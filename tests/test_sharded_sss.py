@@ -447,3 +447,52 @@ def test_sharded_resident_u64_past_4gib_hash():
         print(f"rank {rank}: speculative block accepted={acc} times={tm}")
         assert {"emit", "greedy_chain", "prepare", "sss"} <= set(keys)
         assert z == e["z"] and h == e["stream_sha256"]
+
+
+def _plain_after_sharded_worker(q, wide, window):
+    # (its own process, as the rank workers: the pytest process's HIP state stays out of it)
+    import torch
+
+    sys.path.insert(0, str(ROOT / "lz77-sss_amd"))
+    import lz77sss as L
+    import sharded as SH
+
+    torch.zeros(1, device="cuda")
+    T = L.gen_genome(6 << 20, 1 << 20, 0.001, 31)
+    n = T.size
+    with L.Session(n, 0, pos64=wide) as s:
+        s.load(T)
+        F1 = SH.factorize_sharded_resident(s, n, 0, 1, 0).cpu().numpy().astype(np.uint64)
+        if window:
+            os.environ["LZ77SSS_GREEDY_WINDOW"] = window
+        z = s.factorize()
+        F2 = np.asarray(s.factors(z)).astype(np.uint64)
+        os.environ.pop("LZ77SSS_GREEDY_WINDOW", None)
+        F3 = SH.factorize_sharded_resident(s, n, 0, 1, 0).cpu().numpy().astype(np.uint64)
+    q.put((T, F1, F2, F3))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wide,window", [(False, None), (True, None), (False, "1048576"), (True, "1048576")])
+def test_plain_factorize_after_sharded_same_session(lz, orc, wide, window):
+    """A session that ran the resident sharded path (world 1: sss_range, set_sss, prepare,
+    greedy_block) and then a plain factorize -- also in greedy windows, the form a 50 GiB text
+    takes -- and the sharded path again: all three streams equal the oracle's."""
+    import queue
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    p = ctx.Process(target=_plain_after_sharded_worker, args=(qq, wide, window))
+    p.start()
+    try:
+        T, F1, F2, F3 = qq.get(timeout=150)
+    except queue.Empty:
+        p.kill()
+        raise AssertionError(f"worker failed (exit code {p.exitcode})")
+    p.join(60)
+    assert p.exitcode == 0
+    F_ref = orc.factorize64(T)[0] if wide else orc.factorize(T)[0].astype(np.uint64)
+    for F in (F1, F2, F3):
+        assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
