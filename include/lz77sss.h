@@ -120,10 +120,13 @@ int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_
  * interval samples; lz77_sss.hpp:558-709, transform_to_exact/{naive,with_samples,without_samples}.cpp); their sources are
  * the lighter points the range queries find.  LZ77SSS_TRANSF_FULL_SA computes the
  * same lengths from LPF over the full suffix array of the text (csrc/exact.hip; 44 B
- * per character, n < 2^31) with the PSV/NSV source rule.  Requires n < 2^32 - 16. */
+ * per character, n < 2^31) with the PSV/NSV source rule.  The sample-index modes require
+ * n < 2^32 - 16 and fewer than 2^31 samples (z_aprx + n/delta; LZ77SSS_EINVAL otherwise). */
 int lz77sss_factorize_exact_u32(const uint8_t* text, uint64_t n, const lz77sss_params* prm, int transf_mode,
                                 lz77sss_emit_fn emit, void* user);
-/* pos_t = uint64_t form of the exact factorization (same algorithm and limit n < 2^31). */
+/* pos_t = uint64_t form of the exact factorization: the factors are widened to lz77sss_factor64,
+ * the computation runs on a pos_t = uint32_t session, so the limits of the _u32 form apply
+ * (sample-index modes n < 2^32 - 16, FULL_SA n < 2^31). */
 int lz77sss_factorize_exact_u64(const uint8_t* text, uint64_t n, const lz77sss_params* prm, int transf_mode,
                                 lz77sss_emit64_fn emit, void* user);
 
@@ -170,6 +173,12 @@ int lz77sss_session_get_factors64(lz77sss_session* s, lz77sss_factor64* out, uin
  * positions where the decoded text differs from the loaded one (0 = round trip
  * holds), without leaving HBM.  Timed as phase "decode". */
 int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_t cap, uint64_t* mismatches);
+/* Checks the factors of the last factorization against the loaded text without decoding
+ * them (a 50 GiB stream needs no n-sized decode buffers): *bad_positions = the number of
+ * positions whose factor does not reproduce the text (a literal with another byte, a copy
+ * from a position >= its own, a copied byte that differs); 0 <=> decode(F) == T.  Fails
+ * with LZ77SSS_EINVAL when the lengths do not sum to n. */
+int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positions);
 /* Runs only the string-synchronizing-set pass (kernel 1) on the loaded text. */
 int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs);
 /* Copies the sync set of the last sss/factorize call HBM -> host. */

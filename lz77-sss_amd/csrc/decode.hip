@@ -129,4 +129,91 @@ u64 engine::decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* 
     return cmp ? rd1(flags + 2, st) : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Verification of a factor stream against the text it encodes, without decoding it:
+// decode(F) == T holds iff the lengths sum to n and every position p of every factor
+// (start st, source src) satisfies  literal: T[p] == (u8)src;  copy: src < st and
+// T[p] == T[src + (p - st)]  (induction over p: the decoder's out[src + p - st] is
+// out at an earlier position, which equals T there).  So the check reads the text
+// twice (position and source) and needs only the factor starts (8 B per factor), not
+// the 24 B per position of decode_device: a 50 GiB factorization is verified in HBM.
+// One workgroup per VB-position block: the factors covering it are f0..f1 (binary
+// searches of the starts); their in-block starts are marked in LDS and an inclusive
+// max-scan gives every position its factor.
+constexpr u32 VB_T = 256, VB_PER = 16, VB = VB_T * VB_PER;
+__global__ __launch_bounds__(VB_T) void k_verify_blocks(const pos_t* __restrict__ F, const u64* __restrict__ start,
+                                                         u64 nf, u64 n, const u8* __restrict__ T,
+                                                         unsigned long long* __restrict__ bad) {
+    __shared__ u16 fl[VB];
+    __shared__ u64 s_f0;
+    __shared__ u32 s_wmax[VB_T / 64];
+    const u64 b0 = (u64)blockIdx.x * VB;
+    const u64 b1 = min(n, b0 + VB);
+    if (threadIdx.x == 0) {
+        u64 lo = 0, hi = nf;  // last factor with start <= b0
+        while (hi - lo > 1) {
+            const u64 mid = (lo + hi) >> 1;
+            if (start[mid] <= b0) lo = mid; else hi = mid;
+        }
+        s_f0 = lo;
+    }
+    for (u32 k = threadIdx.x; k < VB; k += VB_T) fl[k] = 0;
+    __syncthreads();
+    const u64 f0 = s_f0;
+    // factors starting inside the block: at most VB of them, in order from f0 + 1
+    for (u64 f = f0 + 1 + threadIdx.x; f < nf && start[f] < b1; f += VB_T) fl[start[f] - b0] = (u16)(f - f0);
+    __syncthreads();
+    // inclusive max-scan of fl: VB_PER consecutive entries per thread, then a block scan
+    const u32 base = threadIdx.x * VB_PER;
+    u32 m = 0;
+    for (u32 k = 0; k < VB_PER; k++) m = max(m, (u32)fl[base + k]);  // (fl[0] = 0: f0 covers b0)
+    const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32 incl = m;
+    for (u32 o = 1; o < 64; o <<= 1) {
+        const u32 y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl = max(incl, y);
+    }
+    if (lane == 63) s_wmax[wv] = incl;
+    __syncthreads();
+    u32 carry = 0;
+    for (u32 w = 0; w < wv; w++) carry = max(carry, s_wmax[w]);
+    // exclusive prefix: the waves before this one, then the lanes before this one
+    const u32 ex = (u32)__shfl_up(incl, 1, 64);
+    u32 run = max(carry, lane ? ex : 0u);
+    u32 cnt = 0;
+    for (u32 k = 0; k < VB_PER; k++) {
+        const u64 p = b0 + base + k;
+        run = max(run, (u32)fl[base + k]);
+        if (p >= b1) break;
+        const u64 f = f0 + run;
+        const pos_t src = F[2 * f], len = F[2 * f + 1];
+        const u8 c = T[p];
+        if (len == 0) {
+            cnt += (p != start[f] || c != (u8)src) ? 1u : 0u;
+        } else {
+            const u64 st = start[f];
+            cnt += ((u64)src >= st || T[(u64)src + (p - st)] != c) ? 1u : 0u;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
+    if (lane == 0 && cnt) atomicAdd(bad, (unsigned long long)cnt);
+}
+
+u64 engine::verify_factors(const pos_t* F, u64 nf, u64 n_out, const u8* T) {
+    if (n_out == 0) return nf ? 1 : 0;
+    if (nf == 0) return n_out;
+    u64* len = dec_len64.get(nf + 1);
+    u64* start = dec_start64.get(nf + 1);
+    k_dec_lens<<<cdiv(nf, 256), 256, 0, st>>>(F, nf, len);
+    LZ_HIP(hipMemsetAsync(len + nf, 0, 8, st));
+    excl_sum64(len, start, (u64)0, nf + 1, scan_tmp, st);
+    if (rd1(start + nf, st) != n_out) throw error(LZ77SSS_EINVAL, "factor lengths do not sum to n");
+    unsigned long long* bad = (unsigned long long*)counters64.get(16) + 15;
+    LZ_HIP(hipMemsetAsync(bad, 0, 8, st));
+    const u64 nblk = (n_out + VB - 1) / VB;  // n <= 2^40: fewer than 2^28 blocks
+    k_verify_blocks<<<(unsigned)nblk, VB_T, 0, st>>>(F, start, nf, n_out, T, bad);
+    LZ_HIP(hipGetLastError());
+    return rd1((u64*)bad, st);
+}
+
 }  // namespace LZ_NS

@@ -285,6 +285,11 @@ struct engine64_impl final : lz::engine_if {
         return E.decode_device(F, nf, n_out, d_out, cmp ? E.d_text : nullptr);
     }
     u8* dec_out(u64 n) override { return E.dec_out.get(n); }
+    u64 verify() override {
+        const u64 bad = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text);
+        LZ_HIP(hipStreamSynchronize(E.st));
+        return bad;
+    }
     void sss(u64* size, int* has_runs) override {
         LZ_HIP(hipSetDevice(E.device));
         E.build_sss(E.d_text);
@@ -538,6 +543,23 @@ LZ77SSS_API int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_
         if (E.stats.size() > 18) E.stats[18] = E.dec_rounds;
         if (mismatches) *mismatches = bad;
         if (d_out) LZ_HIP(hipMemcpyAsync(out, d_out, E.n, hipMemcpyDeviceToHost, E.st));
+        LZ_HIP(hipStreamSynchronize(E.st));
+    });
+}
+
+// the factors of the last factorization checked against the loaded text in HBM (csrc/decode.hip
+// verify_factors): the decode round trip without materialising the decoded text
+LZ77SSS_API int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positions) {
+    if (!s || !bad_positions) return LZ77SSS_EINVAL;
+    return guarded([&] {
+        if (s->E64) {
+            LZ_HIP(hipSetDevice(s->E64->device()));
+            *bad_positions = s->E64->verify();
+            return;
+        }
+        lz::engine& E = s->E;
+        LZ_HIP(hipSetDevice(E.device));
+        *bad_positions = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text);
         LZ_HIP(hipStreamSynchronize(E.st));
     });
 }

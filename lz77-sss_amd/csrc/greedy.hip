@@ -2623,6 +2623,17 @@ void engine::spec_begin(int part, u64 base) {
         throw error(LZ77SSS_EINVAL, "speculative block: parts must follow each other from part 0");
     }
     const u64 nw = m / 32 + 1;
+    // every part keeps a snapshot of the whole carried table: on a pos_t = uint64_t session with a
+    // 2^28-slot index that is 2 GiB per part, so the part count is bounded by free HBM (the caller
+    // stops speculating on ENOMEM; the parts walked so far stay valid)
+    const u64 need = (u64)(part + 1) * m * sizeof(pos_t) + (u64)(part + 1) * nw * 4;
+    const u64 have = g_hsave.cap * sizeof(pos_t) + g_hsused.cap * 4;
+    if (need > have) {
+        size_t fr = 0, tot = 0;
+        LZ_HIP(hipMemGetInfo(&fr, &tot));
+        if ((u64)fr < need - have + (1ull << 30))
+            throw error(LZ77SSS_ENOMEM, "speculative block: no HBM left for another part snapshot");
+    }
     pos_t* sv = g_hsave.grow_keep((u64)(part + 1) * m, (u64)part * m, st);
     u32* used = g_hsused.grow_keep((u64)(part + 1) * nw, (u64)part * nw, st);
     LZ_HIP(hipMemcpyAsync(sv + (u64)part * m, g_Hs.p, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));

@@ -887,8 +887,13 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     const u64 za64 = factorize(phr_mode, rk_seed, log2_override, false, LZ77SSS_GREEDY);
     num_fact = 0;
     if (n == 0) return 0;
-    const u32 za = (u32)za64;
     const u32 delta = (u32)std::min<u64>(n / za64, SMPL_MAX_DELTA);
+    // hipcub scans / radix sorts below take int item counts, and the sample offsets are u32:
+    // c <= za + n / delta samples (one per phrase end, one per delta inside a phrase) must stay
+    // below 2^31 (low-compressibility texts past about 2 GiB reach it)
+    if (za64 + n / std::max<u32>(delta, 1) + 1 >= 0x7FFFFFFFull)
+        throw error(LZ77SSS_EINVAL, "exact-smpl: more than 2^31 samples (za + n/delta); text too incompressible");
+    const u32 za = (u32)za64;
     u32* afact = e_afact.get(2 * (u64)za + 2);
     LZ_HIP(hipMemcpyAsync(afact, fact.p, (size_t)za * 8, hipMemcpyDeviceToDevice, st));
     // approximate phrase starts

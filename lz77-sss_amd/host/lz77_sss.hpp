@@ -4,7 +4,7 @@
 //
 // A caller of
 //     lz77_sss<pos_t>::factorize_approximate<greedy, lpf_opt, 512>(T, n, out, {.num_threads = p});
-//     lz77_sss<uint32_t>::factorize_exact<greedy, lpf_opt, without_samples>(T, n, out);
+//     lz77_sss<uint32_t>::factorize_exact<greedy, lpf_opt, with_samples>(T, n, out);
 //     lz77_sss<uint32_t>::decode(fact_it, out_it, n);
 // keeps its code and links against the HIP library instead.  Differences:
 //   * the factorization runs on an MI355X (device `parameters::device`) with the
@@ -33,8 +33,11 @@ enum factorize_mode { greedy_naive, greedy, skip_phrases };            // lz77_s
 enum transform_mode { naive, with_samples, without_samples };          // lz77_sss.hpp:60-64
 
 // Range structures of the reference's exact modes (data_structures/*_range/*.hpp):
-// accepted as template arguments for source compatibility; the device exact
-// path (csrc/exact.hip) does not use them, every choice gives the same lengths.
+// accepted as template arguments for source compatibility.  The device exact-smpl
+// path (csrc/smpl.hip) always builds the default, a decomposed static weighted
+// square grid (decomposed_range.hpp:78-166, static_weighted_square_grid.hpp:67-185);
+// the factor lengths are the canonical greedy LZ77 ones whichever structure is
+// named, the sources are the lighter points that grid's queries find.
 template <typename> struct static_weighted_kd_tree {};
 template <typename> struct static_weighted_square_grid {};
 template <typename> struct static_weighted_striped_square {};
@@ -135,8 +138,11 @@ class lz77_sss {
             check(lz77sss_factorize_approx_u32(reinterpret_cast<const uint8_t*>(input), input_size, &p, emit, &ctx));
     }
 
-    // lz77_sss.hpp:188-200: exact factorization (greedy LZ77 lengths; sources by the
-    // device's PSV/NSV rule, see include/lz77sss.h)
+    // lz77_sss.hpp:188-200: exact factorization.  Every transf_mode of the reference
+    // (naive, with_samples, without_samples, lz77_sss.hpp:616-661) runs the sample-index
+    // transform on the device (csrc/smpl.hip); with_samples adds the Rabin-Karp prefix
+    // fingerprints and the interval samples (transform_to_exact/with_samples.cpp:31-240).
+    // Lengths are the canonical greedy LZ77 ones; see include/lz77sss.h for the sources.
     template <factorize_mode fact_mode = default_fact_mode, phrase_mode phr_mode = default_phr_mode,
               transform_mode transf_mode = default_transf_mode,
               template <typename> typename range_ds_t = default_range_ds_t, uint64_t tau = default_tau,
@@ -144,9 +150,6 @@ class lz77_sss {
     static void factorize_exact(char_t* input, pos_t input_size, output_fnc_t output, parameters params = {}) {
         static_assert(sizeof(char_t) == 1, "byte alphabet only (lz77_sss.hpp:287)");
         static_assert(fact_mode != skip_phrases, "lz77_sss.hpp:333");
-        static_assert(transf_mode != with_samples,
-                      "with_samples needs the reference's sample index, which the device path does not build "
-                      "(the C-ABI returns LZ77SSS_EINVAL); naive / without_samples give the same lengths");
         lz77sss_params p;
         lz77sss_default_params(&p);
         p.phr_mode = static_cast<int32_t>(phr_mode);

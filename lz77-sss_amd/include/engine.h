@@ -239,6 +239,7 @@ struct engine {
     u64 factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int log2_override, bool log);  // csrc/smpl.hip
     void build_interval_samples(smpl_view& V, u64 nn, u64 za);                                         // csrc/smpl.hip
     u64 decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
+    u64 verify_factors(const pos_t* F, u64 nf, u64 n_out, const u8* T);  // csrc/decode.hip
     lce_view view(const u8* T) const;
 };
 

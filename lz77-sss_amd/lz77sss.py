@@ -25,13 +25,16 @@ GREEDY_NAIVE, GREEDY, SKIP_PHRASES = 0, 1, 2                 # enum factorize_mo
 NAIVE, WITH_SAMPLES, WITHOUT_SAMPLES = 0, 1, 2               # enum transform_mode, lz77_sss.hpp:60-64
 FULL_SA = 3                                                    # device extension: LPF over the full suffix array
 DEFAULT_TAU = 512
+OK, EINVAL, ENODEV, EHIP, ENOMEM, ECALLBACK, EINTERNAL = 0, -1, -2, -3, -4, -5, -6  # include/lz77sss.h
 
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("LZ77SSS_LIB", _HERE / "lib" / "liblz77sss_hip.so"))
 
 
 class Lz77SssError(RuntimeError):
-    pass
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code
 
 
 class Params(ctypes.Structure):
@@ -68,6 +71,7 @@ _SYMBOLS = {
     "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
     "lz77sss_decode_u32_device": (ctypes.c_int, [_P, _U64, _P, _U64, ctypes.c_int]),
     "lz77sss_session_decode": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
+    "lz77sss_session_verify": (ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
     "lz77sss_session_create": (ctypes.c_int, [ctypes.c_int, _U64, ctypes.POINTER(_P)]),
     "lz77sss_session_load": (ctypes.c_int, [_P, _P, _U64]),
     "lz77sss_session_factorize": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.POINTER(_U64)]),
@@ -120,7 +124,7 @@ def load_library(path: Path | str | None = None):
 def _check(rc: int):
     if rc != 0:
         msg = load_library().lz77sss_last_error()
-        raise Lz77SssError(f"lz77sss error {rc}: {msg.decode() if msg else ''}")
+        raise Lz77SssError(f"lz77sss error {rc}: {msg.decode() if msg else ''}", rc)
 
 
 def _as_u8(text) -> np.ndarray:
@@ -274,6 +278,13 @@ class Session:
         _check(load_library().lz77sss_session_decode(self._h, buf.ctypes.data_as(_P) if out else None,
                                                      self.n if out else 0, ctypes.byref(m) if verify else None))
         return (buf[:self.n] if out else None), (m.value if verify else None)
+
+    def verify(self) -> int:
+        """Positions of the loaded text that the last factorization does not reproduce, checked in
+        HBM without decoding (lz77sss_session_verify; 0 <=> decode(F) == T; any size)."""
+        b = _U64()
+        _check(load_library().lz77sss_session_verify(self._h, ctypes.byref(b)))
+        return b.value
 
     def sss(self):
         s, r = _U64(), ctypes.c_int()

@@ -175,33 +175,6 @@ class HipBlocks:
         self.s.close()
 
 
-class OracleBlocks:
-    """The same interface on the CPU oracle (tests; oracle.hpp greedy_block)."""
-
-    def __init__(self, text, n: int, pos64: bool = False, **params):
-        import oracle
-
-        self.o = oracle
-        self.T = np.ascontiguousarray(text)
-        self.wide = pos64
-        self.params = params
-
-    def prepare(self, S, runs: bool) -> int:
-        want, _ = self.o.sss(self.T)
-        assert np.array_equal(np.asarray(S, np.uint64), want.astype(np.uint64)), "gathered sync set differs"
-        return 0
-
-    def run(self, state, end: int, table):
-        start, idxpos, _ = state
-        dt = np.uint64 if self.wide else np.uint32
-        tab = None if table is None else np.frombuffer(np.ascontiguousarray(table).tobytes(), dt)
-        F, (es, ei), tab = self.o.greedy_block(self.T, start, idxpos, end, tab, wide=self.wide, **self.params)
-        return F, (es, ei, 0), tab.view(np.uint8)
-
-    def close(self):
-        pass
-
-
 def _send_bytes(arr: np.ndarray, dst: int, device=None, group=None):
     import torch
     import torch.distributed as dist
@@ -230,7 +203,7 @@ def _recv_bytes(src: int, device=None, group=None) -> np.ndarray:
 def factorize_sharded(text, n: int, rank: int, world: int, device: int | None = None, blocks=None, group=None,
                       sss_compute: Callable | None = None, timings: dict | None = None):
     """The 3-approximation of T (uint64 (z, 2) factors, on every rank) computed with `world`
-    ranks.  `blocks` (HipBlocks / OracleBlocks) holds the whole text; defaults to HipBlocks
+    ranks.  `blocks` (HipBlocks, or the tests' oracle form with the same interface) holds the whole text; defaults to HipBlocks
     on `device` (rank if None).  Call on every rank of the process group."""
     import time
 
@@ -259,7 +232,9 @@ def factorize_sharded(text, n: int, rank: int, world: int, device: int | None = 
         table = _recv_bytes(rank - 1, comm_dev, group)
         if table.size == 0:  # no block before this one ran: nothing inserted yet
             table = None
-    if state[0] < g[rank + 1] or rank == world - 1:
+    # walk only while the chain has not passed this block: g[world] == n, so a chain that an earlier
+    # block's last factor carried to n (a text ending in a long repeat) ends without a last walk
+    if state[0] < g[rank + 1]:
         F, ex, table = blocks.run(state, g[rank + 1], table)
     else:  # an earlier block's last factor covered this whole block: pass the state on
         F, ex = np.zeros((0, 2), np.uint64), state
@@ -370,6 +345,8 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
         return F[: fb // 8]
 
     if spec:
+        import lz77sss as L
+
         ts = time.perf_counter()
         lead0 = g[rank] - spec_lead(n, g, rank)
         _, spec_state = sess.greedy_block(lead0, lead0, 0, False, g[rank], seed=True, **params)
@@ -377,8 +354,13 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
         npart = spec_parts()
         for k in range(npart):
             e_k = g[rank + 1] if k == npart - 1 else g[rank] + (g[rank + 1] - g[rank]) * (k + 1) // npart
-            if st[0] < e_k or (rank == world - 1 and k == npart - 1):
-                sess.spec_begin(len(parts), spec_state[0])
+            if st[0] < e_k:
+                try:
+                    sess.spec_begin(len(parts), spec_state[0])
+                except L.Lz77SssError as err:  # no HBM for another part snapshot: stop speculating
+                    if err.code != L.ENOMEM:
+                        raise
+                    break
                 _, st2 = sess.greedy_block(*st, True, e_k, **params)
                 parts.append((st, tuple(st2), take()))
                 st = tuple(st2)
@@ -408,7 +390,7 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
             del tab
     keep = [F for (_, _, F) in parts[: accepted or 0]]  # factors of the confirmed parts
     F_rest = None
-    if not (parts and accepted == len(parts)) and (state[0] < g[rank + 1] or rank == world - 1):
+    if not (parts and accepted == len(parts)) and state[0] < g[rank + 1]:
         _, state = sess.greedy_block(*state, carried, g[rank + 1], **params)
         state, carried = tuple(state), True
         F_rest = take()

@@ -31,15 +31,46 @@ static int run(int nseeds) {
             std::printf("seed %d: round trip FAILED\n", seed);
             return 1;
         }
-        // exact mode, as tests/test_lz77_sss.cpp:95-133 of the reference (round trip only)
+        // exact mode, as tests/test_lz77_sss.cpp:95-133 of the reference (round trip only), for
+        // every transform_mode of lz77_sss.hpp:60-64 (with_samples: configs[4]); the lengths are the
+        // canonical greedy LZ77 ones, so all three streams have the same factor count
+        size_t zx[3] = {0, 0, 0};
         std::vector<typename lz::factor> FX;
+        auto check_exact = [&](int k, const char* name) -> int {
+            std::string DX;
+            lz::decode(FX.begin(), std::back_inserter(DX), (pos_t)n);
+            if (DX != T || FX.size() > F.size()) {
+                std::printf("seed %d: exact %s round trip FAILED\n", seed, name);
+                return 1;
+            }
+            zx[k] = FX.size();
+            FX.clear();
+            return 0;
+        };
+        auto sink = [&](typename lz::factor f) { FX.push_back(f); };
         lz::template factorize_exact<greedy, lpf_opt, without_samples, decomposed_semi_dynamic_square_grid>(
-            T.data(), (pos_t)n, [&](typename lz::factor f) { FX.push_back(f); });
-        std::string DX;
-        lz::decode(FX.begin(), std::back_inserter(DX), (pos_t)n);
-        if (DX != T || FX.size() > F.size()) {
-            std::printf("seed %d: exact round trip FAILED\n", seed);
+            T.data(), (pos_t)n, sink);
+        if (check_exact(0, "without_samples")) return 1;
+        lz::template factorize_exact<greedy, lpf_opt, with_samples>(T.data(), (pos_t)n, sink);
+        if (check_exact(1, "with_samples")) return 1;
+        lz::template factorize_exact<greedy, lpf_opt, naive, decomposed_static_weighted_kd_tree>(T.data(), (pos_t)n,
+                                                                                               sink);
+        if (check_exact(2, "naive")) return 1;
+        if (zx[0] != zx[1] || zx[0] != zx[2]) {
+            std::printf("seed %d: exact factor counts differ across transform modes\n", seed);
             return 1;
+        }
+        // LPF/LNF phrases (configs[2], lz77_sss.hpp:384-396) and the skip_phrases stream
+        if constexpr (sizeof(pos_t) == 4) {
+            std::vector<typename lz::factor> FL;
+            lz::template factorize_approximate<greedy, lpf_lnf_opt>(T.data(), (pos_t)n,
+                                                                    [&](typename lz::factor f) { FL.push_back(f); });
+            std::string DL;
+            lz::decode(FL.begin(), std::back_inserter(DL), (pos_t)n);
+            if (DL != T) {
+                std::printf("seed %d: lpf_lnf_opt round trip FAILED\n", seed);
+                return 1;
+            }
         }
         // the factor stream form (lz77_sss.hpp:149-173): write and read back
         std::stringstream ss;
@@ -51,7 +82,7 @@ static int run(int nseeds) {
             if (g.src != f.src || g.len != f.len) return 1;
         }
         std::printf("pos_t=%zu seed %d: n=%lld z=%zu z_exact=%zu ok\n", 8 * sizeof(pos_t), seed, (long long)n, F.size(),
-                    FX.size());
+                    zx[0]);
     }
     return 0;
 }

@@ -45,6 +45,24 @@ def test_golden_intermediates(session, name):
     assert np.array_equal(s.lpf(), g["lpf"])
 
 
+@pytest.mark.parametrize("name", golden_names())
+def test_verify_factors_in_hbm(session, name):
+    """lz77sss_session_verify (decode.hip k_verify_blocks): 0 bad positions for the golden stream;
+    after the text in HBM is changed at one position (the factors kept) the check reports it."""
+    g = load_golden(name)
+    T = g["text"]
+    s, F = run(session, T)
+    assert s.verify() == 0
+    if T.size:
+        for p in {0, T.size // 2, T.size - 1}:
+            T2 = T.copy()
+            T2[p] ^= 0x5A
+            s.load(T2)
+            assert s.verify() >= 1, p
+        s.load(T)
+        assert s.verify() == 0
+
+
 @pytest.mark.parametrize("seed", range(1, 17))
 def test_c1_seeds_vs_oracle(session, orc, lz, seed):
     """Config C1: random_repetitive_string(10^4, 2·10^5), p = 1 stream."""

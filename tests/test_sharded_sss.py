@@ -231,6 +231,7 @@ def _fact_worker(rank, world, port, q, use_gpu, T, wide):
     sys.path.insert(0, str(ROOT / "oracle"))
     sys.path.insert(0, str(ROOT / "tests"))
     import sharded as SH
+    from oracle_blocks import OracleBlocks
     from test_sharded_sss import _oracle_block
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -240,7 +241,7 @@ def _fact_worker(rank, world, port, q, use_gpu, T, wide):
             F = SH.factorize_sharded(T, T.size, rank, world, device=0, blocks=blocks)
             blocks.close()
         else:
-            blocks = SH.OracleBlocks(T, T.size, pos64=wide)
+            blocks = OracleBlocks(T, T.size, pos64=wide)
             F = SH.factorize_sharded(T, T.size, rank, world, blocks=blocks, sss_compute=_oracle_block)
         q.put((rank, F))
     finally:
@@ -274,6 +275,27 @@ def test_gloo_sharded_factorization_oracle_blocks(world, wide):
     T = lz77sss.gen_random_repetitive(60000, 60000, 11)
     F_ref = oracle.factorize64(T)[0] if wide else oracle.factorize(T)[0].astype(np.uint64)
     for _, F in _run_fact_ranks(world, False, T, wide):
+        assert np.array_equal(F, F_ref)
+
+
+def _tail_repeat_text(n: int = 60000):
+    """A text whose second half is a copy of the first: the chain's last factor starts in the
+    first rank's block and reaches n, so the last rank receives a state already at n."""
+    import lz77sss
+
+    h = lz77sss.gen_random_repetitive(n // 2, n // 2, 13)
+    return np.concatenate([h, h])
+
+
+def test_gloo_sharded_factorization_tail_repeat():
+    """a last rank whose incoming chain state is already n must not walk (greedy_block
+    rejects start >= end) -- the concatenation still equals the one-process stream."""
+    import oracle
+
+    T = _tail_repeat_text()
+    F_ref = oracle.factorize(T)[0].astype(np.uint64)
+    assert int(F_ref[-1, 1]) >= T.size // 2 - 64  # one factor covers (nearly) the whole copy
+    for _, F in _run_fact_ranks(2, False, T):
         assert np.array_equal(F, F_ref)
 
 
@@ -402,6 +424,17 @@ def test_sharded_resident_ranks_on_gpu(lz, orc, world, wide):
     for _, F, same, keys, _acc in _run_resident(world, T, wide):
         assert same and {"emit", "greedy_chain", "prepare", "sss"} <= set(keys)
         assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("speculate", [False, True])
+def test_sharded_resident_tail_repeat(lz, orc, speculate):
+    """ADVICE r3 on the device path: 2 ranks, the chain reaches n inside rank 0's block, so rank 1
+    must not walk (with and without the speculative parts)."""
+    T = _tail_repeat_text(1 << 20)
+    F_ref = orc.factorize(T)[0].astype(np.uint64)
+    for _, F, same, _keys, _acc in _run_resident(2, T, False, speculate=speculate):
+        assert same and F.shape == F_ref.shape and np.array_equal(F, F_ref)
 
 
 @pytest.mark.gpu
