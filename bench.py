@@ -64,16 +64,26 @@ def aggregate(dt_local: float, n_per_rank: int, world: int, dist=None, device="c
     return dt, world * n_per_rank / dt / 1e6
 
 
-def pmc_traffic(workload: str, n: int):
-    """Per-launch HBM bytes of k_sss_stream from profiles/*_pmc_sss.json (rocprofv3 --pmc passes)."""
+# the SSS kernel set the roofline covers; a PMC summary counts only if it measured
+# all of them (older summaries predate k_sss_runs and cover a different kernel sequence)
+SSS_KERNELS = ("k_sss_stream<false, true>", "k_sss_runs", "k_q_anchors", "k_sss_stream<true, false>")
+
+
+def pmc_traffic(workload: str, n: int, mode: str = "approx"):
+    """Per-call HBM bytes of the SSS kernels from profiles/*_pmc_sss.json (rocprofv3 --pmc passes), for
+    this workload, size and mode (a summary without "mode" is a 3-aprx one), measured over the current
+    kernel set; None when no such summary exists."""
     best = None
     for p in sorted((ROOT / "profiles").glob("*_pmc_sss.json")):
         try:
             d = json.loads(p.read_text())
         except (OSError, ValueError):
             continue
-        if d.get("workload") == workload and int(d.get("n", -1)) == n:
-            best = d
+        if d.get("workload") != workload or int(d.get("n", -1)) != n or d.get("mode", "approx") != mode:
+            continue
+        if not all(any(k in name for name in d.get("fetch_by_kernel_kib", {})) for k in SSS_KERNELS):
+            continue
+        best = d
     return None if best is None else best.get("hbm_bytes_per_launch")
 
 
@@ -294,7 +304,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(args.workload, n),
+                "traffic": pmc_traffic(args.workload, n, "exact" if exact else "approx"),
                 "algorithmic_bytes_per_launch": int(bytes_launch),
                 "avg_launch_ms": round(avg_ms, 4),
             },

@@ -105,8 +105,8 @@ int lz77sss_factorize_approx_u32(const uint8_t* text, uint64_t n, const lz77sss_
 /* The same with pos_t = uint64_t: any n up to 2^40 (texts past 2^32 - 16 bytes need this
  * one).  The gap index is sized by the reference's formula for 8-byte entries
  * (rolling_hash_index_107.hpp:59-70), so the stream is the reference's pos_t = uint64_t
- * stream, which differs from the uint32_t one in general.  phr_mode: lpf_opt or
- * lpf_naive (the LPF/LNF modes are built for uint32_t only). */
+ * stream, which differs from the uint32_t one in general.  Every phr_mode (lpf_naive,
+ * lpf_lnf_naive, lpf_opt, lpf_lnf_opt). */
 int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_params* prm,
                                  lz77sss_emit64_fn emit, void* user);
 
@@ -152,7 +152,7 @@ typedef struct lz77sss_session lz77sss_session;
  * n <= 2^32 - 16). */
 int lz77sss_session_create(int device, uint64_t max_n, lz77sss_session** out);
 /* A pos_t = uint64_t session (lz77_sss<uint64_t>): any n up to 2^40.  Supports load,
- * gen_genome, factorize (lpf_opt / lpf_naive, greedy / skip_phrases), get_factors64,
+ * gen_genome, factorize (every phr_mode; greedy / skip_phrases), verify, get_factors64,
  * decode, sss, get_sss64, get_sa_s, get_lpf64, phase_times, stats, sss_kernel_time;
  * the 32-bit accessors and the exact / LNF / container entry points return LZ77SSS_EINVAL. */
 int lz77sss_session_create64(int device, uint64_t max_n, lz77sss_session** out);

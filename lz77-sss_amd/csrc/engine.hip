@@ -143,12 +143,8 @@ void engine::prepare_phrases(int phr_mode, bool external_sss) {
         trace("lpf");
     } else {
         if (external_sss) throw error(LZ77SSS_EINVAL, "an external sync set needs phr_mode lpf_opt or lpf_naive");
-#ifdef LZ_POS64
-        throw error(LZ77SSS_EINVAL, "LPF/LNF phrase modes are built for pos_t = uint32_t only");
-#else
         build_lpf_lnf(phr_mode == LZ77SSS_LPF_LNF_OPT ? 1 : 0);
         trace("lpf_lnf");
-#endif
     }
 }
 

@@ -25,7 +25,7 @@
 
 #include <hipcub/hipcub.hpp>
 
-namespace lz {
+namespace LZ_NS {
 
 __global__ void k_reverse(const u8* __restrict__ T, u64 n, u8* __restrict__ R) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -61,22 +61,25 @@ __global__ void k_pnv(const u32* __restrict__ SA, u32 s, sa_levels M, int want_m
 }
 
 // candidate record per (sync index, side): valid, diag, end, beg, src
+// (positions are pos_t: the pos_t = uint64_t build serves lz77_sss<uint64_t>::factorize_approximate
+// <greedy, lpf_lnf_opt>, lz77_sss.hpp:384-396 instantiated with either pos_t)
 constexpr int AREC = 5;
 __global__ void k_all_candidates(lce_view L, const u32* __restrict__ SA, const u32* __restrict__ PV,
-                                 const u32* __restrict__ NV, int lnf, int opt, u32* __restrict__ rec) {
+                                 const u32* __restrict__ NV, int lnf, int opt, pos_t* __restrict__ rec) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const u32 s = L.s;
     if (i >= s) return;
-    const u32 Si = L.S[i], r = L.ISA[i];
+    const pos_t Si = L.S[i];
+    const u32 r = L.ISA[i];
     for (int side = 0; side < 2; side++) {
-        u32* o = rec + (2 * i + side) * AREC;
+        pos_t* o = rec + (2 * i + side) * AREC;
         const u32 nb = side ? NV[r] : PV[r];
         if (nb == s) { o[0] = 0; continue; }
-        u32 src = L.S[SA[nb]], beg = Si;
-        const u32 diag = lnf ? src - beg : beg - src;
-        const u32 end = Si + (u32)dev_lce(L, src, Si);
+        pos_t src = L.S[SA[nb]], beg = Si;
+        const pos_t diag = lnf ? src - beg : beg - src;
+        const pos_t end = Si + (pos_t)dev_lce(L, src, Si);
         if (opt && src != 0 && Si != 0) {
-            const u32 l = dev_lce_left(L.T, L.R, src - 1, Si - 1, 0xFFFFFFFFu);
+            const pos_t l = dev_lce_left(L.T, L.R, src - 1, Si - 1, POS_NONE);
             beg -= l;
             src -= l;
         }
@@ -87,16 +90,16 @@ __global__ void k_all_candidates(lce_view L, const u32* __restrict__ SA, const u
         o[4] = src;
     }
 }
-__global__ void k_side_flags(const u32* __restrict__ rec, u32 s, int side, u32* __restrict__ f) {
+__global__ void k_side_flags(const pos_t* __restrict__ rec, u32 s, int side, u32* __restrict__ f) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < s) f[i] = rec[(2 * i + side) * AREC] == 1u;
 }
-__global__ void k_side_compact(const u32* __restrict__ rec, const u32* __restrict__ S, u32 s, int side,
-                               const u32* __restrict__ off, u32* __restrict__ V, u32* __restrict__ bV,
-                               u32* __restrict__ dV, u32* __restrict__ eV) {
+__global__ void k_side_compact(const pos_t* __restrict__ rec, const pos_t* __restrict__ S, u32 s, int side,
+                               const u32* __restrict__ off, u32* __restrict__ V, pos_t* __restrict__ bV,
+                               pos_t* __restrict__ dV, pos_t* __restrict__ eV) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= s) return;
-    const u32* r = rec + (2 * i + side) * AREC;
+    const pos_t* r = rec + (2 * i + side) * AREC;
     if (r[0] != 1u) return;
     const u32 k = off[i];
     V[k] = (u32)i;
@@ -104,7 +107,7 @@ __global__ void k_side_compact(const u32* __restrict__ rec, const u32* __restric
     dV[k] = r[1];
     eV[k] = r[2];
 }
-__global__ void k_diag_change(const u32* __restrict__ dV, u32 nv, u32* __restrict__ chg) {
+__global__ void k_diag_change(const pos_t* __restrict__ dV, u32 nv, u32* __restrict__ chg) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < nv) chg[k] = (k == 0 || dV[k] != dV[k - 1]) ? 1u : 0u;
 }
@@ -113,14 +116,14 @@ __global__ void k_run_starts(const u32* __restrict__ chg, const u32* __restrict_
     if (k < nv && chg[k]) rstart[rid[k] - 1] = (u32)k;
 }
 // next pushed candidate after k (nv = none)
-__global__ void k_stream_next(const u32* __restrict__ bV, const u32* __restrict__ eV, const u32* __restrict__ rid,
+__global__ void k_stream_next(const pos_t* __restrict__ bV, const pos_t* __restrict__ eV, const u32* __restrict__ rid,
                               const u32* __restrict__ rstart, u32 nruns, u32 nv, u32* __restrict__ nxt) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > nv) return;
     if (k == nv) { nxt[nv] = nv; return; }
     const u32 nd = rid[k] < nruns ? rstart[rid[k]] : nv;  // first later candidate on another diagonal
     u32 lo = (u32)k + 1, hi = nd;                          // first one starting at or after end(k)
-    const u32 e = eV[k];
+    const pos_t e = eV[k];
     while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
         if (bV[mid] < e) lo = mid + 1; else hi = mid;
@@ -143,17 +146,17 @@ __global__ void k_mark_nodes(const u32* __restrict__ C, u32 cnt, u32 term, u32* 
     if (m < cnt && C[m] < term) mark[C[m]] = 1;
 }
 // pushed phrase of stream candidate k -> sequence slot (forward coordinates)
-__global__ void k_stream_emit(const u32* __restrict__ rec, const u32* __restrict__ V, const u32* __restrict__ mark,
-                              u32 nv, int side, int lnf, u32 N, u64 slot_base, u32* __restrict__ slots,
+__global__ void k_stream_emit(const pos_t* __restrict__ rec, const u32* __restrict__ V, const u32* __restrict__ mark,
+                              u32 nv, int side, int lnf, pos_t N, u64 slot_base, pos_t* __restrict__ slots,
                               u32* __restrict__ sflag) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nv || !mark[k]) return;
     const u32 i = V[k];
-    const u32* r = rec + (2 * (u64)i + side) * AREC;
-    u32 b = r[3], e = r[2], sr = r[4];
+    const pos_t* r = rec + (2 * (u64)i + side) * AREC;
+    pos_t b = r[3], e = r[2], sr = r[4];
     if (lnf) {  // reversed coordinates -> forward (lpf_lnf.cpp: n - end, n - beg, n - (src + len))
-        const u32 len = e - b;
-        const u32 fb = N - e, fe = N - b, fs = N - (sr + len);
+        const pos_t len = e - b;
+        const pos_t fb = N - e, fe = N - b, fs = N - (sr + len);
         b = fb;
         e = fe;
         sr = fs;
@@ -164,19 +167,26 @@ __global__ void k_stream_emit(const u32* __restrict__ rec, const u32* __restrict
     slots[3 * slot + 2] = sr;
     sflag[slot] = 1;
 }
-__global__ void k_slot_compact(const u32* __restrict__ slots, const u32* __restrict__ sflag, const u32* __restrict__ off,
-                               u64 nslots, u32* __restrict__ P, u64* __restrict__ keys, u32* __restrict__ vals) {
+// sort keys of the merged phrases: (beg asc, end desc), stable -> push order.  32-bit
+// positions pack both into one key; 64-bit ones are sorted twice (~end, then beg: LSD order)
+__global__ void k_slot_compact(const pos_t* __restrict__ slots, const u32* __restrict__ sflag, const u32* __restrict__ off,
+                               u64 nslots, pos_t* __restrict__ P, u64* __restrict__ keys, u32* __restrict__ vals) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nslots || !sflag[t]) return;
     const u32 o = off[t];
-    const u32 b = slots[3 * t], e = slots[3 * t + 1];
+    const pos_t b = slots[3 * t], e = slots[3 * t + 1];
     P[3 * (u64)o] = b;
     P[3 * (u64)o + 1] = e;
     P[3 * (u64)o + 2] = slots[3 * t + 2];
-    keys[o] = ((u64)b << 32) | (u64)(0xFFFFFFFFu - e);  // beg asc, end desc; stable -> push order
+    if constexpr (sizeof(pos_t) == 4) keys[o] = ((u64)b << 32) | (u64)(0xFFFFFFFFu - e);
+    else keys[o] = ~(u64)e;
     vals[o] = o;
 }
-__global__ void k_gather3(const u32* __restrict__ P, const u32* __restrict__ idx, u32 p, u32* __restrict__ Q) {
+__global__ void k_beg_keys(const pos_t* __restrict__ P, const u32* __restrict__ idx, u32 p, u64* __restrict__ keys) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < p) keys[t] = P[3 * (u64)idx[t]];
+}
+__global__ void k_gather3(const pos_t* __restrict__ P, const u32* __restrict__ idx, u32 p, pos_t* __restrict__ Q) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= p) return;
     const u32 j = idx[t];
@@ -184,15 +194,21 @@ __global__ void k_gather3(const u32* __restrict__ P, const u32* __restrict__ idx
     Q[3 * t + 1] = P[3 * (u64)j + 1];
     Q[3 * t + 2] = P[3 * (u64)j + 2];
 }
-// selection: pm[k] = (end, first index) max over [0, k]
-__global__ void k_end_keys(const u32* __restrict__ Q, u32 p, u64* __restrict__ ek) {
-    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < p) ek[t] = ((u64)Q[3 * t + 1] << 32) | (u64)(0xFFFFFFFFu - (u32)t);
-}
-struct max64 {
-    __device__ __forceinline__ u64 operator()(const u64& a, const u64& b) const { return a > b ? a : b; }
+// selection: pm[k] = (end, first index) max over [0, k]; the larger end wins, ties the smaller index
+struct end_key {
+    pos_t e;
+    u32 t;
 };
-__device__ __forceinline__ u32 first_beg_after(const u32* Q, u32 p, u32 e) {  // first t with beg > e
+struct end_max {
+    __device__ __forceinline__ end_key operator()(const end_key& a, const end_key& b) const {
+        return (a.e > b.e || (a.e == b.e && a.t < b.t)) ? a : b;
+    }
+};
+__global__ void k_end_keys(const pos_t* __restrict__ Q, u32 p, end_key* __restrict__ ek) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < p) ek[t] = end_key{Q[3 * t + 1], (u32)t};
+}
+__device__ __forceinline__ u32 first_beg_after(const pos_t* Q, u32 p, pos_t e) {  // first t with beg > e
     u32 lo = 0, hi = p;
     while (lo < hi) {
         const u32 mid = (lo + hi) >> 1;
@@ -200,43 +216,42 @@ __device__ __forceinline__ u32 first_beg_after(const u32* Q, u32 p, u32 e) {  //
     }
     return lo;
 }
-__global__ void k_select_next(const u32* __restrict__ Q, const u64* __restrict__ pm, u32 p, u32* __restrict__ nxt,
+__global__ void k_select_next(const pos_t* __restrict__ Q, const end_key* __restrict__ pm, u32 p, u32* __restrict__ nxt,
                               u32* __restrict__ X) {
     const u64 c = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (c > p) return;
     if (c == p) { nxt[p] = p; return; }
-    const u32 ec = Q[3 * c + 1];
+    const pos_t ec = Q[3 * c + 1];
     const u32 x = first_beg_after(Q, p, ec);
     X[c] = x;
-    const u64 best = pm[x - 1];  // x > c >= 0 since beg_c < end_c
-    const u32 eb = (u32)(best >> 32), m = 0xFFFFFFFFu - (u32)best;
-    nxt[c] = eb > ec ? m : x;
+    const end_key best = pm[x - 1];  // x > c >= 0 since beg_c < end_c
+    nxt[c] = best.e > ec ? best.t : x;
 }
 // i_T of the selection loop along the chain: j_{t+1} = max(j_t, X(c_t) - t - 1)
 __global__ void k_window_terms(const u32* __restrict__ chain, const u32* __restrict__ X, u32 len, int64_t* __restrict__ y) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < len) y[t] = (int64_t)X[chain[t]] - (int64_t)t - 1;
 }
-__global__ void k_first_ge_end0(const u32* __restrict__ Q, u32 p, u32* __restrict__ out) {
+__global__ void k_first_ge_end0(const pos_t* __restrict__ Q, u32 p, u32* __restrict__ out) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     block_min(out, t >= 1 && t < p && Q[3 * t + 1] >= Q[1] ? (u32)t : 0xFFFFFFFFu);
 }
 // trimmed output phrases along the selection chain
-__global__ void k_select_emit(const u32* __restrict__ Q, const u32* __restrict__ chain, u32 len,
-                              u32* __restrict__ outP, u32* __restrict__ keep) {
+__global__ void k_select_emit(const pos_t* __restrict__ Q, const u32* __restrict__ chain, u32 len,
+                              pos_t* __restrict__ outP, u32* __restrict__ keep) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= len) return;
     const u32 c = chain[t];
-    const u32 b = Q[3 * c];
-    u32 e = Q[3 * c + 1];
-    if (t + 1 < len) e = min(e, Q[3 * chain[t + 1]]);
+    const pos_t b = Q[3 * (u64)c];
+    pos_t e = Q[3 * (u64)c + 1];
+    if (t + 1 < len) e = min(e, Q[3 * (u64)chain[t + 1]]);
     outP[3 * t] = b;
     outP[3 * t + 1] = e;
-    outP[3 * t + 2] = Q[3 * c + 2];
+    outP[3 * t + 2] = Q[3 * (u64)c + 2];
     keep[t] = (t + 1 == len || e > b) ? 1u : 0u;
 }
-__global__ void k_compact_keep(const u32* __restrict__ P, const u32* __restrict__ keep, const u32* __restrict__ off,
-                               u32 len, u32* __restrict__ out) {
+__global__ void k_compact_keep(const pos_t* __restrict__ P, const u32* __restrict__ keep, const u32* __restrict__ off,
+                               u32 len, pos_t* __restrict__ out) {
     const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= len || !keep[t]) return;
     const u32 o = off[t];
@@ -286,7 +301,7 @@ void engine::path_marks(u32 m, u32* nxt0, u32* marks) {
 }
 
 // the pushed phrases of one sync-index pass (LNF on the reversed text: lnf = 1)
-void engine::all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slots, u32* sflag) {
+void engine::all_phrases(const u8* T, int lnf, int opt, u64 slot_base, pos_t* slots, u32* sflag) {
     if (s == 0) return;
     const unsigned g = cdiv(s, 256);
     sa_levels M{};
@@ -300,7 +315,7 @@ void engine::all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slot
         M.nlev = lv + 1;
     }
     k_pnv<<<g, 256, 0, st>>>(SA.p, s, M, lnf, PSV.get(s), NSV.get(s));
-    u32* rec = cand.get((u64)s * 2 * AREC);
+    pos_t* rec = cand.get((u64)s * 2 * AREC);
     k_all_candidates<<<g, 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, lnf, opt, rec);
     for (int side = 0; side < 2; side++) {
         u32* f = u32c.get(s + 1);
@@ -309,9 +324,9 @@ void engine::all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slot
         const u32 nv = xscan(f, off, s, scan_tmp, st);
         if (!nv) continue;
         u32* V = l_V.get(nv + 1);
-        u32* bV = l_b.get(nv + 1);
-        u32* dV = l_d.get(nv + 1);
-        u32* eV = l_e.get(nv + 1);
+        pos_t* bV = l_b.get(nv + 1);
+        pos_t* dV = l_d.get(nv + 1);
+        pos_t* eV = l_e.get(nv + 1);
         k_side_compact<<<g, 256, 0, st>>>(rec, S.p, s, side, off, V, bV, dV, eV);
         u32* chg = u32c.get(nv + 1);
         u32* rid = u32d.get(nv + 1);
@@ -329,7 +344,7 @@ void engine::all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slot
         k_stream_next<<<cdiv(nv + 1, 256), 256, 0, st>>>(bV, eV, rid, rstart, nruns, nv, nxt);
         u32* marks = u32e.get(nv + 1);
         path_marks(nv + 1, nxt, marks);
-        k_stream_emit<<<cdiv(nv, 256), 256, 0, st>>>(rec, V, marks, nv, side, lnf, (u32)n, slot_base, slots, sflag);
+        k_stream_emit<<<cdiv(nv, 256), 256, 0, st>>>(rec, V, marks, nv, side, lnf, (pos_t)n, slot_base, slots, sflag);
         LZ_HIP(hipGetLastError());
     }
 }
@@ -349,7 +364,7 @@ void engine::build_lpf_lnf(int opt) {
     timer.mark("lnf_structures");
     const u64 s_rev = s;
     u32* sf_l = l_sflag_lnf.get(2 * s_rev + 1);
-    u32* sl_l = l_slots_lnf.get(3 * (2 * s_rev + 1));
+    pos_t* sl_l = l_slots_lnf.get(3 * (2 * s_rev + 1));
     LZ_HIP(hipMemsetAsync(sf_l, 0, (2 * s_rev + 1) * 4, st));
     all_phrases(d_text_rev, 1, opt, 0, sl_l, sf_l);
     timer.mark("lnf_phrases");
@@ -360,11 +375,11 @@ void engine::build_lpf_lnf(int opt) {
     timer.mark("lpf_structures");
     const u64 nsl = 2 * s_rev + 2 * (u64)s;
     u32* sflag = l_sflag.get(nsl + 1);
-    u32* slots = l_slots.get(3 * (nsl + 1));
+    pos_t* slots = l_slots.get(3 * (nsl + 1));
     LZ_HIP(hipMemsetAsync(sflag, 0, (nsl + 1) * 4, st));
     if (s_rev) {
         LZ_HIP(hipMemcpyAsync(sflag, sf_l, 2 * s_rev * 4, hipMemcpyDeviceToDevice, st));
-        LZ_HIP(hipMemcpyAsync(slots, sl_l, 3 * 2 * s_rev * 4, hipMemcpyDeviceToDevice, st));
+        LZ_HIP(hipMemcpyAsync(slots, sl_l, 3 * 2 * s_rev * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
     }
     all_phrases(d_text, 0, opt, 2 * s_rev, slots, sflag);
     timer.mark("lpf_phrases");
@@ -376,37 +391,42 @@ void engine::build_lpf_lnf(int opt) {
         lpf.get(3);
         return;
     }
-    u32* P = l_P.get(3 * (u64)p);
+    pos_t* P = l_P.get(3 * (u64)p);
     u64* keys = u64a.get(p);
     u64* keys2 = u64b.get(p);
     u32* vals = l_V.get(p);
-    u32* vals2 = l_b.get(p);
+    u32* vals2 = l_V2.get(p);
     k_slot_compact<<<cdiv(nsl, 256), 256, 0, st>>>(slots, sflag, off, nsl, P, keys, vals);
     {
         size_t tb = 0;
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys2, vals, vals2, (int)p, 0, 64, st));
         u8* t = scan_tmp.get(tb);
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, keys2, vals, vals2, (int)p, 0, 64, st));
+        if constexpr (sizeof(pos_t) > 4) {  // second (stable) pass on beg
+            k_beg_keys<<<cdiv(p, 256), 256, 0, st>>>(P, vals2, p, keys);
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, keys, keys2, vals2, vals, (int)p, 0, 64, st));
+            std::swap(vals, vals2);
+        }
     }
-    u32* Q = l_Q.get(3 * (u64)p);
+    pos_t* Q = l_Q.get(3 * (u64)p);
     k_gather3<<<cdiv(p, 256), 256, 0, st>>>(P, vals2, p, Q);
     // selection (approximate/common.cpp:31-96)
-    u64* ek = u64a.get(p);
-    u64* pm = u64b.get(p);
+    end_key* ek = (end_key*)u64a.get(2 * (u64)p);
+    end_key* pm = (end_key*)u64b.get(2 * (u64)p);
     k_end_keys<<<cdiv(p, 256), 256, 0, st>>>(Q, p, ek);
     {
         size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, ek, pm, max64{}, (int)p, st));
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, ek, pm, end_max{}, (int)p, st));
         u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ek, pm, max64{}, (int)p, st));
+        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ek, pm, end_max{}, (int)p, st));
     }
     u32* nxt = jump[0].get(p + 1);
-    u32* X = l_d.get(p + 1);
+    u32* X = l_X.get(p + 1);
     k_select_next<<<cdiv(p + 1, 256), 256, 0, st>>>(Q, pm, p, nxt, X);
     u32* marks = u32e.get(p + 1);
     path_marks(p + 1, nxt, marks);
     // chain in order = marked phrases by index (the path is increasing)
-    u32* coff = l_e.get(p + 1);
+    u32* coff = l_coff.get(p + 1);
     const u32 len = xscan(marks, coff, p, scan_tmp, st);
     u32* chain = l_r.get(len + 2);
     k_marked_positions<<<cdiv(p, 256), 256, 0, st>>>(marks, coff, p, chain);
@@ -435,15 +455,15 @@ void engine::build_lpf_lnf(int opt) {
             len2 = len + 1;
         }
     }
-    u32* outP = l_P.get(3 * (u64)len2);
+    pos_t* outP = l_P.get(3 * (u64)len2);
     u32* keep = u32c.get(len2 + 1);
     k_select_emit<<<cdiv(len2, 256), 256, 0, st>>>(Q, chain, len2, outP, keep);
     u32* koff = u32d.get(len2 + 1);
     num_phr = xscan(keep, koff, len2, scan_tmp, st);
-    u32* dst = lpf.get((u64)(num_phr + 1) * 3);
+    pos_t* dst = lpf.get((u64)(num_phr + 1) * 3);
     k_compact_keep<<<cdiv(len2, 256), 256, 0, st>>>(outP, keep, koff, len2, dst);
     LZ_HIP(hipGetLastError());
     timer.mark("phrase_selection");
 }
 
-}  // namespace lz
+}  // namespace LZ_NS

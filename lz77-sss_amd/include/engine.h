@@ -150,7 +150,8 @@ struct engine {
     dbuf<pos_t> g_ast, g_aen;
     dbuf<u64> g_offs;
     // LPF/LNF mode (csrc/lnf.hip)
-    dbuf<u32> l_V, l_b, l_d, l_e, l_r, l_sflag_lnf, l_slots_lnf, l_sflag, l_slots, l_off, l_P, l_Q;
+    dbuf<u32> l_V, l_V2, l_X, l_coff, l_r, l_sflag_lnf, l_sflag, l_off;
+    dbuf<pos_t> l_b, l_d, l_e, l_slots_lnf, l_slots, l_P, l_Q;
     dbuf<u64> l_tmp64;
     dbuf<u32> g_predk, g_wk, g_ids2;
     dbuf<u32> g_brev;
@@ -224,7 +225,7 @@ struct engine {
     void psv_nsv_s();
     void mark_path(u32* mark);
     void build_lpf_lnf(int opt);  // csrc/lnf.hip
-    void all_phrases(const u8* T, int lnf, int opt, u64 slot_base, u32* slots, u32* sflag);
+    void all_phrases(const u8* T, int lnf, int opt, u64 slot_base, pos_t* slots, u32* sflag);
     void path_marks(u32 m, u32* nxt0, u32* marks);
     u64 factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy_block* blk = nullptr);
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode = 1);

@@ -501,46 +501,50 @@ static inline std::vector<lpf_t<P>> build_lpf_naive(const u8* T, u64 n, const lc
 //  LPF/LNF (lpf_lnf_opt) for p = 1: restates lpf_lnf.cpp:31-249 and
 //  greedy_phrase_selection (approximate/common.cpp:31-96)
 // ===========================================================================
-static inline void build_lpf_all(const u8* T, u64 n, const lce_structure<u32>& L, bool opt, std::vector<lpf>& out) {
+template <class P>
+static inline void build_lpf_all(const u8* T, u64 n, const lce_structure<P>& L, bool opt, std::vector<lpf_t<P>>& out) {
+    using lpf = lpf_t<P>;
     std::vector<u32> PSV, NSV;
     build_psv_nsv(L, PSV, NSV);
     const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
     const u32 s = L.s();
-    const u32 N = (u32)n;
+    const P N = (P)n;
     lpf lst_sm{N, N, N}, lst_gr{N, N, N};
     for (u32 i = 0; i < s; i++) {
         if (PSV[ISA[i]] != s) {
-            u32 beg = S[i], src = S[SA[PSV[ISA[i]]]];
+            P beg = S[i], src = S[SA[PSV[ISA[i]]]];
             if (!(beg < lst_sm.end && beg - src == lst_sm.beg - lst_sm.src)) {
-                u32 end = S[i] + (u32)L.lce(src, S[i]);
-                if (opt && src != 0 && S[i] != 0) { u32 l = lce_left(T, src - 1, S[i] - 1); beg -= l; src -= l; }
+                P end = S[i] + (P)L.lce(src, S[i]);
+                if (opt && src != 0 && S[i] != 0) { P l = lce_left<P>(T, src - 1, S[i] - 1); beg -= l; src -= l; }
                 if (end - beg > 1) { lst_sm = {beg, end, src}; out.push_back(lst_sm); }
             }
         }
         if (NSV[ISA[i]] != s) {
-            u32 beg = S[i], src = S[SA[NSV[ISA[i]]]];
+            P beg = S[i], src = S[SA[NSV[ISA[i]]]];
             if (!(beg < lst_gr.end && beg - src == lst_gr.beg - lst_gr.src)) {
-                u32 end = S[i] + (u32)L.lce(src, S[i]);
-                if (opt && src != 0 && S[i] != 0) { u32 l = lce_left(T, src - 1, S[i] - 1); beg -= l; src -= l; }
+                P end = S[i] + (P)L.lce(src, S[i]);
+                if (opt && src != 0 && S[i] != 0) { P l = lce_left<P>(T, src - 1, S[i] - 1); beg -= l; src -= l; }
                 if (end - beg > 1) { lst_gr = {beg, end, src}; out.push_back(lst_gr); }
             }
         }
     }
 }
 // T here is the REVERSED text; phrases are mapped back to forward coordinates
-static inline void build_lnf_all(const u8* T, u64 n, const lce_structure<u32>& L, bool opt, std::vector<lpf>& out) {
+template <class P>
+static inline void build_lnf_all(const u8* T, u64 n, const lce_structure<P>& L, bool opt, std::vector<lpf_t<P>>& out) {
+    using lpf = lpf_t<P>;
     std::vector<u32> PGV, NGV;
     build_pgv_ngv(L, PGV, NGV);
     const auto& S = L.S; const auto& SA = L.SA; const auto& ISA = L.ISA;
     const u32 s = L.s();
-    const u32 N = (u32)n;
+    const P N = (P)n;
     lpf lst_sm{N, N, N}, lst_gr{N, N, N};
     for (u32 i = 0; i < s; i++) {
         if (PGV[ISA[i]] != s) {
-            u32 src = S[SA[PGV[ISA[i]]]], beg = S[i];
+            P src = S[SA[PGV[ISA[i]]]], beg = S[i];
             if (!(beg < lst_sm.end && src - beg == lst_sm.src - lst_sm.beg)) {
-                u32 end = S[i] + (u32)L.lce(S[i], src);
-                if (opt && src != 0 && S[i] != 0) { u32 l = lce_left(T, src - 1, S[i] - 1); beg -= l; src -= l; }
+                P end = S[i] + (P)L.lce(S[i], src);
+                if (opt && src != 0 && S[i] != 0) { P l = lce_left<P>(T, src - 1, S[i] - 1); beg -= l; src -= l; }
                 if (end - beg > 1) {
                     lst_sm = {beg, end, src};
                     out.push_back({N - end, N - beg, N - (src + (end - beg))});
@@ -548,10 +552,10 @@ static inline void build_lnf_all(const u8* T, u64 n, const lce_structure<u32>& L
             }
         }
         if (NGV[ISA[i]] != s) {
-            u32 src = S[SA[NGV[ISA[i]]]], beg = S[i];
+            P src = S[SA[NGV[ISA[i]]]], beg = S[i];
             if (!(beg < lst_gr.end && src - beg == lst_gr.src - lst_gr.beg)) {
-                u32 end = S[i] + (u32)L.lce(S[i], src);
-                if (opt && src != 0 && S[i] != 0) { u32 l = lce_left(T, src - 1, S[i] - 1); beg -= l; src -= l; }
+                P end = S[i] + (P)L.lce(S[i], src);
+                if (opt && src != 0 && S[i] != 0) { P l = lce_left<P>(T, src - 1, S[i] - 1); beg -= l; src -= l; }
                 if (end - beg > 1) {
                     lst_gr = {beg, end, src};
                     out.push_back({N - end, N - beg, N - (src + (end - beg))});
@@ -560,15 +564,17 @@ static inline void build_lnf_all(const u8* T, u64 n, const lce_structure<u32>& L
         }
     }
 }
-static inline void greedy_phrase_selection(std::vector<lpf>& P) {
+template <class Q>
+static inline void greedy_phrase_selection(std::vector<lpf_t<Q>>& P) {
+    using lpf = lpf_t<Q>;
     if (P.empty()) return;
     std::stable_sort(P.begin(), P.end(), [](const lpf& a, const lpf& b) {
         return a.beg < b.beg || (a.beg == b.beg && a.end > b.end);
     });
-    u32 k = 0, i = 1, p = (u32)P.size();
+    size_t k = 0, i = 1, p = P.size();
     while (i < p && P[i].end < P[k].end) i++;
     while (i < p) {
-        u32 x = p;
+        size_t x = p;
         if (i + 1 < p) {
             x = i + 1;
             while (x < p && P[x].beg <= P[k].end) {
@@ -932,13 +938,11 @@ static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, 
     } else if (phr_mode == lpf_naive) {
         L.build(T, n);
         P = build_lpf_naive(T, n, L);
-    } else if constexpr (sizeof(Q) > 4) {
-        throw std::runtime_error("the oracle's LPF/LNF modes are pos_t = uint32_t only");
     } else if (phr_mode == lpf_lnf_opt || phr_mode == lpf_lnf_naive) {
         bool opt = (phr_mode == lpf_lnf_opt);
         std::reverse(T, T + n);  // lz77_sss.hpp:386 (in place on the caller's buffer)
         {
-            lce_structure<u32> LR;
+            lce_structure<Q> LR;
             LR.build(T, n);
             build_lnf_all(T, n, LR, opt, P);
         }
@@ -1152,69 +1156,126 @@ static inline void greedy_block(u8* T, Q n, int phr_mode, u32 rk_seed, Q start, 
 //  small inputs); parity of the sources against the reference is unpinned.
 // ===========================================================================
 static constexpr u32 NONE32 = 0xFFFFFFFFu;
-static inline void suffix_array(const u8* T, u64 n, std::vector<u32>& SA) {
-    SA.resize(n);
-    std::vector<u32> R(n), tmp(n);
-    for (u64 i = 0; i < n; i++) { SA[i] = (u32)i; R[i] = T[i] + 1u; }
-    for (u64 h = 1;; h *= 2) {
-        auto key = [&](u32 i) { return std::pair<u32, u32>(R[i], i + h < n ? R[i + h] : 0u); };
-        __gnu_parallel::sort(SA.begin(), SA.end(), [&](u32 a, u32 b) { return key(a) < key(b); });
-        tmp[SA[0]] = 1;
-        for (u64 r = 1; r < n; r++) tmp[SA[r]] = tmp[SA[r - 1]] + (key(SA[r - 1]) < key(SA[r]) ? 1u : 0u);
-        R.swap(tmp);
-        if (R[SA[n - 1]] == n || h > n) break;
+// Suffix array by induced sorting (SA-IS, Nong-Zhang-Chan 2009) with a virtual sentinel:
+// linear time and about 5n bytes, so the oracle's exact parse runs on 1 GiB texts (the
+// rr_1gib_exact_lengths fixture).  Any exact suffix sort gives the same output.
+template <class C>
+static void sais(const C* s, u64 n, u32 K, u32* SA) {
+    if (n == 0) return;
+    if (n == 1) { SA[0] = 0; return; }
+    std::vector<uint8_t> t(n);  // 1 = S-type
+    t[n - 1] = 0;               // the virtual sentinel is smaller: the last suffix is L-type
+    for (u64 i = n - 1; i-- > 0;) t[i] = (s[i] < s[i + 1] || (s[i] == s[i + 1] && t[i + 1])) ? 1 : 0;
+    auto lms = [&](u64 i) { return i > 0 && t[i] && !t[i - 1]; };
+    std::vector<u64> cnt(K + 1, 0), bkt(K + 1);
+    for (u64 i = 0; i < n; i++) cnt[s[i]]++;
+    auto heads = [&]() { u64 a = 0; for (u32 c = 0; c < K; c++) { bkt[c] = a; a += cnt[c]; } };
+    auto tails = [&]() { u64 a = 0; for (u32 c = 0; c < K; c++) { a += cnt[c]; bkt[c] = a; } };
+    auto induce = [&]() {
+        heads();
+        SA[bkt[s[n - 1]]++] = (u32)(n - 1);  // induced by the sentinel
+        for (u64 i = 0; i < n; i++) {
+            const u32 j = SA[i];
+            if (j != NONE32 && j > 0 && !t[j - 1]) SA[bkt[s[j - 1]]++] = j - 1;
+        }
+        tails();
+        for (u64 i = n; i-- > 0;) {
+            const u32 j = SA[i];
+            if (j != NONE32 && j > 0 && t[j - 1]) SA[--bkt[s[j - 1]]] = j - 1;
+        }
+    };
+    // 1. LMS positions at their bucket ends, induced sort of the LMS substrings
+    std::fill(SA, SA + n, NONE32);
+    tails();
+    for (u64 i = 1; i < n; i++)
+        if (lms(i)) SA[--bkt[s[i]]] = (u32)i;
+    induce();
+    // 2. names of the sorted LMS substrings (equal substrings share a name)
+    u64 m = 0;
+    for (u64 i = 0; i < n; i++)
+        if (lms(SA[i])) SA[m++] = SA[i];
+    std::fill(SA + m, SA + n, NONE32);
+    u32 name = 0;
+    u64 prev = NONE32;
+    for (u64 i = 0; i < m; i++) {
+        const u64 pos = SA[i];
+        bool diff = prev == NONE32;
+        for (u64 d = 0; !diff; d++) {
+            if (pos + d == n || prev + d == n || s[pos + d] != s[prev + d] || t[pos + d] != t[prev + d]) {
+                diff = true;
+                break;
+            }
+            if (d > 0 && (lms(pos + d) || lms(prev + d))) {
+                diff = !(lms(pos + d) && lms(prev + d));
+                break;
+            }
+        }
+        if (diff) { name++; prev = pos; }
+        SA[m + pos / 2] = name - 1;
     }
+    // 3. the reduced string (names in text order) and its suffix array
+    std::vector<u32> s1(m), pos1(m);
+    for (u64 i = n, k = m; i-- > m;)
+        if (SA[i] != NONE32) s1[--k] = SA[i];
+    for (u64 i = 1, k = 0; i < n; i++)
+        if (lms(i)) pos1[k++] = (u32)i;
+    std::vector<u32> SA1(m);
+    if (name < m) sais(s1.data(), m, name, SA1.data());
+    else for (u64 i = 0; i < m; i++) SA1[s1[i]] = (u32)i;
+    // 4. LMS suffixes in sorted order at their bucket ends, then the final induced sort
+    std::fill(SA, SA + n, NONE32);
+    tails();
+    for (u64 i = m; i-- > 0;) {
+        const u32 j = pos1[SA1[i]];
+        SA[--bkt[s[j]]] = j;
+    }
+    induce();
 }
+static inline void suffix_array(const u8* T, u64 n, std::vector<u32>& SA) {
+    SA.assign(n, 0);
+    sais(T, n, 256, SA.data());
+}
+// LPF_opt-style exact parse without an LCP array (the KKP approach): PSV/NSV of every
+// text position in text order from one stack pass over SA, then at each factor start p the
+// two candidates' LCEs by direct comparison -- both are bounded by the factor length + 1,
+// so the comparisons total O(n).  Same output as an LCP/RMQ formulation.
 static inline std::vector<factor> factorize_exact(const u8* T, u64 n) {
     std::vector<factor> F;
     if (n == 0) return F;
-    std::vector<u32> SA;
-    suffix_array(T, n, SA);
-    std::vector<u32> ISA(n), LCP(n, 0);
-    for (u64 r = 0; r < n; r++) ISA[SA[r]] = (u32)r;
-    for (u64 i = 0, h = 0; i < n; i++) {  // Kasai
-        if (ISA[i] == 0) { h = 0; continue; }
-        const u64 j = SA[ISA[i] - 1];
-        while (i + h < n && j + h < n && T[i + h] == T[j + h]) h++;
-        LCP[ISA[i]] = (u32)h;
-        if (h) h--;
+    if (n >= NONE32) throw std::runtime_error("oracle exact: n >= 2^32 - 1");
+    std::vector<u32> psv, nsv;
+    {
+        std::vector<u32> SA;
+        suffix_array(T, n, SA);
+        psv.assign(n, NONE32);
+        nsv.assign(n, NONE32);
+        // stack of text positions with increasing values over ranks: a popped position's NSV is
+        // the position popping it, its PSV the one below it on the stack
+        std::vector<u32> st;
+        st.reserve(1 << 16);
+        for (u64 r = 0; r <= n; r++) {
+            const u32 v = r < n ? SA[r] : 0;
+            while (!st.empty() && (r == n || st.back() > v)) {
+                const u32 x = st.back();
+                st.pop_back();
+                if (r < n) nsv[x] = v;
+                psv[x] = st.empty() ? NONE32 : st.back();
+            }
+            if (r < n) st.push_back(v);
+        }
     }
-    // sparse table over LCP: min LCP over ranks (a, b]
-    std::vector<std::vector<u32>> sp{LCP};
-    for (u64 k = 1; (1ull << k) <= n; k++) {
-        const auto& pr = sp.back();
-        std::vector<u32> lv(n - (1ull << k) + 1);
-        for (u64 i = 0; i < lv.size(); i++) lv[i] = std::min(pr[i], pr[i + (1ull << (k - 1))]);
-        sp.push_back(std::move(lv));
-    }
-    auto rmq = [&](u64 a, u64 b) {  // min LCP[a+1..b]
-        const u64 l = a + 1, len = b - a, k = 63 - std::countl_zero(len);
-        return std::min(sp[k][l], sp[k][b + 1 - (1ull << k)]);
+    auto lce = [&](u64 a, u64 b) {  // a < b
+        u64 l = 0;
+        while (b + l < n && T[a + l] == T[b + l]) l++;
+        return l;
     };
-    std::vector<u32> psv(n, NONE32), nsv(n, NONE32), st;
-    for (u64 r = 0; r < n; r++) {
-        while (!st.empty() && SA[st.back()] > SA[r]) st.pop_back();
-        if (!st.empty()) psv[r] = st.back();
-        st.push_back((u32)r);
-    }
-    st.clear();
-    for (u64 r = n; r-- > 0;) {
-        while (!st.empty() && SA[st.back()] > SA[r]) st.pop_back();
-        if (!st.empty()) nsv[r] = st.back();
-        st.push_back((u32)r);
-    }
-    std::vector<u32> lpf(n), src(n);
-    for (u64 r = 0; r < n; r++) {
-        const u32 a = psv[r] != NONE32 ? SA[psv[r]] : NONE32, b = nsv[r] != NONE32 ? SA[nsv[r]] : NONE32;
-        const u64 la = a != NONE32 ? rmq(psv[r], r) : 0, lb = b != NONE32 ? rmq(r, nsv[r]) : 0;
-        const bool pick_a = la > lb || (la == lb && a < b);
-        lpf[SA[r]] = (u32)(pick_a ? la : lb);
-        src[SA[r]] = pick_a ? a : b;
-    }
     for (u64 p = 0; p < n;) {
-        const u32 l = lpf[p];
-        F.push_back(l ? factor{src[p], l} : factor{T[p], 0});
-        p += std::max<u32>(1, l);
+        const u32 a = psv[p], b = nsv[p];
+        const u64 la = a != NONE32 ? lce(a, p) : 0, lb = b != NONE32 ? lce(b, p) : 0;
+        const bool pick_a = la > lb || (la == lb && a < b);
+        const u64 l = pick_a ? la : lb;
+        F.push_back(l ? factor{pick_a ? a : b, (u32)l} : factor{T[p], 0});
+        p += std::max<u64>(1, l);
     }
     return F;
 }

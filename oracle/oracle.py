@@ -233,11 +233,15 @@ def factorize_exact(T):
     """Exact greedy LZ77 restatement (factorize_exact lengths; PSV/NSV source rule) -> (z,2) u32 factors."""
     buf = _padded(T)
     n = _u8(T).size
-    out = np.zeros((n + 1, 2), np.uint32)
-    z = lib().oracle_factorize_exact(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), n + 1)
-    if z < 0:
-        raise RuntimeError("oracle exact factorization failed")
-    return out[:z].copy()
+    cap = n // 64 + 65536
+    while True:
+        out = np.zeros((cap, 2), np.uint32)
+        z = lib().oracle_factorize_exact(buf.ctypes.data_as(_P), n, out.ctypes.data_as(_P), cap)
+        if z >= 0:
+            return out[:z].copy()
+        if cap >= n + 1:
+            raise RuntimeError("oracle exact factorization failed")
+        cap = n + 1
 
 
 def factorize_exact_timed(T):

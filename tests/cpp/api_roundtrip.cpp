@@ -60,8 +60,8 @@ static int run(int nseeds) {
             std::printf("seed %d: exact factor counts differ across transform modes\n", seed);
             return 1;
         }
-        // LPF/LNF phrases (configs[2], lz77_sss.hpp:384-396) and the skip_phrases stream
-        if constexpr (sizeof(pos_t) == 4) {
+        // LPF/LNF phrases (configs[2], lz77_sss.hpp:384-396; either pos_t)
+        {
             std::vector<typename lz::factor> FL;
             lz::template factorize_approximate<greedy, lpf_lnf_opt>(T.data(), (pos_t)n,
                                                                     [&](typename lz::factor f) { FL.push_back(f); });

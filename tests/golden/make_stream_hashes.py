@@ -4,7 +4,8 @@ full-size texts the GPU tests cannot afford to re-run the oracle on (test infras
 
 Each entry: the generator call that makes the text (the same seeded generators the GPU side uses,
 so the box regenerates the bytes instead of loading them), the text's SHA-256, n, z, the oracle's
-stats and the SHA-256 of the factor stream as little-endian (src, len) pairs of pos_t.
+stats and the SHA-256 of the factor stream as little-endian (src, len) pairs of pos_t (mode
+"exact_lengths": of the exact parse's length column, little-endian uint32).
 
     python3 tests/golden/make_stream_hashes.py [names...]      (default: all; ~2-6 min each)
 
@@ -37,6 +38,13 @@ STREAMS = {
     "genome_1gib": ("genome", dict(n=1 << 30, base_len=64 << 20, mut=0.001, seed=7), 32),
     # C4-style: chr19-like 59 MiB ACGT block, 0.1 % mutations, positions past 2^32 (pos_t = uint64_t)
     "chr19_4gib_u64": ("genome_pos", dict(n=(1 << 32) + (3 << 20) + 12345, base_len=59 << 20, mut=0.001, seed=7), 64),
+    # configs[2]: the headline text with LPF/LNF phrases (factorize_approximate<greedy, lpf_lnf_opt>)
+    "rr_1gib_lpf_lnf": ("random_repetitive", dict(n=1 << 30, seed=42, rep=0.5, run=0.05), 32, "lpf_lnf_opt"),
+    # configs[4]: exact greedy LZ77 of the headline and genome texts -- the length column only (the
+    # canonical lengths; sources follow the range structure's visit order)
+    "rr_1gib_exact_lengths": ("random_repetitive", dict(n=1 << 30, seed=42, rep=0.5, run=0.05), 32, "exact_lengths"),
+    "genome_1gib_exact_lengths": ("genome", dict(n=1 << 30, base_len=64 << 20, mut=0.001, seed=7), 32,
+                                  "exact_lengths"),
 }
 
 
@@ -59,17 +67,21 @@ def sha(a: np.ndarray) -> str:
 def main(names):
     db = json.loads(OUT.read_text()) if OUT.exists() else {}
     for name in names:
-        kind, a, bits = STREAMS[name]
+        kind, a, bits, *rest = STREAMS[name]
+        mode = rest[0] if rest else "lpf_opt"
         t0 = time.time()
         T = make_text(kind, a, pad=4096)
         n = a["n"]
-        if bits == 32:
-            F, st = oracle.factorize(T[:n])
+        st = []
+        if mode == "exact_lengths":  # oracle.hpp factorize_exact (SA-IS + PSV/NSV): the length column
+            F = oracle.factorize_exact(T[:n])[:, 1].astype("<u4")
+        elif bits == 32:
+            F, st = oracle.factorize(T[:n], phr_mode=oracle.LPF_LNF_OPT if mode == "lpf_lnf_opt" else oracle.LPF_OPT)
             F = F.astype("<u4")
         else:
             F, st = oracle.factorize64(T[:n], buf=T)
             F = F.astype("<u8")
-        db[name] = {"kind": kind, "args": a, "pos_bits": bits, "n": n, "text_sha256": sha(T[:n]),
+        db[name] = {"kind": kind, "args": a, "pos_bits": bits, "mode": mode, "n": n, "text_sha256": sha(T[:n]),
                     "z": int(F.shape[0]), "stats": [int(x) for x in st[:12]], "stream_sha256": sha(F),
                     "oracle_seconds": round(time.time() - t0, 1)}
         print(name, json.dumps(db[name]), flush=True)

@@ -94,9 +94,10 @@ def test_u64_medium_vs_oracle(session64, orc, lz, kind, mib):
     assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
 
 
-@pytest.mark.parametrize("phr_mode", [0, 2])
+@pytest.mark.parametrize("phr_mode", [0, 1, 2, 3])
 @pytest.mark.parametrize("seed", [2, 7])
 def test_u64_phrase_modes_and_skip_phrases(session64, orc, lz, phr_mode, seed):
+    """Every phrase mode with pos_t = uint64_t (lz77_sss.hpp:384-396 for any pos_t), incl. LPF/LNF."""
     T = lz.gen_random_repetitive(20000, 150000, seed)
     _, F = run64(session64, T, phr_mode=phr_mode)
     assert np.array_equal(F, orc.factorize64(T, phr_mode=phr_mode)[0])
@@ -159,8 +160,6 @@ def test_u64_session_rejects_32bit_accessors(session64, lz):
     s = session64(1 << 16)
     s.load(lz.gen_random_repetitive(20000, 20000, 1))
     s.factorize()
-    with pytest.raises(lz.Lz77SssError):
-        s.factorize(phr_mode=lz.LPF_LNF_OPT)
     with pytest.raises(lz.Lz77SssError):
         s.factorize_exact()
     with pytest.raises(lz.Lz77SssError):

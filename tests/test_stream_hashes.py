@@ -22,7 +22,8 @@ def _sha(a) -> str:
 
 
 def test_hash_db_complete():
-    assert {"rr_1gib", "genome_1gib"} <= set(DB), "run tests/golden/make_stream_hashes.py"
+    assert {"rr_1gib", "genome_1gib", "rr_1gib_lpf_lnf", "rr_1gib_exact_lengths"} <= set(DB), \
+        "run tests/golden/make_stream_hashes.py"
     for e in DB.values():
         assert len(e["stream_sha256"]) == 64 and e["z"] > 0
 
@@ -47,7 +48,15 @@ def test_full_size_stream_hash(lz, name):
             del T
         else:  # generated in HBM (the host generator of make_stream_hashes.py makes the same bytes)
             s.gen_genome(n, a["base_len"], a["mut"], a["seed"])
-        z = s.factorize()
+        mode = e.get("mode", "lpf_opt")
+        if mode == "exact_lengths":  # configs[4]: the sample-index path with interval samples
+            z = s.factorize_exact(transf_mode=lz.WITH_SAMPLES)
+            F = s.factors(z)
+            assert s.verify() == 0
+            assert z == e["z"]
+            assert _sha(F[:, 1].astype("<u4")) == e["stream_sha256"]
+            return
+        z = s.factorize(phr_mode=lz.LPF_LNF_OPT if mode == "lpf_lnf_opt" else lz.LPF_OPT)
         st = s.stats()
         F = s.factors(z)
     assert z == e["z"]
