@@ -176,9 +176,10 @@ int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_t cap, uint6
 /* Checks the factors of the last factorization against the loaded text without decoding
  * them (a 50 GiB stream needs no n-sized decode buffers): *bad_positions = the number of
  * positions whose factor does not reproduce the text (a literal with another byte, a copy
- * from a position >= its own, a copied byte that differs); 0 <=> decode(F) == T.  Fails
- * with LZ77SSS_EINVAL when the lengths do not sum to n. */
-int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positions);
+ * from a position >= its own, a copied byte that differs); 0 <=> decode(F) == T; first_bad
+ * (may be NULL) the smallest such position (UINT64_MAX if none).  Fails with LZ77SSS_EINVAL
+ * when the lengths do not sum to n. */
+int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positions, uint64_t* first_bad);
 /* Runs only the string-synchronizing-set pass (kernel 1) on the loaded text. */
 int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs);
 /* Copies the sync set of the last sss/factorize call HBM -> host. */

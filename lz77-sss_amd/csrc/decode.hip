@@ -14,13 +14,14 @@
 
 namespace LZ_NS {
 
+// (the per-factor and per-position kernels loop over a capped grid: n and z pass 2^32 with
+// pos_t = uint64_t, GRID_CAP in lz77sss_internal.h)
 __global__ void k_dec_lens(const pos_t* __restrict__ F, u64 nf, u64* __restrict__ len) {
-    const u64 f = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f < nf) len[f] = F[2 * f + 1] ? F[2 * f + 1] : 1u;
+    for (u64 f = gtid(); f < nf; f += gstride()) len[f] = F[2 * f + 1] ? F[2 * f + 1] : 1u;
 }
 __global__ void k_dec_heads(const u64* __restrict__ start, u64 nf, u64 n, u32* __restrict__ head) {
-    const u64 f = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f < nf && start[f] < n) head[start[f]] = (u32)f;
+    for (u64 f = gtid(); f < nf; f += gstride())
+        if (start[f] < n) head[start[f]] = (u32)f;
 }
 struct max_u32 {
     __device__ __forceinline__ u32 operator()(const u32& a, const u32& b) const { return a > b ? a : b; }
@@ -28,19 +29,19 @@ struct max_u32 {
 // ref[p]: p for literals, the source position for copies; err on a forward reference
 __global__ void k_dec_refs(const pos_t* __restrict__ F, const u64* __restrict__ start, const u32* __restrict__ fid, u64 n,
                            pos_t* __restrict__ ref, u32* __restrict__ err) {
-    const u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const u32 f = fid[p];
-    const pos_t len = F[2 * (u64)f + 1];
-    if (len == 0) { ref[p] = (pos_t)p; return; }
-    const pos_t src = F[2 * (u64)f], st = (pos_t)start[f];
-    if (src >= st) { atomicOr(err, 1u); ref[p] = (pos_t)p; return; }  // only on an invalid stream
-    // a self-overlapping copy (distance d < len) is d-periodic: fold the offset
-    // into the first period so the reference lands before the factor start
-    const pos_t d = st - src;
-    pos_t off = (pos_t)(p - st);
-    if (off >= d) off %= d;
-    ref[p] = src + off;
+    for (u64 p = gtid(); p < n; p += gstride()) {
+        const u32 f = fid[p];
+        const pos_t len = F[2 * (u64)f + 1];
+        if (len == 0) { ref[p] = (pos_t)p; continue; }
+        const pos_t src = F[2 * (u64)f], st = (pos_t)start[f];
+        if (src >= st) { atomicOr(err, 1u); ref[p] = (pos_t)p; continue; }  // only on an invalid stream
+        // a self-overlapping copy (distance d < len) is d-periodic: fold the offset
+        // into the first period so the reference lands before the factor start
+        const pos_t d = st - src;
+        pos_t off = (pos_t)(p - st);
+        if (off >= d) off %= d;
+        ref[p] = src + off;
+    }
 }
 // one pointer-jumping round.  Grid-stride over a fixed grid so that the change
 // flag costs one atomic per block: millions of same-address atomics (even one
@@ -78,11 +79,11 @@ __global__ void __launch_bounds__(256) k_dec_jump(const pos_t* __restrict__ ref,
 }
 __global__ void k_dec_bytes(const pos_t* __restrict__ F, const u32* __restrict__ fid, const pos_t* __restrict__ ref, u64 n,
                             const u8* __restrict__ cmp, u8* __restrict__ out, u32* __restrict__ mism) {
-    const u64 p = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const u8 c = (u8)F[2 * (u64)fid[ref[p]]];
-    if (out) out[p] = c;
-    if (cmp && cmp[p] != c) atomicAdd(mism, 1u);  // only on a failed round trip
+    for (u64 p = gtid(); p < n; p += gstride()) {
+        const u8 c = (u8)F[2 * (u64)fid[ref[p]]];
+        if (out) out[p] = c;
+        if (cmp && cmp[p] != c) atomicAdd(mism, 1u);  // only on a failed round trip
+    }
 }
 
 // decodes nf factors (device array, 2 x u32 each) of a text of length n; writes
@@ -100,20 +101,20 @@ u64 engine::decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* 
     // starts in 64 bits: lengths of an invalid stream may sum past 2^32 (the sum check must see it)
     u64* len = dec_len64.get(nf + 1);
     u64* start = dec_start64.get(nf + 1);
-    k_dec_lens<<<cdiv(nf, 256), 256, 0, st>>>(F, nf, len);
+    k_dec_lens<<<capped_grid(nf, 256), 256, 0, st>>>(F, nf, len);
     LZ_HIP(hipMemsetAsync(len + nf, 0, 8, st));
     excl_sum64(len, start, (u64)0, nf + 1, scan_tmp, st);
     if (rd1(start + nf, st) != n_out) throw error(LZ77SSS_EINVAL, "factor lengths do not sum to n");
     u32* head = dec_fid.get(n_out);
     u32* fid = dec_fid2.get(n_out);
     LZ_HIP(hipMemsetAsync(head, 0, n_out * 4, st));
-    k_dec_heads<<<cdiv(nf, 256), 256, 0, st>>>(start, nf, n_out, head);
+    k_dec_heads<<<capped_grid(nf, 256), 256, 0, st>>>(start, nf, n_out, head);
     incl_scan64(head, fid, n_out, max_u32{}, scan_tmp, st);
     pos_t* ref = dec_ref.get(n_out);
     pos_t* ref2 = dec_ref2.get(n_out);
     u32* flags = counters.get(16);
     LZ_HIP(hipMemsetAsync(flags, 0, 8, st));
-    k_dec_refs<<<cdiv(n_out, 256), 256, 0, st>>>(F, start, fid, n_out, ref, flags);
+    k_dec_refs<<<capped_grid(n_out, 256), 256, 0, st>>>(F, start, fid, n_out, ref, flags);
     if (rd1(flags, st)) throw error(LZ77SSS_EINVAL, "factor source not before its position");
     dec_rounds = 0;
     for (int round = 0; round < 40; round++) {
@@ -124,7 +125,7 @@ u64 engine::decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* 
         if (!rd1(flags + 1, st)) break;
     }
     LZ_HIP(hipMemsetAsync(flags + 2, 0, 4, st));
-    k_dec_bytes<<<cdiv(n_out, 256), 256, 0, st>>>(F, fid, ref, n_out, cmp, out, flags + 2);
+    k_dec_bytes<<<capped_grid(n_out, 256), 256, 0, st>>>(F, fid, ref, n_out, cmp, out, flags + 2);
     LZ_HIP(hipGetLastError());
     return cmp ? rd1(flags + 2, st) : 0;
 }
@@ -143,11 +144,13 @@ u64 engine::decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* 
 constexpr u32 VB_T = 256, VB_PER = 16, VB = VB_T * VB_PER;
 __global__ __launch_bounds__(VB_T) void k_verify_blocks(const pos_t* __restrict__ F, const u64* __restrict__ start,
                                                          u64 nf, u64 n, const u8* __restrict__ T,
-                                                         unsigned long long* __restrict__ bad) {
+                                                         unsigned long long* __restrict__ bad) {  // [0] count, [1] first
     __shared__ u16 fl[VB];
     __shared__ u64 s_f0;
     __shared__ u32 s_wmax[VB_T / 64];
-    const u64 b0 = (u64)blockIdx.x * VB;
+    const u64 nblk = (n + VB - 1) / VB;
+    for (u64 blk = blockIdx.x; blk < nblk; blk += gridDim.x) {  // (block-uniform loop: barriers inside)
+    const u64 b0 = blk * VB;
     const u64 b1 = min(n, b0 + VB);
     if (threadIdx.x == 0) {
         u64 lo = 0, hi = nf;  // last factor with start <= b0
@@ -181,8 +184,10 @@ __global__ __launch_bounds__(VB_T) void k_verify_blocks(const pos_t* __restrict_
     const u32 ex = (u32)__shfl_up(incl, 1, 64);
     u32 run = max(carry, lane ? ex : 0u);
     u32 cnt = 0;
+    u64 first = ~0ull;
     for (u32 k = 0; k < VB_PER; k++) {
         const u64 p = b0 + base + k;
+        const u32 c0 = cnt;
         run = max(run, (u32)fl[base + k]);
         if (p >= b1) break;
         const u64 f = f0 + run;
@@ -194,26 +199,109 @@ __global__ __launch_bounds__(VB_T) void k_verify_blocks(const pos_t* __restrict_
             const u64 st = start[f];
             cnt += ((u64)src >= st || T[(u64)src + (p - st)] != c) ? 1u : 0u;
         }
+        if (cnt != c0 && first == ~0ull) first = p;
     }
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
-    if (lane == 0 && cnt) atomicAdd(bad, (unsigned long long)cnt);
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_down(cnt, o, 64);
+        first = min(first, (u64)__shfl_down(first, o, 64));
+    }
+    if (lane == 0 && cnt) {
+        atomicAdd(bad, (unsigned long long)cnt);
+        atomicMin(bad + 1, (unsigned long long)first);
+    }
+    __syncthreads();  // fl / s_f0 / s_wmax are rewritten by the next block of the loop
+    }
 }
 
-u64 engine::verify_factors(const pos_t* F, u64 nf, u64 n_out, const u8* T) {
+// LZ77SSS_DEBUG_VERIFY: every LPF phrase (beg, end, src) copies equal bytes and its source lies
+// before it; [0] bad phrases, [1] the first bad phrase index
+__global__ void k_verify_phrases(const pos_t* __restrict__ P, u64 m, const u8* __restrict__ T,
+                                 unsigned long long* __restrict__ bad) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    bool b = false;
+    if (k < m) {
+        const pos_t beg = P[3 * k], end = P[3 * k + 1], src = P[3 * k + 2];
+        b = end <= beg || src >= beg || dev_naive_lce(T, src, beg, end - beg) != (u64)(end - beg) ||
+            (k > 0 && beg < P[3 * (k - 1) + 1]);
+    }
+    if (b) {
+        atomicAdd(bad, 1ull);
+        atomicMin(bad + 1, (unsigned long long)k);
+    }
+}
+// LZ77SSS_DEBUG_VERIFY: SA_S order and LCP against bounded direct comparisons (2^20 bytes);
+// [0] bad LCP, [1] bad order, [2] first bad rank; the successor table against a binary search
+__global__ void k_verify_sa_lcp(const u8* __restrict__ T, u64 n, const pos_t* __restrict__ S, const u32* __restrict__ SA,
+                                const u32* __restrict__ LCP, u32 s, unsigned long long* __restrict__ bad) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r == 0 || r >= s) return;
+    const u64 a = S[SA[r - 1]], b = S[SA[r]];
+    const u64 lim = min<u64>(1ull << 20, n - max(a, b));
+    const u64 l = dev_naive_lce(T, a, b, lim);
+    const bool bl = l < lim && LCP[r] != (u32)l;
+    const bool bo = l < lim && !(T[a + l] < T[b + l]);
+    if (bl) atomicAdd(bad, 1ull);
+    if (bo) atomicAdd(bad + 1, 1ull);
+    if (bl || bo) atomicMin(bad + 2, (unsigned long long)r);
+}
+__global__ void k_verify_succ(const pos_t* __restrict__ S, u32 s, const u32* __restrict__ succ, u64 nb,
+                              unsigned long long* __restrict__ bad) {
+    const u64 bkt = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (bkt >= nb) return;
+    const u32 k = succ[bkt];
+    const u64 x = bkt << 9;
+    const bool ok = k <= s && (k == s || (u64)S[k] >= x) && (k == 0 || (u64)S[k - 1] < x);
+    if (!ok) {
+        atomicAdd(bad + 3, 1ull);
+        atomicMin(bad + 4, (unsigned long long)bkt);
+    }
+}
+void engine::debug_verify_lce(const char* what) {
+    unsigned long long* bad = (unsigned long long*)counters64.get(24) + 18;
+    LZ_HIP(hipMemsetAsync(bad, 0, 48, st));
+    LZ_HIP(hipMemsetAsync(bad + 2, 0xFF, 8, st));
+    LZ_HIP(hipMemsetAsync(bad + 4, 0xFF, 8, st));
+    if (s > 1) k_verify_sa_lcp<<<cdiv(s, 256), 256, 0, st>>>(d_text, n, S.p, SA.p, lcp_rmq[0].p, s, bad);
+    const u64 nb = (n >> 9) + 2;
+    k_verify_succ<<<cdiv(nb, 256), 256, 0, st>>>(S.p, s, succ_tab.p, nb, bad);
+    u64 h[6];
+    LZ_HIP(hipMemcpyAsync(h, bad, 48, hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    std::fprintf(stderr, "[lz77sss-verify] %s: |S|=%u bad LCP=%llu bad order=%llu first rank=%lld; succ buckets=%llu bad=%llu first=%lld\n",
+                 what, s, (unsigned long long)h[0], (unsigned long long)h[1], (long long)h[2], (unsigned long long)nb,
+                 (unsigned long long)h[3], (long long)h[4]);
+}
+void engine::debug_verify_phrases(const char* what) {
+    unsigned long long* bad = (unsigned long long*)counters64.get(24) + 18;
+    LZ_HIP(hipMemsetAsync(bad, 0, 8, st));
+    LZ_HIP(hipMemsetAsync(bad + 1, 0xFF, 8, st));
+    if (num_phr) k_verify_phrases<<<cdiv(num_phr, 256), 256, 0, st>>>(lpf.p, num_phr, d_text, bad);
+    const auto [cnt, first] = rd2((const u64*)bad, (const u64*)bad + 1, st);
+    pos_t ph[3] = {0, 0, 0};
+    if (cnt) LZ_HIP(hipMemcpy(ph, lpf.p + 3 * first, sizeof(ph), hipMemcpyDeviceToHost));
+    std::fprintf(stderr, "[lz77sss-verify] %s: phrases=%u bad=%llu first=%llu (beg=%llu end=%llu src=%llu)\n", what,
+                 num_phr, (unsigned long long)cnt, (unsigned long long)(cnt ? first : 0), (unsigned long long)ph[0],
+                 (unsigned long long)ph[1], (unsigned long long)ph[2]);
+}
+
+u64 engine::verify_factors(const pos_t* F, u64 nf, u64 n_out, const u8* T, u64* first_bad) {
+    if (first_bad) *first_bad = ~0ull;
     if (n_out == 0) return nf ? 1 : 0;
     if (nf == 0) return n_out;
     u64* len = dec_len64.get(nf + 1);
     u64* start = dec_start64.get(nf + 1);
-    k_dec_lens<<<cdiv(nf, 256), 256, 0, st>>>(F, nf, len);
+    k_dec_lens<<<capped_grid(nf, 256), 256, 0, st>>>(F, nf, len);
     LZ_HIP(hipMemsetAsync(len + nf, 0, 8, st));
     excl_sum64(len, start, (u64)0, nf + 1, scan_tmp, st);
     if (rd1(start + nf, st) != n_out) throw error(LZ77SSS_EINVAL, "factor lengths do not sum to n");
-    unsigned long long* bad = (unsigned long long*)counters64.get(16) + 15;
+    unsigned long long* bad = (unsigned long long*)counters64.get(24) + 16;  // (0..15: the greedy's slots)
     LZ_HIP(hipMemsetAsync(bad, 0, 8, st));
-    const u64 nblk = (n_out + VB - 1) / VB;  // n <= 2^40: fewer than 2^28 blocks
-    k_verify_blocks<<<(unsigned)nblk, VB_T, 0, st>>>(F, start, nf, n_out, T, bad);
+    LZ_HIP(hipMemsetAsync(bad + 1, 0xFF, 8, st));
+    k_verify_blocks<<<capped_grid(n_out, VB), VB_T, 0, st>>>(F, start, nf, n_out, T, bad);
     LZ_HIP(hipGetLastError());
-    return rd1((u64*)bad, st);
+    const auto [cnt, first] = rd2((const u64*)bad, (const u64*)bad + 1, st);
+    if (first_bad) *first_bad = first;
+    return cnt;
 }
 
 }  // namespace LZ_NS

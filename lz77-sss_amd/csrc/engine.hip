@@ -137,10 +137,12 @@ void engine::prepare_phrases(int phr_mode, bool external_sss) {
         build_lcp_rmq(d_text);
         timer.mark("lcp_rmq");
         trace("lcp_rmq");
+        if (std::getenv("LZ77SSS_DEBUG_VERIFY")) debug_verify_lce("sa_s + lcp");
         if (phr_mode == LZ77SSS_LPF_OPT) build_lpf_opt(d_text);
         else build_lpf_naive(d_text);
         timer.mark("lpf");
         trace("lpf");
+        if (std::getenv("LZ77SSS_DEBUG_VERIFY")) debug_verify_phrases("lpf");
     } else {
         if (external_sss) throw error(LZ77SSS_EINVAL, "an external sync set needs phr_mode lpf_opt or lpf_naive");
         build_lpf_lnf(phr_mode == LZ77SSS_LPF_LNF_OPT ? 1 : 0);
@@ -179,6 +181,12 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
     } else {
         num_fact = factorize_greedy(d_text, rk_seed, log2_override);
         timer.mark("greedy");
+    }
+    if (std::getenv("LZ77SSS_DEBUG_VERIFY") && fact_mode != LZ77SSS_SKIP_PHRASES) {
+        u64 first = 0;
+        const u64 bad = verify_factors(fact.p, num_fact, n, d_text, &first);
+        std::fprintf(stderr, "[lz77sss-verify] factors: z=%llu bad positions=%llu first=%llu\n",
+                     (unsigned long long)num_fact, (unsigned long long)bad, (unsigned long long)first);
     }
     if (debug_enabled()) std::fprintf(stderr, "[lz77sss-debug] done greedy (|S|=%u phrases=%u)\n", s, num_phr);
     LZ_HIP(hipStreamSynchronize(st));
@@ -281,8 +289,8 @@ struct engine64_impl final : lz::engine_if {
         return E.decode_device(F, nf, n_out, d_out, cmp ? E.d_text : nullptr);
     }
     u8* dec_out(u64 n) override { return E.dec_out.get(n); }
-    u64 verify() override {
-        const u64 bad = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text);
+    u64 verify(u64* first_bad) override {
+        const u64 bad = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text, first_bad);
         LZ_HIP(hipStreamSynchronize(E.st));
         return bad;
     }
@@ -545,17 +553,17 @@ LZ77SSS_API int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_
 
 // the factors of the last factorization checked against the loaded text in HBM (csrc/decode.hip
 // verify_factors): the decode round trip without materialising the decoded text
-LZ77SSS_API int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positions) {
+LZ77SSS_API int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positions, uint64_t* first_bad) {
     if (!s || !bad_positions) return LZ77SSS_EINVAL;
     return guarded([&] {
         if (s->E64) {
             LZ_HIP(hipSetDevice(s->E64->device()));
-            *bad_positions = s->E64->verify();
+            *bad_positions = s->E64->verify(first_bad);
             return;
         }
         lz::engine& E = s->E;
         LZ_HIP(hipSetDevice(E.device));
-        *bad_positions = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text);
+        *bad_positions = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text, first_bad);
         LZ_HIP(hipStreamSynchronize(E.st));
     });
 }
@@ -676,8 +684,7 @@ __device__ __forceinline__ lz::u64 gen_mix(lz::u64 x) {  // splitmix64 finalizer
 }
 __global__ void k_gen_genome(lz::u8* __restrict__ out, lz::u64 n, lz::u64 offset, lz::u64 base_len,
                              lz::u64 mut_thr, lz::u64 seed) {
-    const lz::u64 i0 = ((lz::u64)blockIdx.x * blockDim.x + threadIdx.x) * 16;
-    if (i0 >= n) return;
+    for (lz::u64 i0 = lz::gtid() * 16; i0 < n; i0 += lz::gstride() * 16) {
     lz::u32 w[4] = {0, 0, 0, 0};
     for (int k = 0; k < 16 && i0 + k < n; k++) {
         const lz::u64 p = offset + i0 + k;
@@ -694,6 +701,7 @@ __global__ void k_gen_genome(lz::u8* __restrict__ out, lz::u64 n, lz::u64 offset
     } else {
         for (int k = 0; i0 + k < n; k++) out[i0 + k] = (lz::u8)(w[k >> 2] >> (8 * (k & 3)));
     }
+    }
 }
 
 LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint64_t base_len, double mut_rate,
@@ -709,7 +717,7 @@ LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint6
         if (s->E64) s->E64->set_n(n);
         else s->E.n = n;
         const lz::u64 thr = mut_rate >= 1.0 ? ~0ull : (lz::u64)(mut_rate * 18446744073709551616.0);
-        if (n) k_gen_genome<<<(unsigned)((n + 4095) / 4096), 256, 0, st>>>(text, n, offset, base_len, thr, seed);
+        if (n) k_gen_genome<<<lz::capped_grid((n + 15) / 16, 256), 256, 0, st>>>(text, n, offset, base_len, thr, seed);
         LZ_HIP(hipGetLastError());
         LZ_HIP(hipMemsetAsync(text + n, 0, lz::TEXT_PAD, st));
         LZ_HIP(hipStreamSynchronize(st));

@@ -1161,9 +1161,8 @@ __device__ __forceinline__ void bm_set_range_wave(u32* bm, pos_t a, pos_t b, u32
 // positions), the rest per phrase (one thread: at most 48 positions)
 __global__ void k_gap_bitmaps(seg_tab S, u32 nseg, pos_t N, pos_t nt, pos_t hi, pos_t off, u32* __restrict__ bmI,
                               u32* __restrict__ bmSup) {
-    const u64 id = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per segment
     const u32 lane = threadIdx.x & 63;
-    if (id >= nseg) return;
+    for (u64 id = gtid() >> 6; id < nseg; id += gstride() >> 6) {  // one wave per segment (grid-stride)
     // the segment table (k_gap_segs) holds each segment's start and gap; a segment ends
     // where the next one of its gap starts, the last one at the (clipped) gap end
     const seg_in g = S.sin[id];
@@ -1176,6 +1175,7 @@ __global__ void k_gap_bitmaps(seg_tab S, u32 nseg, pos_t N, pos_t nt, pos_t hi, 
     if (x0 < x1) {
         bm_set_range_wave(bmI, x0 - off, x1 - off, lane);
         bm_set_range_wave(bmSup, x0 - off, x1 - off, lane);
+    }
     }
 }
 __global__ void k_gap_bitmaps_phr(const pos_t* __restrict__ P, u32 m, pos_t N, pos_t nt, pos_t lo, pos_t hi, pos_t off,
@@ -1540,16 +1540,16 @@ __global__ void k_chain_expand(jump_levels JL, u32 len, u32 c0, u32* __restrict_
 // (clipped to the window's bitmap range [off, hi), hi <= nt)
 __global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, pos_t hi, pos_t off,
                                 u32* __restrict__ bm) {
-    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per chain node
     const u32 lane = threadIdx.x & 63;
-    if (k >= cnt) return;
-    const u32 g = chain[k];
-    const seg_out& o = S.sout[g];
-    const pos_t a = S.sin[g].start, b = min(o.e, hi);
-    if (a < b) bm_set_range_wave(bm, a - off, b - off, lane);
-    if (lane < o.nsingle && lane < 4 && o.single[lane] < hi) {
-        const pos_t r = o.single[lane] - off;
-        atomicOr(&bm[r >> 5], 1u << (r & 31));
+    for (u64 k = gtid() >> 6; k < cnt; k += gstride() >> 6) {  // one wave per chain node (grid-stride)
+        const u32 g = chain[k];
+        const seg_out& o = S.sout[g];
+        const pos_t a = S.sin[g].start, b = min(o.e, hi);
+        if (a < b) bm_set_range_wave(bm, a - off, b - off, lane);
+        if (lane < o.nsingle && lane < 4 && o.single[lane] < hi) {
+            const pos_t r = o.single[lane] - off;
+            atomicOr(&bm[r >> 5], 1u << (r & 31));
+        }
     }
 }
 // the window's entry segment: the exact chain state handed over by the previous window
@@ -1582,18 +1582,18 @@ __global__ void k_exit_state(seg_tab S, u32 term, seg_in* __restrict__ out) {
 // carried table (pos + 1, 0 = none): every insert of the window's chain, for the next window
 __global__ void k_h_export(const u8* __restrict__ T, gap_cfg G, seg_tab S, const u32* __restrict__ chain, u32 cnt,
                            pos_t* __restrict__ Hs) {
-    const u64 k = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per chain node
     const u32 lane = threadIdx.x & 63;
-    if (k >= cnt) return;
-    const u32 g = chain[k];
-    const seg_out& o = S.sout[g];
-    const pos_t a = S.sin[g].start;
     auto put = [&](pos_t q) {
         for (int x = 0; x < 5; x++)
             atomic_max_pos(&Hs[(u32)((u64)kr_direct(T, q, G.lens[x], G.base[x]) & G.mask)], q + 1);
     };
-    for (pos_t q = a + lane; q < o.e; q += 64) put(q);
-    if (lane < o.nsingle && lane < 4) put(o.single[lane]);
+    for (u64 k = gtid() >> 6; k < cnt; k += gstride() >> 6) {  // one wave per chain node (grid-stride)
+        const u32 g = chain[k];
+        const seg_out& o = S.sout[g];
+        const pos_t a = S.sin[g].start;
+        for (pos_t q = a + lane; q < o.e; q += 64) put(q);
+        if (lane < o.nsingle && lane < 4) put(o.single[lane]);
+    }
 }
 // the lead-in table of a speculative block: the speculated insert set of
 // [0, upto) -- every gap position and the query position past each gap, as the first
@@ -1730,6 +1730,10 @@ __global__ void k_invalidate_all(seg_tab S, u32 nseg) {
     S.succ[g] = NONE;
 }
 
+__global__ void k_set_u32x2(u32* p, u32 a, u32 b) {
+    p[0] = a;
+    p[1] = b;
+}
 __global__ void k_put3(pos_t* p, pos_t a, pos_t b, pos_t c) {
     p[0] = a;
     p[1] = b;
@@ -1767,8 +1771,9 @@ u64 engine::carried_entries(int log2_override) {
         LZ_HIP(hipMemsetAsync(acc, 0, 16, st));
         k_phrase_info<<<cdiv(m, 256), 256, 0, st>>>(P, m, N, acc);
         u64 h2[2];
-        LZ_HIP(hipMemcpyAsync(h2, acc, 16, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
+        hread rb(st);
+        rb.add(h2, acc, 2);
+        rb.sync();
         len_lpf_phr = (pos_t)h2[0];
         num_gaps = h2[1];
     }
@@ -1799,8 +1804,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         LZ_HIP(hipMemsetAsync(acc, 0, 16, st));
         k_phrase_info<<<cdiv(m, 256), 256, 0, st>>>(P, m, N, acc);
         u64 h2[2];
-        LZ_HIP(hipMemcpyAsync(h2, acc, 16, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
+        hread rb(st);
+        rb.add(h2, acc, 2);
+        rb.sync();
         len_lpf_phr = (pos_t)h2[0];
         num_gaps = h2[1];
     }
@@ -1812,15 +1818,25 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         std::mt19937_64 g(rk_seed);
         for (int i = 0; i < 5; i++) bases[i] = std::uniform_int_distribution<u64>(257, (1ull << 20) - 1)(g);
     }
-    std::vector<u128> negpow(5 * 256);
-    for (int x = 0; x < 5; x++) {
-        const u128 bp = powmod107_host(bases[x], gp.patt_lens[x]);
-        const u128 nbp = (P107 - bp) % P107;
-        negpow[x * 256] = 0;
-        for (int o = 1; o < 256; o++) negpow[x * 256 + o] = mod107(negpow[x * 256 + o - 1] + nbp);
-    }
+    // the influence tables depend only on (bases, pattern lengths): uploaded once per change
     u128* d_negpow = (u128*)tmp_greedy.get(5 * 256 * sizeof(u128));
-    LZ_HIP(hipMemcpyAsync(d_negpow, negpow.data(), 5 * 256 * sizeof(u128), hipMemcpyHostToDevice, st));
+    {
+        std::array<u64, 10> key;
+        for (int x = 0; x < 5; x++) { key[x] = bases[x]; key[5 + x] = gp.patt_lens[x]; }
+        if (key != negpow_key || d_negpow != negpow_dev) {
+            std::vector<u128> negpow(5 * 256);
+            for (int x = 0; x < 5; x++) {
+                const u128 bp = powmod107_host(bases[x], gp.patt_lens[x]);
+                const u128 nbp = (P107 - bp) % P107;
+                negpow[x * 256] = 0;
+                for (int o = 1; o < 256; o++) negpow[x * 256 + o] = mod107(negpow[x * 256 + o - 1] + nbp);
+            }
+            LZ_HIP(hipMemcpyAsync(d_negpow, negpow.data(), 5 * 256 * sizeof(u128), hipMemcpyHostToDevice, st));
+            LZ_HIP(hipStreamSynchronize(st));  // (the host vector goes out of scope)
+            negpow_key = key;
+            negpow_dev = d_negpow;
+        }
+    }
 
     stats.assign(24, 0);
     stats[0] = s; stats[1] = has_runs; stats[2] = num_lpf; stats[3] = len_lpf_phr; stats[4] = num_gaps;
@@ -1920,9 +1936,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         excl_scan_nr(cnt_seg, off_seg, m + 1, scan_tmp, st);
         excl_scan_nr(cnt_cb, off_cb, m + 1, scan_tmp, st);
         u32 nseg0, ncb;
-        LZ_HIP(hipMemcpyAsync(&nseg0, off_seg + m + 1, 4, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipMemcpyAsync(&ncb, off_cb + m + 1, 4, hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
+        {
+            hread rb(st);
+            rb.add(&nseg0, off_seg + m + 1);
+            rb.add(&ncb, off_cb + m + 1);
+            rb.sync();
+        }
         pos_t* cbv = g_cbv.get(ncb + 1);
         if (ncb) k_gap_cbv<<<cdiv(ncb, 256), 256, 0, st>>>(P, m, CH, a, bw, off_cb, ncb, cbv);
         u32 cap = nseg0 + nseg0 / 2 + (1u << 16);
@@ -1949,8 +1968,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         S.segoff = a;
         S.nseg = (u32*)counters64.get(16);  // [0] nseg/err, [1] c0, [2..3] phrase info, [4..] entry seg_in
         S.err = S.nseg + 1;
-        LZ_HIP(hipMemsetAsync(S.nseg, 0, 8, st));
-        LZ_HIP(hipMemcpyAsync(S.nseg, &nseg0, 4, hipMemcpyHostToDevice, st));
+        k_set_u32x2<<<1, 1, 0, st>>>(S.nseg, nseg0, 0);
         S.cbv = cbv; S.ncb = ncb; S.P = P; S.m = m; S.N = bw; S.zmask0 = zmask0;
         if (nseg0) k_gap_segs<<<cdiv(nseg0, 256), 256, 0, st>>>(S, CH, off_seg, nseg0);
         u32* d_c0 = (u32*)(counters64.p + 1);
@@ -1967,16 +1985,19 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
         LZ_HIP(hipMemsetAsync(bmIb, 0, nw * 4, st));
         if (nseg0)
-            k_gap_bitmaps<<<cdiv((u64)nseg0 * 64, 256), 256, 0, st>>>(S, nseg0, N, G.nt, hi_ins, off, bmI, bmIb);
+            k_gap_bitmaps<<<capped_grid((u64)nseg0 * 64, 256), 256, 0, st>>>(S, nseg0, N, G.nt, hi_ins, off, bmI, bmIb);
         k_gap_bitmaps_phr<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmIb);
         u32 hn[2];
-        LZ_HIP(hipMemcpyAsync(hn, S.nseg, 8, hipMemcpyDeviceToHost, st));
         u32 c0 = 0;
-        LZ_HIP(hipMemcpyAsync(&c0, d_c0, 4, hipMemcpyDeviceToHost, st));
         // the exact entry of the window as the completion path sees it
         seg_in entry_in;
-        LZ_HIP(hipMemcpyAsync(&entry_in, d_entry, sizeof(seg_in), hipMemcpyDeviceToHost, st));
-        LZ_HIP(hipStreamSynchronize(st));
+        {
+            hread rb(st);
+            rb.add(hn, S.nseg, 2);
+            rb.add(&c0, d_c0);
+            rb.add(&entry_in, d_entry);
+            rb.sync();
+        }
         const u32 nseg_init = hn[0];
         lap("greedy setup");
 
@@ -2003,8 +2024,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             if (from_entry) LZ_HIP(hipMemsetAsync(d_y0, 0, 8, st));
             k_chain_cut<<<1, 1, 0, st>>>(S, chain, from_entry ? 0u : nall, d_y0, entry_in, d_cutp);
             chain_cut cut;
-            LZ_HIP(hipMemcpyAsync(&cut, d_cutp, sizeof(cut), hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipStreamSynchronize(st));
+            {
+                hread rb(st);
+                rb.add(&cut, (const chain_cut*)d_cutp);
+                rb.sync();
+            }
             const u64 offk = cut.k ? rd1(offs + cut.k, st) : 0;
             pos_t* fo = fact.get(2 * (offk + (u64)(N - cut.in.start) + 2) + 2);
             if (cut.k) {
@@ -2022,8 +2046,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                                          W.blk_start);
             LZ_HIP(hipGetLastError());
             u64 hc[4];
-            LZ_HIP(hipMemcpyAsync(hc, d_sq, 32, hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipStreamSynchronize(st));
+            {
+                hread rb(st);
+                rb.add(hc, (const u64*)d_sq, 4);
+                rb.sync();
+            }
             if (hc[1]) throw error(-6, "greedy: sequential completion guard tripped (internal error)");
             if (!last && hc[2] >= (u64)G.nt) {
                 redo = true;  // the hand-over point lies in the tail region
@@ -2317,8 +2344,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     for (;;) {  // link; grow the table when full
                         k_link<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
                         u32 h2[2];
-                        LZ_HIP(hipMemcpyAsync(h2, S.nseg, 8, hipMemcpyDeviceToHost, st));
-                        LZ_HIP(hipStreamSynchronize(st));
+                        {
+                            hread rb(st);
+                            rb.add(h2, (const u32*)S.nseg, 2);
+                            rb.sync();
+                        }
                         if (!(h2[1] & 1)) { nseg = h2[0]; break; }
                         const u32 ncap = cap * 2;
                         g_sin.grow_keep(ncap, cap, st); g_sout.grow_keep(ncap, cap, st);
@@ -2353,8 +2383,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     JL.nlv = nlv;
                     for (u32 l = 0; l < nlv; l++) JL.J[l] = jump[l].p;
                     k_chain_status<<<1, 1, 0, st>>>(S, jump[nlv - 1].p, D0, c0, d_cs);
-                    LZ_HIP(hipMemcpyAsync(&cs, d_cs, sizeof(cs), hipMemcpyDeviceToHost, st));
-                    LZ_HIP(hipStreamSynchronize(st));
+                    {
+                        hread rb(st);
+                        rb.add(&cs, (const chain_status*)d_cs);
+                        rb.sync();
+                    }
                     lap("link");
                     if (cs.err & 6) { restart_seq = true; break; }  // 2: LPF-start query overflow, 4: walk guard
                     if (dbg)
@@ -2389,15 +2422,18 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 u64 hc[3] = {0, 0, 0};
                 if (tail) {
                     seg_in tin;
-                    LZ_HIP(hipMemcpyAsync(&tin, g_sin.p + cs.term, sizeof(seg_in), hipMemcpyDeviceToHost, st));
                     seg_out prev{};
-                    if (nall >= 2) {
-                        u32 pg;
-                        LZ_HIP(hipMemcpyAsync(&pg, chain + nall - 2, 4, hipMemcpyDeviceToHost, st));
-                        LZ_HIP(hipStreamSynchronize(st));
-                        LZ_HIP(hipMemcpyAsync(&prev, g_sout.p + pg, sizeof(seg_out), hipMemcpyDeviceToHost, st));
+                    {
+                        hread rb(st);
+                        rb.add(&tin, (const seg_in*)(g_sin.p + cs.term));
+                        u32 pg = 0;
+                        if (nall >= 2) rb.add(&pg, (const u32*)(chain + nall - 2));
+                        rb.sync();
+                        if (nall >= 2) {
+                            rb.add(&prev, (const seg_out*)(g_sout.p + pg));
+                            rb.sync();
+                        }
                     }
-                    LZ_HIP(hipStreamSynchronize(st));
                     if (nall >= 2) {  // exact chain state entering the tail walk
                         tin.idxpos = prev.idxpos;
                         tin.zmask = prev.zmask;
@@ -2415,9 +2451,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     pos_t* d_tins = tail_ins_buf.get(16);
                     k_tail<<<1, 64, 0, st>>>(W, tin, fo, chain_fact, d_tc, d_tins);
                     LZ_HIP(hipGetLastError());
-                    LZ_HIP(hipMemcpyAsync(hc, d_tc, 24, hipMemcpyDeviceToHost, st));
-                    LZ_HIP(hipMemcpyAsync(tail_pairs, d_tins, sizeof(tail_pairs), hipMemcpyDeviceToHost, st));
-                    LZ_HIP(hipStreamSynchronize(st));
+                    {
+                        hread rb(st);
+                        rb.add(hc, (const u64*)d_tc, 3);
+                        rb.add(tail_pairs, (const pos_t*)d_tins, 16);
+                        rb.sync();
+                    }
                     if (hc[2]) throw error(-6, "greedy tail: insert overflow or guard tripped");
                     tail_count = hc[0];
                     lap("tail");
@@ -2427,7 +2466,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 // ---- the insert set the chain actually produced vs the speculation
                 LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
                 if (nchain)
-                    k_chain_inserts<<<cdiv((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2);
+                    k_chain_inserts<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2);
                 if (tail && hc[1]) {
                     pos_t* d_tins = tail_ins_buf.p;
                     k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], off, bmI2);
@@ -2478,9 +2517,10 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     if (!last) {
                         seg_in* d_ex = (seg_in*)(d_sq + 16);
                         k_exit_state<<<1, 1, 0, st>>>(S, cs.term, d_ex);
-                        LZ_HIP(hipMemcpyAsync(&exit_in, d_ex, sizeof(seg_in), hipMemcpyDeviceToHost, st));
-                        k_h_export<<<cdiv((u64)nchain * 64, 256), 256, 0, st>>>(T, G, S, chain, nchain, Hs);
-                        LZ_HIP(hipStreamSynchronize(st));
+                        hread rb(st);
+                        rb.add(&exit_in, (const seg_in*)d_ex);
+                        k_h_export<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(T, G, S, chain, nchain, Hs);
+                        rb.sync();
                     }
                     wfact = chain_fact + tail_count;
                     break;
@@ -2501,7 +2541,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 const u64 outside = bmb_scan(bm_bits{bmI2, bmIb}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
                 if (outside * 8 > nb) {
                     k_bm_or<<<gw, 256, 0, st>>>(bmI2, bmIb, nw, bmT);
-                    std::swap(g_bmI.p, g_bmI2.p);
+                    std::swap(g_bmI.p, g_bmI2.p), std::swap(g_bmI.cap, g_bmI2.cap);
                     bmI = g_bmI.p;
                     bmI2 = g_bmI2.p;
                     build_base(bmT);
@@ -2512,7 +2552,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 }
                 if (ny > nseg) {
                     // too many changes for dirty tracking to pay off: new state, re-walk everything
-                    std::swap(g_bmI.p, g_bmI2.p);
+                    std::swap(g_bmI.p, g_bmI2.p), std::swap(g_bmI.cap, g_bmI2.cap);
                     bmI = g_bmI.p;
                     bmI2 = g_bmI2.p;
                     set_state();
@@ -2528,7 +2568,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
                 k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + ny);
                 k_flip<<<cdiv(ny, 256), 256, 0, st>>>(W, d_y, d_j, ny, (u8*)W.rem, d_j + ny);
-                std::swap(g_bmI.p, g_bmI2.p);
+                std::swap(g_bmI.p, g_bmI2.p), std::swap(g_bmI.cap, g_bmI2.cap);
                 bmI = g_bmI.p;
                 bmI2 = g_bmI2.p;
                 LZ_HIP(hipMemsetAsync(d_cnt, 0, 4, st));

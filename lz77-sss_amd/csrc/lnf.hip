@@ -28,8 +28,7 @@
 namespace LZ_NS {
 
 __global__ void k_reverse(const u8* __restrict__ T, u64 n, u8* __restrict__ R) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) R[i] = T[n - 1 - i];
+    for (u64 i = gtid(); i < n; i += gstride()) R[i] = T[n - 1 - i];
 }
 __global__ void k_sa_lvl(const u32* __restrict__ prev, u32 cnt, u32 half, int want_max, u32* __restrict__ out) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -356,7 +355,7 @@ void engine::build_lpf_lnf(int opt) {
         LZ_HIP(hipMalloc(&d_text_rev, max_n + TEXT_PAD));
         LZ_HIP(hipMemsetAsync(d_text_rev, 0, max_n + TEXT_PAD, st));
     }
-    k_reverse<<<cdiv(N, 256), 256, 0, st>>>(d_text, N, d_text_rev);
+    k_reverse<<<capped_grid(N, 256), 256, 0, st>>>(d_text, N, d_text_rev);
     // LNF phrases of the reversed text (lz77_sss.hpp:385-393)
     build_sss(d_text_rev);
     build_sa_s(d_text_rev);

@@ -278,17 +278,17 @@ __device__ int wave_key_cmp(const u8* T, const run_tab& R, const pos_t* S, const
 __global__ __launch_bounds__(256) void k_group_verify(const u8* T, run_tab R, const pos_t* S, const pos_t* KL,
                                                       const u64* __restrict__ Hs, const u32* __restrict__ idx,
                                                       u32 s, u32* __restrict__ flag, u32* __restrict__ collide) {
-    const u64 t = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const u32 lane = threadIdx.x & 63;
-    if (t >= s) return;
-    if (t == 0 || Hs[t] != Hs[t - 1]) {
-        if (lane == 0) flag[t] = 1;
-        return;
-    }
-    const int c = wave_key_cmp(T, R, S, KL, idx[t - 1], idx[t], lane);
-    if (lane == 0) {
-        flag[t] = 0;
-        if (c != 0) atomicOr(collide, 1u);
+    for (u64 t = gtid() >> 6; t < s; t += gstride() >> 6) {  // one wave per key (grid-stride: s * 64 threads)
+        if (t == 0 || Hs[t] != Hs[t - 1]) {
+            if (lane == 0) flag[t] = 1;
+            continue;
+        }
+        const int c = wave_key_cmp(T, R, S, KL, idx[t - 1], idx[t], lane);
+        if (lane == 0) {
+            flag[t] = 0;
+            if (c != 0) atomicOr(collide, 1u);
+        }
     }
 }
 __global__ void k_reps(const u32* __restrict__ flag, const u32* __restrict__ grp, const u32* __restrict__ idx, u32 s,
@@ -327,9 +327,10 @@ __global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const 
                                                   const u32* __restrict__ sbeg, const u32* __restrict__ uoff, u32 nseg,
                                                   u32 nunits, const u32* __restrict__ in, u32* __restrict__ out, u32 w,
                                                   u32 opw) {
-    const u32 unit = (u32)(((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const u32 lane = threadIdx.x & 63;
-    if (unit >= nunits || unit >= uoff[nseg]) return;  // nunits: launch bound, uoff[nseg]: exact count
+    const u32 nu = min(nunits, uoff[nseg]);  // nunits: launch bound, uoff[nseg]: exact count
+    for (u64 uu = gtid() >> 6; uu < nu; uu += gstride() >> 6) {  // one wave per output run (grid-stride)
+    const u32 unit = (u32)uu;
     u32 lo = 0, hi = nseg;  // last k with uoff[k] <= unit
     while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
@@ -354,6 +355,7 @@ __global__ __launch_bounds__(256) void k_segmerge(const u8* T, run_tab R, const 
         else takeA = !(wave_key_cmp(T, R, S, KL, in[b0 + j], in[a0 + i], lane) < 0);
         const u32 v = takeA ? in[a0 + i++] : in[b0 + j++];
         if (lane == 0) out[p] = v;
+    }
     }
 }
 // ranks in a tie segment (tie with the previous or the next rank) and segment starts
@@ -455,7 +457,7 @@ void engine::build_sa_s(const u8* T) {
         u32* ctr = counters.get(16);
         LZ_HIP(hipMemsetAsync(ctr + 2, 0, 4, st));
         SA_DBG("hash sort");
-        k_group_verify<<<cdiv((u64)s * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, Hs, idx, s, flag, ctr + 2);
+        k_group_verify<<<capped_grid((u64)s * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, Hs, idx, s, flag, ctr + 2);
         scan_incl(flag, rank, s, scan_tmp, st);  // rank[t] = group id + 1
         const auto [collide, d] = rd2(ctr + 2, rank + s - 1, st);
         if (debug_enabled()) fprintf(stderr, "[sa_s] s=%u collide=%u\n", s, collide);
@@ -540,7 +542,7 @@ void engine::build_sa_s(const u8* T) {
                         LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tq, tb, units, uoff, (int)(nseg + 1), st));
                     }
                     const u32 nunits = cdiv(mt, opw) + nseg;
-                    k_segmerge<<<cdiv((u64)nunits * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, dsb, uoff, nseg, nunits,
+                    k_segmerge<<<capped_grid((u64)nunits * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, dsb, uoff, nseg, nunits,
                                                                             it_a, it_b, (u32)w, opw);
                     std::swap(it_a, it_b);
                     SA_DBG("segmerge");

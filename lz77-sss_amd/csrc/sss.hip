@@ -1799,7 +1799,7 @@ void engine::run_chains(u64 nanch, const u32* tiles, u64 m) {
         runs_valid = true;
         return;
     }
-    if (m >= (1ull << 32) - 1) throw error(LZ77SSS_EINVAL, "too many anchors for the run-chain scans");
+    if (m >= 0x7FFFFFFFull) throw error(LZ77SSS_EINVAL, "too many anchors for the run-chain scans (int item counts)");
     u32* ka = (u32*)run_scan_a.get(m);  // 2 x m u32
     u32* kb = (u32*)run_scan_b.get(m);
     k_run_keys<<<cdiv(m, 256), 256, 0, st>>>(run_p.p, run_hi.p, run_lo.p, nanch, tiles, m, ka, ka + m);

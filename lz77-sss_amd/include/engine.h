@@ -7,6 +7,7 @@
 
 #include <array>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <utility>
 #include <vector>
@@ -161,6 +162,8 @@ struct engine {
     dbuf<u32> g_bstart, g_abeg, g_abeg2, g_bmA, g_x32;
     dbuf<pos_t> g_xpos;
     dbuf<pos_t> g_stash;  // per segment: factors of its last speculative walk (csrc/greedy.hip STASH_CAP)
+    std::array<u64, 10> negpow_key{};  // (bases, pattern lengths) of the influence tables in tmp_greedy
+    const void* negpow_dev = nullptr;
     dbuf<pos_t> g_H;    // materialized gap-index table of the sequential completion
     dbuf<pos_t> g_Hs;   // greedy windows: last insert per slot before the window (pos + 1)
     // speculative blocks of a sharded run, walked as consecutive parts: the
@@ -240,27 +243,82 @@ struct engine {
     u64 factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int log2_override, bool log);  // csrc/smpl.hip
     void build_interval_samples(smpl_view& V, u64 nn, u64 za);                                         // csrc/smpl.hip
     u64 decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
-    u64 verify_factors(const pos_t* F, u64 nf, u64 n_out, const u8* T);  // csrc/decode.hip
+    u64 verify_factors(const pos_t* F, u64 nf, u64 n_out, const u8* T, u64* first_bad = nullptr);  // csrc/decode.hip
+    void debug_verify_phrases(const char* what);  // LZ77SSS_DEBUG_VERIFY (csrc/decode.hip)
+    void debug_verify_lce(const char* what);
     lce_view view(const u8* T) const;
 };
 
-// small host helpers
+// small host helpers.  Device values are read back through a pinned (page-locked) staging
+// slot per thread: a copy into pageable memory goes through the runtime's bounce buffer, one
+// more copy and a longer round trip on every count the host needs
+inline u8* pinned_slot() {
+    struct slot {
+        u8* p = nullptr;
+        slot() {
+            if (hipHostMalloc((void**)&p, 4096, hipHostMallocDefault) != hipSuccess) p = nullptr;
+        }
+        ~slot() {
+            if (p) (void)hipHostFree(p);
+        }
+    };
+    static thread_local slot s;
+    if (!s.p) throw error(-4 /* LZ77SSS_ENOMEM */, "pinned staging slot");
+    return s.p;
+}
 template <class T>
 static inline T rd1(const T* dptr, hipStream_t st) {
-    T v;
-    LZ_HIP(hipMemcpyAsync(&v, dptr, sizeof(T), hipMemcpyDeviceToHost, st));
+    static_assert(sizeof(T) <= 32);
+    u8* h = pinned_slot();
+    LZ_HIP(hipMemcpyAsync(h, dptr, sizeof(T), hipMemcpyDeviceToHost, st));
     LZ_HIP(hipStreamSynchronize(st));
+    T v;
+    std::memcpy(&v, h, sizeof(T));
     return v;
 }
+// several device values of any small types with one synchronization, staged in the pinned
+// slot (bytes 64.. of it; rd1 / rd2 use the first 64): add() enqueues, sync() waits and copies out
+struct hread {
+    hipStream_t st;
+    u8* h;
+    size_t off = 64;
+    struct item { void* dst; size_t off, bytes; };
+    item items[16];
+    int n = 0;
+    explicit hread(hipStream_t s) : st(s), h(pinned_slot()) {}
+    template <class T>
+    void add(T* dst, const T* src, size_t count = 1) {
+        const size_t b = sizeof(T) * count;
+        off = (off + 15) & ~(size_t)15;
+        if (off + b > 4096 || n == 16) throw error(-6 /* LZ77SSS_EINTERNAL */, "hread: staging slot full");
+        LZ_HIP(hipMemcpyAsync(h + off, src, b, hipMemcpyDeviceToHost, st));
+        items[n++] = {dst, off, b};
+        off += b;
+    }
+    void sync() {
+        LZ_HIP(hipStreamSynchronize(st));
+        for (int k = 0; k < n; k++) std::memcpy(items[k].dst, h + items[k].off, items[k].bytes);
+        n = 0;
+        off = 64;
+    }
+};
 // two device values with one synchronization
 template <class T>
 static inline std::pair<T, T> rd2(const T* a, const T* b, hipStream_t st) {
-    T v[2];
-    LZ_HIP(hipMemcpyAsync(&v[0], a, sizeof(T), hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipMemcpyAsync(&v[1], b, sizeof(T), hipMemcpyDeviceToHost, st));
+    static_assert(sizeof(T) <= 32);
+    u8* h = pinned_slot();
+    LZ_HIP(hipMemcpyAsync(h, a, sizeof(T), hipMemcpyDeviceToHost, st));
+    LZ_HIP(hipMemcpyAsync(h + 32, b, sizeof(T), hipMemcpyDeviceToHost, st));
     LZ_HIP(hipStreamSynchronize(st));
+    T v[2];
+    std::memcpy(&v[0], h, sizeof(T));
+    std::memcpy(&v[1], h + 32, sizeof(T));
     return {v[0], v[1]};
 }
 static inline unsigned cdiv(u64 a, u64 b) { return (unsigned)((a + b - 1) / b); }
+// blocks of a grid-stride launch over `items` work-items (at least 1, at most GRID_CAP)
+static inline unsigned capped_grid(u64 items, u64 threads) {
+    return (unsigned)std::min<u64>(std::max<u64>((items + threads - 1) / threads, 1), GRID_CAP);
+}
 
 }  // namespace LZ_NS

@@ -24,7 +24,7 @@ struct engine_if {
     virtual u64* factors_buf(u64 nf) = 0;    // device buffer for nf factors (decode input)
     virtual u64 decode(const u64* F, u64 nf, u64 n_out, u8* d_out, bool cmp_with_text) = 0;
     virtual u8* dec_out(u64 n) = 0;
-    virtual u64 verify() = 0;                // the factors against the loaded text (csrc/decode.hip)
+    virtual u64 verify(u64* first_bad) = 0;  // the factors against the loaded text (csrc/decode.hip)
     virtual void sss(u64* size, int* has_runs) = 0;
     virtual u64 sss_size() const = 0;
     virtual const u64* sss_ptr() const = 0;

@@ -35,6 +35,16 @@ constexpr u32 NONE = 0xFFFFFFFFu;
 // the SSS lane streams run past the end without bounds checks
 constexpr u64 TEXT_PAD = 64 * 1024;
 
+// A dispatch's grid size is a 32-bit count of work-items (the HSA kernel dispatch packet), so a
+// launch of 2^32 or more threads wraps around silently and covers only part of its domain (a
+// wave-per-item kernel over more than 2^26 items, a thread-per-byte kernel over more than 4 GiB).
+// Kernels whose domain can reach that loop over a capped grid (grid-stride), GRID_CAP blocks.
+constexpr uint64_t GRID_CAP = 1ull << 20;
+#ifdef __HIPCC__
+__device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t gstride() { return (uint64_t)gridDim.x * blockDim.x; }
+#endif
+
 // wall clock in ms (debug laps)
 inline double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();

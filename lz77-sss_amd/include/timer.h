@@ -11,21 +11,26 @@ namespace lz {
 struct phase_timer {
     hipStream_t st = nullptr;
     std::vector<std::pair<std::string, hipEvent_t>> marks;
-    bool on = false;
+    std::vector<hipEvent_t> pool;  // events are reused across calls (created once)
+    size_t used = 0;
     void begin(hipStream_t s) {
         st = s;
         clear();
         mark("start");
     }
     void mark(const char* name) {
-        hipEvent_t e;
-        LZ_HIP(hipEventCreate(&e));
+        if (used == pool.size()) {
+            hipEvent_t e;
+            LZ_HIP(hipEventCreate(&e));
+            pool.push_back(e);
+        }
+        hipEvent_t e = pool[used++];
         LZ_HIP(hipEventRecord(e, st));
         marks.emplace_back(name, e);
     }
     void clear() {
-        for (auto& m : marks) (void)hipEventDestroy(m.second);
         marks.clear();
+        used = 0;
     }
     // (name, ms since previous mark)
     std::vector<std::pair<std::string, double>> read() {
@@ -39,7 +44,9 @@ struct phase_timer {
         }
         return out;
     }
-    ~phase_timer() { clear(); }
+    ~phase_timer() {
+        for (auto& e : pool) (void)hipEventDestroy(e);
+    }
 };
 
 }  // namespace lz

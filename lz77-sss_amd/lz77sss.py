@@ -71,7 +71,7 @@ _SYMBOLS = {
     "lz77sss_decode_u32": (ctypes.c_int, [_P, _U64, _P, _U64]),
     "lz77sss_decode_u32_device": (ctypes.c_int, [_P, _U64, _P, _U64, ctypes.c_int]),
     "lz77sss_session_decode": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
-    "lz77sss_session_verify": (ctypes.c_int, [_P, ctypes.POINTER(_U64)]),
+    "lz77sss_session_verify": (ctypes.c_int, [_P, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "lz77sss_session_create": (ctypes.c_int, [ctypes.c_int, _U64, ctypes.POINTER(_P)]),
     "lz77sss_session_load": (ctypes.c_int, [_P, _P, _U64]),
     "lz77sss_session_factorize": (ctypes.c_int, [_P, ctypes.POINTER(Params), ctypes.POINTER(_U64)]),
@@ -279,11 +279,14 @@ class Session:
                                                      self.n if out else 0, ctypes.byref(m) if verify else None))
         return (buf[:self.n] if out else None), (m.value if verify else None)
 
-    def verify(self) -> int:
+    def verify(self, first: bool = False):
         """Positions of the loaded text that the last factorization does not reproduce, checked in
-        HBM without decoding (lz77sss_session_verify; 0 <=> decode(F) == T; any size)."""
-        b = _U64()
-        _check(load_library().lz77sss_session_verify(self._h, ctypes.byref(b)))
+        HBM without decoding (lz77sss_session_verify; 0 <=> decode(F) == T; any size).  With
+        first=True: (count, smallest bad position or None)."""
+        b, f = _U64(), _U64()
+        _check(load_library().lz77sss_session_verify(self._h, ctypes.byref(b), ctypes.byref(f)))
+        if first:
+            return b.value, (None if f.value == (1 << 64) - 1 else f.value)
         return b.value
 
     def sss(self):

@@ -196,3 +196,29 @@ def test_u64_greedy_windows(session64, orc, lz, window, monkeypatch):
     s, F = run64(session64, T)
     assert np.array_equal(F, orc.factorize64(T)[0])
     assert s.stats()[21] >= 2
+
+
+@pytest.mark.slow
+def test_c4_sharded_then_plain_past_2pow26_sync_positions(lz):
+    """configs[3]'s failure of round 3: on ONE pos_t = uint64_t session, the resident
+    sharded path (world 1) and then a plain factorize of a chr19-style text with more than 2^26 sync
+    positions.  Root cause: wave-per-key kernels launched with |S| * 64 > 2^32 work-items, which the
+    dispatch packet's 32-bit grid size wraps (k_group_verify left flags unwritten -> wrong SA_S and LCP
+    -> invalid LPF phrases, and k_reps wrote out of bounds); they now loop over a capped grid.  Both
+    streams are checked against the text in HBM (lz77sss_session_verify: no n-sized decode buffers)
+    and against each other."""
+    import torch
+    import sharded
+
+    n = 17 << 30  # |S| ~ 2n/512 = 7.1e7 > 2^26
+    torch.zeros(1, device="cuda")
+    with lz.Session(n, pos64=True) as s:
+        s.gen_genome(n, 59 << 20, 0.001, 7)
+        F1 = sharded.factorize_sharded_resident(s, n, 0, 1, 0)
+        assert s.stats()[0] > (1 << 26)
+        assert s.verify(first=True) == (0, None)
+        z = s.factorize()
+        assert s.verify(first=True) == (0, None)
+        F2 = torch.empty(2 * z, dtype=torch.int64, device="cuda:0")
+        s.copy_factors(F2.data_ptr(), 16 * z)
+        assert z == F1.shape[0] and torch.equal(F2.view(-1, 2), F1)
