@@ -343,8 +343,9 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
     (--size-mib); chr19: configs[3]'s chr19-style text of --size-gib GiB generated in HBM with
     pos_t = uint64_t (every rank holds the whole text: the phrases are replicated).  The greedy
     chain is walked block by block in rank order (speculative concurrent blocks are opt-in,
-    LZ77SSS_SPECULATE=1: sharded.py); total work is fixed (strong scaling).  After the timed region rank 0 checks the stream against a
-    one-GPU factorize of the same text in a fresh session."""
+    LZ77SSS_SPECULATE=1: sharded.py); total work is fixed (strong scaling).  After the timed
+    region rank 0 checks the stream against a one-GPU factorize of the same text on the same session, and
+    both against the text in HBM."""
     import sharded
 
     chr19 = args.workload == "chr19"
@@ -391,17 +392,12 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
     z = int(F.shape[0])
     same = None
     st = sess.stats()
+    verified = None
     if rank == 0:
-        # the one-GPU stream from a fresh session (the sharded session's buffers released first:
-        # at 50 GiB the two together do not fit, and the plain call is kept independent of it)
-        sess.close()
-        sess = lz.Session(n, device=local_rank, pos64=pos64)
-        if chr19:
-            sess.gen_genome(n, 59 << 20, 0.001, 7)
-        else:
-            T = make_text(lz, args.workload, n, 0)
-            sess.load(T)
-            del T
+        # the one-GPU stream of the same text on the same session (round 3 took it from a fresh session
+        # to dodge a fault whose cause, 2^32+ work-item launches past 2^26 sync positions, is fixed:
+        # DESIGN.md 8), both streams checked against the text in HBM (lz77sss_session_verify)
+        bad_sharded = sess.verify() if world == 1 else None
         t_1 = time.perf_counter()
         z1 = sess.factorize(device=local_rank)
         print(f"[bench --shard] one-GPU factorize {time.perf_counter() - t_1:.2f} s, z={z1}", file=sys.stderr,
@@ -410,6 +406,8 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
         if z1:
             sess.copy_factors(ref.data_ptr(), z1 * (16 if pos64 else 8))
         same = bool(z1 == z and torch.equal(ref[: 2 * z1].view(-1, 2), F))
+        verified = {"one_gpu_stream_bad_positions": int(sess.verify()),
+                    "sharded_stream_bad_positions": None if bad_sharded is None else int(bad_sharded)}
     if rank == 0:
         if chr19:
             data = "synthetic chr19-style (59 MiB ACGT base block, 0.1% mutations per copy), generated in HBM"
@@ -429,7 +427,7 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
                        "parallelism": f"sharded x{world}: S by block + all-gather, replicated phrases, "
                                       f"rank-ordered greedy blocks (speculative blocks opt-in: "
                                       f"LZ77SSS_SPECULATE=1), gathered emission",
-                       "factors": z, "equals_one_gpu_stream": same,
+                       "factors": z, "equals_one_gpu_stream": same, "verify_in_hbm": verified,
                        "sss_size": int(st[0]) if st else None, "lpf_phrases": int(st[2]) if st else None,
                        "text_gen_s": round(t_gen, 3), "rank0_phase_ms": phases},
             "roofline": None, "cpu_baseline": None,

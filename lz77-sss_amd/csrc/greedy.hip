@@ -28,6 +28,7 @@
 // one thread (k_tail) with an exact local model of the table.
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
+#include "../include/prim.h"
 #include "../include/lce_dev.h"
 
 #include <hipcub/hipcub.hpp>
@@ -1746,11 +1747,7 @@ __global__ void k_sum_u8(const u8* __restrict__ f, u64 m, u32* __restrict__ acc)
 // exclusive scan of cnt[0..m) into off[0..m] (off[m] = total); cnt needs m+1 entries
 template <class T>
 static void excl_scan_nr(T* cnt, T* off, u64 m, dbuf<u8>& tmp, hipStream_t st) {  // total left at off[m]
-    LZ_HIP(hipMemsetAsync(cnt + m, 0, sizeof(T), st));
-    size_t tb = 0;
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)(m + 1), st));
-    u8* t = tmp.get(tb);
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, cnt, off, (int)(m + 1), st));
+    excl_sum_total(cnt, off, m, tmp, st);  // (include/prim.h: one launch up to 64 Ki items)
 }
 template <class T>
 static T excl_scan(T* cnt, T* off, u64 m, dbuf<u8>& tmp, hipStream_t st) {

@@ -21,6 +21,7 @@
 //     loop's window start only matters for its last-phrase quirk
 //     (common.cpp:58-75) and is recovered by a max-scan along the path.
 #include "../include/engine.h"
+#include "../include/prim.h"
 #include "../include/lce_dev.h"
 
 #include <hipcub/hipcub.hpp>
@@ -268,11 +269,7 @@ __global__ void k_set1(u32* p, u32 v) { *p = v; }
 
 // exclusive scan (off[m] = total)
 static u32 xscan(u32* cnt, u32* off, u64 m, dbuf<u8>& tmp, hipStream_t st) {
-    LZ_HIP(hipMemsetAsync(cnt + m, 0, 4, st));
-    size_t tb = 0;
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)(m + 1), st));
-    u8* t = tmp.get(tb);
-    LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, cnt, off, (int)(m + 1), st));
+    excl_sum_total(cnt, off, m, tmp, st);
     return rd1(off + m, st);
 }
 

@@ -14,6 +14,7 @@
 //  4. Phrases are then formed independently per processed index and compacted
 //     in text order.
 #include "../include/engine.h"
+#include "../include/prim.h"
 #include "../include/lce_dev.h"
 
 #include <hipcub/hipcub.hpp>
@@ -350,12 +351,7 @@ void engine::build_lpf_naive(const u8* T) {
     u32* push = u32d.get(s);
     k_phrase_naive<<<g, 256, 0, st>>>(S.p, s, cd, mark, ph3, push);
     u32* off = mark;  // mark no longer needed
-    {
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, push, off, (int)s, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, push, off, (int)s, st));
-    }
+    scan_dev(push, off, s, s, 0u, 0u, op_sum{}, true, scan_tmp, st);
     {
         const auto [lo, lp] = rd2(off + s - 1, push + s - 1, st);
         num_phr = lo + lp;
@@ -396,23 +392,13 @@ void engine::build_lpf_opt(const u8* T) {
     pos_t* Em = p_Em.get(s);
     k_masked_E<<<g, 256, 0, st>>>(cd, mark, s, Em);
     pos_t* lst = p_lst.get(s);
-    {
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, Em, lst, max_op{}, (pos_t)0, (int)s, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveScan(t, tb, Em, lst, max_op{}, (pos_t)0, (int)s, st));
-    }
+    scan_dev(Em, lst, s, s, (pos_t)0, (pos_t)0, op_max{}, true, scan_tmp, st);
     // 4. phrases + compaction
     pos_t* ph3 = p_ph3.get((u64)s * 3);
     u32* push = u32d.get(s);
     k_phrase<<<g, 256, 0, st>>>(S.p, s, cd, mark, lst, ph3, push);
     u32* off = mark;  // mark no longer needed after k_phrase
-    {
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, push, off, (int)s, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, push, off, (int)s, st));
-    }
+    scan_dev(push, off, s, s, 0u, 0u, op_sum{}, true, scan_tmp, st);
     const auto [last_off, last_push] = rd2(off + s - 1, push + s - 1, st);
     num_phr = last_off + last_push;
     pos_t* out = lpf.get((u64)(num_phr + 1) * 3);

@@ -11,6 +11,7 @@
 // until all ranks are distinct.  LCP between SA-neighbours comes from binary
 // lifting over the stored R_h levels plus one bounded key comparison.
 #include "../include/engine.h"
+#include "../include/prim.h"
 #include "../include/lce_dev.h"
 #include "../include/msort_dev.h"
 
@@ -418,10 +419,7 @@ __global__ void k_key_to_grp(const u32* __restrict__ flag, const u32* __restrict
         }                                                                             \
     } while (0)
 static void scan_incl(u32* in, u32* out, u32 m, dbuf<u8>& tmp, hipStream_t st) {
-    size_t tb = 0;
-    LZ_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, in, out, (int)m, st));
-    u8* t = tmp.get(tb);
-    LZ_HIP(hipcub::DeviceScan::InclusiveSum(t, tb, in, out, (int)m, st));
+    incl_sum(in, out, m, tmp, st);  // (include/prim.h: one launch up to 64 Ki items)
 }
 
 void engine::build_sa_s(const u8* T) {
@@ -535,12 +533,7 @@ void engine::build_sa_s(const u8* T) {
                     const u32 opw = (u32)std::min<u64>(opw_cap, 2 * w);  // short output runs: more waves on long segments
                     // no host read-back: launch for the upper bound cdiv(members, opw) + segments
                     k_seg_units<<<cdiv(nseg + 1, 256), 256, 0, st>>>(dsb, nseg, opw, units);
-                    {
-                        size_t tb = 0;
-                        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, units, uoff, (int)(nseg + 1), st));
-                        u8* tq = scan_tmp.get(tb);
-                        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tq, tb, units, uoff, (int)(nseg + 1), st));
-                    }
+                    scan_dev(units, uoff, (u64)nseg + 1, (u64)nseg + 1, 0u, 0u, op_sum{}, true, scan_tmp, st);
                     const u32 nunits = cdiv(mt, opw) + nseg;
                     k_segmerge<<<capped_grid((u64)nunits * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, dsb, uoff, nseg, nunits,
                                                                             it_a, it_b, (u32)w, opw);

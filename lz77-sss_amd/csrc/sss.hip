@@ -24,6 +24,7 @@
 //   k_sss_compact-- per-stripe outputs -> sorted S
 #include "../../include/lz77sss.h"
 #include "../include/engine.h"
+#include "../include/prim.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -1803,13 +1804,8 @@ void engine::run_chains(u64 nanch, const u32* tiles, u64 m) {
     u32* ka = (u32*)run_scan_a.get(m);  // 2 x m u32
     u32* kb = (u32*)run_scan_b.get(m);
     k_run_keys<<<cdiv(m, 256), 256, 0, st>>>(run_p.p, run_hi.p, run_lo.p, nanch, tiles, m, ka, ka + m);
-    size_t tb = 0;
-    LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, ka, kb, hipcub::Min(), (int)m, st));
-    size_t tb2 = 0;
-    LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, ka + m, kb + m, hipcub::Max(), (int)m, st));
-    u8* t = scan_tmp.get(std::max(tb, tb2));
-    LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, ka, kb, hipcub::Min(), (int)m, st));
-    LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb2, ka + m, kb + m, hipcub::Max(), (int)m, st));
+    scan_dev(ka, kb, m, m, 0xFFFFFFFFu, 0xFFFFFFFFu, op_min{}, false, scan_tmp, st);
+    scan_dev(ka + m, kb + m, m, m, 0u, 0u, op_max{}, false, scan_tmp, st);
     k_run_apply<<<cdiv(m, 256), 256, 0, st>>>(kb, kb + m, run_p.p, tmp_bytes.p, nanch, tiles, m, run_hi.p, run_lo.p);
     LZ_HIP(hipGetLastError());
     runs_valid = true;
@@ -2006,13 +2002,7 @@ void engine::build_sss(const u8* T) {
 
     // exclusive scan of stripe counts -> offsets; total = |S|
     u32* off = u32a.get(nlanes + 1);
-    auto scan_counts = [&]() {
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lc, off, (int)(nlanes + 1), st));
-        u8* tmp = scan_tmp.get(tb);
-        LZ_HIP(hipMemsetAsync(lc + nlanes, 0, sizeof(u32), st));
-        LZ_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, lc, off, (int)(nlanes + 1), st));
-    };
+    auto scan_counts = [&]() { excl_sum_total(lc, off, nlanes, scan_tmp, st); };
     scan_counts();
     LZ_HIP(hipMemcpyAsync(hp, ctr, 2 * sizeof(u32), hipMemcpyDeviceToHost, st));
     LZ_HIP(hipMemcpyAsync(hp + 2, off + nlanes, sizeof(u32), hipMemcpyDeviceToHost, st));
