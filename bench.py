@@ -88,6 +88,7 @@ def pmc_traffic(workload: str, n: int, mode: str = "approx"):
 
 
 PHR = {"lpf_opt": 2, "lpf_lnf_opt": 3}
+TRANSF = {"naive": 0, "with_samples": 1, "without_samples": 2, "full_sa": 3}
 
 
 def cpu_model() -> str:
@@ -164,6 +165,9 @@ def main():
     ap.add_argument("--mode", default="approx", choices=["approx", "exact", "sss"],
                     help="approx = configs[1]/[2] (3-aprx); exact = configs[4] (exact factorization); "
                          "sss = the sharded pos_t=uint64 sync-set pass of configs[3] (chr19-style text)")
+    ap.add_argument("--transf-mode", default="with_samples", choices=["naive", "with_samples", "without_samples", "full_sa"],
+                    help="--mode exact: factorize_exact's transform_mode (configs[4]: with_samples, the sample index "
+                         "with interval sampling; full_sa is the device extension)")
     ap.add_argument("--size-gib", type=float, default=50.0,
                     help="--mode sss / --workload chr19: text size in GiB (configs[3]: 50)")
     ap.add_argument("--cpu-sample-mib", type=int, default=-1,
@@ -213,7 +217,7 @@ def main():
     out_buf = [None]
 
     def step():
-        z = sess.factorize_exact(device=local_rank) if exact else \
+        z = sess.factorize_exact(TRANSF[args.transf_mode], device=local_rank) if exact else \
             sess.factorize(device=local_rank, phr_mode=PHR[args.phr_mode])
         if out_buf[0] is not None and z * 8 <= out_buf[0].numel():
             sess.copy_factors(out_buf[0].data_ptr(), out_buf[0].numel())
@@ -264,7 +268,8 @@ def main():
         bytes_launch = kern_bytes[-1]
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
         out = {
-            "metric": "factorization MB/s (exact greedy LZ77, factorize_exact, tau=512)" if exact else
+            "metric": f"factorization MB/s (exact greedy LZ77, factorize_exact<greedy, lpf_opt, {args.transf_mode}>, "
+                      f"tau=512)" if exact else
                       f"factorization MB/s (3-aprx LZ77, greedy + {args.phr_mode}, tau=512)",
             "value": round(value, 2),
             "unit": "MB/s",
@@ -281,7 +286,8 @@ def main():
             "config": {
                 "workload": f"{args.workload} n={n} ({args.size_mib} MiB) per GPU, pos_t=uint32",
                 "n": n, "tau": 512, "phr_mode": args.phr_mode, "fact_mode": "greedy", "virtual_p": 1,
-                "mode": "exact (configs[4])" if exact else "3-aprx",
+                "mode": f"exact (configs[4]), transf_mode={args.transf_mode}" if exact else
+                        ("3-aprx (configs[2])" if args.phr_mode == "lpf_lnf_opt" else "3-aprx (configs[1])"),
                 "parallelism": f"independent-texts x{world}" if world > 1 else "single GPU",
                 "factors_to_host_in_step": True,
                 "factors": int(z), "comp_ratio": round(n / max(z, 1), 2),

@@ -171,12 +171,17 @@ __device__ __forceinline__ u64 kh_pow(u64 e) {  // R^e mod 2^64
     }
     return r;
 }
-__global__ void k_key_prep(const pos_t* __restrict__ KL, u32 s, u64* __restrict__ H, u32* __restrict__ CC) {
+// (one launch: the key lengths (k_key_len's rule), H = mix(len), the piece counts, idx = iota)
+__global__ void k_key_prep(const pos_t* __restrict__ S, u32 s, u64 n, pos_t* __restrict__ KL, u64* __restrict__ H,
+                           u32* __restrict__ CC, u32* __restrict__ idx) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s) return;
-    const u64 len = KL[k];
+    const u64 beg = S[k];
+    const u64 len = min<u64>((k + 1 < s) ? max<u64>(3 * TAU, (u64)S[k + 1] - beg + 2 * TAU) : n - beg, n - beg);
+    KL[k] = (pos_t)len;
     H[k] = mix64(len ^ 0xd6e8feb86659fd93ull);
     CC[k] = (u32)max<u64>(1, (len + KH_CHUNK - 1) / KH_CHUNK);
+    idx[k] = (u32)k;
 }
 // OFF = inclusive scan of the piece counts; wave w hashes pieces [w*per, (w+1)*per)
 __global__ __launch_bounds__(256) void k_key_hash(const u8* __restrict__ T, const pos_t* __restrict__ S,
@@ -430,7 +435,6 @@ void engine::build_sa_s(const u8* T) {
     const pos_t* dS = S.p;
     pos_t* KL = key_len.get(s);
     const unsigned g = cdiv(s, 256);
-    k_key_len<<<g, 256, 0, st>>>(dS, s, n, KL);
     // ---- R_0: lexicographic rank of the keys (equal keys share a rank)
     u32* idx_in = u32a.get(s);
     u32* idx = u32b.get(s);
@@ -443,11 +447,10 @@ void engine::build_sa_s(const u8* T) {
         u64* H = u64a.get(s);
         u64* Hs = u64b.get(s);
         u32* CC = u32e.get(s);
-        k_key_prep<<<g, 256, 0, st>>>(KL, s, H, CC);
+        k_key_prep<<<g, 256, 0, st>>>(dS, s, n, KL, H, CC, idx_in);
         scan_incl(CC, CC, s, scan_tmp, st);
         k_key_hash<<<KH_WAVES * 64 / 256, 256, 0, st>>>(T, dS, KL, CC, s, runs(), H);
         SA_DBG("key hash");
-        k_iota<<<g, 256, 0, st>>>(idx_in, s);
         size_t tb = 0;
         LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, H, Hs, idx_in, idx, (int)s, 0, 64, st));
         u8* t = scan_tmp.get(tb);
@@ -469,14 +472,18 @@ void engine::build_sa_s(const u8* T) {
                 u32* v2 = sa_tmp2.get(d);
                 u64* wk = u64b.get(2 * (u64)d);  // sorted hashes no longer needed
                 u64* wk2 = wk + d;
+                // double buffers: the sort alternates between the two halves, no copy per word
+                hipcub::DoubleBuffer<u64> kb(wk, wk2);
+                hipcub::DoubleBuffer<u32> vb(srt, v2);
                 size_t tb2 = 0;
-                LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, wk, wk2, srt, v2, (int)d, 0, 64, st));
+                LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, kb, vb, (int)d, 0, 64, st));
                 u8* t2 = scan_tmp.get(tb2);
                 for (int i = (int)PRESORT_WORDS - 1; i >= 0; i--) {
-                    k_word_keys<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, srt, d, (u32)i, wk);
-                    LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, wk, wk2, srt, v2, (int)d, 0, 64, st));
-                    LZ_HIP(hipMemcpyAsync(srt, v2, (size_t)d * 4, hipMemcpyDeviceToDevice, st));
+                    k_word_keys<<<cdiv(d, 256), 256, 0, st>>>(T, dS, KL, vb.Current(), d, (u32)i, kb.Current());
+                    LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t2, tb2, kb, vb, (int)d, 0, 64, st));
                 }
+                if (vb.Current() != srt)
+                    LZ_HIP(hipMemcpyAsync(srt, vb.Current(), (size_t)d * 4, hipMemcpyDeviceToDevice, st));
             }
             SA_DBG("presort");
             u8* tie = tmp_bytes.get(d);
@@ -529,11 +536,16 @@ void engine::build_sa_s(const u8* T) {
                 u64 opw_cap = 16;
                 while (opw_cap > 4 && mt / opw_cap < 16384) opw_cap /= 2;
                 if (const char* e = std::getenv("LZ77SSS_SEGMERGE_OPW")) opw_cap = std::max<u64>(1, std::strtoull(e, nullptr, 10));
+                u32 opw_prev = 0;
                 for (u64 w = 1; w < maxl; w *= 2) {
                     const u32 opw = (u32)std::min<u64>(opw_cap, 2 * w);  // short output runs: more waves on long segments
-                    // no host read-back: launch for the upper bound cdiv(members, opw) + segments
-                    k_seg_units<<<cdiv(nseg + 1, 256), 256, 0, st>>>(dsb, nseg, opw, units);
-                    scan_dev(units, uoff, (u64)nseg + 1, (u64)nseg + 1, 0u, 0u, op_sum{}, true, scan_tmp, st);
+                    // no host read-back: launch for the upper bound cdiv(members, opw) + segments; the
+                    // unit offsets depend on opw only (it saturates at opw_cap after a few passes)
+                    if (opw != opw_prev) {
+                        k_seg_units<<<cdiv(nseg + 1, 256), 256, 0, st>>>(dsb, nseg, opw, units);
+                        scan_dev(units, uoff, (u64)nseg + 1, (u64)nseg + 1, 0u, 0u, op_sum{}, true, scan_tmp, st);
+                        opw_prev = opw;
+                    }
                     const u32 nunits = cdiv(mt, opw) + nseg;
                     k_segmerge<<<capped_grid((u64)nunits * 64, 256), 256, 0, st>>>(T, runs(), dS, KL, dsb, uoff, nseg, nunits,
                                                                             it_a, it_b, (u32)w, opw);
