@@ -107,6 +107,7 @@ u64 engine::emit_skip_phrases() {
 
 void engine::prepare_phrases(int phr_mode, bool external_sss) {
     const bool dbg = debug_enabled();
+    phr_info.valid = false;
     if (std::getenv("LZ77SSS_LCE_DEBUG") && !lce_dbg) {
         LZ_HIP(hipMalloc(&lce_dbg, 8 * sizeof(unsigned long long)));
         LZ_HIP(hipMemset(lce_dbg, 0, 8 * sizeof(unsigned long long)));
@@ -168,7 +169,7 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
         throw error(LZ77SSS_EINVAL, sizeof(pos_t) == 4 ? "n too large for pos_t = uint32_t" : "n too large");
     num_fact = 0;
     last_fact_mode = fact_mode;
-    stats.assign(24, 0);
+    stats.assign(28, 0);
     if (n == 0) return 0;
     const auto t_start = std::chrono::steady_clock::now();
     const u64 peak0 = g_dev_bytes.load();
@@ -189,7 +190,7 @@ u64 engine::factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, in
                      (unsigned long long)num_fact, (unsigned long long)bad, (unsigned long long)first);
     }
     if (debug_enabled()) std::fprintf(stderr, "[lz77sss-debug] done greedy (|S|=%u phrases=%u)\n", s, num_phr);
-    LZ_HIP(hipStreamSynchronize(st));
+    stream_wait(st);
     if (log) {
         for (auto& [name, ms] : timer.read()) std::fprintf(stderr, "[lz77sss] %-10s %9.3f ms\n", name.c_str(), ms);
         std::fprintf(stderr, "[lz77sss] n=%llu |S|=%u phrases=%u factors=%llu outer=%llu rounds=%llu\n",
@@ -234,7 +235,7 @@ static u64 block_prepare(engine& E, int phr_mode, bool external_sss, int log2_ov
     if (E.n > POS_MAX_N) throw error(LZ77SSS_EINVAL, "n too large for pos_t");
     E.num_fact = 0;
     E.last_fact_mode = LZ77SSS_GREEDY;
-    E.stats.assign(24, 0);
+    E.stats.assign(28, 0);
     E.spec_track = false;
     E.timer.begin(E.st);
     E.prepare_phrases(phr_mode, external_sss);

@@ -361,7 +361,7 @@ u64 engine::factorize_exact(bool log) {
     LZ_HIP(hipSetDevice(device));
     if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
     num_fact = 0;
-    stats.assign(24, 0);
+    stats.assign(28, 0);
     x_rounds = 0;
     if (n == 0) return 0;
     timer.begin(st);

@@ -32,6 +32,7 @@
 #include "../include/lce_dev.h"
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
@@ -1195,6 +1196,24 @@ __global__ void k_gap_bitmaps_phr(const pos_t* __restrict__ P, u32 m, pos_t N, p
         if (P[3 * k + 1] - P[3 * k] <= 48 && pb < pe) bm_set_range(bmSup, pb - off, pe - off);
     }
 }
+// OR `mask` into bm[w]; counts the newly set bits (c[0]) and those of them not in the insert set
+// bmI (c[1]) -- exact whatever the overlaps between ranges, as every bit is new exactly once
+__device__ __forceinline__ void bm_or_count(u32* bm, u64 w, u32 mask, const u32* bmI, u32* c) {
+    const u32 nw = mask & ~atomicOr(&bm[w], mask);
+    c[0] += __popc(nw);
+    c[1] += __popc(nw & ~bmI[w]);
+}
+__device__ __forceinline__ void wave_count_add(u32* c, u32* acc) {  // whole wave; lane 0 adds the sums
+    u32 a = c[0], b = c[1];
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_down(a, o, 64);
+        b += __shfl_down(b, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (a) atomicAdd(&acc[0], a);
+        if (b) atomicAdd(&acc[1], b);
+    }
+}
 __global__ void k_bm_xor(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (w < nw) x[w] = a[w] ^ b[w];
@@ -1349,13 +1368,16 @@ __global__ void k_iv_chunks(const pos_t* __restrict__ st, const pos_t* __restric
 }
 // rem[r] = base position r not in I
 __global__ void k_rem_from_bm(const pos_t* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, pos_t off,
-                              u8* __restrict__ rem, pos_t* __restrict__ iposr) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nb) return;
-    const pos_t p = ipos[r], q = p - off;
-    const bool in = (bmI[q >> 5] >> (q & 31)) & 1;
-    rem[r] = in ? 0 : 1;
-    if (iposr) iposr[r] = p | (in ? (pos_t)0 : POS_RFLAG);
+                              u8* __restrict__ rem, pos_t* __restrict__ iposr, u32* __restrict__ n_in = nullptr) {
+    u32 cnt = 0;
+    for (u64 r = gtid(); r < nb; r += gstride()) {  // grid-stride: one count atomic per block
+        const pos_t p = ipos[r], q = p - off;
+        const bool in = (bmI[q >> 5] >> (q & 31)) & 1;
+        rem[r] = in ? 0 : 1;
+        if (iposr) iposr[r] = p | (in ? (pos_t)0 : POS_RFLAG);
+        cnt += in ? 1u : 0u;
+    }
+    if (n_in) block_add(n_in, cnt);  // |I| when I lies within the base set
 }
 
 // walks over a list of segment ids (outputs in the table; WRITE: factors at offs)
@@ -1540,18 +1562,52 @@ __global__ void k_chain_expand(jump_levels JL, u32 len, u32 c0, u32* __restrict_
 // I' bitmap: what the chain inserted below nt ([start, e) + LPF-start queries)
 // (clipped to the window's bitmap range [off, hi), hi <= nt)
 __global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, pos_t hi, pos_t off,
-                                u32* __restrict__ bm) {
+                                u32* __restrict__ bm, const u32* __restrict__ bmI = nullptr, u32* __restrict__ acc = nullptr) {
     const u32 lane = threadIdx.x & 63;
+    u32 c[2] = {0, 0};
     for (u64 k = gtid() >> 6; k < cnt; k += gstride() >> 6) {  // one wave per chain node (grid-stride)
         const u32 g = chain[k];
         const seg_out& o = S.sout[g];
         const pos_t a = S.sin[g].start, b = min(o.e, hi);
-        if (a < b) bm_set_range_wave(bm, a - off, b - off, lane);
+        if (a < b) {
+            if (!acc) {
+                bm_set_range_wave(bm, a - off, b - off, lane);
+            } else {
+                // 8 words per lane and step: the returning atomics of a long gap (one wave walks it)
+                // are in flight together instead of one round trip per word
+                const pos_t x0 = a - off, x1 = b - off;
+                const u64 w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
+                for (u64 wb = w0 + lane; wb <= w1; wb += 64 * 8) {
+                    u32 old[8], msk[8], iw[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const u64 w = wb + 64ull * j;
+                        msk[j] = 0;
+                        if (w > w1) continue;
+                        u32 mask = 0xFFFFFFFFu;
+                        if (w == w0) mask &= ~((1u << (x0 & 31)) - 1);
+                        if (w == w1 && (x1 & 31)) mask &= (1u << (x1 & 31)) - 1;
+                        msk[j] = mask;
+                        old[j] = atomicOr(&bm[w], mask);
+                        iw[j] = bmI[w];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        if (!msk[j]) continue;
+                        const u32 nw = msk[j] & ~old[j];
+                        c[0] += __popc(nw);
+                        c[1] += __popc(nw & ~iw[j]);
+                    }
+                }
+            }
+        }
         if (lane < o.nsingle && lane < 4 && o.single[lane] < hi) {
             const pos_t r = o.single[lane] - off;
-            atomicOr(&bm[r >> 5], 1u << (r & 31));
+            if (acc) bm_or_count(bm, r >> 5, 1u << (r & 31), bmI, c);
+            else atomicOr(&bm[r >> 5], 1u << (r & 31));
         }
     }
+    if (acc) wave_count_add(c, acc);
 }
 // the window's entry segment: the exact chain state handed over by the previous window
 // (a default segment starting there takes it over); *c0 = its id
@@ -1699,9 +1755,23 @@ __global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, 
     }
     *out = c;
 }
-__global__ void k_set_pairs(const pos_t* __restrict__ pairs, u32 np, pos_t off, u32* __restrict__ bm) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < np && pairs[2 * k] >= off) bm_set_range(bm, pairs[2 * k] - off, pairs[2 * k + 1] - off);
+__global__ void k_set_pairs(const pos_t* __restrict__ pairs, u32 np, pos_t off, u32* __restrict__ bm,
+                            const u32* __restrict__ bmI = nullptr, u32* __restrict__ acc = nullptr) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // one wave
+    u32 c[2] = {0, 0};
+    if (k < np && pairs[2 * k] >= off) {
+        pos_t a = pairs[2 * k] - off;
+        const pos_t b = pairs[2 * k + 1] - off;
+        while (a < b) {
+            const u64 w = a >> 5;
+            const u32 lo = a & 31, hi = (u32)min<u64>(32u, lo + (u64)(b - a));
+            const u32 mask = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & ~((1u << lo) - 1);
+            if (acc) bm_or_count(bm, w, mask, bmI, c);
+            else atomicOr(&bm[w], mask);
+            a += hi - lo;
+        }
+    }
+    if (acc) wave_count_add(c, acc);
 }
 __global__ void k_chain_nfact(seg_tab S, const u32* __restrict__ chain, u32 cnt, u64* __restrict__ nf) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1755,6 +1825,120 @@ static T excl_scan(T* cnt, T* off, u64 m, dbuf<u8>& tmp, hipStream_t st) {
     return rd1(off + m, st);
 }
 
+// LZ77SSS_LSD_CHECK: first index where two u32 arrays differ (atomic min), and the count
+__global__ void k_first_diff_u32(const u32* __restrict__ a, const u32* __restrict__ b, u64 m, u64* __restrict__ out) {
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < m && a[t] != b[t]) {
+        atomicMin((unsigned long long*)&out[0], (unsigned long long)t);
+        atomicAdd((unsigned long long*)&out[1], 1ull);
+    }
+}
+// ---------------------------------------------------------------------------
+// LSD radix sort of the base entries (key = slot or dense slot id, value = entry id) by
+// reduce-then-scan: per digit a histogram pass over the tiles of its input, a
+// scan, a scatter pass.  A tile is block-sorted in LDS on its digit and leaves as
+// contiguous runs per digit (coalesced); pass 0 reads the raw slots (the dense-id map is
+// applied on the fly: no separate key array), the last pass writes only the entry ids plus
+// the first sorted index of every key (atomic min per key and tile).  Against rocprim's
+// onesweep on the dense rr keys (a dense-key pass, two passes writing keys and ids, a
+// predecessor/head pass): 32 instead of about 52 bytes per entry moved.
+constexpr u32 LS_T = 256, LS_IPT = 8, LS_TILE = LS_T * LS_IPT, LS_DB = 7, LS_NB = 1u << LS_DB, LS_MAXP = 5;
+struct ls_dense {  // pass-0 key of entry e: the dense id of its slot
+    const u32* keys;
+    const u32* pbm;
+    const u32* pwp;
+    __device__ __forceinline__ u32 operator()(u64 e) const { return slot_rank(pbm, pwp, keys[e]); }
+};
+struct ls_plain {
+    const u32* keys;
+    __device__ __forceinline__ u32 operator()(u64 e) const { return keys[e]; }
+};
+// H[digit * ntile + tile]: counts of digit `pass` per tile of this pass's input (the tiles of pass
+// p > 0 are tiles of pass p - 1's output, so every pass counts its own input)
+template <class KF>
+__global__ __launch_bounds__(LS_T) void k_ls_hist(KF kf, u64 m, u32 pass, u32 ntile, u32* __restrict__ H) {
+    __shared__ u32 h[LS_NB];
+    for (u32 i = threadIdx.x; i < LS_NB; i += LS_T) h[i] = 0;
+    __syncthreads();
+    const u64 t0 = (u64)blockIdx.x * LS_TILE;
+    const u32 sh = pass * LS_DB;
+    for (u32 i = 0; i < LS_IPT; i++) {
+        const u64 e = t0 + (u64)i * LS_T + threadIdx.x;
+        if (e >= m) break;
+        atomicAdd(&h[(kf(e) >> sh) & (LS_NB - 1)], 1u);
+    }
+    __syncthreads();
+    for (u32 i = threadIdx.x; i < LS_NB; i += LS_T) H[(u64)i * ntile + blockIdx.x] = h[i];
+}
+// one pass: items of tile `blockIdx` (pass 0: key kf(e), value e; later: kin / vin), sorted in LDS on
+// digit `pass`, written at G[digit] + (rank within the digit).  LAST: values only, plus
+// head[key] = min sorted index of the key
+template <class KF, bool FIRST, bool LAST>
+__global__ __launch_bounds__(LS_T) void k_ls_scatter(KF kf, const u32* __restrict__ kin, const u32* __restrict__ vin, u64 m,
+                                                     u32 pass, u32 ntile, const u32* __restrict__ G, u32* __restrict__ kout,
+                                                     u32* __restrict__ vout, u32* __restrict__ head) {
+    using bsort = rocprim::block_radix_sort<u32, LS_T, LS_IPT, u32>;
+    __shared__ union {
+        typename bsort::storage_type sort;
+        struct { u32 dig[LS_TILE]; u32 start[LS_NB]; u32 base[LS_NB]; } w;
+    } sm;
+    const u64 t0 = (u64)blockIdx.x * LS_TILE;
+    u32 k[LS_IPT], v[LS_IPT];
+#pragma unroll
+    for (u32 i = 0; i < LS_IPT; i++) {
+        const u64 e = t0 + (u64)threadIdx.x * LS_IPT + i;
+        if (e < m) {
+            k[i] = FIRST ? kf(e) : kin[e];
+            v[i] = FIRST ? (u32)e : vin[e];
+        } else {
+            k[i] = 0xFFFFFFFFu;  // past the end: sorts after every item of the top digit
+            v[i] = NONE;
+        }
+    }
+    const u32 b0 = pass * LS_DB;
+    bsort().sort_to_striped(k, v, sm.sort, b0, min(b0 + LS_DB, 32u));
+    __syncthreads();
+    // sorted position j = i * LS_T + tid; the first position of every digit in the tile
+    const u32 nvalid = (u32)min<u64>(LS_TILE, m - t0);
+#pragma unroll
+    for (u32 i = 0; i < LS_IPT; i++) sm.w.dig[i * LS_T + threadIdx.x] = (k[i] >> b0) & (LS_NB - 1);
+    __syncthreads();
+#pragma unroll
+    for (u32 i = 0; i < LS_IPT; i++) {
+        const u32 j = i * LS_T + threadIdx.x;
+        const u32 d = sm.w.dig[j];
+        if (j < nvalid && (j == 0 || sm.w.dig[j - 1] != d)) sm.w.start[d] = j;
+    }
+    for (u32 d = threadIdx.x; d < LS_NB; d += LS_T) sm.w.base[d] = G[(u64)d * ntile + blockIdx.x];
+    __syncthreads();
+#pragma unroll
+    for (u32 i = 0; i < LS_IPT; i++) {
+        const u32 j = i * LS_T + threadIdx.x;
+        if (j >= nvalid) break;
+        const u32 d = sm.w.dig[j];
+        const u32 pos = sm.w.base[d] + (j - sm.w.start[d]);
+        vout[pos] = v[i];
+        if (!LAST) kout[pos] = k[i];
+    }
+    if (LAST && head) {
+        // the first item of every key in this tile (sorted by the whole key: the earlier passes
+        // ordered the tile's input by the lower digits)
+        __syncthreads();
+#pragma unroll
+        for (u32 i = 0; i < LS_IPT; i++) sm.w.dig[i * LS_T + threadIdx.x] = k[i];
+        __syncthreads();
+#pragma unroll
+        for (u32 i = 0; i < LS_IPT; i++) {
+            const u32 j = i * LS_T + threadIdx.x;
+            if (j >= nvalid) break;
+            if (j == 0 || sm.w.dig[j - 1] != k[i]) {
+                const u32 d = (k[i] >> b0) & (LS_NB - 1);
+                atomicMin(&head[k[i]], sm.w.base[d] + (j - sm.w.start[d]));
+            }
+        }
+    }
+}
+
 // gap-index slot count (the carried table's entries) of the current phrases
 u64 engine::carried_entries(int log2_override) {
     const pos_t N = (pos_t)n;
@@ -1792,11 +1976,14 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
     const pos_t N = (pos_t)n;
     const u32 m = num_phr;  // phrases; P[m] = sentinel
     pos_t* P = lpf.get((u64)(m + 1) * 3);
-    k_put3<<<1, 1, 0, st>>>(P + 3 * (u64)m, N, N + 1, 0);
     // ---- phrase statistics -> parameters (lz77_sss.hpp:420-461)
     u64 num_lpf = m, num_gaps = 1;
     pos_t len_lpf_phr = 0;
-    if (m > 0) {
+    if (!phr_info.valid) k_put3<<<1, 1, 0, st>>>(P + 3 * (u64)m, N, N + 1, 0);
+    if (phr_info.valid && m > 0) {
+        len_lpf_phr = (pos_t)phr_info.len;  // (build_lpf_opt: statistics and sentinel done)
+        num_gaps = phr_info.gaps;
+    } else if (m > 0) {
         u64* acc = counters64.get(16) + 2;
         LZ_HIP(hipMemsetAsync(acc, 0, 16, st));
         k_phrase_info<<<cdiv(m, 256), 256, 0, st>>>(P, m, N, acc);
@@ -1835,7 +2022,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         }
     }
 
-    stats.assign(24, 0);
+    stats.assign(28, 0);
     stats[0] = s; stats[1] = has_runs; stats[2] = num_lpf; stats[3] = len_lpf_phr; stats[4] = num_gaps;
     for (int x = 0; x < 5; x++) stats[5 + x] = gp.patt_lens[x];
     stats[10] = gp.roll_threshold; stats[11] = gp.log2_size_h;
@@ -2110,6 +2297,36 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             if (nch) k_iv_chunks<<<cdiv(nch, 256), 256, 0, st>>>(ra, rb, ni, choff, nch, chl, rk, ch);
             return ch;
         };
+        // LSD sort of m entries on `bits` key bits (pass-0 keys from kf0): entry ids to vout, the first
+        // sorted index of every key to head (pre-set to NONE); ka / va: scratch for the middle passes
+        auto lsd_sort = [&](auto kf0, u64 m, u32 bits, u32* ka, u32* va, u32* vout, u32* head) {
+            const u32 npass = std::max<u32>(1, (bits + LS_DB - 1) / LS_DB);
+            if (npass > LS_MAXP) throw error(-6, "lsd_sort: too many key bits");
+            const u32 ntile = cdiv(m, LS_TILE);
+            const u64 per = (u64)LS_NB * ntile;
+            u32* H = g_ls_h.get(per + 1);
+            u32* Gs = g_ls_g.get(per + 1);
+            // ping-pong: pass p reads what pass p - 1 wrote
+            u32 *kb[2] = {ka, npass > 2 ? g_predk.get(m + 1) : nullptr}, *vb[2] = {va, npass > 2 ? g_ids2.get(m + 1) : nullptr};
+            for (u32 p = 0; p < npass; p++) {
+                const bool first = p == 0, lastp = p + 1 == npass;
+                u32 *ko = kb[p & 1], *vo = lastp ? vout : vb[p & 1];
+                const u32 *ki = kb[(p + 1) & 1], *vi = vb[(p + 1) & 1];
+                const ls_plain kp{ki};
+                if (first) k_ls_hist<<<ntile, LS_T, 0, st>>>(kf0, m, p, ntile, H);
+                else k_ls_hist<<<ntile, LS_T, 0, st>>>(kp, m, p, ntile, H);
+                excl_sum64(H, Gs, 0u, per, scan_tmp, st);
+                if (first && lastp)
+                    k_ls_scatter<decltype(kf0), true, true><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                else if (first)
+                    k_ls_scatter<decltype(kf0), true, false><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                else if (lastp)
+                    k_ls_scatter<ls_plain, false, true><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                else
+                    k_ls_scatter<ls_plain, false, false><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, ko, vo, head);
+            }
+            LZ_HIP(hipGetLastError());
+        };
         // base sets this large get their predecessors in sorted order and moved back to
         // entry order in buckets (random 4-byte scatters over the whole array are slower)
         auto build_base = [&](const u32* bm) {
@@ -2141,7 +2358,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             u32* pred5 = occ_buf.get(ne5 + 1);
             u8* rem = rem_buf.get(nb + 1);
             LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
-            bool dense = false;
+            bool dense = false, ls = false;
             u32 D = 0, dense_bits = 0;
             const u64 npw = ((u64)nslots + 31) / 32;
             u32* pbm = g_pbm.get(npw + 1);
@@ -2166,7 +2383,50 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 }
                 u32* sk_in = keys;
                 u32 sbits = gp.log2_size_h;
-                if (dense) {
+                // dense ids and bucket-search lookups (no predecessors): the LSD sort over the raw
+                // slots, dense-id map fused into its first pass, entry ids and dense-id starts out
+                ls = dense && !W.use_pred && !std::getenv("LZ77SSS_NO_LSD");
+                if (ls) {
+                    u32* dstart = g_dstart.get((u64)D + 2);
+                    LZ_HIP(hipMemsetAsync(dstart, 0xFF, (u64)D * 4, st));
+                    k_set_u32x2<<<1, 1, 0, st>>>(dstart + D, (u32)ne5, 0u);
+                    lsd_sort(ls_dense{keys, pbm, pwp}, ne5, dense_bits, skeys, vals, svals, dstart);
+                    if (std::getenv("LZ77SSS_LSD_CHECK")) {
+                        // the rocprim path into scratch, compared entry by entry
+                        u32* dk = g_sdk.get(ne5 + 1);
+                        u32* ck = g_predk.get(ne5 + 1);
+                        u32* cv = g_ids2.get(ne5 + 1);
+                        k_dense_keys<<<cdiv(cdiv(ne5, 4), 256), 256, 0, st>>>(keys, ne5, pbm, pwp, dk);
+                        size_t tb = 0;
+                        const rocprim::counting_iterator<u32> ids(0);
+                        LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb, dk, ck, ids, cv, (size_t)ne5, 0u, dense_bits, st));
+                        u8* t = scan_tmp.get(tb);
+                        LZ_HIP(rocprim::radix_sort_pairs(t, tb, dk, ck, ids, cv, (size_t)ne5, 0u, dense_bits, st));
+                        u32* ds2 = g_pcnt.get(std::max<u64>(npw + 1, (u64)D + 2));
+                        k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(ck, cv, ne5, D, nullptr, ds2);
+                        u64* r = (u64*)g_cut.get(sizeof(chain_cut) + 256) + 20;
+                        const u64 init[4] = {~0ull, 0, ~0ull, 0};
+                        LZ_HIP(hipMemcpyAsync(r, init, 32, hipMemcpyHostToDevice, st));
+                        k_first_diff_u32<<<cdiv(ne5, 256), 256, 0, st>>>(svals, cv, ne5, r);
+                        k_first_diff_u32<<<cdiv((u64)D + 1, 256), 256, 0, st>>>(dstart, ds2, (u64)D + 1, r + 2);
+                        u64 h[4];
+                        LZ_HIP(hipMemcpyAsync(h, r, 32, hipMemcpyDeviceToHost, st));
+                        LZ_HIP(hipStreamSynchronize(st));
+                        std::fprintf(stderr, "[lz77sss-lsd-check] m=%llu D=%u bits=%u: svals diff=%llu first=%lld, dstart diff=%llu first=%lld\n",
+                                     (unsigned long long)ne5, D, dense_bits, (unsigned long long)h[1], (long long)h[0],
+                                     (unsigned long long)h[3], (long long)h[2]);
+                        if (h[1] || h[3]) {
+                            u32 a[8], b[8];
+                            const u64 f = h[1] ? std::min<u64>(h[0], ne5 - 8) : 0;
+                            LZ_HIP(hipMemcpy(a, svals + f, 32, hipMemcpyDeviceToHost));
+                            LZ_HIP(hipMemcpy(b, cv + f, 32, hipMemcpyDeviceToHost));
+                            for (int q = 0; q < 8; q++) std::fprintf(stderr, "  [%llu] lsd %u rocprim %u\n", (unsigned long long)(f + q), a[q], b[q]);
+                        }
+                    }
+                    if (dbg)
+                        std::fprintf(stderr, "[lz77sss-debug] greedy base: %u distinct slots, LSD sort on %u bits\n", D,
+                                     dense_bits);
+                } else if (dense) {
                     // (a transform iterator mapping the ids inside the sort was slower: rr sort
                     // passes +234 us against this pass's 211 us)
                     k_dense_keys<<<cdiv(cdiv(ne5, 4), 256), 256, 0, st>>>(keys, ne5, pbm, pwp, skeys);
@@ -2174,52 +2434,55 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     skeys = g_sdk.get(ne5 + 1);
                     sbits = dense_bits;
                 }
-                if (dbg)
-                    std::fprintf(stderr, "[lz77sss-debug] greedy base: %u distinct slots, %s sort on %u bits\n", D,
-                                 dense ? "dense-id" : "slot", sbits);
-                size_t tb = 0;
-                // values = entry ids: a counting iterator, so the ids are never written or read
-                const rocprim::counting_iterator<u32> ids(0);
-                LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
-                u8* t = scan_tmp.get(tb);
-                LZ_HIP(rocprim::radix_sort_pairs(t, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
-                if (dense && ne5 < pred_sorted_min) {
-                    // predecessors and dense-id starts in one pass (buckets below reuse dstart)
-                    k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, svals, ne5, D, W.use_pred ? pred5 : nullptr,
-                                                                      g_dstart.get((u64)D + 1));
-                } else if (W.use_pred && ne5 < pred_sorted_min) {
-                    k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
-                } else if (W.use_pred) {
-                    // pred5[e] = predecessor of entry e in its slot: the sorted-order predecessors
-                    // moved back to entry order (a random scatter of 4-byte writes is ~3x slower)
-                    if (std::getenv("LZ77SSS_PRED_RADIX")) {  // reference path: radix sort by entry id
-                        u32* pv = vals;  // the unsorted values are no longer needed
-                        k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
-                        u32* kdump = g_predk.get(ne5 + 1);
-                        int eb = 1;
-                        while (eb < 32 && (1ull << eb) < ne5) eb++;
-                        size_t tb2 = 0;
-                        LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u,
-                                                         (unsigned)eb, st));
-                        u8* t2 = scan_tmp.get(tb2);
-                        LZ_HIP(rocprim::radix_sort_pairs(t2, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u, (unsigned)eb,
-                                                         st));
-                    } else {
-                        const u32 nbk = (u32)((ne5 + (1ull << PB_SH) - 1) >> PB_SH);
-                        u32* cursor = g_pbcur.get(nbk + 1);
-                        u64* tmp = g_pbtmp.get(ne5);
-                        const u32 ntile = (u32)std::min<u64>(1024, cdiv(ne5, PB_T));
-                        const u64 tile = (ne5 + ntile - 1) / ntile;
-                        k_pb_init<<<cdiv(nbk, 256), 256, 0, st>>>(cursor, nbk);
-                        k_pb_move<<<ntile, PB_T, 0, st>>>(svals, skeys, ne5, tile, nbk, cursor, tmp);
-                        k_pb_apply<<<cdiv(cdiv(ne5, 256), N_XCD) * N_XCD, 256, 0, st>>>(tmp, ne5, pred5);
+                if (!ls) {
+                    if (dbg)
+                        std::fprintf(stderr, "[lz77sss-debug] greedy base: %u distinct slots, %s sort on %u bits\n", D,
+                                     dense ? "dense-id" : "slot", sbits);
+                    size_t tb = 0;
+                    // values = entry ids: a counting iterator, so the ids are never written or read
+                    const rocprim::counting_iterator<u32> ids(0);
+                    LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
+                    u8* t = scan_tmp.get(tb);
+                    LZ_HIP(rocprim::radix_sort_pairs(t, tb, sk_in, skeys, ids, svals, (size_t)ne5, 0u, sbits, st));
+                    if (dense && ne5 < pred_sorted_min) {
+                        // predecessors and dense-id starts in one pass (buckets below reuse dstart)
+                        k_pred_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, svals, ne5, D, W.use_pred ? pred5 : nullptr,
+                                                                          g_dstart.get((u64)D + 1));
+                    } else if (W.use_pred && ne5 < pred_sorted_min) {
+                        k_pred<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pred5);
+                    } else if (W.use_pred) {
+                        // pred5[e] = predecessor of entry e in its slot: the sorted-order predecessors
+                        // moved back to entry order (a random scatter of 4-byte writes is ~3x slower)
+                        if (std::getenv("LZ77SSS_PRED_RADIX")) {  // reference path: radix sort by entry id
+                            u32* pv = vals;  // the unsorted values are no longer needed
+                            k_pred_sorted<<<cdiv(ne5, 256), 256, 0, st>>>(skeys, svals, ne5, pv);
+                            u32* kdump = g_predk.get(ne5 + 1);
+                            int eb = 1;
+                            while (eb < 32 && (1ull << eb) < ne5) eb++;
+                            size_t tb2 = 0;
+                            LZ_HIP(rocprim::radix_sort_pairs(nullptr, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u,
+                                                             (unsigned)eb, st));
+                            u8* t2 = scan_tmp.get(tb2);
+                            LZ_HIP(rocprim::radix_sort_pairs(t2, tb2, svals, kdump, pv, pred5, (size_t)ne5, 0u, (unsigned)eb,
+                                                             st));
+                        } else {
+                            const u32 nbk = (u32)((ne5 + (1ull << PB_SH) - 1) >> PB_SH);
+                            u32* cursor = g_pbcur.get(nbk + 1);
+                            u64* tmp = g_pbtmp.get(ne5);
+                            const u32 ntile = (u32)std::min<u64>(1024, cdiv(ne5, PB_T));
+                            const u64 tile = (ne5 + ntile - 1) / ntile;
+                            k_pb_init<<<cdiv(nbk, 256), 256, 0, st>>>(cursor, nbk);
+                            k_pb_move<<<ntile, PB_T, 0, st>>>(svals, skeys, ne5, tile, nbk, cursor, tmp);
+                            k_pb_apply<<<cdiv(cdiv(ne5, 256), N_XCD) * N_XCD, 256, 0, st>>>(tmp, ne5, pred5);
+                        }
                     }
                 }
             }
             lap("base sort + pred");
             if (dense) {
                 u32* dstart = g_dstart.get((u64)D + 1);
-                if (ne5 >= pred_sorted_min) k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
+                if (ne5 >= pred_sorted_min && !ls)
+                    k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
                 k_bstart_rank<<<cdiv(cdiv((u64)nslots + 1, 4), 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
                                                                           g_bstart.get((u64)nslots + 1));
             } else {
@@ -2239,6 +2502,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         // positions that join later and are missing from it go to the small extra list.
         u32* bmA = g_bmA.get(nw);
         u64 na_main = 0;
+        bool bmA_zero = false;
+        // I_fresh: I was set by set_state(true) and not changed since, so |I| is the count of base
+        // ranks in I (i_cnt[2]) and I' == I is decided by counting the chain's inserts (i_cnt[0]:
+        // new bits of I', i_cnt[1]: those outside I) instead of a full-length xor and count
+        bool I_fresh = false;
+        u32* i_cnt = counters.get(16) + 12;  // the main list is empty and bmA was not computed (I within the base set)
         auto build_list = [&](const u32* bm, dbuf<u32>& k32, dbuf<pos_t>& kpos, dbuf<u64>& ka, dbuf<u64>& kb,
                               dbuf<u32>& bucket, const u64*& keys_out, u64& nkeys, const u32*& bk_out,
                               const pos_t*& apos_out, u64& napos_out) -> u64 {
@@ -2269,6 +2538,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             return na;
         };
         auto rebuild_main = [&]() {
+            bmA_zero = false;
             k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmA);
             na_main = build_list(bmA, add_keys32, add_pos, add_keys, add_keys2, g_abeg, W.akeys, W.nadd, W.abeg, W.apos,
                                  W.napos);
@@ -2278,16 +2548,26 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         auto rebuild_added = [&](bool main_list) {
             if (main_list) return rebuild_main();
             k_bm_andnot<<<gw, 256, 0, st>>>(bmI, bmIb, nw, bmT);
-            k_bm_andnot<<<gw, 256, 0, st>>>(bmT, bmA, nw, bmT);
+            if (!bmA_zero) k_bm_andnot<<<gw, 256, 0, st>>>(bmT, bmA, nw, bmT);
             const u64 nx = build_list(bmT, g_x32, g_xpos, g_xk, g_xk2, g_abeg2, W.akeys2, W.nadd2, W.abeg2, W.apos2,
                                       W.napos2);
             if (nx * 4 > na_main + (1u << 16)) rebuild_main();
         };
-        auto set_state = [&]() {  // rem + added for the current I
+        // rem + added for the current I; within_base: I is a subset of the base set (the first
+        // speculation, or a base rebuilt as I' u I_b), so no position is added and the main list
+        // (I - I_b, a full-length bitmap pass and a count) is empty without computing it
+        auto set_state = [&](bool within_base) {
             W.bmI = bmI;
+            I_fresh = within_base;
+            if (within_base) LZ_HIP(hipMemsetAsync(i_cnt + 2, 0, 4, st));
             if (nb)
-                k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem, (pos_t*)W.iposr);
-            rebuild_added(true);
+                k_rem_from_bm<<<std::min<u64>(cdiv(nb, 256), 4096), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem, (pos_t*)W.iposr,
+                                                            within_base ? i_cnt + 2 : nullptr);
+            if (!within_base) return rebuild_added(true);
+            bmA_zero = true;
+            na_main = 0;
+            W.akeys = nullptr; W.nadd = 0; W.abeg = nullptr; W.apos = nullptr; W.napos = 0;
+            W.akeys2 = nullptr; W.nadd2 = 0;
         };
         // same-slot predecessors (pred5) pay for their scatter when the walks make many
         // lookups: short gaps (many factors per gap position).  Texts with few, long gaps
@@ -2310,7 +2590,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             wfact = seq_complete(nullptr, 0, nullptr, nullptr, true);
         } else {
             build_base(bmIb);  // superset: gaps + short phrase interiors
-            set_state();
+            set_state(true);
             bool restart_seq = false;  // a walk overflowed or linking ran away: complete from the entry
             for (;; outer++) {
                 for (int round = 0;; round++) {
@@ -2462,11 +2742,25 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 }
                 // ---- the insert set the chain actually produced vs the speculation
                 LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
+                const bool fast = I_fresh && !std::getenv("LZ77SSS_NO_FAST_CHECK");
+                if (fast) LZ_HIP(hipMemsetAsync(i_cnt, 0, 8, st));
                 if (nchain)
-                    k_chain_inserts<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2);
+                    k_chain_inserts<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2,
+                                                                                     bmI, fast ? i_cnt : nullptr);
                 if (tail && hc[1]) {
                     pos_t* d_tins = tail_ins_buf.p;
-                    k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], off, bmI2);
+                    k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], off, bmI2, bmI, fast ? i_cnt : nullptr);
+                }
+                bool same = false;
+                if (fast) {
+                    u32 ic[3];
+                    hread rb(st);
+                    rb.add(ic, (const u32*)i_cnt, 3);
+                    rb.sync();
+                    same = ic[1] == 0 && ic[0] == ic[2];  // I' within I and |I'| = |I|
+                    if (dbg)
+                        std::fprintf(stderr, "[lz77sss-debug] greedy fast check: |I'|=%u outside I=%u |I|=%u -> %s\n", ic[0],
+                                     ic[1], ic[2], same ? "equal" : "full check");
                 }
                 if (dbg) {  // (before the scan below: k_bmb_write reads its offsets from g_bincl)
                     const u64 c1 = bmb_scan(bm_bits{bmI, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
@@ -2474,8 +2768,11 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     std::fprintf(stderr, "[lz77sss-debug] greedy |I|=%llu |I'|=%llu base=%llu chain=%u\n",
                                  (unsigned long long)c1, (unsigned long long)c2, (unsigned long long)nb, nchain);
                 }
-                k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
-                const u64 ny = bmb_scan(bm_bits{bmT, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
+                u64 ny = 0;
+                if (!same) {
+                    k_bm_xor<<<gw, 256, 0, st>>>(bmI2, bmI, nw, bmT);
+                    ny = bmb_scan(bm_bits{bmT, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
+                }
                 lap("insert set");
                 if (ny == 0 && dbg && std::getenv("LZ77SSS_DEBUG_JUMP")) {
                     // which phrases the converged chain rolled over (interior in I), by log2 length
@@ -2542,7 +2839,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     bmI = g_bmI.p;
                     bmI2 = g_bmI2.p;
                     build_base(bmT);
-                    set_state();
+                    set_state(true);
                     k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
                     if (dbg) std::fprintf(stderr, "[lz77sss-debug] greedy rebuild: outside=%llu\n", (unsigned long long)outside);
                     continue;
@@ -2552,7 +2849,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     std::swap(g_bmI.p, g_bmI2.p), std::swap(g_bmI.cap, g_bmI2.cap);
                     bmI = g_bmI.p;
                     bmI2 = g_bmI2.p;
-                    set_state();
+                    set_state(false);
                     k_invalidate_all<<<cdiv(nseg, 256), 256, 0, st>>>(S, nseg);
                     lap("delta (full)");
                     if (dbg)
@@ -2565,6 +2862,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 LZ_HIP(hipMemcpyAsync(d_d, d_y, ny * sizeof(pos_t), hipMemcpyDeviceToDevice, st));
                 k_dirty<<<cdiv(ny, 64), 64, 0, st>>>(W, d_y, ny, d_d + ny);
                 k_flip<<<cdiv(ny, 256), 256, 0, st>>>(W, d_y, d_j, ny, (u8*)W.rem, d_j + ny);
+                I_fresh = false;
                 std::swap(g_bmI.p, g_bmI2.p), std::swap(g_bmI.cap, g_bmI2.cap);
                 bmI = g_bmI.p;
                 bmI2 = g_bmI2.p;

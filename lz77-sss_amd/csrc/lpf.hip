@@ -202,6 +202,30 @@ __global__ void k_compact3(const pos_t* __restrict__ ph, const u32* __restrict__
     out[o * 3 + 2] = ph[i * 3 + 2];
 }
 
+// after k_compact3: the phrase count m (from the last push offset), the sentinel {n, n+1, 0}
+// at P[m], and the greedy's phrase statistics (total phrase length, gaps: approximate/common.cpp
+// get_phrase_info as k_phrase_info) -- so one host read gives all three
+__global__ void k_phrase_finish(pos_t* __restrict__ P, const u32* __restrict__ push, const u32* __restrict__ off, u32 s,
+                                pos_t n, u64* __restrict__ acc) {
+    const u32 m = off[s - 1] + push[s - 1];
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    u64 len = 0, gaps = 0;
+    if (k < m) {
+        const pos_t b = P[3 * k], e = P[3 * k + 1];
+        len = e - b;
+        if (k == 0 ? b > 0 : b > P[3 * (k - 1) + 1]) gaps++;
+        if (k == m - 1 && e < n) gaps++;
+    }
+    if (k == 0) {
+        acc[2] = m;
+        P[3 * (u64)m] = n;
+        P[3 * (u64)m + 1] = n + 1;
+        P[3 * (u64)m + 2] = 0;
+    }
+    block_add64(&acc[0], len);
+    block_add64(&acc[1], gaps);
+}
+
 struct max_op {
     __device__ pos_t operator()(const pos_t& a, const pos_t& b) const { return a > b ? a : b; }
 };
@@ -399,11 +423,20 @@ void engine::build_lpf_opt(const u8* T) {
     k_phrase<<<g, 256, 0, st>>>(S.p, s, cd, mark, lst, ph3, push);
     u32* off = mark;  // mark no longer needed after k_phrase
     scan_dev(push, off, s, s, 0u, 0u, op_sum{}, true, scan_tmp, st);
-    const auto [last_off, last_push] = rd2(off + s - 1, push + s - 1, st);
-    num_phr = last_off + last_push;
-    pos_t* out = lpf.get((u64)(num_phr + 1) * 3);
+    // compaction for the bound s, then the count, sentinel and the greedy's phrase statistics in
+    // one pass and one host read (the emitter reuses them: phr_info)
+    pos_t* out = lpf.get((u64)(s + 1) * 3);
     k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);
+    u64* acc = counters64.get(16) + 2;  // [2] total length, [3] gaps, [4] m (factorize_greedy's slots)
+    LZ_HIP(hipMemsetAsync(acc, 0, 16, st));
+    k_phrase_finish<<<cdiv((u64)s + 1, 256), 256, 0, st>>>(out, push, off, s, (pos_t)n, acc);
     LZ_HIP(hipGetLastError());
+    u64 h3[3];
+    hread rb(st);
+    rb.add(h3, (const u64*)acc, 3);
+    rb.sync();
+    num_phr = (u32)h3[2];
+    phr_info = {true, h3[0], h3[1]};
 }
 
 }  // namespace LZ_NS

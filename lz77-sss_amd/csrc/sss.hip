@@ -1914,10 +1914,7 @@ void engine::build_sss(const u8* T) {
         k_flag_list<<<nfb, FL_T, 0, st>>>(tfl, nfw, fc, tl, ctr + 2);
     }
     LZ_HIP(hipGetLastError());
-    u32* hp = h_pin + 32;
-    LZ_HIP(hipMemcpyAsync(hp, ctr + 2, sizeof(u32), hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipStreamSynchronize(st));
-    const u32 ndirty = hp[0];
+    const u32 ndirty = rd1(ctr + 2, st);
     stats_sss_tiles = ndirty;
     if (debug_enabled()) {
         u32 dc[3];
@@ -2004,12 +2001,17 @@ void engine::build_sss(const u8* T) {
     u32* off = u32a.get(nlanes + 1);
     auto scan_counts = [&]() { excl_sum_total(lc, off, nlanes, scan_tmp, st); };
     scan_counts();
-    LZ_HIP(hipMemcpyAsync(hp, ctr, 2 * sizeof(u32), hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipMemcpyAsync(hp + 2, off + nlanes, sizeof(u32), hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipStreamSynchronize(st));
+    u32 hp[3];
+    {
+        hread rb(st);
+        rb.add(hp, (const u32*)ctr, 2);
+        rb.add(hp + 2, (const u32*)(off + nlanes));
+        rb.sync();
+    }
     has_runs = hp[0] != 0;
     u32 total = hp[2];
     float ms = 0;
+    LZ_HIP(hipEventSynchronize(e1));  // (complete: the read-back ran after it)
     LZ_HIP(hipEventElapsedTime(&ms, e0, e1));
     sss_kernel_ms = ms;
     (void)hipEventDestroy(e0);

@@ -125,6 +125,9 @@ struct engine {
     dbuf<pos_t> p_Em, p_lst, p_ph3;  // running max_end scan and phrase scratch (csrc/lpf.hip)
     dbuf<pos_t> lpf;                 // phrases as (beg,end,src) triples + sentinel
     u32 num_phr = 0;
+    // the emitter's phrase statistics (total phrase length, gaps), when the phrase builder already
+    // computed them and wrote the sentinel (build_lpf_opt); any other phrase source clears it
+    struct { bool valid; u64 len, gaps; } phr_info{false, 0, 0};
 
     // ---- greedy ----
     dbuf<pos_t> fact;                // output factors (src,len) pairs
@@ -180,6 +183,7 @@ struct engine {
     dbuf<pos_t> fact_acc;  // greedy windows: the stream so far
     dbuf<u8> g_cut;     // chain_cut + completion counters
     dbuf<u64> g_xk, g_xk2;
+    dbuf<u32> g_ls_h, g_ls_g;  // LSD base sort: digit counts per tile and their scans (csrc/greedy.hip)
     // exact mode (csrc/exact.hip)
     dbuf<u64> x_key, x_key2, x_off, x_wide;
     dbuf<u32> x_idx, x_idx2, x_sa, x_rank, x_flag, x_tree, x_ltree, x_lcp, x_lpf, x_src, x_mark, x_chunk;
@@ -249,71 +253,128 @@ struct engine {
     lce_view view(const u8* T) const;
 };
 
-// small host helpers.  Device values are read back through a pinned (page-locked) staging
-// slot per thread: a copy into pageable memory goes through the runtime's bounce buffer, one
-// more copy and a longer round trip on every count the host needs
-inline u8* pinned_slot() {
-    struct slot {
-        u8* p = nullptr;
-        slot() {
-            if (hipHostMalloc((void**)&p, 4096, hipHostMallocDefault) != hipSuccess) p = nullptr;
+// small host helpers: device values the host needs (counts, sizes, states).  A read-back is a
+// round trip the whole pipeline waits on, so it is made as short as the hardware allows: one tiny
+// kernel copies every requested value into host-coherent pinned memory (mapped into the device
+// address space) and then writes a sequence number there; the host spins on that word.  Against
+// hipMemcpyAsync per value + hipStreamSynchronize this saves a copy launch per value and the
+// runtime's wait-and-wake (LZ77SSS_NO_SPIN selects the copy + synchronize form for A/B runs).
+struct sync_slot {
+    u8* h = nullptr;  // host pointer (fine-grained, coherent)
+    u8* d = nullptr;  // the same memory as the device sees it
+    u32 seq = 0;
+    bool spin = std::getenv("LZ77SSS_NO_SPIN") == nullptr;
+    sync_slot() {
+        if (hipHostMalloc((void**)&h, 8192, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
+            h = nullptr;
+            return;
         }
-        ~slot() {
-            if (p) (void)hipHostFree(p);
+        if (hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) d = h;
+        std::memset(h, 0, 8192);
+    }
+    ~sync_slot() {
+        if (h) (void)hipHostFree(h);
+    }
+};
+inline sync_slot& host_slot() {
+    static thread_local sync_slot s;
+    if (!s.h) throw error(-4 /* LZ77SSS_ENOMEM */, "pinned staging slot");
+    return s;
+}
+struct hread_job {
+    const u8* src[16];
+    u32 off[16], bytes[16];
+    u32 n, seq;
+};
+// copies the requested values into the slot, then publishes the sequence number (offset 0)
+static __global__ __launch_bounds__(64) void k_hread(hread_job J, u8* __restrict__ dst) {
+    for (u32 i = 0; i < J.n; i++)
+        for (u32 b = threadIdx.x; b < J.bytes[i]; b += 64) dst[J.off[i] + b] = J.src[i][b];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        *(volatile u32*)dst = J.seq;
+    }
+}
+// waits for the slot's sequence number `seq` (the stream's error state is checked while spinning)
+inline void spin_wait(sync_slot& S, u32 seq, hipStream_t st) {
+    for (u64 it = 1;; it++) {
+        if (__atomic_load_n((volatile u32*)S.h, __ATOMIC_ACQUIRE) == seq) return;
+        if ((it & 255) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) {
+                if (__atomic_load_n((volatile u32*)S.h, __ATOMIC_ACQUIRE) == seq) return;
+                throw error(-6 /* LZ77SSS_EINTERNAL */, "read-back: stream idle but the value never arrived");
+            }
+            if (e != hipErrorNotReady) LZ_HIP(e);
         }
-    };
-    static thread_local slot s;
-    if (!s.p) throw error(-4 /* LZ77SSS_ENOMEM */, "pinned staging slot");
-    return s.p;
+        __builtin_ia32_pause();
+    }
 }
-template <class T>
-static inline T rd1(const T* dptr, hipStream_t st) {
-    static_assert(sizeof(T) <= 32);
-    u8* h = pinned_slot();
-    LZ_HIP(hipMemcpyAsync(h, dptr, sizeof(T), hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipStreamSynchronize(st));
-    T v;
-    std::memcpy(&v, h, sizeof(T));
-    return v;
-}
-// several device values of any small types with one synchronization, staged in the pinned
-// slot (bytes 64.. of it; rd1 / rd2 use the first 64): add() enqueues, sync() waits and copies out
+// several device values of any small types with one round trip: add() records, sync() copies
+// them all (the values as of sync(): nothing enqueued between may change them) and waits
 struct hread {
     hipStream_t st;
-    u8* h;
+    sync_slot& S;
     size_t off = 64;
-    struct item { void* dst; size_t off, bytes; };
+    struct item { void* dst; const void* src; size_t off, bytes; };
     item items[16];
     int n = 0;
-    explicit hread(hipStream_t s) : st(s), h(pinned_slot()) {}
+    explicit hread(hipStream_t s) : st(s), S(host_slot()) {}
     template <class T>
     void add(T* dst, const T* src, size_t count = 1) {
         const size_t b = sizeof(T) * count;
         off = (off + 15) & ~(size_t)15;
-        if (off + b > 4096 || n == 16) throw error(-6 /* LZ77SSS_EINTERNAL */, "hread: staging slot full");
-        LZ_HIP(hipMemcpyAsync(h + off, src, b, hipMemcpyDeviceToHost, st));
-        items[n++] = {dst, off, b};
+        if (off + b > 8192 || n == 16) throw error(-6 /* LZ77SSS_EINTERNAL */, "hread: staging slot full");
+        items[n++] = {dst, src, off, b};
         off += b;
     }
     void sync() {
-        LZ_HIP(hipStreamSynchronize(st));
-        for (int k = 0; k < n; k++) std::memcpy(items[k].dst, h + items[k].off, items[k].bytes);
+        if (S.spin) {
+            hread_job J{};
+            for (int k = 0; k < n; k++) {
+                J.src[k] = (const u8*)items[k].src;
+                J.off[k] = (u32)items[k].off;
+                J.bytes[k] = (u32)items[k].bytes;
+            }
+            J.n = (u32)n;
+            J.seq = ++S.seq;
+            k_hread<<<1, 64, 0, st>>>(J, S.d);
+            LZ_HIP(hipGetLastError());
+            spin_wait(S, J.seq, st);
+        } else {
+            for (int k = 0; k < n; k++)
+                LZ_HIP(hipMemcpyAsync(S.h + items[k].off, items[k].src, items[k].bytes, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));
+        }
+        for (int k = 0; k < n; k++) std::memcpy(items[k].dst, S.h + items[k].off, items[k].bytes);
         n = 0;
         off = 64;
     }
 };
+template <class T>
+static inline T rd1(const T* dptr, hipStream_t st) {
+    T v;
+    hread rb(st);
+    rb.add(&v, dptr);
+    rb.sync();
+    return v;
+}
 // two device values with one synchronization
 template <class T>
 static inline std::pair<T, T> rd2(const T* a, const T* b, hipStream_t st) {
-    static_assert(sizeof(T) <= 32);
-    u8* h = pinned_slot();
-    LZ_HIP(hipMemcpyAsync(h, a, sizeof(T), hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipMemcpyAsync(h + 32, b, sizeof(T), hipMemcpyDeviceToHost, st));
-    LZ_HIP(hipStreamSynchronize(st));
     T v[2];
-    std::memcpy(&v[0], h, sizeof(T));
-    std::memcpy(&v[1], h + 32, sizeof(T));
+    hread rb(st);
+    rb.add(&v[0], a);
+    rb.add(&v[1], b);
+    rb.sync();
     return {v[0], v[1]};
+}
+// everything enqueued on st so far has completed (the spin form of hipStreamSynchronize)
+inline void stream_wait(hipStream_t st) {
+    hread rb(st);
+    rb.sync();
 }
 static inline unsigned cdiv(u64 a, u64 b) { return (unsigned)((a + b - 1) / b); }
 // blocks of a grid-stride launch over `items` work-items (at least 1, at most GRID_CAP)

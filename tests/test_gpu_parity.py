@@ -318,6 +318,35 @@ def test_dense_slot_ids_match_slot_sort(session, lz, kind, mib, monkeypatch):
     assert F1.shape == F0.shape and np.array_equal(F1, F0)
 
 
+@pytest.mark.parametrize("mib,seed", [(1, 7), (32, 5), (64, 9)])
+def test_lsd_base_sort_vs_oracle(session, orc, lz, mib, seed, monkeypatch):
+    """Bucket-search lookups on dense slot ids: the base set sorted by the LSD sort (reduce-then-scan,
+    dense-id map fused, csrc/greedy.hip) equals rocprim's radix sort (LZ77SSS_NO_LSD) and the oracle."""
+    n = mib << 20
+    T = lz.gen_random_repetitive(n, n, seed, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    monkeypatch.setenv("LZ77SSS_NO_PRED", "1")
+    _, F1 = run(session, T)
+    assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    monkeypatch.setenv("LZ77SSS_NO_LSD", "1")
+    _, F0 = run(session, T)
+    assert np.array_equal(F0, F_ref)
+
+
+@pytest.mark.parametrize("log2", [6, 10, 14, 18])
+def test_lsd_base_sort_table_sizes(session, lz, log2, monkeypatch):
+    """Gap-index tables of 2^6 .. 2^18 slots: one to three LSD passes of 7 bits; the stream equals the
+    rocprim-sorted one and decodes to the text."""
+    n = 16 << 20
+    T = lz.gen_random_repetitive(n, n, 3, 0.5, 0.05)
+    monkeypatch.setenv("LZ77SSS_NO_PRED", "1")
+    _, F1 = run(session, T, index_log2_size=log2)
+    monkeypatch.setenv("LZ77SSS_NO_LSD", "1")
+    _, F0 = run(session, T, index_log2_size=log2)
+    assert F1.shape == F0.shape and np.array_equal(F1, F0)
+    assert np.array_equal(lz.decode(F1, n), T)
+
+
 @pytest.mark.parametrize("kind,mib", [("genome", 16), ("rr", 32)])
 def test_sorted_predecessor_paths_vs_oracle(session, orc, lz, kind, mib, monkeypatch):
     """Base sets above LZ77SSS_PRED_SORTED_MIN move their predecessors back by bucket scatter
