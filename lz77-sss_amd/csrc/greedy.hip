@@ -258,12 +258,24 @@ __global__ void k_pred_heads(const u32* __restrict__ sdk, const u32* __restrict_
     if (head) dstart[sdk[t]] = (u32)t;
     if (pred5) pred5[svals[t]] = head ? NONE : svals[t - 1];
 }
-// first sorted index of every dense id (all ids occur), dstart[D] = m
+// first sorted index of every dense id (all ids occur), dstart[D] = m; four keys per thread
 __global__ void k_dense_heads(const u32* __restrict__ sdk, u64 m, u32 D, u32* __restrict__ dstart) {
-    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > m) return;
-    if (t == m) { dstart[D] = (u32)m; return; }
-    if (t == 0 || sdk[t - 1] != sdk[t]) dstart[sdk[t]] = (u32)t;
+    const u64 t = 4 * ((u64)blockIdx.x * blockDim.x + threadIdx.x);
+    if (t == 0) dstart[D] = (u32)m;
+    if (t >= m) return;
+    u32 k[4];
+    if (t + 3 < m) {
+        const uint4 q = *(const uint4*)(sdk + t);
+        k[0] = q.x; k[1] = q.y; k[2] = q.z; k[3] = q.w;
+    } else {
+        for (u64 j = 0; j < 4; j++) k[j] = t + j < m ? sdk[t + j] : NONE;
+    }
+    u32 prev = t ? sdk[t - 1] : NONE;
+#pragma unroll
+    for (u32 j = 0; j < 4; j++) {
+        if (t + j < m && k[j] != prev) dstart[k[j]] = (u32)(t + j);
+        prev = k[j];
+    }
 }
 // slot -> first sorted index with slot >= s: the start of the next present slot's id
 // four slots per thread (one presence word, a 16-byte store)
@@ -1196,24 +1208,6 @@ __global__ void k_gap_bitmaps_phr(const pos_t* __restrict__ P, u32 m, pos_t N, p
         if (P[3 * k + 1] - P[3 * k] <= 48 && pb < pe) bm_set_range(bmSup, pb - off, pe - off);
     }
 }
-// OR `mask` into bm[w]; counts the newly set bits (c[0]) and those of them not in the insert set
-// bmI (c[1]) -- exact whatever the overlaps between ranges, as every bit is new exactly once
-__device__ __forceinline__ void bm_or_count(u32* bm, u64 w, u32 mask, const u32* bmI, u32* c) {
-    const u32 nw = mask & ~atomicOr(&bm[w], mask);
-    c[0] += __popc(nw);
-    c[1] += __popc(nw & ~bmI[w]);
-}
-__device__ __forceinline__ void wave_count_add(u32* c, u32* acc) {  // whole wave; lane 0 adds the sums
-    u32 a = c[0], b = c[1];
-    for (int o = 32; o > 0; o >>= 1) {
-        a += __shfl_down(a, o, 64);
-        b += __shfl_down(b, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        if (a) atomicAdd(&acc[0], a);
-        if (b) atomicAdd(&acc[1], b);
-    }
-}
 __global__ void k_bm_xor(const u32* __restrict__ a, const u32* __restrict__ b, u64 nw, u32* __restrict__ x) {
     const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (w < nw) x[w] = a[w] ^ b[w];
@@ -1368,16 +1362,13 @@ __global__ void k_iv_chunks(const pos_t* __restrict__ st, const pos_t* __restric
 }
 // rem[r] = base position r not in I
 __global__ void k_rem_from_bm(const pos_t* __restrict__ ipos, u64 nb, const u32* __restrict__ bmI, pos_t off,
-                              u8* __restrict__ rem, pos_t* __restrict__ iposr, u32* __restrict__ n_in = nullptr) {
-    u32 cnt = 0;
-    for (u64 r = gtid(); r < nb; r += gstride()) {  // grid-stride: one count atomic per block
-        const pos_t p = ipos[r], q = p - off;
-        const bool in = (bmI[q >> 5] >> (q & 31)) & 1;
-        rem[r] = in ? 0 : 1;
-        if (iposr) iposr[r] = p | (in ? (pos_t)0 : POS_RFLAG);
-        cnt += in ? 1u : 0u;
-    }
-    if (n_in) block_add(n_in, cnt);  // |I| when I lies within the base set
+                              u8* __restrict__ rem, pos_t* __restrict__ iposr) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nb) return;
+    const pos_t p = ipos[r], q = p - off;
+    const bool in = (bmI[q >> 5] >> (q & 31)) & 1;
+    rem[r] = in ? 0 : 1;
+    if (iposr) iposr[r] = p | (in ? (pos_t)0 : POS_RFLAG);
 }
 
 // walks over a list of segment ids (outputs in the table; WRITE: factors at offs)
@@ -1561,53 +1552,92 @@ __global__ void k_chain_expand(jump_levels JL, u32 len, u32 c0, u32* __restrict_
 }
 // I' bitmap: what the chain inserted below nt ([start, e) + LPF-start queries)
 // (clipped to the window's bitmap range [off, hi), hi <= nt)
+// the range words [w0, w1] of chain node g ([start, min(e, hi)) relative to off) and the masks of its
+// end words
+__device__ __forceinline__ bool chain_range(const seg_tab& S, u32 g, pos_t hi, pos_t off, pos_t& x0, pos_t& x1) {
+    const pos_t a = S.sin[g].start, b = min(S.sout[g].e, hi);
+    x0 = a - off;
+    x1 = b - off;
+    return a < b;
+}
+__device__ __forceinline__ u32 range_mask(u64 w, pos_t x0, pos_t x1) {
+    const u64 w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
+    u32 mask = 0xFFFFFFFFu;
+    if (w == w0) mask &= ~((1u << (x0 & 31)) - 1);
+    if (w == w1 && (x1 & 31)) mask &= (1u << (x1 & 31)) - 1;
+    return mask;
+}
+// one wave per chain node: its gap walk range and single inserts into bm; a node whose range is
+// longer than long_words (0: none) is appended to `lng` (count lng[0], ranges from lng + 2) for
+// k_chain_inserts_long.  outside: inserted positions not in bmI (duplicates only add: 0 iff none)
 __global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cnt, pos_t hi, pos_t off,
-                                u32* __restrict__ bm, const u32* __restrict__ bmI = nullptr, u32* __restrict__ acc = nullptr) {
+                                u32* __restrict__ bm, const u32* __restrict__ bmI = nullptr, u32* __restrict__ outside = nullptr,
+                                u32 long_words = 0, u32* __restrict__ lng = nullptr, u32 lng_cap = 0) {
     const u32 lane = threadIdx.x & 63;
-    u32 c[2] = {0, 0};
+    u32 c = 0;
     for (u64 k = gtid() >> 6; k < cnt; k += gstride() >> 6) {  // one wave per chain node (grid-stride)
         const u32 g = chain[k];
         const seg_out& o = S.sout[g];
-        const pos_t a = S.sin[g].start, b = min(o.e, hi);
-        if (a < b) {
-            if (!acc) {
-                bm_set_range_wave(bm, a - off, b - off, lane);
-            } else {
-                // 8 words per lane and step: the returning atomics of a long gap (one wave walks it)
-                // are in flight together instead of one round trip per word
-                const pos_t x0 = a - off, x1 = b - off;
-                const u64 w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
-                for (u64 wb = w0 + lane; wb <= w1; wb += 64 * 8) {
-                    u32 old[8], msk[8], iw[8];
-#pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const u64 w = wb + 64ull * j;
-                        msk[j] = 0;
-                        if (w > w1) continue;
-                        u32 mask = 0xFFFFFFFFu;
-                        if (w == w0) mask &= ~((1u << (x0 & 31)) - 1);
-                        if (w == w1 && (x1 & 31)) mask &= (1u << (x1 & 31)) - 1;
-                        msk[j] = mask;
-                        old[j] = atomicOr(&bm[w], mask);
-                        iw[j] = bmI[w];
-                    }
-#pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        if (!msk[j]) continue;
-                        const u32 nw = msk[j] & ~old[j];
-                        c[0] += __popc(nw);
-                        c[1] += __popc(nw & ~iw[j]);
-                    }
+        pos_t x0, x1;
+        if (chain_range(S, g, hi, off, x0, x1)) {
+            const u64 w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
+            bool here = true;
+            if (long_words && w1 - w0 >= long_words && lane == 0) {
+                const u32 slot = atomicAdd(lng, 1u);
+                if (slot < lng_cap) {
+                    ((u64*)(lng + 2))[2 * slot] = x0;
+                    ((u64*)(lng + 2))[2 * slot + 1] = x1;
+                } else {
+                    atomicOr(lng + 1, 1u);  // list full: handled here
                 }
+            }
+            if (long_words && w1 - w0 >= long_words) here = false;
+            if (!here && __shfl(lng[1], 0, 64)) here = true;
+            if (here) {
+                // loads first, atomics after: an atomic without return still counts against the
+                // load counter, so a load behind it would wait for its round trip
+                if (outside)
+                    for (u64 w = w0 + lane; w <= w1; w += 64) c += __popc(range_mask(w, x0, x1) & ~bmI[w]);
+                for (u64 w = w0 + lane; w <= w1; w += 64) atomicOr(&bm[w], range_mask(w, x0, x1));
             }
         }
         if (lane < o.nsingle && lane < 4 && o.single[lane] < hi) {
             const pos_t r = o.single[lane] - off;
-            if (acc) bm_or_count(bm, r >> 5, 1u << (r & 31), bmI, c);
-            else atomicOr(&bm[r >> 5], 1u << (r & 31));
+            if (outside) c += ((bmI[r >> 5] >> (r & 31)) & 1) ? 0u : 1u;
+            atomicOr(&bm[r >> 5], 1u << (r & 31));
         }
     }
-    if (acc) wave_count_add(c, acc);
+    if (outside) {
+        for (int o2 = 32; o2 > 0; o2 >>= 1) c += __shfl_down(c, o2, 64);
+        if (lane == 0 && c) atomicAdd(outside, c);
+    }
+}
+// the listed long ranges, every thread of the grid on each
+__global__ void k_chain_inserts_long(const u32* __restrict__ lng, u32 lng_cap, u32* __restrict__ bm, const u32* __restrict__ bmI,
+                                     u32* __restrict__ outside) {
+    u32 c = 0;
+    const u32 nl = min(lng[0], lng_cap);
+    for (u32 k = 0; k < nl; k++) {
+        const pos_t x0 = (pos_t)((const u64*)(lng + 2))[2 * k], x1 = (pos_t)((const u64*)(lng + 2))[2 * k + 1];
+        const u64 w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
+        for (u64 w = w0 + gtid(); w <= w1; w += gstride()) {
+            const u32 mask = range_mask(w, x0, x1);
+            if (outside) c += __popc(mask & ~bmI[w]);
+            atomicOr(&bm[w], mask);
+        }
+    }
+    if (outside) block_add(outside, c);
+}
+// I within I': base ranks in I (rem = 0) whose position the chain did not insert -> *missing
+__global__ void k_subset_check(const pos_t* __restrict__ ipos, const u8* __restrict__ rem, u64 nb, const u32* __restrict__ bm2,
+                               pos_t off, u32* __restrict__ missing) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    bool miss = false;
+    if (r < nb && !rem[r]) {
+        const pos_t q = ipos[r] - off;
+        miss = !((bm2[q >> 5] >> (q & 31)) & 1);
+    }
+    if (__any(miss) && (threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(miss)) - 1) atomicAdd(missing, 1u);
 }
 // the window's entry segment: the exact chain state handed over by the previous window
 // (a default segment starting there takes it over); *c0 = its id
@@ -1756,22 +1786,22 @@ __global__ void k_chain_cut(seg_tab S, const u32* __restrict__ chain, u32 nall, 
     *out = c;
 }
 __global__ void k_set_pairs(const pos_t* __restrict__ pairs, u32 np, pos_t off, u32* __restrict__ bm,
-                            const u32* __restrict__ bmI = nullptr, u32* __restrict__ acc = nullptr) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;  // one wave
-    u32 c[2] = {0, 0};
+                            const u32* __restrict__ bmI = nullptr, u32* __restrict__ outside = nullptr) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < np && pairs[2 * k] >= off) {
         pos_t a = pairs[2 * k] - off;
         const pos_t b = pairs[2 * k + 1] - off;
+        u32 c = 0;
         while (a < b) {
             const u64 w = a >> 5;
             const u32 lo = a & 31, hi = (u32)min<u64>(32u, lo + (u64)(b - a));
             const u32 mask = (hi == 32 ? 0xFFFFFFFFu : ((1u << hi) - 1)) & ~((1u << lo) - 1);
-            if (acc) bm_or_count(bm, w, mask, bmI, c);
-            else atomicOr(&bm[w], mask);
+            atomicOr(&bm[w], mask);
+            if (outside) c += __popc(mask & ~bmI[w]);
             a += hi - lo;
         }
+        if (outside && c) atomicAdd(outside, c);
     }
-    if (acc) wave_count_add(c, acc);
 }
 __global__ void k_chain_nfact(seg_tab S, const u32* __restrict__ chain, u32 cnt, u64* __restrict__ nf) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1853,22 +1883,46 @@ struct ls_plain {
     const u32* keys;
     __device__ __forceinline__ u32 operator()(u64 e) const { return keys[e]; }
 };
+// h[d] += number of lanes of the wave holding digit d: one LDS atomic per distinct digit of the
+// wave (the same-address atomics of a hot digit otherwise serialize lane by lane: rr's dense keys
+// are few per tile, 176 us per histogram pass)
+__device__ __forceinline__ void wave_agg_add(u32* h, u32 d, bool valid) {
+    const u32 lane = threadIdx.x & 63;
+    u64 todo = __ballot(valid);
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const u32 dl = __shfl(d, leader, 64);
+        const u64 same = __ballot(valid && d == dl);
+        if (lane == (u32)leader) atomicAdd(&h[dl], (u32)__popcll(same));
+        todo &= ~same;
+    }
+}
 // H[digit * ntile + tile]: counts of digit `pass` per tile of this pass's input (the tiles of pass
 // p > 0 are tiles of pass p - 1's output, so every pass counts its own input)
-template <class KF>
+// AGG: wave-aggregated atomics, for inputs sorted on the lower digits (few distinct digits per
+// wave); the unsorted first pass keeps plain atomics (aggregation measured slower there)
+template <class KF, bool AGG>
 __global__ __launch_bounds__(LS_T) void k_ls_hist(KF kf, u64 m, u32 pass, u32 ntile, u32* __restrict__ H) {
-    __shared__ u32 h[LS_NB];
-    for (u32 i = threadIdx.x; i < LS_NB; i += LS_T) h[i] = 0;
+    __shared__ u32 hw[LS_T / 64][LS_NB];  // per-wave histograms: same-address atomics only within a wave
+    for (u32 i = threadIdx.x; i < LS_NB * (LS_T / 64); i += LS_T) (&hw[0][0])[i] = 0;
     __syncthreads();
+    u32* h = hw[threadIdx.x >> 6];
     const u64 t0 = (u64)blockIdx.x * LS_TILE;
     const u32 sh = pass * LS_DB;
     for (u32 i = 0; i < LS_IPT; i++) {
         const u64 e = t0 + (u64)i * LS_T + threadIdx.x;
-        if (e >= m) break;
-        atomicAdd(&h[(kf(e) >> sh) & (LS_NB - 1)], 1u);
+        const bool valid = e < m;
+        const u32 d = valid ? (kf(e) >> sh) & (LS_NB - 1) : 0u;
+        if (AGG) wave_agg_add(h, d, valid);
+        else if (valid) atomicAdd(&h[d], 1u);
     }
     __syncthreads();
-    for (u32 i = threadIdx.x; i < LS_NB; i += LS_T) H[(u64)i * ntile + blockIdx.x] = h[i];
+    for (u32 i = threadIdx.x; i < LS_NB; i += LS_T) {
+        u32 t = 0;
+#pragma unroll
+        for (u32 w = 0; w < LS_T / 64; w++) t += hw[w][i];
+        H[(u64)i * ntile + blockIdx.x] = t;
+    }
 }
 // one pass: items of tile `blockIdx` (pass 0: key kf(e), value e; later: kin / vin), sorted in LDS on
 // digit `pass`, written at G[digit] + (rank within the digit).  LAST: values only, plus
@@ -1936,6 +1990,71 @@ __global__ __launch_bounds__(LS_T) void k_ls_scatter(KF kf, const u32* __restric
                 atomicMin(&head[k[i]], sm.w.base[d] + (j - sm.w.start[d]));
             }
         }
+    }
+}
+
+// one pass by ballot ranking instead of a block sort: the tile's items (striped, in input
+// order) go round by round; in a round every wave groups its lanes by digit (one ballot per
+// distinct digit: few on these skewed keys), the per-wave digit counts in LDS give each item
+// its rank behind the earlier waves of the round and the earlier rounds (running per-digit
+// bases), and the item is written straight from registers.  Stable; no LDS exchange.
+template <class KF, bool FIRST, bool LAST>
+__global__ __launch_bounds__(LS_T) void k_ls_rank(KF kf, const u32* __restrict__ kin, const u32* __restrict__ vin, u64 m,
+                                                  u32 pass, u32 ntile, const u32* __restrict__ G, u32* __restrict__ kout,
+                                                  u32* __restrict__ vout) {
+    __shared__ u32 s_base[LS_NB];
+    __shared__ u32 s_wc[LS_T / 64][LS_NB];
+    const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (u32 d = threadIdx.x; d < LS_NB; d += LS_T) s_base[d] = G[(u64)d * ntile + blockIdx.x];
+    for (u32 d = lane; d < LS_NB; d += 64) s_wc[w][d] = 0;
+    const u64 t0 = (u64)blockIdx.x * LS_TILE;
+    const u32 b0 = pass * LS_DB;
+    u32 k[LS_IPT], v[LS_IPT];
+#pragma unroll
+    for (u32 i = 0; i < LS_IPT; i++) {
+        const u64 e = t0 + (u64)i * LS_T + threadIdx.x;
+        k[i] = v[i] = 0;
+        if (e < m) {
+            k[i] = FIRST ? kf(e) : kin[e];
+            v[i] = FIRST ? (u32)e : vin[e];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 i = 0; i < LS_IPT; i++) {
+        const bool valid = t0 + (u64)i * LS_T + threadIdx.x < m;
+        const u32 d = (k[i] >> b0) & (LS_NB - 1);
+        u64 todo = __ballot(valid);
+        u32 below = 0;
+        while (todo) {
+            const int leader = __ffsll((long long)todo) - 1;
+            const u32 dl = __shfl(d, leader, 64);
+            const u64 same = __ballot(valid && d == dl);
+            if (valid && d == dl) below = (u32)__popcll(same & ((1ull << lane) - 1));
+            if (lane == (u32)leader) s_wc[w][dl] = (u32)__popcll(same);
+            todo &= ~same;
+        }
+        __syncthreads();
+        u32 pos = 0;
+        if (valid) {
+            pos = s_base[d] + below;
+            for (u32 w2 = 0; w2 < w; w2++) pos += s_wc[w2][d];
+        }
+        __syncthreads();
+        for (u32 dd = threadIdx.x; dd < LS_NB; dd += LS_T) {
+            u32 t = 0;
+#pragma unroll
+            for (u32 w2 = 0; w2 < LS_T / 64; w2++) {
+                t += s_wc[w2][dd];
+                s_wc[w2][dd] = 0;
+            }
+            s_base[dd] += t;
+        }
+        if (valid) {
+            vout[pos] = v[i];
+            if (kout) kout[pos] = k[i];
+        }
+        __syncthreads();
     }
 }
 
@@ -2299,32 +2418,56 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         };
         // LSD sort of m entries on `bits` key bits (pass-0 keys from kf0): entry ids to vout, the first
         // sorted index of every key to head (pre-set to NONE); ka / va: scratch for the middle passes
-        auto lsd_sort = [&](auto kf0, u64 m, u32 bits, u32* ka, u32* va, u32* vout, u32* head) {
+        auto lsd_sort = [&](auto kf0, u64 m, u32 bits, u32* ka, u32* va, u32* vout, u32* head, u32 nkeys) {
             const u32 npass = std::max<u32>(1, (bits + LS_DB - 1) / LS_DB);
             if (npass > LS_MAXP) throw error(-6, "lsd_sort: too many key bits");
             const u32 ntile = cdiv(m, LS_TILE);
             const u64 per = (u64)LS_NB * ntile;
             u32* H = g_ls_h.get(per + 1);
             u32* Gs = g_ls_g.get(per + 1);
-            // ping-pong: pass p reads what pass p - 1 wrote
-            u32 *kb[2] = {ka, npass > 2 ? g_predk.get(m + 1) : nullptr}, *vb[2] = {va, npass > 2 ? g_ids2.get(m + 1) : nullptr};
+            // the first pass (entry order: many distinct digits per wave) block-sorts its tiles, the
+            // later ones (inputs sorted on the lower digits: few per wave) rank by ballots
+            // (rr 13-bit dense keys: pass 0 278 vs 369 us, pass 1 167 vs 284 us); LZ77SSS_LS_BLOCKSORT /
+            // LZ77SSS_LS_RANK force either for every pass
+            const bool all_bs = std::getenv("LZ77SSS_LS_BLOCKSORT") != nullptr, all_rk = std::getenv("LZ77SSS_LS_RANK") != nullptr;
+            auto use_bsort = [&](u32 p) { return all_bs || (!all_rk && p == 0); };
+            const bool bsort = use_bsort(npass - 1);  // the last pass: heads in the block-sort kernel
+            // ping-pong: pass p reads what pass p - 1 wrote (the ranking form writes the last pass's
+            // keys too, for the key heads)
+            const bool kb1 = npass > 2 || (head && !bsort && npass > 1);
+            u32 *kb[2] = {ka, kb1 ? g_predk.get(m + 1) : nullptr}, *vb[2] = {va, npass > 2 ? g_ids2.get(m + 1) : nullptr};
+            u32* klast = nullptr;
             for (u32 p = 0; p < npass; p++) {
                 const bool first = p == 0, lastp = p + 1 == npass;
                 u32 *ko = kb[p & 1], *vo = lastp ? vout : vb[p & 1];
                 const u32 *ki = kb[(p + 1) & 1], *vi = vb[(p + 1) & 1];
                 const ls_plain kp{ki};
-                if (first) k_ls_hist<<<ntile, LS_T, 0, st>>>(kf0, m, p, ntile, H);
-                else k_ls_hist<<<ntile, LS_T, 0, st>>>(kp, m, p, ntile, H);
+                if (first) k_ls_hist<decltype(kf0), false><<<ntile, LS_T, 0, st>>>(kf0, m, p, ntile, H);
+                else k_ls_hist<ls_plain, true><<<ntile, LS_T, 0, st>>>(kp, m, p, ntile, H);
                 excl_sum64(H, Gs, 0u, per, scan_tmp, st);
-                if (first && lastp)
-                    k_ls_scatter<decltype(kf0), true, true><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, ko, vo, head);
-                else if (first)
-                    k_ls_scatter<decltype(kf0), true, false><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, ko, vo, head);
-                else if (lastp)
-                    k_ls_scatter<ls_plain, false, true><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, ko, vo, head);
-                else
-                    k_ls_scatter<ls_plain, false, false><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                if (use_bsort(p)) {
+                    if (first && lastp)
+                        k_ls_scatter<decltype(kf0), true, true><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                    else if (first)
+                        k_ls_scatter<decltype(kf0), true, false><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                    else if (lastp)
+                        k_ls_scatter<ls_plain, false, true><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                    else
+                        k_ls_scatter<ls_plain, false, false><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, ko, vo, head);
+                } else {
+                    u32* kw = (lastp && !head) ? nullptr : ko;
+                    if (lastp) klast = kw;
+                    if (first && lastp)
+                        k_ls_rank<decltype(kf0), true, true><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, kw, vo);
+                    else if (first)
+                        k_ls_rank<decltype(kf0), true, false><<<ntile, LS_T, 0, st>>>(kf0, ki, vi, m, p, ntile, Gs, kw, vo);
+                    else if (lastp)
+                        k_ls_rank<ls_plain, false, true><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, kw, vo);
+                    else
+                        k_ls_rank<ls_plain, false, false><<<ntile, LS_T, 0, st>>>(kp, ki, vi, m, p, ntile, Gs, kw, vo);
+                }
             }
+            if (head && !bsort) k_dense_heads<<<cdiv(cdiv(m + 1, 4), 256), 256, 0, st>>>(klast, m, nkeys, head);
             LZ_HIP(hipGetLastError());
         };
         // base sets this large get their predecessors in sorted order and moved back to
@@ -2390,7 +2533,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     u32* dstart = g_dstart.get((u64)D + 2);
                     LZ_HIP(hipMemsetAsync(dstart, 0xFF, (u64)D * 4, st));
                     k_set_u32x2<<<1, 1, 0, st>>>(dstart + D, (u32)ne5, 0u);
-                    lsd_sort(ls_dense{keys, pbm, pwp}, ne5, dense_bits, skeys, vals, svals, dstart);
+                    lsd_sort(ls_dense{keys, pbm, pwp}, ne5, dense_bits, skeys, vals, svals, dstart, D);
                     if (std::getenv("LZ77SSS_LSD_CHECK")) {
                         // the rocprim path into scratch, compared entry by entry
                         u32* dk = g_sdk.get(ne5 + 1);
@@ -2482,7 +2625,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             if (dense) {
                 u32* dstart = g_dstart.get((u64)D + 1);
                 if (ne5 >= pred_sorted_min && !ls)
-                    k_dense_heads<<<cdiv(ne5 + 1, 256), 256, 0, st>>>(skeys, ne5, D, dstart);
+                    k_dense_heads<<<cdiv(cdiv(ne5 + 1, 4), 256), 256, 0, st>>>(skeys, ne5, D, dstart);
                 k_bstart_rank<<<cdiv(cdiv((u64)nslots + 1, 4), 256), 256, 0, st>>>(pbm, pwp, dstart, nslots, D,
                                                                           g_bstart.get((u64)nslots + 1));
             } else {
@@ -2502,12 +2645,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         // positions that join later and are missing from it go to the small extra list.
         u32* bmA = g_bmA.get(nw);
         u64 na_main = 0;
-        bool bmA_zero = false;
-        // I_fresh: I was set by set_state(true) and not changed since, so |I| is the count of base
-        // ranks in I (i_cnt[2]) and I' == I is decided by counting the chain's inserts (i_cnt[0]:
-        // new bits of I', i_cnt[1]: those outside I) instead of a full-length xor and count
+        bool bmA_zero = false;  // the main list is empty and bmA was not computed (I within the base set)
+        // I_fresh: I was set by set_state(true) and not changed since (I lies within the base set), so
+        // I' == I is decided by two checks over the chain's inserts and the base ranks (i_cnt[0]:
+        // inserts outside I, i_cnt[1]: positions of I not inserted) instead of a full-length xor and count
         bool I_fresh = false;
-        u32* i_cnt = counters.get(16) + 12;  // the main list is empty and bmA was not computed (I within the base set)
+        u32* i_cnt = counters.get(16) + 12;
         auto build_list = [&](const u32* bm, dbuf<u32>& k32, dbuf<pos_t>& kpos, dbuf<u64>& ka, dbuf<u64>& kb,
                               dbuf<u32>& bucket, const u64*& keys_out, u64& nkeys, const u32*& bk_out,
                               const pos_t*& apos_out, u64& napos_out) -> u64 {
@@ -2559,10 +2702,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         auto set_state = [&](bool within_base) {
             W.bmI = bmI;
             I_fresh = within_base;
-            if (within_base) LZ_HIP(hipMemsetAsync(i_cnt + 2, 0, 4, st));
             if (nb)
-                k_rem_from_bm<<<std::min<u64>(cdiv(nb, 256), 4096), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem, (pos_t*)W.iposr,
-                                                            within_base ? i_cnt + 2 : nullptr);
+                k_rem_from_bm<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, nb, bmI, off, (u8*)W.rem, (pos_t*)W.iposr);
             if (!within_base) return rebuild_added(true);
             bmA_zero = true;
             na_main = 0;
@@ -2744,29 +2885,34 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
                 const bool fast = I_fresh && !std::getenv("LZ77SSS_NO_FAST_CHECK");
                 if (fast) LZ_HIP(hipMemsetAsync(i_cnt, 0, 8, st));
-                if (nchain)
+                if (nchain) {
+                    // a long gap is walked by one wave: with few chain nodes, the long ranges go to the
+                    // whole grid instead
+                    constexpr u32 LNG_CAP = 1024;
+                    u32* lng = (u32*)g_lng.get(2 + 4 * LNG_CAP);
+                    LZ_HIP(hipMemsetAsync(lng, 0, 8, st));
                     k_chain_inserts<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2,
-                                                                                     bmI, fast ? i_cnt : nullptr);
+                                                                                     bmI, fast ? i_cnt : nullptr, 2048u, lng,
+                                                                                     LNG_CAP);
+                    k_chain_inserts_long<<<1024, 256, 0, st>>>(lng, LNG_CAP, bmI2, bmI, fast ? i_cnt : nullptr);
+                }
                 if (tail && hc[1]) {
                     pos_t* d_tins = tail_ins_buf.p;
                     k_set_pairs<<<1, 64, 0, st>>>(d_tins, (u32)hc[1], off, bmI2, bmI, fast ? i_cnt : nullptr);
                 }
                 bool same = false;
                 if (fast) {
-                    u32 ic[3];
+                    // I' == I  <=>  no insert outside I  and  every position of I (all base ranks
+                    // not removed: I lies within the base set) inserted
+                    if (nb) k_subset_check<<<cdiv(nb, 256), 256, 0, st>>>(W.ipos, W.rem, nb, bmI2, off, i_cnt + 1);
+                    u32 ic[2];
                     hread rb(st);
-                    rb.add(ic, (const u32*)i_cnt, 3);
+                    rb.add(ic, (const u32*)i_cnt, 2);
                     rb.sync();
-                    same = ic[1] == 0 && ic[0] == ic[2];  // I' within I and |I'| = |I|
+                    same = ic[0] == 0 && ic[1] == 0;
                     if (dbg)
-                        std::fprintf(stderr, "[lz77sss-debug] greedy fast check: |I'|=%u outside I=%u |I|=%u -> %s\n", ic[0],
-                                     ic[1], ic[2], same ? "equal" : "full check");
-                }
-                if (dbg) {  // (before the scan below: k_bmb_write reads its offsets from g_bincl)
-                    const u64 c1 = bmb_scan(bm_bits{bmI, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
-                    const u64 c2 = bmb_scan(bm_bits{bmI2, nullptr}, nw, g_bsum, g_bincl, scan_tmp, st) >> 32;
-                    std::fprintf(stderr, "[lz77sss-debug] greedy |I|=%llu |I'|=%llu base=%llu chain=%u\n",
-                                 (unsigned long long)c1, (unsigned long long)c2, (unsigned long long)nb, nchain);
+                        std::fprintf(stderr, "[lz77sss-debug] greedy fast check: inserts outside I=%u, waves with I positions "
+                                     "not inserted=%u -> %s\n", ic[0], ic[1], same ? "equal" : "full check");
                 }
                 u64 ny = 0;
                 if (!same) {

@@ -184,6 +184,7 @@ struct engine {
     dbuf<u8> g_cut;     // chain_cut + completion counters
     dbuf<u64> g_xk, g_xk2;
     dbuf<u32> g_ls_h, g_ls_g;  // LSD base sort: digit counts per tile and their scans (csrc/greedy.hip)
+    dbuf<u32> g_lng;           // long chain ranges for k_chain_inserts_long
     // exact mode (csrc/exact.hip)
     dbuf<u64> x_key, x_key2, x_off, x_wide;
     dbuf<u32> x_idx, x_idx2, x_sa, x_rank, x_flag, x_tree, x_ltree, x_lcp, x_lpf, x_src, x_mark, x_chunk;
@@ -286,26 +287,40 @@ struct hread_job {
     u32 off[16], bytes[16];
     u32 n, seq;
 };
-// copies the requested values into the slot, then publishes the sequence number (offset 0)
-static __global__ __launch_bounds__(64) void k_hread(hread_job J, u8* __restrict__ dst) {
-    for (u32 i = 0; i < J.n; i++)
-        for (u32 b = threadIdx.x; b < J.bytes[i]; b += 64) dst[J.off[i] + b] = J.src[i][b];
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();
-        *(volatile u32*)dst = J.seq;
+// copies the requested values into the slot as 8-byte words (sequence number << 32 | 4 value
+// bytes): a word is complete when the host sees its sequence number, so no fence orders the
+// payload before a flag (a system-scope fence writes back the whole L2 first: 60 us after the
+// bitmap fills of the greedy setup)
+static __global__ __launch_bounds__(64) void k_hread(hread_job J, u64* __restrict__ dst) {
+    if (J.n == 0 && threadIdx.x == 0)  // a plain wait: one word
+        __hip_atomic_store(&dst[0], (u64)J.seq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (u32 i = 0; i < J.n; i++) {
+        const u32* src = (const u32*)J.src[i];
+        for (u32 w = threadIdx.x; w < J.bytes[i] / 4; w += 64)
+            __hip_atomic_store(&dst[J.off[i] / 4 + w], ((u64)J.seq << 32) | src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
-// waits for the slot's sequence number `seq` (the stream's error state is checked while spinning)
-inline void spin_wait(sync_slot& S, u32 seq, hipStream_t st) {
+// waits until the nw words from word w0 carry sequence number seq (the stream's error state is
+// checked while spinning), then unpacks them into out
+inline void spin_wait(sync_slot& S, u32 seq, u64 w0, u64 nw, u32* out, hipStream_t st) {
+    volatile u64* W = (volatile u64*)S.h + w0;
+    u64 done = 0;
     for (u64 it = 1;; it++) {
-        if (__atomic_load_n((volatile u32*)S.h, __ATOMIC_ACQUIRE) == seq) return;
+        while (done < nw) {
+            const u64 v = W[done];
+            if ((u32)(v >> 32) != seq) break;
+            out[done++] = (u32)v;
+        }
+        if (done == nw) return;
         if ((it & 255) == 0) {
             const hipError_t e = hipStreamQuery(st);
             if (e == hipSuccess) {
-                if (__atomic_load_n((volatile u32*)S.h, __ATOMIC_ACQUIRE) == seq) return;
-                throw error(-6 /* LZ77SSS_EINTERNAL */, "read-back: stream idle but the value never arrived");
+                for (; done < nw; done++) {
+                    const u64 v = W[done];
+                    if ((u32)(v >> 32) != seq) throw error(-6 /* LZ77SSS_EINTERNAL */, "read-back: stream idle but a value never arrived");
+                    out[done] = (u32)v;
+                }
+                return;
             }
             if (e != hipErrorNotReady) LZ_HIP(e);
         }
@@ -317,16 +332,17 @@ inline void spin_wait(sync_slot& S, u32 seq, hipStream_t st) {
 struct hread {
     hipStream_t st;
     sync_slot& S;
-    size_t off = 64;
+    size_t off = 0;  // payload bytes so far (4 per 8-byte slot word)
     struct item { void* dst; const void* src; size_t off, bytes; };
     item items[16];
     int n = 0;
+    u32 tmp[1024];
     explicit hread(hipStream_t s) : st(s), S(host_slot()) {}
     template <class T>
     void add(T* dst, const T* src, size_t count = 1) {
+        static_assert(sizeof(T) % 4 == 0, "read-back values are whole 4-byte words");
         const size_t b = sizeof(T) * count;
-        off = (off + 15) & ~(size_t)15;
-        if (off + b > 8192 || n == 16) throw error(-6 /* LZ77SSS_EINTERNAL */, "hread: staging slot full");
+        if (off + b > 4 * 1024 || n == 16) throw error(-6 /* LZ77SSS_EINTERNAL */, "hread: staging slot full");
         items[n++] = {dst, src, off, b};
         off += b;
     }
@@ -340,17 +356,18 @@ struct hread {
             }
             J.n = (u32)n;
             J.seq = ++S.seq;
-            k_hread<<<1, 64, 0, st>>>(J, S.d);
+            if (J.seq == 0) J.seq = S.seq = 1;  // (0: the slot's initial contents)
+            k_hread<<<1, 64, 0, st>>>(J, (u64*)S.d);
             LZ_HIP(hipGetLastError());
-            spin_wait(S, J.seq, st);
+            spin_wait(S, J.seq, 0, n ? off / 4 : 1, tmp, st);
         } else {
             for (int k = 0; k < n; k++)
-                LZ_HIP(hipMemcpyAsync(S.h + items[k].off, items[k].src, items[k].bytes, hipMemcpyDeviceToHost, st));
+                LZ_HIP(hipMemcpyAsync((u8*)tmp + items[k].off, items[k].src, items[k].bytes, hipMemcpyDeviceToHost, st));
             LZ_HIP(hipStreamSynchronize(st));
         }
-        for (int k = 0; k < n; k++) std::memcpy(items[k].dst, S.h + items[k].off, items[k].bytes);
+        for (int k = 0; k < n; k++) std::memcpy(items[k].dst, (const u8*)tmp + items[k].off, items[k].bytes);
         n = 0;
-        off = 64;
+        off = 0;
     }
 };
 template <class T>

@@ -328,6 +328,11 @@ def test_lsd_base_sort_vs_oracle(session, orc, lz, mib, seed, monkeypatch):
     monkeypatch.setenv("LZ77SSS_NO_PRED", "1")
     _, F1 = run(session, T)
     assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    for knob in ("LZ77SSS_LS_RANK", "LZ77SSS_LS_BLOCKSORT"):  # every pass by ballot ranking / by block sort
+        monkeypatch.setenv(knob, "1")
+        _, F2 = run(session, T)
+        assert np.array_equal(F2, F_ref), knob
+        monkeypatch.delenv(knob)
     monkeypatch.setenv("LZ77SSS_NO_LSD", "1")
     _, F0 = run(session, T)
     assert np.array_equal(F0, F_ref)
