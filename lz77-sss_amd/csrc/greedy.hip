@@ -83,13 +83,37 @@ struct gap_cfg {
     const u128* negpow; // [5][256]: -(o * b^len) mod P
 };
 
+// fp * b + negpow_out + in mod P, canonical: fp, negpow_out < P, b < 2^20, so the sum is below
+// 2^128 and one 64 x 64 product with its high half, one 43-bit x 20-bit product and two folds at
+// bit 107 replace the generic 128-bit product and the inner reduction (k_slots is VALU-bound on
+// these rolls)
 __device__ __forceinline__ u128 kr_roll(u128 fp, u64 b, u128 negpow_out, u32 in) {
-    return mod107(fp * b + mod107((u128)in + negpow_out));
+    constexpr u64 M43 = (1ull << 43) - 1;
+    const u64 lo = (u64)fp, hi = (u64)(fp >> 64);
+    const u64 clo = (u64)negpow_out, chi = (u64)(negpow_out >> 64);
+    u64 xlo = lo * b;
+    u64 xhi = __umul64hi(lo, b) + hi * b;
+    const u64 t = xlo + clo;
+    u64 carry = t < xlo ? 1u : 0u;
+    const u64 t2 = t + in;
+    carry += t2 < t ? 1u : 0u;
+    xlo = t2;
+    xhi += chi + carry;
+#pragma unroll
+    for (int f = 0; f < 2; f++) {  // x = (x mod 2^107) + (x >> 107)
+        const u64 q = xhi >> 43;
+        xhi &= M43;
+        const u64 s2 = xlo + q;
+        xhi += s2 < xlo ? 1u : 0u;
+        xlo = s2;
+    }
+    if (xhi == M43 && xlo == ~0ull) return 0;  // x == P
+    return ((u128)xhi << 64) | xlo;
 }
 // Phi_x(T[q..q+len)) mod P by direct evaluation (roll-ins only)
 __device__ __forceinline__ u128 kr_direct(const u8* T, u64 q, u32 len, u64 b) {
     u128 fp = 0;
-    for (u32 j = 0; j < len; j++) fp = mod107(fp * b + T[q + j]);
+    for (u32 j = 0; j < len; j++) fp = kr_roll(fp, b, 0, T[q + j]);
     return fp;
 }
 
@@ -140,7 +164,6 @@ __global__ __launch_bounds__(SL_T) void k_slots(const u8* __restrict__ T, gap_cf
             const u32 key = (u32)((u64)fp & G.mask);
             s_key[(cl * SL_K + j) * 5 + ord] = key;
             if (x == 4) s_pos[cl * SL_K + j] = q;
-            if (pf && !pf[key]) pf[key] = 1;  // slot presence (dense ids): plain stores, a hot slot is read far more often
             if (q + 1 < ch.q1) fp = kr_roll(fp, b, np[T[q]], T[q + len]);
         }
         __syncthreads();
@@ -152,8 +175,12 @@ __global__ __launch_bounds__(SL_T) void k_slots(const u8* __restrict__ T, gap_cf
             const u64 left = (u64)(cc.q1 - cc.q0);
             if (k0 >= left || r >= 5 * min<u64>(SL_K, left - k0)) continue;
             const u64 e = 5ull * (cc.rank0 + k0) + r;
-            keys[e] = s_key[idx];
+            const u32 key = s_key[idx];
+            keys[e] = key;
             if (vals) vals[e] = (u32)e;
+            // slot presence (dense ids): plain stores, a hot slot is read far more often.  Here, off
+            // the fingerprint chains: in the roll loop the test's load stalled every step of a chain
+            if (pf && !pf[key]) pf[key] = 1;
         }
         if (ipos) {
             for (u32 idx = tid; idx < SL_CH * SL_K; idx += SL_T) {
@@ -2409,7 +2436,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 u32* ncs = g_tmp8.get(ni + 1);
                 k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(ra, rb, ni, nc, ncs, len);
                 npos = excl_scan(len, rk, ni, scan_tmp, st);
-                if (npos < (u64)SLOT_CHUNK_LONG << 18) chl = SLOT_CHUNK_SHORT;
+                if (npos < (u64)SLOT_CHUNK_LONG << (std::getenv("LZ77SSS_SLOT_CHUNK_SH") ? std::atoi(std::getenv("LZ77SSS_SLOT_CHUNK_SH")) : 18)) chl = SLOT_CHUNK_SHORT;
                 nch = excl_scan(chl == SLOT_CHUNK_LONG ? nc : ncs, choff, ni, scan_tmp, st);
             }
             ichunk* ch = (ichunk*)dch.get(std::max<u64>(1, nch) * sizeof(ichunk));
