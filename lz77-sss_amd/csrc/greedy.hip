@@ -1772,7 +1772,16 @@ __global__ void k_spec_check(const u32* __restrict__ used, int parts, u64 nw, co
         }
     if (any && bad[1] != 0xFFFFFFFFu) {  // debug counters (bad[1] = ~0: off): used slots, differing ones
         atomicAdd(bad + 1, 1u);
-        if (differs) atomicAdd(bad + 2, 1u);
+        if (differs) {
+            atomicAdd(bad + 2, 1u);
+            const u32 x = atomicAdd(bad + 3, 1u);  // up to 8 examples (slot, speculated, true) from bad + 4
+            if (x < 8) {
+                u64* ex = (u64*)(bad + 4) + 3 * x;
+                ex[0] = k;
+                ex[1] = (u64)spec[k];
+                ex[2] = (u64)tru[k];
+            }
+        }
     }
 }
 // the carried table for the rest: the speculative block's writes (values > its start) over the true table
@@ -3161,10 +3170,10 @@ int engine::spec_resolve(const void* true_tab, u64 bytes, int parts) {
     LZ_HIP(hipMemcpyAsync(tru, true_tab, m * sizeof(pos_t), hipMemcpyDefault, st));
     int acc = 0;
     if (tracked) {
-        u32* bad = g_specbad.get(4);
+        u32* bad = g_specbad.get(4 + 2 * 3 * 8);
         const bool dbg = debug_enabled() || std::getenv("LZ77SSS_SPEC_DEBUG");
-        const u32 init[3] = {(u32)parts, dbg ? 0u : 0xFFFFFFFFu, 0};
-        LZ_HIP(hipMemcpyAsync(bad, init, 12, hipMemcpyHostToDevice, st));
+        const u32 init[4] = {(u32)parts, dbg ? 0u : 0xFFFFFFFFu, 0, 0};
+        LZ_HIP(hipMemcpyAsync(bad, init, 16, hipMemcpyHostToDevice, st));
         k_spec_check<<<cdiv(m, 256), 256, 0, st>>>(g_hsused.p, parts, spec_m / 32 + 1, g_hsave.p, tru, m, bad);
         u32 hb[3];
         LZ_HIP(hipMemcpyAsync(hb, bad, 12, hipMemcpyDeviceToHost, st));
@@ -3175,6 +3184,13 @@ int engine::spec_resolve(const void* true_tab, u64 bytes, int parts) {
                          "[lz77sss] speculative block at %llu: %u entry-table slots used, %u differ; %d of %d parts "
                          "accepted\n",
                          (unsigned long long)spec_base, hb[1], hb[2], acc, parts);
+        if (dbg && hb[2]) {
+            u64 ex[24];
+            LZ_HIP(hipMemcpy(ex, bad + 4, sizeof(ex), hipMemcpyDeviceToHost));
+            for (u32 x = 0; x < std::min<u32>(hb[2], 8); x++)
+                std::fprintf(stderr, "[lz77sss]   slot %llu: speculated %lld, true %lld (positions + 1)\n",
+                             (unsigned long long)ex[3 * x], (long long)ex[3 * x + 1], (long long)ex[3 * x + 2]);
+        }
     }
     if (tracked && acc < parts)  // the table the first rejected part started from
         LZ_HIP(hipMemcpyAsync(g_Hs.p, g_hsave.p + (u64)acc * spec_m, m * sizeof(pos_t), hipMemcpyDeviceToDevice, st));

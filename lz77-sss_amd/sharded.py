@@ -331,11 +331,14 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     # state); the rest of the block is walked again from the exit state of the last confirmed
     # part, with their writes over the true table, exactly as without speculation.
     g = chain_bounds(n, world)
-    if speculate is None:  # off by default
-        speculate = os.environ.get("LZ77SSS_SPECULATE", "0") == "1"
-    spec = speculate and multi and rank > 0 and g[rank] > 0
+    if speculate is None:  # off by default; LZ77SSS_SPECULATE=1: lead-in, =2: ring
+        speculate = {"1": True, "2": "ring"}.get(os.environ.get("LZ77SSS_SPECULATE", "0"), False)
+    ring = speculate == "ring" and multi
+    spec = bool(speculate) and multi and rank > 0 and g[rank] > 0
     t_spec = 0.0
     spec_state, parts = None, []  # parts: (entry state, exit state, factors)
+    F0 = None  # ring: rank 0's block (its round-A walk is the true chain)
+    state0 = None
 
     def take():  # the session's last factors, as a device tensor
         fb = sess.factor_bytes()
@@ -344,12 +347,73 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
             sess.copy_factors(F.data_ptr(), fb)
         return F[: fb // 8]
 
+    def table_out():  # the session's carried table as a device tensor (uint8 view)
+        t = torch.empty(max(tab_bytes, 1), dtype=torch.uint8, device=dev)
+        sess.carried_get(tab_bytes, device_ptr=t.data_ptr())
+        return t
+
+    wide = getattr(sess, "pos64", False)
+
+    def as_pos(t):  # table bytes -> int64 positions + 1 (uint32 tables widened)
+        return t.view(torch.int64) if wide else t.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+
+    def as_bytes(v):
+        return v.view(torch.uint8) if wide else v.to(torch.int32).view(torch.uint8)
+
+    def send_state(st, tab):
+        hdr = torch.tensor([st[0], st[1], st[2], 1], dtype=torch.int64, device=cdev)
+        dist.send(hdr, rank + 1, group=group)
+        dist.send(tab.to(cdev), rank + 1, group=group)
+
+    def recv_state():
+        hdr = torch.zeros(4, dtype=torch.int64, device=cdev)
+        dist.recv(hdr, rank - 1, group=group)
+        tab = torch.empty(max(tab_bytes, 1), dtype=torch.uint8, device=cdev)
+        dist.recv(tab, rank - 1, group=group)
+        if nccl:
+            ready()
+        return (int(hdr[0]), int(hdr[1]), int(hdr[2])), tab.to(dev)
+
+    if ring:
+        # round A (every rank at once): rank 0 walks its block exactly; rank r > 0 walks a lead-in
+        # and its block from the lead-in's exit.  The prefix max over the ranks of the tables of
+        # each block's own inserts (rank 0: its whole exit table), passed along the ranks, is the
+        # speculated entry table of round B; the previous rank's round-A exit state its entry state
+        ts = time.perf_counter()
+        if rank == 0:
+            st = (0, 0, 0)
+            if g[1] > 0:
+                _, st = sess.greedy_block(0, 0, 0, False, g[1], **params)
+            state0, F0 = tuple(st), take()
+            prefix = table_out()
+            if world > 1:
+                send_state(state0, prefix)
+        else:
+            st = (0, 0, 0)
+            if g[rank] > 0:
+                lead0 = g[rank] - spec_lead(n, g, rank)
+                _, st = sess.greedy_block(lead0, lead0, 0, False, g[rank], seed=True, **params)
+                st = tuple(st)
+                if st[0] < g[rank + 1]:
+                    _, st = sess.greedy_block(*st, True, g[rank + 1], **params)
+                    st = tuple(st)
+            mine = as_pos(table_out())
+            own = torch.where(mine > g[rank], mine, torch.zeros_like(mine))  # inserts at or after g_r
+            del mine
+            spec_state, tin = recv_state()
+            if rank + 1 < world:
+                send_state(st, as_bytes(torch.maximum(as_pos(tin), own)))
+            del own
+            sess.carried_set(nbytes=tab_bytes, device_ptr=tin.data_ptr())
+            del tin
+        t_spec = time.perf_counter() - ts
     if spec:
         import lz77sss as L
 
         ts = time.perf_counter()
-        lead0 = g[rank] - spec_lead(n, g, rank)
-        _, spec_state = sess.greedy_block(lead0, lead0, 0, False, g[rank], seed=True, **params)
+        if not ring:
+            lead0 = g[rank] - spec_lead(n, g, rank)
+            _, spec_state = sess.greedy_block(lead0, lead0, 0, False, g[rank], seed=True, **params)
         spec_state = st = tuple(spec_state)
         npart = spec_parts()
         for k in range(npart):
@@ -364,10 +428,12 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
                 _, st2 = sess.greedy_block(*st, True, e_k, **params)
                 parts.append((st, tuple(st2), take()))
                 st = tuple(st2)
-        t_spec = time.perf_counter() - ts
+        t_spec += time.perf_counter() - ts
     t_wait = time.perf_counter()
     state, carried = (0, 0, 0), False
     accepted = None  # speculation: the number of parts that stood
+    if ring and rank == 0:
+        state, carried = state0, True  # block 0 is done (round A)
     if rank > 0:
         hdr = torch.zeros(4, dtype=torch.int64, device=cdev)
         dist.recv(hdr, rank - 1, group=group)
@@ -389,8 +455,8 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
                 sess.carried_set(nbytes=tab_bytes, device_ptr=tab.data_ptr())
             del tab
     keep = [F for (_, _, F) in parts[: accepted or 0]]  # factors of the confirmed parts
-    F_rest = None
-    if not (parts and accepted == len(parts)) and state[0] < g[rank + 1]:
+    F_rest = F0
+    if F0 is None and not (parts and accepted == len(parts)) and state[0] < g[rank + 1]:
         _, state = sess.greedy_block(*state, carried, g[rank + 1], **params)
         state, carried = tuple(state), True
         F_rest = take()

@@ -466,8 +466,32 @@ def test_sharded_resident_speculative_blocks(lz, orc, world, lead, parts):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,lead,parts", [(2, None, None), (3, None, None), (3, 100000, None), (4, 30000, 3),
+                                              (3, 1, 1)])
+def test_sharded_resident_ring_speculation(lz, orc, world, lead, parts):
+    """Ring speculation: round A walks every block at once (rank 0 exactly, the others
+    after a lead-in), the prefix max of the blocks' own-insert tables along the ranks is each rank's
+    round-B entry table (the previous rank's round-A exit its entry state); round B's parts are then
+    confirmed against the true table in rank order.  The stream equals the one-process stream and
+    the non-speculative run whatever the lead-in and the part count; rank 1 (entered from rank 0's
+    true exit) keeps every part."""
+    T = lz.gen_genome(4 << 20, 1 << 20, 0.001, 37)
+    F_ref = orc.factorize(T)[0].astype(np.uint64)
+    env = {} if lead is None else {"LZ77SSS_SPEC_LEAD": str(lead)}
+    if parts is not None:
+        env["LZ77SSS_SPEC_PARTS"] = str(parts)
+    res = _run_resident(world, T, False, env=env, speculate="ring")
+    for rank, F, same, keys, (acc, npart) in res:
+        assert same and {"spec_walk", "chain_wait", "spec_accepted"} <= set(keys)
+        assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+        if rank == 1:
+            assert npart is not None and acc == npart
+
+
+@pytest.mark.gpu
 @pytest.mark.slow
-def test_sharded_resident_u64_past_4gib_hash():
+@pytest.mark.parametrize("world,speculate", [(2, True), (3, "ring")])
+def test_sharded_resident_u64_past_4gib_hash(world, speculate):
     """configs[3] at C4's mutation rate past 2^32: a 4 GiB + 3 MiB chr19-style text (0.1 %
     mutations, pos_t = uint64_t) factorized by 2 ranks (gloo, sharing the GPU) with
     factorize_sharded_resident == the oracle's stream (SHA-256 fixture of
@@ -476,8 +500,8 @@ def test_sharded_resident_u64_past_4gib_hash():
 
     e = json.loads((ROOT / "tests" / "golden" / "stream_hashes.json").read_text())["chr19_4gib_u64"]
     gen = dict(n=e["n"], base_len=e["args"]["base_len"], mut=e["args"]["mut"], seed=e["args"]["seed"])
-    for rank, z, h, keys, acc, tm in _run_resident(2, np.zeros(0, np.uint8), True, gen):
-        print(f"rank {rank}: speculative block accepted={acc} times={tm}")
+    for rank, z, h, keys, acc, tm in _run_resident(world, np.zeros(0, np.uint8), True, gen, speculate=speculate):
+        print(f"rank {rank}: speculation {speculate}: accepted={acc} times={tm}")
         assert {"emit", "greedy_chain", "prepare", "sss"} <= set(keys)
         assert z == e["z"] and h == e["stream_sha256"]
 
