@@ -1911,10 +1911,17 @@ __global__ void k_first_diff_u32(const u32* __restrict__ a, const u32* __restric
 constexpr u32 LS_T = 256, LS_IPT = 8, LS_TILE = LS_T * LS_IPT, LS_DB = 7, LS_NB = 1u << LS_DB, LS_MAXP = 5;
 struct ls_dense {  // pass-0 key of entry e: the dense id of its slot
     const u32* keys;
-    const u32* pbm;
-    const u32* pwp;
-    __device__ __forceinline__ u32 operator()(u64 e) const { return slot_rank(pbm, pwp, keys[e]); }
+    const u64* pbw;  // per presence word: rank of its first slot << 32 | the word (one load per key)
+    __device__ __forceinline__ u32 operator()(u64 e) const {
+        const u32 k = keys[e];
+        const u64 w = pbw[k >> 5];
+        return (u32)(w >> 32) + __popc((u32)w & ((1u << (k & 31)) - 1u));
+    }
 };
+__global__ void k_pack_pbw(const u32* __restrict__ pbm, const u32* __restrict__ pwp, u64 nw, u64* __restrict__ pbw) {
+    const u64 w = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w < nw) pbw[w] = ((u64)pwp[w] << 32) | pbm[w];
+}
 struct ls_plain {
     const u32* keys;
     __device__ __forceinline__ u32 operator()(u64 e) const { return keys[e]; }
@@ -2569,7 +2576,9 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     u32* dstart = g_dstart.get((u64)D + 2);
                     LZ_HIP(hipMemsetAsync(dstart, 0xFF, (u64)D * 4, st));
                     k_set_u32x2<<<1, 1, 0, st>>>(dstart + D, (u32)ne5, 0u);
-                    lsd_sort(ls_dense{keys, pbm, pwp}, ne5, dense_bits, skeys, vals, svals, dstart, D);
+                    u64* pbw = (u64*)g_pbw.get(2 * npw);
+                    k_pack_pbw<<<cdiv(npw, 256), 256, 0, st>>>(pbm, pwp, npw, pbw);
+                    lsd_sort(ls_dense{keys, pbw}, ne5, dense_bits, skeys, vals, svals, dstart, D);
                     if (std::getenv("LZ77SSS_LSD_CHECK")) {
                         // the rocprim path into scratch, compared entry by entry
                         u32* dk = g_sdk.get(ne5 + 1);

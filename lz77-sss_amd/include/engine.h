@@ -185,6 +185,7 @@ struct engine {
     dbuf<u64> g_xk, g_xk2;
     dbuf<u32> g_ls_h, g_ls_g;  // LSD base sort: digit counts per tile and their scans (csrc/greedy.hip)
     dbuf<u32> g_lng;           // long chain ranges for k_chain_inserts_long
+    dbuf<u32> g_pbw;           // presence words with their ranks, packed (the LSD sort's dense-id map)
     // exact mode (csrc/exact.hip)
     dbuf<u64> x_key, x_key2, x_off, x_wide;
     dbuf<u32> x_idx, x_idx2, x_sa, x_rank, x_flag, x_tree, x_ltree, x_lcp, x_lpf, x_src, x_mark, x_chunk;
