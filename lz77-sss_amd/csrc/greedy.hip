@@ -1366,13 +1366,13 @@ static u64 bmb_scan(M mk, u64 nw, dbuf<u64>& bs, dbuf<u64>& bi, dbuf<u8>& tmp, h
 // chunk length is 128, or 32 when that leaves fewer than ~2^18 chunks.
 constexpr u32 SLOT_CHUNK_LONG = 128, SLOT_CHUNK_SHORT = 32;
 __global__ void k_iv_chunk_counts(const pos_t* __restrict__ st, const pos_t* __restrict__ en, u32 ni, u32* __restrict__ nch,
-                                  u32* __restrict__ nch_short, u32* __restrict__ len) {
+                                  u32* __restrict__ nch_short, u32* __restrict__ len, u32 short_len) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= ni) return;
     const u32 l = (u32)(en[k] - st[k]);  // intervals hold < 2^32 / 5 positions (entry ids are 32-bit)
     len[k] = l;
     nch[k] = (l + SLOT_CHUNK_LONG - 1) / SLOT_CHUNK_LONG;
-    nch_short[k] = (l + SLOT_CHUNK_SHORT - 1) / SLOT_CHUNK_SHORT;
+    nch_short[k] = (l + short_len - 1) / short_len;
 }
 // one thread per chunk; its interval by binary search over the chunk offsets
 __global__ void k_iv_chunks(const pos_t* __restrict__ st, const pos_t* __restrict__ en, u32 ni, const u32* __restrict__ choff,
@@ -2450,9 +2450,12 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             u32 chl = SLOT_CHUNK_LONG;
             if (ni) {
                 u32* ncs = g_tmp8.get(ni + 1);
-                k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(ra, rb, ni, nc, ncs, len);
+                // short chunks (test/tuning knob LZ77SSS_SLOT_CHUNK, <= SLOT_CHUNK_LONG)
+                const char* sce = std::getenv("LZ77SSS_SLOT_CHUNK");
+                const u32 scl = sce ? std::max(8u, std::min<u32>(SLOT_CHUNK_LONG, (u32)std::atoi(sce))) : SLOT_CHUNK_SHORT;
+                k_iv_chunk_counts<<<cdiv(ni, 256), 256, 0, st>>>(ra, rb, ni, nc, ncs, len, scl);
                 npos = excl_scan(len, rk, ni, scan_tmp, st);
-                if (npos < (u64)SLOT_CHUNK_LONG << (std::getenv("LZ77SSS_SLOT_CHUNK_SH") ? std::atoi(std::getenv("LZ77SSS_SLOT_CHUNK_SH")) : 18)) chl = SLOT_CHUNK_SHORT;
+                if (npos < (u64)SLOT_CHUNK_LONG << (std::getenv("LZ77SSS_SLOT_CHUNK_SH") ? std::atoi(std::getenv("LZ77SSS_SLOT_CHUNK_SH")) : 18)) chl = scl;
                 nch = excl_scan(chl == SLOT_CHUNK_LONG ? nc : ncs, choff, ni, scan_tmp, st);
             }
             ichunk* ch = (ichunk*)dch.get(std::max<u64>(1, nch) * sizeof(ichunk));
