@@ -62,32 +62,47 @@ __global__ void k_psv_nsv(const u32* __restrict__ SA, u32 s, sa_min_levels M, u3
 // candidate record per sync index: [srcP, endP, lP, srcN, endN, lN, hasP|hasN<<1, E]
 constexpr int CREC = 8;
 
+// two lanes per sync index (adjacent: side 0 = PSV, side 1 = NSV), each with its own LCE pair,
+// combined by a shuffle: the LCEs are dependent load chains, and one lane doing both sides
+// left 54 K indices (rr) on 848 waves
 __global__ void k_lpf_candidates(lce_view L, const u32* __restrict__ SA, const u32* __restrict__ PSV,
                                  const u32* __restrict__ NSV, pos_t* __restrict__ cand) {
-    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 i = t >> 1;
+    const int side = (int)(t & 1);
     const u32 s = L.s;
-    if (i >= s) return;
-    const pos_t* S = L.S;
-    const u32 r = L.ISA[i];
-    const pos_t Si = S[i];
-    const pos_t capmax = i >= 2 ? Si - S[i - 1] : Si;
-    pos_t rec[CREC] = {0, 0, 0, 0, 0, 0, 0, 0};
-    pos_t E = 0;
-#pragma unroll
-    for (int side = 0; side < 2; side++) {
+    pos_t src = 0, end = 0, l = 0;
+    int has = 0;
+    pos_t Si = 0;
+    if (i < s) {
+        const pos_t* S = L.S;
+        const u32 r = L.ISA[i];
+        Si = S[i];
+        const pos_t capmax = i >= 2 ? Si - S[i - 1] : Si;
         const u32 nb = side == 0 ? PSV[r] : NSV[r];
-        if (nb == s) continue;
-        const pos_t src = S[SA[nb]];
-        const pos_t end = Si + (pos_t)dev_lce(L, src, Si);
-        pos_t l = 0;
-        if (src != 0 && Si != 0) l = dev_lce_left(L.T, L.R, src - 1, Si - 1, capmax);
-        rec[side * 3 + 0] = src;
-        rec[side * 3 + 1] = end;
-        rec[side * 3 + 2] = l;
-        rec[6] |= 1u << side;
-        E = max(E, end);
+        if (nb != s) {
+            src = S[SA[nb]];
+            end = Si + (pos_t)dev_lce(L, src, Si);
+            if (src != 0 && Si != 0) l = dev_lce_left(L.T, L.R, src - 1, Si - 1, capmax);
+            has = 1;
+        }
     }
-    rec[7] = E;
+    const pos_t o_src = __shfl_xor(src, 1), o_end = __shfl_xor(end, 1), o_l = __shfl_xor(l, 1);
+    const int o_has = __shfl_xor(has, 1);
+    if (i >= s || side) return;
+    pos_t rec[CREC] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (has) {
+        rec[0] = src;
+        rec[1] = end;
+        rec[2] = l;
+    }
+    if (o_has) {
+        rec[3] = o_src;
+        rec[4] = o_end;
+        rec[5] = o_l;
+    }
+    rec[6] = (pos_t)(has | (o_has << 1));
+    rec[7] = max(has ? end : (pos_t)0, o_has ? o_end : (pos_t)0);
 #pragma unroll
     for (int x = 0; x < CREC; x++) cand[i * CREC + x] = rec[x];
 }
@@ -397,7 +412,7 @@ void engine::build_lpf_opt(const u8* T) {
     }
     // 2. candidates
     pos_t* cd = cand.get((u64)s * CREC);
-    k_lpf_candidates<<<g, 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, cd);
+    k_lpf_candidates<<<cdiv(2ull * s, 256), 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, cd);
     // 3. skip chain: pointer doubling over next[], nodes 0..s (s = end)
     const u32 m = s + 1;
     u32 T_lv = 0;
