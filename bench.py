@@ -374,7 +374,8 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
         t = time.perf_counter()
         F = sharded.factorize_sharded_resident(sess, n, rank, world, local_rank, timings=tm)
         print(f"[bench --shard] rank {rank}: step {time.perf_counter() - t:.2f} s, phases "
-              f"{ {k: round(v, 3) for k, v in tm.items()} }", file=sys.stderr, flush=True)
+              f"{ {k: (round(v, 3) if isinstance(v, float) else v) for k, v in tm.items()} }", file=sys.stderr,
+              flush=True)
         return F
 
     for _ in range(args.warmup):
@@ -394,7 +395,7 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
     t1 = time.perf_counter()
     barrier()
     dt, _ = aggregate((t1 - t0) / args.steps, n, world, dist, device="cuda")  # max over ranks
-    phases = {k: round(v * 1e3, 3) for k, v in tm.items()}
+    phases = {k: (round(v * 1e3, 3) if isinstance(v, float) else v) for k, v in tm.items()}
     z = int(F.shape[0])
     same = None
     st = sess.stats()

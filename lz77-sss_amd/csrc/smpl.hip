@@ -718,13 +718,29 @@ __global__ void k_adj_lce(lce_view L, const u32* __restrict__ C, const u32* __re
 }
 // interval samples of one sampled length (construction.cpp:265-305): every maximal rank
 // interval whose adjacent LCEs are >= len, keyed by the fingerprint of its context
+// the interval's end: the last e with adj[r + 1 .. e] >= len, by binary lifting over the
+// sparse-table minima of adj (levels mn[l][i] = min adj[i .. i + 2^l)); a linear scan took
+// seconds on repetitive text, where one interval spans millions of samples
+struct iv_levels { const u32* mn[MAX_LV]; u32 nlv; };
+__device__ __forceinline__ u32 iv_end(const iv_levels& M, const u32* adj, u32 c, u32 r, u32 len) {
+    u64 pos = (u64)r + 1;  // adj[r + 1 .. pos) are all >= len
+    for (int l = (int)M.nlv - 1; l >= 0; l--) {
+        const u64 w = 1ull << l;
+        if (pos + w <= c && M.mn[l][pos] >= len) pos += w;
+    }
+    return (u32)(pos - 1);
+}
+__global__ void k_iv_min_level(const u32* __restrict__ prev, u64 cnt, u64 half, u32* __restrict__ out) {
+    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < cnt) out[k] = min(prev[k], prev[k + half]);
+}
 __global__ void k_iv_insert(const smpl_view V, const u32* __restrict__ X, const u32* __restrict__ adj, u32 c,
-                            int left, u32 k, u32 len, u64* __restrict__ hkey, u64* __restrict__ hval, u64 hmask) {
+                            int left, u32 k, u32 len, u64* __restrict__ hkey, u64* __restrict__ hval, u64 hmask,
+                            iv_levels M) {
     const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= c) return;
     if (r > 0 && adj[r] >= len) return;  // not an interval start
-    u32 e = (u32)r;
-    while (e + 1 < c && adj[e + 1] >= len) e++;
+    const u32 e = iv_end(M, adj, c, (u32)r, len);
     const u32 pm = V.C[X[r]];
     if (left ? pm + 1 < len : (u64)pm + len > V.L.n) return;  // context shorter than len
     const u32 fp = left ? rks_sub(V, pm + 1 - len, len) : rks_sub(V, pm, len);
@@ -1202,10 +1218,21 @@ void engine::build_interval_samples(smpl_view& V, u64 nn, u64 za) {
     V.hkey = hkey;
     V.hval = hval;
     V.hmask = hs - 1;
-    for (int side = 0; side < 2; side++)
+    for (int side = 0; side < 2; side++) {
+        // sparse-table minima of adj[0 .. c) (level 0 is adj itself) for the interval ends
+        iv_levels M{};
+        M.mn[0] = adj[side];
+        M.nlv = 1;
+        while ((2ull << (M.nlv - 1)) <= c && M.nlv < (u32)MAX_LV) {
+            const u64 half = 1ull << (M.nlv - 1), cnt = (u64)c - 2 * half + 1;
+            u32* out = e_ivmin[M.nlv].get(cnt);
+            k_iv_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(M.mn[M.nlv - 1], cnt, half, out);
+            M.mn[M.nlv++] = out;
+        }
         for (u32 q = 2; q < V.nlen[side]; q++)
             k_iv_insert<<<cdiv(c, 256), 256, 0, st>>>(V, side == 0 ? V.PA : V.SA, adj[side], c, side == 0, q,
-                                                     V.slen[side][q], hkey, hval, hs - 1);
+                                                     V.slen[side][q], hkey, hval, hs - 1, M);
+    }
     LZ_HIP(hipGetLastError());
     timer.mark("smpl_ivs");
 }
