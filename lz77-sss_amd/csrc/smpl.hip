@@ -44,6 +44,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include <hipcub/hipcub.hpp>
@@ -89,6 +90,7 @@ struct smpl_view {
     const u32* afact;        // approximate factors (src, len)
     u32 za;
     int mode;                // LZ77SSS_TRANSF_*
+    u32 small_t;             // intersect queries with a side of at most this many ranks run on their own lane
     // with_samples: RKS + interval samples
     const u32* rks;          // fps[k] = fp(T[0 .. k * RKS_RATE))
     const u32* pw_lo;        // b^e, e <= sq
@@ -251,7 +253,7 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
     bool qq = q;
     if (q && V.mode != LZ77SSS_TRANSF_NAIVE) {
         const u32 rx = xe - xb + 1, ry = ye - yb + 1;
-        if (min(rx, ry) <= SMALL_T) {
+        if (min(rx, ry) <= V.small_t) {
             qq = false;
             if (rx <= ry) {
                 for (u32 x = xb; x <= xe; x++) {
@@ -523,6 +525,21 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
                     bin = true;
                 }
                 if (hi - lo <= 1) run = false;
+            }
+            // a lane whose longest possible phrase (lce_l + hi - 2) cannot beat the wave's
+            // best confirmed one (longer, or as long at a smaller j) or f stops searching; the
+            // winner is never stopped and its search is unchanged, so the result is the same
+            u32 bl = got ? lce_l + lo - 1 : 0u, bjj = got ? j : 0xFFFFFFFFu;
+            for (int o = 32; o >= 1; o >>= 1) {
+                const u32 l2 = __shfl_xor(bl, o, 64), j2 = __shfl_xor(bjj, o, 64);
+                if (l2 > bl || (l2 == bl && j2 < bjj)) {
+                    bl = l2;
+                    bjj = j2;
+                }
+            }
+            if (run) {
+                const u32 ub = lce_l + hi - 2;
+                if (ub <= f_len || ub < bl || (ub == bl && j > bjj)) run = false;
             }
         }
         // the longest of the wave (the smallest j on ties) improves f (intersect: lce > f.len)
@@ -1045,6 +1062,8 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.afact = afact;
     V.za = za;
     V.mode = transf_mode;
+    V.small_t = SMALL_T;
+    if (const char* e = std::getenv("LZ77SSS_SMPL_SMALL")) V.small_t = (u32)std::max(0L, std::atol(e));
     V.nlen[0] = V.nlen[1] = 0;
     if (transf_mode == LZ77SSS_TRANSF_WITH_SAMPLES) build_interval_samples(V, n, za64);
     // the chain (chunk walks + bridges, then the path from position 0 by pointer doubling).
@@ -1172,20 +1191,29 @@ void engine::build_interval_samples(smpl_view& V, u64 nn, u64 za) {
     // adjacent LCEs and sampled lengths per side
     const u32 c = V.c;
     const u64 max_smpl_right = (u64)std::llround((double)nn / za * (1.0 + 0.5 * std::exp(-(double)nn / za / 1000.0)));
-    std::vector<u32> adjh[2];
+    // the adjacent LCEs are sorted on the device (a radix sort of c - 1 keys) and only the
+    // sorted column goes to the host for the quantile picks (a host sort took 0.6 s per side
+    // on the genome-like text's 2^24+ samples)
+    std::vector<u32> srth[2];
     u32* adj[2] = {e_adjL.get((u64)c + 1), e_adjR.get((u64)c + 1)};
+    u32* srtd = e_adjS.get((u64)c + 1);
     for (int side = 0; side < 2; side++) {
         k_adj_lce<<<cdiv((u64)c + 1, 256), 256, 0, st>>>(V.L, V.C, side == 0 ? V.PA : V.SA, c, V.delta, side == 0,
                                                         adj[side]);
-        adjh[side].resize((size_t)c + 1);
-        LZ_HIP(hipMemcpyAsync(adjh[side].data(), adj[side], ((size_t)c + 1) * 4, hipMemcpyDeviceToHost, st));
+        srth[side].resize(c > 1 ? (size_t)c - 1 : 0);
+        if (c > 1) {
+            size_t tb = 0;
+            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, adj[side] + 1, srtd, (int)(c - 1), 0, 32, st));
+            u8* t = scan_tmp.get(tb);
+            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, adj[side] + 1, srtd, (int)(c - 1), 0, 32, st));
+            LZ_HIP(hipMemcpyAsync(srth[side].data(), srtd, ((size_t)c - 1) * 4, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));  // srtd is reused by the other side
+        }
     }
-    LZ_HIP(hipStreamSynchronize(st));
     u64 total_iv = 0;
     for (int side = 0; side < 2; side++) {
         // construction.cpp:136-199: quantiles of the sorted adjacent LCEs in [3, max]
-        std::vector<u32> srt(adjh[side].begin() + 1, adjh[side].begin() + c);
-        std::sort(srt.begin(), srt.end());
+        const std::vector<u32>& srt = srth[side];
         const u64 maxlen = side == 0 ? V.delta : std::min<u64>(srt.empty() ? 0 : srt.back(), max_smpl_right);
         V.slen[side][0] = 1;
         V.slen[side][1] = 2;

@@ -194,7 +194,7 @@ struct engine {
     // exact-smpl mode (csrc/smpl.hip): approximate factors, samples, PA / SA, grid, RKS,
     // interval samples, phrase tasks
     dbuf<u32> e_afact, e_afst, e_tmp1, e_tmp2, e_C, e_PA, e_SA, e_PAR, e_SAR, e_Pi, e_Psi, e_CS;
-    dbuf<u32> e_gx, e_gy, e_gw, e_cell, e_rks, e_rkspw, e_adjL, e_adjR;
+    dbuf<u32> e_gx, e_gy, e_gw, e_cell, e_rks, e_rkspw, e_adjL, e_adjR, e_adjS;
     dbuf<u32> e_rst[10];  // exact-smpl: row sparse tables of the grid cells' lightest weights
     dbuf<u32> e_ivmin[MAX_LV];  // with_samples: sparse-table minima of the adjacent LCEs (interval ends)
     dbuf<u32> e_tpos, e_tlen, e_tsrc, e_thop, e_tkeys, e_tvals;
