@@ -41,6 +41,7 @@ void engine::load(const u8* h_text, u64 n_) {
     n = n_;
     runs_valid = false;
     brk_valid = false;
+    last_fact_mode = -1;  // the factors in HBM (if any) describe another text
     if (n) LZ_HIP(hipMemcpyAsync(d_text, h_text, n, hipMemcpyHostToDevice, st));
     LZ_HIP(hipMemsetAsync(d_text + n, 0, TEXT_PAD, st));
     LZ_HIP(hipStreamSynchronize(st));
@@ -278,7 +279,10 @@ struct engine64_impl final : lz::engine_if {
     u64 max_n() const override { return E.max_n; }
     u8* text() override { return E.d_text; }
     hipStream_t stream() override { return E.st; }
-    void set_n(u64 n) override { E.n = n; }
+    void set_n(u64 n) override {
+        E.n = n;
+        E.last_fact_mode = -1;
+    }
     void load(const u8* t, u64 n) override { E.load(t, n); }
     u64 factorize(int phr, u32 seed, int log2, bool log, int fact_mode) override {
         return E.factorize(phr, seed, log2, log, fact_mode);
@@ -291,6 +295,7 @@ struct engine64_impl final : lz::engine_if {
     }
     u8* dec_out(u64 n) override { return E.dec_out.get(n); }
     u64 verify(u64* first_bad) override {
+        E.check_verifiable();
         const u64 bad = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text, first_bad);
         LZ_HIP(hipStreamSynchronize(E.st));
         return bad;
@@ -563,6 +568,7 @@ LZ77SSS_API int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positio
             return;
         }
         lz::engine& E = s->E;
+        E.check_verifiable();
         LZ_HIP(hipSetDevice(E.device));
         *bad_positions = E.verify_factors(E.fact.p, E.num_fact, E.n, E.d_text, first_bad);
         LZ_HIP(hipStreamSynchronize(E.st));
@@ -716,7 +722,10 @@ LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint6
         if (n > cap) throw lz::error(LZ77SSS_EINVAL, "text larger than the session capacity");
         LZ_HIP(hipSetDevice(dev));
         if (s->E64) s->E64->set_n(n);
-        else s->E.n = n;
+        else {
+            s->E.n = n;
+            s->E.last_fact_mode = -1;
+        }
         const lz::u64 thr = mut_rate >= 1.0 ? ~0ull : (lz::u64)(mut_rate * 18446744073709551616.0);
         if (n) k_gen_genome<<<lz::capped_grid((n + 15) / 16, 256), 256, 0, st>>>(text, n, offset, base_len, thr, seed);
         LZ_HIP(hipGetLastError());

@@ -361,6 +361,7 @@ u64 engine::factorize_exact(bool log) {
     LZ_HIP(hipSetDevice(device));
     if (n > 0xFFFFFFF0ull) throw error(LZ77SSS_EINVAL, "n too large for pos_t = uint32_t");
     num_fact = 0;
+    last_fact_mode = LZ77SSS_GREEDY;
     stats.assign(28, 0);
     x_rounds = 0;
     if (n == 0) return 0;

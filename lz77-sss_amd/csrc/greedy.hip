@@ -1609,17 +1609,22 @@ __global__ void k_chain_inserts(seg_tab S, const u32* __restrict__ chain, u32 cn
         if (chain_range(S, g, hi, off, x0, x1)) {
             const u64 w0 = x0 >> 5, w1 = (x1 - 1) >> 5;
             bool here = true;
-            if (long_words && w1 - w0 >= long_words && lane == 0) {
-                const u32 slot = atomicAdd(lng, 1u);
-                if (slot < lng_cap) {
-                    ((u64*)(lng + 2))[2 * slot] = x0;
-                    ((u64*)(lng + 2))[2 * slot + 1] = x1;
-                } else {
-                    atomicOr(lng + 1, 1u);  // list full: handled here
+            if (long_words && w1 - w0 >= long_words) {
+                // the overflow decision comes from lane 0's own atomic result: a plain load of
+                // lng[1] may hit a stale L1 line while the atomics are performed in L2
+                u32 ovf = 0;
+                if (lane == 0) {
+                    const u32 slot = atomicAdd(lng, 1u);
+                    if (slot < lng_cap) {
+                        ((u64*)(lng + 2))[2 * slot] = x0;
+                        ((u64*)(lng + 2))[2 * slot + 1] = x1;
+                    } else {
+                        ovf = 1;
+                        atomicOr(lng + 1, 1u);  // list full: handled here (lng[1] for the host / debug)
+                    }
                 }
+                here = __shfl(ovf, 0, 64) != 0;
             }
-            if (long_words && w1 - w0 >= long_words) here = false;
-            if (!here && __shfl(lng[1], 0, 64)) here = true;
             if (here) {
                 // loads first, atomics after: an atomic without return still counts against the
                 // load counter, so a load behind it would wait for its round trip
@@ -2937,12 +2942,21 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     // a long gap is walked by one wave: with few chain nodes, the long ranges go to the
                     // whole grid instead
                     constexpr u32 LNG_CAP = 1024;
+                    // test knobs: a small list and a short "long" range make the overflow path run
+                    const u32 lng_cap = [&] {
+                        const char* e = std::getenv("LZ77SSS_TEST_LNG_CAP");
+                        return e ? (u32)std::min<long>(LNG_CAP, std::max<long>(0, std::atol(e))) : LNG_CAP;
+                    }();
+                    const u32 long_words = [] {
+                        const char* e = std::getenv("LZ77SSS_TEST_LONG_WORDS");
+                        return e ? (u32)std::max<long>(1, std::atol(e)) : 2048u;
+                    }();
                     u32* lng = (u32*)g_lng.get(2 + 4 * LNG_CAP);
                     LZ_HIP(hipMemsetAsync(lng, 0, 8, st));
                     k_chain_inserts<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2,
-                                                                                     bmI, fast ? i_cnt : nullptr, 2048u, lng,
-                                                                                     LNG_CAP);
-                    k_chain_inserts_long<<<1024, 256, 0, st>>>(lng, LNG_CAP, bmI2, bmI, fast ? i_cnt : nullptr);
+                                                                                     bmI, fast ? i_cnt : nullptr, long_words,
+                                                                                     lng, lng_cap);
+                    k_chain_inserts_long<<<1024, 256, 0, st>>>(lng, lng_cap, bmI2, bmI, fast ? i_cnt : nullptr);
                 }
                 if (tail && hc[1]) {
                     pos_t* d_tins = tail_ins_buf.p;

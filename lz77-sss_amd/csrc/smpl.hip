@@ -919,6 +919,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     // the 3-approximation (compute_approximation, lz77_sss.hpp:324)
     const u64 za64 = factorize(phr_mode, rk_seed, log2_override, false, LZ77SSS_GREEDY);
     num_fact = 0;
+    last_fact_mode = LZ77SSS_GREEDY;
     if (n == 0) return 0;
     const u32 delta = (u32)std::min<u64>(n / za64, SMPL_MAX_DELTA);
     // hipcub scans / radix sorts below take int item counts, and the sample offsets are u32:

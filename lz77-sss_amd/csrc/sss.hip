@@ -814,23 +814,7 @@ stripe_done:
             *(u64*)(q_init + t) = 0xFF00FF00FF00FF00ull;
             *(u32*)(rp_init + t) = 0u;
         }
-        // the per-block run records start out unknown (k_sss_runs writes the stripes it settles);
-        // the last stripe also clears the blocks past its own, up to nbk inclusive
-        {
-            const u64 gk = w * (u64)SNB + lane;
-            if (gk <= nbk) {
-                blk_p[gk] = 0;
-                blk_fo[gk] = 0;
-                blk_lo[gk] = 0;
-            }
-            if (w + 1 == nstripes) {
-                for (u64 g2 = gk + 64; g2 <= nbk; g2 += 64) {
-                    blk_p[g2] = 0;
-                    blk_fo[g2] = 0;
-                    blk_lo[g2] = 0;
-                }
-            }
-        }
+        // (the per-block run records are valid only for the stripes k_sss_runs runs on: blk_recs)
         if (dirty) nout = 0;  // re-run
     }
     if (lane == 0) {
@@ -1208,13 +1192,32 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
             const u32 cs = c;
             const u32 ol = lane + (p >> 3), sh = 8 * (p & 7);
             u64 d;
+            // RB blocks per round: their ring reads are issued together and the first dirty one
+            // found from the ballots (one LDS round trip per RB blocks instead of per block).  At c
+            // the ring holds blocks c - c % 8 .. c - c % 8 + 15, so blocks c + 2 .. c + RB + 2 are
+            // in it; the refills of the blocks crossed run after the reads
+            constexpr u32 RB = 6;
+            static_assert(RB + 2 <= RSL - RCH, "run-crossing batch must stay inside the ring");
             for (;;) {
-                const u32 o = ((c + 2) % RSL) * 64;
-                const u64 lo = ring[(o + ol) % (RSL * 64)], hi = ring[(o + ol + 1) % (RSL * 64)];
-                d = ring[o + lane] ^ (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo);
-                if (__ballot(d != 0)) break;
-                if (++c >= nblk) break;
-                refill(c);
+                u64 dd[RB];
+#pragma unroll
+                for (u32 j = 0; j < RB; j++) {
+                    const u32 o = ((c + 2 + j) % RSL) * 64;
+                    const u64 lo = ring[(o + ol) % (RSL * 64)], hi = ring[(o + ol + 1) % (RSL * 64)];
+                    dd[j] = ring[o + lane] ^ (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo);
+                }
+                u32 f = RB;  // first block of the round with a p-break (uniform)
+#pragma unroll
+                for (int j = (int)RB - 1; j >= 0; j--)
+                    if (__ballot(dd[j] != 0)) f = (u32)j;
+                const u32 lim = nblk - c;  // >= 1
+                const u32 adv = min(f, lim);
+#pragma unroll
+                for (u32 j = 0; j < RB; j++)
+                    if (j == f) d = dd[j];
+                for (u32 j = 1; j <= adv; j++) refill(c + j);
+                c += adv;
+                if (f < RB || c >= nblk) break;
             }
             if (c > cs) {
                 if (lane > cs && lane <= c) {
@@ -1346,6 +1349,10 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         blk_fo[gk0 + lane] = (u16)rf;
         blk_lo[gk0 + lane] = (u16)rl;
     }
+    // some block has a record: the segment kernels run (one flag for the text, no atomic once set)
+    if (__ballot(gk0 + lane < nbk && rp != 0) && lane == 0 &&
+        __hip_atomic_load(any_q + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicOr(any_q + 4, 1u);
     // a stripe whose sync set overflows goes to the exact path too (k_sss_fallback reads the Q
     // intervals of k_q_anchors)
     if (nout > scap) fail = true;
@@ -1368,16 +1375,32 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         if (fl != old) atomicAdd(ovf_ctr, fl ? 1u : 0xFFFFFFFFu);
     }
 }
+// The per-block run records as k_sss_runs left them: a block's record is valid when k_sss_runs ran
+// on its stripe (hitw bit 63: forced, 62: settled by it); every other block reads as "no record"
+// (period 0, no break known), so pass 1 no longer clears 5 bytes per block on every call.
+struct blk_recs {
+    const u8* bp;
+    const u16* fo;
+    const u16* lo;
+    const u64* hitw;
+    u64 nstripes, nbk;
+    __device__ __forceinline__ bool ok(u64 b) const {
+        const u64 w = b / SNB;
+        return w < nstripes && (hitw[3 * w + 2] >> 62) != 0;
+    }
+    __device__ __forceinline__ u32 p(u64 b) const { return ok(b) ? bp[b] : 0u; }
+    __device__ __forceinline__ u32 f(u64 b) const { return ok(b) ? fo[b] : 0u; }
+    __device__ __forceinline__ u32 l(u64 b) const { return ok(b) ? lo[b] : 0u; }
+};
 // per-block run end / start packed for one-load lookups (lce_dev.h run_tab::re / rs): the
 // segment's end made exact by the first break of its period in the block after it (fo), its
 // start by the last break in the block before it (lo); offsets + 1, 0 = unknown, 0xFFFF = none
 // in that block (a bound one block further)
-__global__ void k_blk_runinfo(const u8* __restrict__ bp, const u16* __restrict__ fo, const u16* __restrict__ lo,
-                              const pos_t* __restrict__ ser, const pos_t* __restrict__ ss, u64 nbk,
+__global__ void k_blk_runinfo(blk_recs B, const pos_t* __restrict__ ser, const pos_t* __restrict__ ss, u64 nbk,
                               u64* __restrict__ re, u64* __restrict__ rs) {
     const u64 b = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nbk) return;
-    const u64 p = bp[b];
+    const u64 p = B.p(b);
     if (!p) {
         re[b] = 0;
         rs[b] = 0;
@@ -1386,14 +1409,14 @@ __global__ void k_blk_runinfo(const u8* __restrict__ bp, const u16* __restrict__
     const u64 se = ser[nbk - 1 - b], eb = se >> 9;
     u64 e = se + p, xe = 0;
     if (eb < nbk) {
-        const u32 f = fo[eb];
+        const u32 f = B.f(eb);
         if (f == 0xFFFFu) e = se + TAU + p;
         else if (f) { e = se + (f - 1) + p; xe = 1; }
     }
     const u64 s0 = ss[b], sb = s0 >> 9;
     u64 st = s0, xs = 0;
     if (sb) {
-        const u32 l = lo[sb];
+        const u32 l = B.l(sb);
         if (l == 0xFFFFu) st = s0 - TAU;
         else if (l) { st = s0 - TAU + l; xs = 1; }
     }
@@ -1409,15 +1432,15 @@ __global__ void k_blk_runinfo(const u8* __restrict__ bp, const u16* __restrict__
 // marker + min/max-scan formulation (k_blk_marks + two device scans + k_blk_runinfo).
 constexpr u32 BT_T = 1024, BT_PER = 4, BT_TILE = BT_T * BT_PER;
 constexpr u64 BT_NONE = ~0ull;
-__device__ __forceinline__ bool blk_cont_f(const u8* __restrict__ bp, u64 nbk, u64 b) {
-    const u32 p = bp[b];
-    return p && b + 1 < nbk && bp[b + 1] == p;
+__device__ __forceinline__ bool blk_cont_f(const blk_recs& B, u64 nbk, u64 b) {
+    const u32 p = B.p(b);
+    return p && b + 1 < nbk && B.p(b + 1) == p;
 }
-__device__ __forceinline__ bool blk_cont_b(const u8* __restrict__ bp, u64 b) {
-    const u32 p = bp[b];
-    return p && b > 0 && bp[b - 1] == p;
+__device__ __forceinline__ bool blk_cont_b(const blk_recs& B, u64 b) {
+    const u32 p = B.p(b);
+    return p && b > 0 && B.p(b - 1) == p;
 }
-__global__ __launch_bounds__(BT_T) void k_blk_seg_tiles(const u8* __restrict__ bp, u64 nbk, u64* __restrict__ tfe,
+__global__ __launch_bounds__(BT_T) void k_blk_seg_tiles(blk_recs bp, u64 nbk, u64* __restrict__ tfe,
                                                         u64* __restrict__ tls) {
     __shared__ u64 s_e[BT_T / 64], s_s[BT_T / 64];
     const u32 t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1449,8 +1472,7 @@ __global__ __launch_bounds__(BT_T) void k_blk_seg_tiles(const u8* __restrict__ b
         tls[blockIdx.x] = l;
     }
 }
-__global__ __launch_bounds__(BT_T) void k_blk_seg_info(const u8* __restrict__ bp, const u16* __restrict__ fo,
-                                                       const u16* __restrict__ lo, u64 nbk,
+__global__ __launch_bounds__(BT_T) void k_blk_seg_info(blk_recs bp, u64 nbk,
                                                        const u64* __restrict__ tfe, const u64* __restrict__ tls,
                                                        u64 ntile, u64* __restrict__ re, u64* __restrict__ rs) {
     __shared__ u64 s_end[BT_TILE];  // per block: its segment's last block inside the tile, or BT_NONE
@@ -1517,7 +1539,7 @@ __global__ __launch_bounds__(BT_T) void k_blk_seg_info(const u8* __restrict__ bp
         const u32 i = k * BT_T + t;
         if (i >= tn) break;
         const u64 b = t0 + i;
-        const u64 p = bp[b];
+        const u64 p = bp.p(b);
         if (!p) {
             re[b] = 0;
             rs[b] = 0;
@@ -1530,14 +1552,14 @@ __global__ __launch_bounds__(BT_T) void k_blk_seg_info(const u8* __restrict__ bp
         const u64 se = (eb + 1) * TAU, ebn = eb + 1;
         u64 e = se + p, xe = 0;
         if (ebn < nbk) {
-            const u32 f = fo[ebn];
+            const u32 f = bp.f(ebn);
             if (f == 0xFFFFu) e = se + TAU + p;
             else if (f) { e = se + (f - 1) + p; xe = 1; }
         }
         const u64 s0 = sb0 * TAU, sb = sb0;
         u64 st = s0, xs = 0;
         if (sb) {
-            const u32 l = lo[sb];
+            const u32 l = bp.l(sb);
             if (l == 0xFFFFu) st = s0 - TAU;
             else if (l) { st = s0 - TAU + l; xs = 1; }
         }
@@ -1546,11 +1568,10 @@ __global__ __launch_bounds__(BT_T) void k_blk_seg_info(const u8* __restrict__ bp
     }
 }
 // run-record segment markers: ends (stored reversed, for a min-scan) and starts (max-scan)
-__global__ void k_blk_marks(const u8* __restrict__ bp, u64 nbk, pos_t* __restrict__ end_rev, pos_t* __restrict__ beg) {
+__global__ void k_blk_marks(blk_recs B, u64 nbk, pos_t* __restrict__ end_rev, pos_t* __restrict__ beg) {
     const u64 b = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nbk) return;
-    const u32 p = bp[b];
-    const bool cont_f = p && b + 1 < nbk && bp[b + 1] == p, cont_b = p && b > 0 && bp[b - 1] == p;
+    const bool cont_f = blk_cont_f(B, nbk, b), cont_b = blk_cont_b(B, b);
     end_rev[nbk - 1 - b] = cont_f ? (pos_t)~(pos_t)0 : (pos_t)((b + 1) * TAU);
     beg[b] = cont_b ? (pos_t)0 : (pos_t)(b * TAU);
 }
@@ -1772,15 +1793,18 @@ __global__ __launch_bounds__(FB_T) void k_sss_fallback(const u8* __restrict__ T,
         for (u32 bits = mask[w]; bits; bits &= bits - 1) out[o++] = (pos_t)(i0 + d0 + 32 * w + __builtin_ctz(bits));
 }
 
+// one wave per stripe, its outputs copied by the 64 lanes (coalesced; one thread per stripe
+// copying its ~128 outputs alone took 48 us on a 1 GiB genome-like text)
 __global__ void k_sss_compact(const pos_t* __restrict__ lane_out, const u32* __restrict__ lane_cnt,
                               const u32* __restrict__ lane_off, const u32* __restrict__ lane_flag,
                               const u32* __restrict__ ovf_slot, const pos_t* __restrict__ ovf_out, u64 nlanes,
                               pos_t* __restrict__ S) {
-    const u64 lane = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (lane >= nlanes) return;
-    const u32 c = lane_cnt[lane], o = lane_off[lane];
-    const pos_t* src = lane_flag[lane] ? ovf_out + (u64)ovf_slot[lane] * SD : lane_out + lane * SCAP;
-    for (u32 x = 0; x < c; x++) S[o + x] = src[x];
+    const u32 lane = threadIdx.x & 63;
+    for (u64 w = gtid() >> 6; w < nlanes; w += gstride() >> 6) {
+        const u32 c = lane_cnt[w], o = lane_off[w];
+        const pos_t* src = lane_flag[w] ? ovf_out + (u64)ovf_slot[w] * SD : lane_out + w * SCAP;
+        for (u32 x = lane; x < c; x += 64) S[(u64)o + x] = src[x];
+    }
 }
 
 static u32 pow32_host(u32 b, u64 e) {
@@ -1800,7 +1824,8 @@ void engine::run_chains(u64 nanch, const u32* tiles, u64 m) {
         runs_valid = true;
         return;
     }
-    if (m >= 0x7FFFFFFFull) throw error(LZ77SSS_EINVAL, "too many anchors for the run-chain scans (int item counts)");
+    // the chain keys are u32 element indices + 1 (k_run_keys); the scans take size_t counts
+    if (m >= 0xFFFFFFFFull) throw error(LZ77SSS_EINVAL, "too many anchors for the run-chain scans (u32 chain keys)");
     u32* ka = (u32*)run_scan_a.get(m);  // 2 x m u32
     u32* kb = (u32*)run_scan_b.get(m);
     k_run_keys<<<cdiv(m, 256), 256, 0, st>>>(run_p.p, run_hi.p, run_lo.p, nanch, tiles, m, ka, ka + m);
@@ -1861,7 +1886,7 @@ void engine::build_sss(const u8* T) {
     pos_t* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
     u32* ctr = counters.get(16);
-    LZ_HIP(hipMemsetAsync(ctr, 0, 12 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes; 8..10: k_sss_runs counters
+    LZ_HIP(hipMemsetAsync(ctr, 0, 12 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes, any block record; 8..10: k_sss_runs counters
     pos_t* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
@@ -1914,7 +1939,13 @@ void engine::build_sss(const u8* T) {
         k_flag_list<<<nfb, FL_T, 0, st>>>(tfl, nfw, fc, tl, ctr + 2);
     }
     LZ_HIP(hipGetLastError());
-    const u32 ndirty = rd1(ctr + 2, st);
+    u32 ndirty, any_rec;
+    {
+        hread rb(st);
+        rb.add(&ndirty, (const u32*)ctr + 2);
+        rb.add(&any_rec, (const u32*)ctr + 4);
+        rb.sync();
+    }
     stats_sss_tiles = ndirty;
     if (debug_enabled()) {
         u32 dc[3];
@@ -1936,12 +1967,14 @@ void engine::build_sss(const u8* T) {
         LZ_HIP(hipGetLastError());
     }
     runs_valid = true;  // period 0 outside the marked tiles
-    {
+    brk_valid = false;
+    if (any_rec) {
         // run-record segments -> packed per-block run end / start (two launches)
         const u64 ntile = (nbk + BT_TILE - 1) / BT_TILE;
         u64* tt = (u64*)blk_mk.get(4 * ntile + 4);  // 2 x ntile u64 (the buffer is pos_t-typed)
-        k_blk_seg_tiles<<<(unsigned)ntile, BT_T, 0, st>>>(bp, nbk, tt, tt + ntile);
-        k_blk_seg_info<<<(unsigned)ntile, BT_T, 0, st>>>(bp, bfo, blo, nbk, tt, tt + ntile, ntile, blk_re.get(nbk),
+        const blk_recs BR{bp, bfo, blo, hw, nlanes, nbk};
+        k_blk_seg_tiles<<<(unsigned)ntile, BT_T, 0, st>>>(BR, nbk, tt, tt + ntile);
+        k_blk_seg_info<<<(unsigned)ntile, BT_T, 0, st>>>(BR, nbk, tt, tt + ntile, ntile, blk_re.get(nbk),
                                                          blk_rs.get(nbk));
         LZ_HIP(hipGetLastError());
         if (std::getenv("LZ77SSS_BLK_CHECK") && nbk < 0x7FFFFFFFull) {
@@ -1949,7 +1982,7 @@ void engine::build_sss(const u8* T) {
             pos_t* mk = (pos_t*)u64a.get(2 * nbk + 2);
             pos_t* ser = (pos_t*)u64b.get(nbk + 1);
             pos_t* bss = (pos_t*)u32e.get(2 * nbk + 2);
-            k_blk_marks<<<cdiv(nbk, 256), 256, 0, st>>>(bp, nbk, mk, mk + nbk);
+            k_blk_marks<<<cdiv(nbk, 256), 256, 0, st>>>(BR, nbk, mk, mk + nbk);
             size_t tb = 0, tb2 = 0;
             LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, mk, ser, hipcub::Min(), (int)nbk, st));
             LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
@@ -1958,7 +1991,7 @@ void engine::build_sss(const u8* T) {
             LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb2, mk + nbk, bss, hipcub::Max(), (int)nbk, st));
             u64* re2 = (u64*)u32d.get(4 * nbk + 4);
             u64* rs2 = re2 + nbk;
-            k_blk_runinfo<<<cdiv(nbk, 256), 256, 0, st>>>(bp, bfo, blo, ser, bss, nbk, re2, rs2);
+            k_blk_runinfo<<<cdiv(nbk, 256), 256, 0, st>>>(BR, ser, bss, nbk, re2, rs2);
             std::vector<u64> a(2 * nbk), c(2 * nbk);
             LZ_HIP(hipMemcpyAsync(a.data(), blk_re.p, 8 * nbk, hipMemcpyDeviceToHost, st));
             LZ_HIP(hipMemcpyAsync(a.data() + nbk, blk_rs.p, 8 * nbk, hipMemcpyDeviceToHost, st));
@@ -2044,7 +2077,7 @@ void engine::build_sss(const u8* T) {
     s = total;
     sss_kernel_bytes = n + sizeof(pos_t) * (u64)s;
     pos_t* dS = S.get((u64)s + 1);
-    k_sss_compact<<<cdiv(nlanes, 256), 256, 0, st>>>(lo, lc, off, lf, ovf_slot, ovf_out, nlanes, dS);
+    k_sss_compact<<<capped_grid(nlanes * 64, 256), 256, 0, st>>>(lo, lc, off, lf, ovf_slot, ovf_out, nlanes, dS);
     LZ_HIP(hipGetLastError());
 }
 

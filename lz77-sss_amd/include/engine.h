@@ -1,6 +1,7 @@
 // engine.h -- the device-resident LZ77-SSS engine (one per session / GPU).
 // Data layout in HBM is documented in DESIGN.md section 5.
 #pragma once
+#include "../../include/lz77sss.h"
 #include "lz77sss_internal.h"
 #include "lce_dev.h"
 #include "timer.h"
@@ -206,7 +207,13 @@ struct engine {
     dbuf<u8> dec_out;
     u32 dec_rounds = 0;
     u64 num_fact = 0;
-    int last_fact_mode = -1;  // fact_mode of the last factorize call
+    int last_fact_mode = -1;  // fact_mode of the last factorize call (-1: none for the loaded text)
+    // the factors in HBM are a factorization of the loaded text (lz77sss_session_verify)
+    void check_verifiable() const {
+        if (last_fact_mode == -1) throw error(LZ77SSS_EINVAL, "no factorization of the loaded text to verify");
+        if (last_fact_mode == LZ77SSS_SKIP_PHRASES)
+            throw error(LZ77SSS_EINVAL, "a skip_phrases stream is not a factorization (nothing to verify)");
+    }
     dbuf<u8> ssz_out;         // ssszip gapped container (csrc/ssszip.hip)
     dbuf<u8> hf_tabs, hf_words, hf_out;  // Huffman factor container (csrc/huffman.hip)
     u64 ssz_size = 0;
@@ -279,9 +286,10 @@ struct sync_slot {
         if (h) (void)hipHostFree(h);
     }
 };
+// (a slot whose pinned allocation failed has h == nullptr: hread then uses the copy +
+// synchronize form instead of failing every entry point)
 inline sync_slot& host_slot() {
     static thread_local sync_slot s;
-    if (!s.h) throw error(-4 /* LZ77SSS_ENOMEM */, "pinned staging slot");
     return s;
 }
 struct hread_job {
@@ -349,7 +357,7 @@ struct hread {
         off += b;
     }
     void sync() {
-        if (S.spin) {
+        if (S.spin && S.h) {
             hread_job J{};
             for (int k = 0; k < n; k++) {
                 J.src[k] = (const u8*)items[k].src;

@@ -388,6 +388,38 @@ def test_pred_and_bucket_search_paths_vs_oracle(session, orc, lz, kind, mib, mon
     assert np.array_equal(F2, F_ref)
 
 
+@pytest.mark.parametrize("kind,mib", [("rr", 32), ("genome", 16)])
+def test_fast_convergence_check_vs_full_check(session, orc, lz, kind, mib, monkeypatch):
+    """The fast I' == I decision (insert counts outside I + the subset check, csrc/greedy.hip) and the
+    full xor/count path (LZ77SSS_NO_FAST_CHECK) give the same stream, equal to the oracle's."""
+    n = mib << 20
+    T = lz.gen_genome(n, 2 << 20, 0.001, 19) if kind == "genome" else lz.gen_random_repetitive(n, n, 13, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    _, F1 = run(session, T)
+    assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    monkeypatch.setenv("LZ77SSS_NO_FAST_CHECK", "1")
+    _, F0 = run(session, T)
+    assert np.array_equal(F0, F_ref)
+
+
+@pytest.mark.parametrize("cap", ["0", "1", "3"])
+def test_long_range_list_overflow(session, orc, lz, cap, monkeypatch):
+    """k_chain_inserts hands ranges longer than LZ77SSS_TEST_LONG_WORDS words to the whole grid through
+    a list of LZ77SSS_TEST_LNG_CAP entries; a wave whose range did not fit inserts it itself (decided
+    from its own atomic's result).  With tiny caps most ranges overflow: the stream stays the oracle's,
+    with the fast check and with the full one."""
+    n = 8 << 20
+    T = lz.gen_random_repetitive(n, n, 21, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    monkeypatch.setenv("LZ77SSS_TEST_LONG_WORDS", "4")
+    monkeypatch.setenv("LZ77SSS_TEST_LNG_CAP", cap)
+    _, F1 = run(session, T)
+    assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    monkeypatch.setenv("LZ77SSS_NO_FAST_CHECK", "1")
+    _, F0 = run(session, T)
+    assert np.array_equal(F0, F_ref)
+
+
 CHUNKS_PROBE = ["16", "64", "128", "256", "512", "1024", "100000"]
 
 

@@ -62,3 +62,22 @@ def test_gpu_skip_c1(session, orc, lz, seed):
     F = s.factors(z)
     assert np.array_equal(F, orc.factorize_skip(T))
     assert covered(F) == T.size
+
+
+@pytest.mark.gpu
+def test_verify_refuses_skip_stream_and_stale_factors(session, lz):
+    """lz77sss_session_verify checks a factorization of the loaded text: after a skip_phrases call, or
+    after load() of another text, it refuses (LZ77SSS_EINVAL) instead of reporting bad positions."""
+    T = lz.gen_random_repetitive(10000, 200000, 4)
+    s = session(T.size)
+    s.load(T)
+    s.factorize()
+    assert s.verify() == 0
+    s.factorize(fact_mode=lz.SKIP_PHRASES)
+    with pytest.raises(lz.Lz77SssError):
+        s.verify()
+    s.factorize()
+    assert s.verify() == 0
+    s.load(T[::-1].copy())
+    with pytest.raises(lz.Lz77SssError):
+        s.verify()
