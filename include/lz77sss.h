@@ -178,7 +178,8 @@ int lz77sss_session_decode(lz77sss_session* s, uint8_t* out, uint64_t cap, uint6
  * positions whose factor does not reproduce the text (a literal with another byte, a copy
  * from a position >= its own, a copied byte that differs); 0 <=> decode(F) == T; first_bad
  * (may be NULL) the smallest such position (UINT64_MAX if none).  Fails with LZ77SSS_EINVAL
- * when the lengths do not sum to n. */
+ * when the lengths do not sum to n, when the session holds no factorization yet, and after a
+ * skip_phrases call (its gapped stream is not a factorization). */
 int lz77sss_session_verify(lz77sss_session* s, uint64_t* bad_positions, uint64_t* first_bad);
 /* Runs only the string-synchronizing-set pass (kernel 1) on the loaded text. */
 int lz77sss_session_sss(lz77sss_session* s, uint64_t* size_sss, int* has_runs);

@@ -41,13 +41,15 @@ void engine::load(const u8* h_text, u64 n_) {
     n = n_;
     runs_valid = false;
     brk_valid = false;
-    last_fact_mode = -1;  // the factors in HBM (if any) describe another text
     if (n) LZ_HIP(hipMemcpyAsync(d_text, h_text, n, hipMemcpyHostToDevice, st));
     LZ_HIP(hipMemsetAsync(d_text + n, 0, TEXT_PAD, st));
     LZ_HIP(hipStreamSynchronize(st));
 }
 
 void engine::destroy() {
+    if (sss_ev0) (void)hipEventDestroy(sss_ev0);
+    if (sss_ev1) (void)hipEventDestroy(sss_ev1);
+    sss_ev0 = sss_ev1 = nullptr;
     if (d_text) (void)hipFree(d_text);
     if (d_text_rev) (void)hipFree(d_text_rev);
     d_text = d_text_rev = nullptr;
@@ -279,10 +281,7 @@ struct engine64_impl final : lz::engine_if {
     u64 max_n() const override { return E.max_n; }
     u8* text() override { return E.d_text; }
     hipStream_t stream() override { return E.st; }
-    void set_n(u64 n) override {
-        E.n = n;
-        E.last_fact_mode = -1;
-    }
+    void set_n(u64 n) override { E.n = n; }
     void load(const u8* t, u64 n) override { E.load(t, n); }
     u64 factorize(int phr, u32 seed, int log2, bool log, int fact_mode) override {
         return E.factorize(phr, seed, log2, log, fact_mode);
@@ -323,7 +322,7 @@ struct engine64_impl final : lz::engine_if {
     const u32* lcp_ptr() const override { return E.lcp_rmq[0].p; }
     std::vector<u64>& stats() override { return E.stats; }
     lz::phase_timer& timer() override { return E.timer; }
-    double sss_kernel_ms() const override { return E.sss_kernel_ms; }
+    double sss_kernel_ms() const override { return E.sss_ms(); }
     u64 sss_kernel_bytes() const override { return E.sss_kernel_bytes; }
     u32 dec_rounds() const override { return E.dec_rounds; }
     void set_sss(const u64* S_any, u64 count, bool runs) override { E.set_sss(S_any, count, runs); }
@@ -722,10 +721,7 @@ LZ77SSS_API int lz77sss_session_gen_genome(lz77sss_session* s, uint64_t n, uint6
         if (n > cap) throw lz::error(LZ77SSS_EINVAL, "text larger than the session capacity");
         LZ_HIP(hipSetDevice(dev));
         if (s->E64) s->E64->set_n(n);
-        else {
-            s->E.n = n;
-            s->E.last_fact_mode = -1;
-        }
+        else s->E.n = n;
         const lz::u64 thr = mut_rate >= 1.0 ? ~0ull : (lz::u64)(mut_rate * 18446744073709551616.0);
         if (n) k_gen_genome<<<lz::capped_grid((n + 15) / 16, 256), 256, 0, st>>>(text, n, offset, base_len, thr, seed);
         LZ_HIP(hipGetLastError());
@@ -848,7 +844,7 @@ LZ77SSS_API int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap
 
 LZ77SSS_API int lz77sss_session_sss_kernel_time(lz77sss_session* s, double* ms, uint64_t* bytes) {
     if (!s) return LZ77SSS_EINVAL;
-    if (ms) *ms = s->E64 ? s->E64->sss_kernel_ms() : s->E.sss_kernel_ms;
+    if (ms) *ms = s->E64 ? s->E64->sss_kernel_ms() : s->E.sss_ms();
     if (bytes) *bytes = s->E64 ? s->E64->sss_kernel_bytes() : s->E.sss_kernel_bytes;
     return LZ77SSS_OK;
 }

@@ -490,7 +490,13 @@ __device__ __forceinline__ u32 min3u(u32 a, u32 b, u32 c) {
 // kp in (85, 170] (a multiple of p) and contains [A, A + 186) for its filter anchor A
 // in [j, j + 256), so T[A..A+16) recurs at A + kp.  Lane l < 22 of half h tests the 4
 // shifts 84 + 4l + k of A_h (its bytes gathered from 2-3 lanes by ds_bpermute); an
-// 8-byte repeat (about one block in 400 on ACGT text) is confirmed on bytes 8..15.
+// 8-byte repeat (about one block in 400 on ACGT text) is confirmed on bytes 8..15, and a 16-byte
+// repeat at shift d in [86, 170] on the whole stretch a Q window would force: T[A..A+186-d) ==
+// T[A+d..A+186) (the window holds [A, A+186) and has the period d; shifts 84, 85 and 171 are never
+// such a multiple).  The chance 16-byte repeats of a random ACGT text then pass only at d close to
+// 170, where the stretch is short (all inside the block: A + 186 <= 442, compared from the
+// registers by cross-lane moves).
+__device__ __forceinline__ u64 shfl64(u64 v, u32 src);
 __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
     const u32 lo = (u32)B, hi = (u32)(B >> 32);
     const u32 li = lane & 31, grp = lane >> 5;
@@ -518,14 +524,42 @@ __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
     const u32 ch = grp ? (u32)__builtin_amdgcn_readlane((int)hi, 33) : (u32)__builtin_amdgcn_readlane((int)hi, 1);
     const u32 s2l = (u32)__shfl((int)lo, l0 + 2, 64), s2h = (u32)__shfl((int)hi, l0 + 2, 64);
     const u32 d3 = ev ? s2l : s1h, d4 = ev ? s2h : s2l;
-    bool hit = false;
+    u32 hk = 0;  // the lane's shifts (bit k: d = 84 + 4 li + k) with a 16-byte repeat
 #pragma unroll
     for (int k = 0; k < 4; k++)
-        hit |= __builtin_amdgcn_alignbyte(d1, d0, k) == (u32)A && __builtin_amdgcn_alignbyte(d2, d1, k) == (u32)(A >> 32) &&
-               __builtin_amdgcn_alignbyte(d3, d2, k) == cl && __builtin_amdgcn_alignbyte(d4, d3, k) == ch;
-    if (li >= (u32)FA_LANES) hit = false;
-    const u64 hm = __ballot(hit);
-    return ((u32)hm ? 1u : 0u) | ((u32)(hm >> 32) ? 2u : 0u);
+        hk |= (__builtin_amdgcn_alignbyte(d1, d0, k) == (u32)A && __builtin_amdgcn_alignbyte(d2, d1, k) == (u32)(A >> 32) &&
+               __builtin_amdgcn_alignbyte(d3, d2, k) == cl && __builtin_amdgcn_alignbyte(d4, d3, k) == ch)
+                  ? 1u << k : 0u;
+    if (li >= (u32)FA_LANES) hk = 0;
+    u32 res = 0;
+    for (u64 hm = __ballot(hk != 0); hm; hm &= hm - 1) {
+        const u32 L = (u32)__builtin_ctzll(hm);
+        const u32 g = L >> 5;
+        if (res & (1u << g)) continue;
+        const u64 x = shfl64(B, (32 * g + lane) & 63);  // bytes A + 8 lane .. + 7
+        for (u32 bits = (u32)__builtin_amdgcn_readlane((int)hk, (int)L); bits; bits &= bits - 1) {
+            const u32 d = 84 + 4 * (L & 31) + (u32)__builtin_ctz(bits);
+            if (d < 86 || d > 170) continue;
+            const u32 len = 186 - d, o = 8 * lane;  // <= 100 bytes: lanes 0..12
+            const u32 q = (32 * g + (d >> 3) + lane) & 63, sh = 8 * (d & 7);
+            const u64 y0 = shfl64(B, q), y1 = shfl64(B, (q + 1) & 63);
+            u64 y = sh ? (y0 >> sh) | (y1 << (64 - sh)) : y0, xx = x;
+            bool bad = false;
+            if (o < len) {
+                if (len - o < 8) {
+                    const u64 m = (1ull << (8 * (len - o))) - 1;
+                    xx &= m;
+                    y &= m;
+                }
+                bad = xx != y;
+            }
+            if (!__ballot(bad)) {
+                res |= 1u << g;
+                break;
+            }
+        }
+    }
+    return res;
 }
 
 template <bool QSKIP, bool PASS1>
@@ -538,7 +572,8 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
                                                            const u32* __restrict__ list,
                                                            const u32* __restrict__ list_cnt,
                                                            u8* __restrict__ blk_p, u16* __restrict__ blk_fo,
-                                                           u16* __restrict__ blk_lo, u64 nbk) {
+                                                           u16* __restrict__ blk_lo, u64 nbk,
+                                                           u32* __restrict__ mark_flag, u32* __restrict__ tot) {
     const u32 lane = threadIdx.x & 63;
     // the stripe index is wave-uniform: keep it (and every address derived from it) in SGPRs
     const u64 wi = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -563,12 +598,17 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
 #if SSS_VAR == 1
         return;
 #endif
-        const u32 f = sss_filter(Bk, lane);
+        // (filter anchors past jmax + 255 have no full window: the zero padding past n is periodic)
+        const u64 a0 = i0 + (u64)k * TAU;
+        const u32 f = sss_filter(Bk, lane) & ((a0 <= jmax + 255 ? 1u : 0u) | (a0 + 256 <= jmax + 255 ? 2u : 0u));
         // branch-free (a conditional target makes the compiler spill the words to scratch)
         const u64 lowk = k < 64 ? 1ull << (k & 63) : 0ull;
         hw0 |= (f & 1) ? lowk : 0ull;
         hw1 |= (f & 2) ? lowk : 0ull;
         hw2 |= k >= 64 ? (u64)f << ((2 * k) & 63) : 0ull;  // blocks 64, 65: bits 0..3
+        // (a hit in the two halo blocks is left to the Q-anchor chain: stopping the stripe sends its
+        // 64 blocks through k_sss_runs' slow path on one wave, 130 us for one stray hit on the
+        // genome-like text against about 60 us of the chain)
         if (f && k < nblk) dirty = true;
     };
     u32 nout = 0;  // outputs of this stripe so far (uniform)
@@ -806,6 +846,18 @@ stripe_done:
             hitw[3 * w] = hw0;
             hitw[3 * w + 1] = hw1;
             hitw[3 * w + 2] = hw2 | (dirty ? 1ull << 63 : 0ull);
+            // filter hits of a stripe that runs on (halo blocks): their tiles need the Q-anchor pass
+            // (the stopped stripes are k_sss_runs' to report); one flag, no atomic once it is set
+            if (!dirty && (hw0 | hw1 | hw2) && __hip_atomic_load(mark_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+                atomicOr(mark_flag, 1u);
+        }
+        // the anchors past the last stripe's own (its halo and the read pad) start out empty too
+        if (w + 1 == nstripes) {
+            const u64 nanch = (n - TAU) / QA + 2, t_tail = w * (u64)(SD / QA) + 4 * nblk;
+            for (u64 t = t_tail + lane; t < nanch + 64; t += 64) {
+                q_init[t] = 0xFF00;
+                if (t < nanch) rp_init[t] = 0;
+            }
         }
         // Q intervals and periods of the stripe's own anchors start out empty (k_q_anchors
         // overwrites the tiles the filter marked)
@@ -814,12 +866,32 @@ stripe_done:
             *(u64*)(q_init + t) = 0xFF00FF00FF00FF00ull;
             *(u32*)(rp_init + t) = 0u;
         }
-        // (the per-block run records are valid only for the stripes k_sss_runs runs on: blk_recs)
+        // the per-block run records start out unknown (k_sss_runs writes the stripes it settles);
+        // the last stripe also clears the blocks past its own, up to nbk inclusive
+        {
+            const u64 gk = w * (u64)SNB + lane;
+            if (gk <= nbk) {
+                blk_p[gk] = 0;
+                blk_fo[gk] = 0;
+                blk_lo[gk] = 0;
+            }
+            if (w + 1 == nstripes) {
+                for (u64 g2 = gk + 64; g2 <= nbk; g2 += 64) {
+                    blk_p[g2] = 0;
+                    blk_fo[g2] = 0;
+                    blk_lo[g2] = 0;
+                }
+            }
+        }
         if (dirty) nout = 0;  // re-run
     }
     if (lane == 0) {
         const u32 fl = nout > scap ? 1u : 0u;
         const u32 old = PASS1 ? 0u : s_flag[w];
+        // |S| as 64 partial sums (same-address atomics from every stripe would serialize); a re-run
+        // replaces the stripe's earlier count
+        const u32 dn = nout - (PASS1 ? 0u : s_cnt[w]);
+        if (dn) atomicAdd(tot + (w & 63), dn);
         s_cnt[w] = nout;
         s_flag[w] = fl;
         if (fl != old) atomicAdd(ovf_ctr, fl ? 1u : 0xFFFFFFFFu);
@@ -953,13 +1025,13 @@ __device__ __forceinline__ int last_diff(u64 d) {
 
 // (113 VGPRs = 4 waves per SIMD; bounding it to the 5 its LDS allows spills 17 VGPRs and was
 // slower on rr: 0.518 vs 0.483 ms for the SSS kernels, tools/gpu_r03b.sh)
-__global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__ T, u64 n, u64 last_i, u64 nstripes,
+__global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restrict__ T, u64 n, u64 last_i, u64 nstripes,
                                                         pos_t* __restrict__ s_out, u32* __restrict__ s_cnt,
                                                         u32* __restrict__ s_flag, u32* __restrict__ ovf_ctr, u32 b,
                                                         sss_pow32 PW, u32 scap, u64* __restrict__ hitw,
                                                         u8* __restrict__ blk_p, u16* __restrict__ blk_fo,
                                                         u16* __restrict__ blk_lo, u64 nbk, u32* __restrict__ any_q,
-                                                        u32* __restrict__ dbg) {
+                                                        u32* __restrict__ dbg, u32* __restrict__ tot) {
     // a ring of RSL blocks per wave in LDS: the bytes at offset p of a block are two aligned word
     // reads (the block after it follows in the ring).  The text arrives RCH blocks at a time in
     // registers, loaded one chunk ahead (a register rotation per block would make every load
@@ -1080,7 +1152,12 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
             // a change of period: classify again with the smallest period of block k + 1 (where
             // the windows of block k end), then of block k, then of the first unsettled window;
             // the period that settles them is kept for the blocks after
-            for (int t = 0; t < 3 && __ballot(u != 0); t++) {
+            // The third try's period search also decides the first unsettled window exactly
+            // (find_period: 0 = not in Q, else in Q).  More tries settle few more stripes and cost
+            // far more (12 tries: k_sss_runs 320 -> 546 us on the 1 GiB repetitive text, 31 -> 24
+            // stripes left to the Q-anchor path)
+            constexpr int MAX_TRY = 3;
+            for (int t = 0; t < MAX_TRY && __ballot(u != 0); t++) {
                 u32 p2;
                 if (t == 0) {
                     p2 = block_period(k + 1, B1k);
@@ -1091,6 +1168,10 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
                     const u32 L = (u32)__builtin_ctzll(ub);
                     const u32 e = (u32)__builtin_ctz((u32)__builtin_amdgcn_readlane((int)u, (int)L));
                     p2 = find_period(T, i0 + (u64)k * TAU + 8 * L + e, lane);
+                    if (lane == L) {
+                        u &= ~(1u << e);
+                        if (p2) q |= 1u << e;
+                    }
                 }
                 n_find++;
                 if (!p2 || p2 == p) continue;
@@ -1198,23 +1279,19 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
             // in it; the refills of the blocks crossed run after the reads
             constexpr u32 RB = 6;
             static_assert(RB + 2 <= RSL - RCH, "run-crossing batch must stay inside the ring");
+            auto pdiff = [&](u32 k) -> u64 {  // p-differences of ring block k
+                const u32 o = (k % RSL) * 64;
+                const u64 lo = ring[(o + ol) % (RSL * 64)], hi = ring[(o + ol + 1) % (RSL * 64)];
+                return ring[o + lane] ^ (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo);
+            };
             for (;;) {
-                u64 dd[RB];
-#pragma unroll
-                for (u32 j = 0; j < RB; j++) {
-                    const u32 o = ((c + 2 + j) % RSL) * 64;
-                    const u64 lo = ring[(o + ol) % (RSL * 64)], hi = ring[(o + ol + 1) % (RSL * 64)];
-                    dd[j] = ring[o + lane] ^ (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo);
-                }
                 u32 f = RB;  // first block of the round with a p-break (uniform)
 #pragma unroll
-                for (int j = (int)RB - 1; j >= 0; j--)
-                    if (__ballot(dd[j] != 0)) f = (u32)j;
+                for (u32 j = 0; j < RB; j++)
+                    if (__ballot(pdiff(c + 2 + j) != 0) && f == RB) f = j;
                 const u32 lim = nblk - c;  // >= 1
                 const u32 adv = min(f, lim);
-#pragma unroll
-                for (u32 j = 0; j < RB; j++)
-                    if (j == f) d = dd[j];
+                if (f < lim) d = pdiff(c + 2 + f);  // (read again: no array of RB values held live)
                 for (u32 j = 1; j <= adv; j++) refill(c + j);
                 c += adv;
                 if (f < RB || c >= nblk) break;
@@ -1355,14 +1432,19 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         atomicOr(any_q + 4, 1u);
     // a stripe whose sync set overflows goes to the exact path too (k_sss_fallback reads the Q
     // intervals of k_q_anchors)
-    if (nout > scap) fail = true;
+    const bool ovf = !fail && nout > scap;
+    if (ovf) fail = true;
     if (lane == 0) {
         if (dbg) {  // (same-address atomics from every wave serialize: debug runs only)
             atomicAdd(dbg + 0, n_cls);
             atomicAdd(dbg + 1, n_find);
             atomicAdd(dbg + 2, fail ? 1u : 0u);
+            atomicAdd(dbg + 3, ovf ? 1u : 0u);
         }
-        if (fail) return;  // left to the Q-anchor path (still forced)
+        if (fail) {  // left to the Q-anchor path (still forced)
+            if (__hip_atomic_load(any_q + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(any_q + 5, 1u);
+            return;
+        }
         hitw[3 * w] = 0;
         hitw[3 * w + 1] = 0;
         hitw[3 * w + 2] = 1ull << 62;  // settled here
@@ -1370,27 +1452,22 @@ __global__ __launch_bounds__(64 * SWAVES) void k_sss_runs(const u8* __restrict__
         if (anyq && __hip_atomic_load(any_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(any_q, 1u);
         const u32 fl = nout > scap ? 1u : 0u;
         const u32 old = s_flag[w];
+        if (nout) atomicAdd(tot + (w & 63), nout);  // |S| partial sums (pass 1 counted 0 here)
         s_cnt[w] = nout;
         s_flag[w] = fl;
         if (fl != old) atomicAdd(ovf_ctr, fl ? 1u : 0xFFFFFFFFu);
     }
 }
-// The per-block run records as k_sss_runs left them: a block's record is valid when k_sss_runs ran
-// on its stripe (hitw bit 63: forced, 62: settled by it); every other block reads as "no record"
-// (period 0, no break known), so pass 1 no longer clears 5 bytes per block on every call.
+// The per-block run records (pass 1 clears them, k_sss_runs writes the stripes it runs on; the
+// clearing stores cost nothing measurable beside pass 1's work, where gating every read by the
+// stripe's state made the segment kernels 11 us slower on the 1 GiB repetitive text)
 struct blk_recs {
     const u8* bp;
     const u16* fo;
     const u16* lo;
-    const u64* hitw;
-    u64 nstripes, nbk;
-    __device__ __forceinline__ bool ok(u64 b) const {
-        const u64 w = b / SNB;
-        return w < nstripes && (hitw[3 * w + 2] >> 62) != 0;
-    }
-    __device__ __forceinline__ u32 p(u64 b) const { return ok(b) ? bp[b] : 0u; }
-    __device__ __forceinline__ u32 f(u64 b) const { return ok(b) ? fo[b] : 0u; }
-    __device__ __forceinline__ u32 l(u64 b) const { return ok(b) ? lo[b] : 0u; }
+    __device__ __forceinline__ u32 p(u64 b) const { return bp[b]; }
+    __device__ __forceinline__ u32 f(u64 b) const { return fo[b]; }
+    __device__ __forceinline__ u32 l(u64 b) const { return lo[b]; }
 };
 // per-block run end / start packed for one-load lookups (lce_dev.h run_tab::re / rs): the
 // segment's end made exact by the first break of its period in the block after it (fo), its
@@ -1475,16 +1552,33 @@ __global__ __launch_bounds__(BT_T) void k_blk_seg_tiles(blk_recs bp, u64 nbk, u6
 __global__ __launch_bounds__(BT_T) void k_blk_seg_info(blk_recs bp, u64 nbk,
                                                        const u64* __restrict__ tfe, const u64* __restrict__ tls,
                                                        u64 ntile, u64* __restrict__ re, u64* __restrict__ rs) {
-    __shared__ u64 s_end[BT_TILE];  // per block: its segment's last block inside the tile, or BT_NONE
-    __shared__ u64 s_beg[BT_TILE];  // per block: its segment's first block inside the tile, or BT_NONE
+    // the tile's 64 groups of 64 blocks: per group the ballot masks of its segment ends
+    // (!cont_f) and starts (!cont_b); a block's segment end is the first end at or after it (in
+    // its group, else in the first later group that has one, else past the tile: s_after), its
+    // start the last start at or before it.  One barrier, no scans (the LDS Hillis-Steele form
+    // took 38-42 us on the 1 GiB repetitive text)
+    static_assert(BT_TILE == 64 * 64, "64 groups of 64 blocks per tile");
+    __shared__ u64 s_em[64], s_bm[64];
     __shared__ u64 s_after, s_before;
-    const u32 t = threadIdx.x, lane = t & 63;
+    const u32 t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const u64 tile = blockIdx.x, t0 = tile * BT_TILE;
     const u64 tn = min<u64>(BT_TILE, nbk - t0);
-    for (u32 k = t; k < BT_TILE; k += BT_T) {
-        const u64 b = t0 + k;
-        s_end[k] = (k < tn && !blk_cont_f(bp, nbk, b)) ? b : BT_NONE;
-        s_beg[k] = (k < tn && !blk_cont_b(bp, b)) ? b : BT_NONE;
+    constexpr u32 GPW = BT_TILE / BT_T;  // groups per wave (4)
+    u32 pv[GPW];
+#pragma unroll
+    for (u32 k = 0; k < GPW; k++) {
+        const u32 g = wv * GPW + k, i = g * 64 + lane;
+        const u64 b = t0 + i;
+        const bool in = i < tn;
+        const u32 p = in ? bp.p(b) : 0u;
+        pv[k] = p;
+        const bool cf = in && p && b + 1 < nbk && bp.p(b + 1) == p;
+        const bool cb = in && p && b > 0 && bp.p(b - 1) == p;
+        const u64 em = __ballot(in && !cf), bm = __ballot(in && !cb);
+        if (lane == 0) {
+            s_em[g] = em;
+            s_bm[g] = bm;
+        }
     }
     // the first segment end at or after the next tile, the last segment start before this
     // tile (wave 0 / wave 1 search the tile table 64 tiles per step)
@@ -1517,38 +1611,45 @@ __global__ __launch_bounds__(BT_T) void k_blk_seg_info(blk_recs bp, u64 nbk,
         if (lane == 0) s_before = r;
     }
     __syncthreads();
-    // in-tile scans: s_end by a suffix minimum, s_beg by a prefix maximum (Hillis-Steele in LDS;
-    // BT_NONE acts as +inf for the minimum and is skipped by the maximum)
-    for (u32 d = 1; d < BT_TILE; d <<= 1) {
-        u64 ve[BT_PER], vb[BT_PER];
-        for (u32 k = 0; k < BT_PER; k++) {
-            const u32 i = k * BT_T + t;
-            const u64 e = s_end[i], e2 = i + d < BT_TILE ? s_end[i + d] : BT_NONE;
-            ve[k] = min(e, e2);
-            const u64 g = s_beg[i], g2 = i >= d ? s_beg[i - d] : BT_NONE;
-            vb[k] = g == BT_NONE ? g2 : (g2 == BT_NONE ? g : max(g, g2));
-        }
-        __syncthreads();
-        for (u32 k = 0; k < BT_PER; k++) {
-            s_end[k * BT_T + t] = ve[k];
-            s_beg[k * BT_T + t] = vb[k];
-        }
-        __syncthreads();
-    }
-    for (u32 k = 0; k < BT_PER; k++) {
-        const u32 i = k * BT_T + t;
+    const u64 em_l = s_em[lane], bm_l = s_bm[lane];
+    const u64 ge = __ballot(em_l != 0), gb = __ballot(bm_l != 0);  // groups holding an end / a start
+#pragma unroll
+    for (u32 k = 0; k < GPW; k++) {
+        const u32 g = wv * GPW + k, i = g * 64 + lane;
         if (i >= tn) break;
         const u64 b = t0 + i;
-        const u64 p = bp.p(b);
+        const u64 p = pv[k];
         if (!p) {
             re[b] = 0;
             rs[b] = 0;
             continue;
         }
-        u64 eb = s_end[i];
-        if (eb == BT_NONE) eb = s_after;     // always found: the last block ends every segment
-        u64 sb0 = s_beg[i];
-        if (sb0 == BT_NONE) sb0 = s_before;  // always found: block 0 starts every segment
+        u64 eb;
+        const u64 me = s_em[g] >> lane;  // ends at or after the block in its group
+        if (me) {
+            eb = b + (u64)__builtin_ctzll(me);
+        } else {
+            const u64 nx = g < 63 ? ge & (~0ull << (g + 1)) : 0ull;
+            if (nx) {
+                const u32 g2 = (u32)__builtin_ctzll(nx);
+                eb = t0 + (u64)g2 * 64 + (u64)__builtin_ctzll(s_em[g2]);
+            } else {
+                eb = s_after;  // always found: the last block ends every segment
+            }
+        }
+        u64 sb0;
+        const u64 mb = s_bm[g] & (lane == 63 ? ~0ull : ((2ull << lane) - 1));  // starts at or before it
+        if (mb) {
+            sb0 = t0 + (u64)g * 64 + (63u - (u32)__builtin_clzll(mb));
+        } else {
+            const u64 pr = gb & ((1ull << g) - 1);
+            if (pr) {
+                const u32 g2 = 63u - (u32)__builtin_clzll(pr);
+                sb0 = t0 + (u64)g2 * 64 + (63u - (u32)__builtin_clzll(s_bm[g2]));
+            } else {
+                sb0 = s_before;  // always found: block 0 starts every segment
+            }
+        }
         const u64 se = (eb + 1) * TAU, ebn = eb + 1;
         u64 e = se + p, xe = 0;
         if (ebn < nbk) {
@@ -1807,6 +1908,95 @@ __global__ void k_sss_compact(const pos_t* __restrict__ lane_out, const u32* __r
     }
 }
 
+// Compaction with the offsets found in the kernel (no overflowing stripe): workgroup b copies the
+// outputs of stripes [64 b, 64 b + 64), its base the sum of all earlier stripes' counts (read by
+// the whole workgroup from L2, 32 loads per thread at most at 1 GiB); the block's outputs are one
+// contiguous range of S, copied by all threads (an output finds its stripe by a binary search
+// over the block's 64 offsets)
+constexpr u32 CC_T = 1024, CC_SPB = 64;
+__global__ __launch_bounds__(CC_T) void k_sss_compact_scan(const pos_t* __restrict__ lane_out,
+                                                           const u32* __restrict__ lane_cnt, u64 nlanes,
+                                                           pos_t* __restrict__ S) {
+    __shared__ u32 s_part[CC_T / 64];
+    __shared__ u32 s_off[CC_SPB + 1];
+    const u32 t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const u64 w0 = (u64)blockIdx.x * CC_SPB;
+    u32 sum = 0;
+#pragma unroll 8
+    for (u64 k = t; k < w0; k += CC_T) sum += lane_cnt[k];
+    for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) s_part[wv] = sum;
+    const u32 c = t < CC_SPB && w0 + t < nlanes ? lane_cnt[w0 + t] : 0u;
+    __syncthreads();
+    if (t < CC_SPB) {  // wave 0: the block's offsets (relative), s_off[64] = its total
+        const u32 inc = wave_prefix_add(c);
+        s_off[t] = inc - c;
+        if (t == CC_SPB - 1) s_off[CC_SPB] = inc;
+    }
+    u32 base = 0;
+    for (u32 k = 0; k < CC_T / 64; k++) base += s_part[k];
+    __syncthreads();
+    const u32 tot = s_off[CC_SPB];
+    for (u32 j = t; j < tot; j += CC_T) {
+        u32 lo = 0, hi = CC_SPB - 1;  // the last stripe k with s_off[k] <= j
+        while (lo < hi) {
+            const u32 mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= j) lo = mid;
+            else hi = mid - 1;
+        }
+        S[(u64)base + j] = lane_out[(w0 + lo) * SCAP + (j - s_off[lo])];
+    }
+}
+
+// exclusive scan of the stripe counts in one workgroup (off[m] = the total): one launch where the
+// pad fill and rocprim's scan took three (about 15 us of the phase on a 1 GiB text).  Wave w holds
+// the chunks w, w + 16, ... of 64 counts in registers (all loads issued at once: a loop of
+// dependent load-scan steps took 25-60 us), their totals are scanned across the workgroup
+constexpr u32 CS_T = 1024, CS_CPW = 64, CS_MAX = CS_T * CS_CPW;
+__global__ __launch_bounds__(CS_T) void k_count_scan(const u32* __restrict__ cnt, u64 m, u32* __restrict__ off) {
+    __shared__ u32 s_c[CS_T];
+    __shared__ u32 s_w[CS_T / 64];
+    const u32 t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const u32 nch = (u32)((m + 63) / 64);
+    u32 x[CS_CPW];
+#pragma unroll
+    for (u32 k = 0; k < CS_CPW; k++) {
+        const u64 i = ((u64)(wv + 16 * k)) * 64 + lane;
+        x[k] = i < m ? cnt[i] : 0u;
+    }
+#pragma unroll
+    for (u32 k = 0; k < CS_CPW; k++) {
+        const u32 c = wv + 16 * k;
+        if (c < nch) {  // (uniform)
+            x[k] = wave_prefix_add(x[k]);  // inclusive, per chunk
+            if (lane == 63) s_c[c] = x[k];
+        }
+    }
+    __syncthreads();
+    const u32 v = t < nch ? s_c[t] : 0u;
+    const u32 incl = wave_prefix_add(v);
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    if (t < 64) {
+        const u32 y = t < CS_T / 64 ? s_w[t] : 0u;
+        const u32 iy = wave_prefix_add(y);
+        if (t < CS_T / 64) s_w[t] = iy - y;
+    }
+    __syncthreads();
+    if (t < nch) s_c[t] = s_w[wv] + incl - v;  // chunk bases
+    __syncthreads();
+#pragma unroll
+    for (u32 k = 0; k < CS_CPW; k++) {
+        const u32 c = wv + 16 * k;
+        if (c < nch) {
+            const u64 i = (u64)c * 64 + lane;
+            const u32 ex = (u32)__shfl_up((int)x[k], 1, 64);  // the inclusive sum of the lane before
+            if (i < m) off[i] = s_c[c] + (lane ? ex : 0u);
+            if (c + 1 == nch && lane == 63) off[m] = s_c[c] + x[k];
+        }
+    }
+}
+
 static u32 pow32_host(u32 b, u64 e) {
     u32 r = 1;
     while (e) {
@@ -1886,7 +2076,9 @@ void engine::build_sss(const u8* T) {
     pos_t* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
     u32* ctr = counters.get(16);
-    LZ_HIP(hipMemsetAsync(ctr, 0, 12 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes, any block record; 8..10: k_sss_runs counters
+    LZ_HIP(hipMemsetAsync(ctr, 0, 12 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes, any block record, marks needed; 8..11: k_sss_runs counters
+    u32* tot = sss_tot.get(64);  // |S| as 64 partial sums (stripe w adds to w & 63)
+    LZ_HIP(hipMemsetAsync(tot, 0, 64 * sizeof(u32), st));
     pos_t* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
@@ -1905,10 +2097,12 @@ void engine::build_sss(const u8* T) {
     // test knob: a lower overflow threshold sends more stripes down the exact fallback
     const char* scap_env = std::getenv("LZ77SSS_TEST_SCAP");
     const u32 scap = scap_env ? (u32)std::min<long>(SCAP, std::max<long>(0, std::atol(scap_env))) : (u32)SCAP;
-    hipEvent_t e0, e1;
-    LZ_HIP(hipEventCreate(&e0));
-    LZ_HIP(hipEventCreate(&e1));
-    LZ_HIP(hipEventRecord(e0, st));
+    if (!sss_ev0) {
+        LZ_HIP(hipEventCreate(&sss_ev0));
+        LZ_HIP(hipEventCreate(&sss_ev1));
+    }
+    sss_ev_pending = false;
+    LZ_HIP(hipEventRecord(sss_ev0, st));
     // per-block run records (0: unknown), cleared by pass 1
     const u64 nbk = (n + TAU - 1) / TAU;
     u8* bp = blk_p.get(nbk + 1);
@@ -1916,42 +2110,49 @@ void engine::build_sss(const u8* T) {
     u16* blo = blk_lo.get(nbk + 1);
     k_sss_stream<false, true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(
         T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, hw, qi, rp, nullptr, nullptr, bp, bfo,
-        blo, nbk);
+        blo, nbk, ctr + 5, tot);
     LZ_HIP(hipGetLastError());
     // the stripes pass 1 stopped: settled in one pass where their periodic windows are runs
     // (k_sss_runs), which also writes the per-block run records of the LCE
-    if (!std::getenv("LZ77SSS_NO_RUNS_KERNEL"))  // test knob: every stopped stripe through the Q-anchor path
+    const bool runs_kernel = !std::getenv("LZ77SSS_NO_RUNS_KERNEL");  // test knob: every stopped stripe through the Q-anchor path
+    if (runs_kernel)
         k_sss_runs<<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, nlanes, lo, lc, lf, ctr + 1,
                                                                 (u32)SSS_BASE, PW, scap, hw, bp, bfo, blo, nbk, ctr + 0,
-                                                                debug_enabled() ? ctr + 8 : nullptr);
+                                                                debug_enabled() ? ctr + 8 : nullptr, tot);
     LZ_HIP(hipGetLastError());
-    // tiles the filter marked; anchors past the last stripe's own start out empty
-    const u64 nblk_last = std::min<u64>(SNB, (last_i - (nlanes - 1) * SD) / TAU + 1);
-    const u64 t_tail = (nlanes - 1) * (SD / QA) + 4 * nblk_last, q_end = nanch + 64;
-    const u64 nthr = std::max<u64>(std::max<u64>(nlanes, tpad), q_end - t_tail);
-    k_sss_marks<<<cdiv(nthr, 256), 256, 0, st>>>(hw, nlanes, ntiles, tpad, nanch, tfl, sfl, sl, ctr + 3, t_tail, q_end,
-                                                qi, rp);
+    // one read: any Q window, overflowing stripes, does any block have a run record, does any tile
+    // need the Q-anchor pass (a hit in a stripe pass 1 ran through, or a stripe k_sss_runs could not
+    // settle); |S| as 64 partial sums (final unless the Q-anchor pass re-runs stripes)
+    u32 hc[6], htot[64];
     {
+        hread rb(st);
+        rb.add(hc, (const u32*)ctr, 6);
+        rb.add(htot, (const u32*)tot, 64);
+        rb.sync();
+    }
+    const u32 need_marks = hc[5], any_rec = hc[4];
+    u32 ndirty = 0;
+    if (need_marks || !runs_kernel) {
+        // tiles the filter marked (the stopped stripes k_sss_runs settled have no hit bits left)
+        const u64 nblk_last = std::min<u64>(SNB, (last_i - (nlanes - 1) * SD) / TAU + 1);
+        const u64 t_tail = (nlanes - 1) * (SD / QA) + 4 * nblk_last, q_end = nanch + 64;
+        const u64 nthr = std::max<u64>(std::max<u64>(nlanes, tpad), q_end - t_tail);
+        k_sss_marks<<<cdiv(nthr, 256), 256, 0, st>>>(hw, nlanes, ntiles, tpad, nanch, tfl, sfl, sl, ctr + 3, t_tail,
+                                                    q_end, qi, rp);
         const u64 nfw = (ntiles + 15) / 16;  // 16-byte flag words (the flag array is padded to tpad)
         const unsigned nfb = cdiv(nfw, FL_T);
         u32* fc = sss_fcnt.get(nfb);
         k_flag_count<<<nfb, FL_T, 0, st>>>(tfl, nfw, fc);
         k_flag_list<<<nfb, FL_T, 0, st>>>(tfl, nfw, fc, tl, ctr + 2);
-    }
-    LZ_HIP(hipGetLastError());
-    u32 ndirty, any_rec;
-    {
-        hread rb(st);
-        rb.add(&ndirty, (const u32*)ctr + 2);
-        rb.add(&any_rec, (const u32*)ctr + 4);
-        rb.sync();
+        LZ_HIP(hipGetLastError());
+        ndirty = rd1(ctr + 2, st);
     }
     stats_sss_tiles = ndirty;
     if (debug_enabled()) {
-        u32 dc[3];
-        LZ_HIP(hipMemcpy(dc, ctr + 8, 12, hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[lz77sss-debug] sss: k_sss_runs slow classifications=%u period searches=%u unsettled stripes=%u tiles=%u\n",
-                     dc[0], dc[1], dc[2], ndirty);
+        u32 dc[4];
+        LZ_HIP(hipMemcpy(dc, ctr + 8, 16, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[lz77sss-debug] sss: k_sss_runs slow classifications=%u period searches=%u unsettled stripes=%u (overflowing %u) tiles=%u\n",
+                     dc[0], dc[1], dc[2], dc[3], ndirty);
     }
     if (ndirty) {
         k_q_anchors<<<ndirty, QT_THREADS, 0, st>>>(T, n, nanch, qi, ctr + 0, rp, rhi, rlo, rcap, tl, sfl, sl, ctr + 3,
@@ -1963,7 +2164,7 @@ void engine::build_sss(const u8* T) {
         const u64 maxw = std::min<u64>(nlanes, 4ull * ndirty + 4);
         k_sss_stream<true, false><<<cdiv(maxw, SWAVES), 64 * SWAVES, 0, st>>>(
             T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, nullptr, nullptr, nullptr, sl,
-            ctr + 3, nullptr, nullptr, nullptr, 0);
+            ctr + 3, nullptr, nullptr, nullptr, 0, nullptr, tot);
         LZ_HIP(hipGetLastError());
     }
     runs_valid = true;  // period 0 outside the marked tiles
@@ -1972,7 +2173,7 @@ void engine::build_sss(const u8* T) {
         // run-record segments -> packed per-block run end / start (two launches)
         const u64 ntile = (nbk + BT_TILE - 1) / BT_TILE;
         u64* tt = (u64*)blk_mk.get(4 * ntile + 4);  // 2 x ntile u64 (the buffer is pos_t-typed)
-        const blk_recs BR{bp, bfo, blo, hw, nlanes, nbk};
+        const blk_recs BR{bp, bfo, blo};
         k_blk_seg_tiles<<<(unsigned)ntile, BT_T, 0, st>>>(BR, nbk, tt, tt + ntile);
         k_blk_seg_info<<<(unsigned)ntile, BT_T, 0, st>>>(BR, nbk, tt, tt + ntile, ntile, blk_re.get(nbk),
                                                          blk_rs.get(nbk));
@@ -2028,13 +2229,31 @@ void engine::build_sss(const u8* T) {
         }
     }
     // sss_kernel_ms: pass 1 through the re-run (the phase's kernels and its one host read)
-    LZ_HIP(hipEventRecord(e1, st));
+    LZ_HIP(hipEventRecord(sss_ev1, st));
+    sss_ev_pending = true;
 
-    // exclusive scan of stripe counts -> offsets; total = |S|
-    u32* off = u32a.get(nlanes + 1);
-    auto scan_counts = [&]() { excl_sum_total(lc, off, nlanes, scan_tmp, st); };
-    scan_counts();
     u32 hp[3];
+    u32 total = 0;
+    for (u32 v : htot) total += v;
+    u32* off = u32a.get(nlanes + 1);
+    auto scan_counts = [&]() {
+        if (nlanes <= CS_MAX) k_count_scan<<<1, CS_T, 0, st>>>(lc, nlanes, off);
+        else excl_sum_total(lc, off, nlanes, scan_tmp, st);
+    };
+    if (!ndirty && !hc[1]) {
+        // the usual case: the counts are final and nothing overflowed, so |S| is known and the
+        // compaction finds the stripes' offsets itself (no scan launch, no second read)
+        has_runs = hc[0] != 0;
+        if (total >= 0x7FFFFFFFu) throw error(LZ77SSS_EINVAL, "sync set of 2^31 or more positions (split the text)");
+        s = total;
+        sss_kernel_bytes = n + sizeof(pos_t) * (u64)s;
+        pos_t* dS = S.get((u64)s + 1);
+        k_sss_compact_scan<<<cdiv(nlanes, CC_SPB), CC_T, 0, st>>>(lo, lc, nlanes, dS);
+        LZ_HIP(hipGetLastError());
+        return;
+    }
+    // exclusive scan of stripe counts -> offsets; total = |S|
+    scan_counts();
     {
         hread rb(st);
         rb.add(hp, (const u32*)ctr, 2);
@@ -2042,13 +2261,7 @@ void engine::build_sss(const u8* T) {
         rb.sync();
     }
     has_runs = hp[0] != 0;
-    u32 total = hp[2];
-    float ms = 0;
-    LZ_HIP(hipEventSynchronize(e1));  // (complete: the read-back ran after it)
-    LZ_HIP(hipEventElapsedTime(&ms, e0, e1));
-    sss_kernel_ms = ms;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    total = hp[2];
 
     // overflowing stripes -> exact workgroup-parallel path
     u32* ovf_slot = u32c.get(nlanes);
@@ -2126,7 +2339,7 @@ void engine::build_sss_range(u64 first, u64 end, u64 base, u64 window) {
             const u64 e = std::min(end, b + window);
             n = e - b + 2 * TAU - 1;  // the view: its last decision is e - 1
             build_sss(d_text + b);
-            kms += sss_kernel_ms;
+            kms += sss_ms();
             kbytes += sss_kernel_bytes;
             has_runs64 |= has_runs;
             stats_sss_windows++;

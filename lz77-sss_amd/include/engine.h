@@ -65,7 +65,21 @@ struct engine {
     dbuf<u32> counters;        // small scratch counters
     u32 s = 0;
     bool has_runs = false;
-    double sss_kernel_ms = 0;  // dominant kernel (SSS main pass) duration
+    // dominant kernel (SSS phase) duration: HIP events recorded around the phase's kernels, read
+    // when asked (sss_ms), so the phase needs no synchronization of its own for them
+    mutable double sss_kernel_ms = 0;
+    hipEvent_t sss_ev0 = nullptr, sss_ev1 = nullptr;
+    mutable bool sss_ev_pending = false;
+    double sss_ms() const {
+        if (sss_ev_pending) {
+            float ms = 0;
+            LZ_HIP(hipEventSynchronize(sss_ev1));
+            LZ_HIP(hipEventElapsedTime(&ms, sss_ev0, sss_ev1));
+            sss_kernel_ms = ms;
+            sss_ev_pending = false;
+        }
+        return sss_kernel_ms;
+    }
     u64 sss_kernel_bytes = 0;  // its algorithmic bytes (text + 4|S|) per launch
     u64 stats_fallback_lanes = 0;
     dbuf<u8> run_p;            // periodic-run table per Q anchor (lce_dev.h run_tab)
@@ -87,6 +101,7 @@ struct engine {
     dbuf<u8> blk_p;
     dbuf<u16> blk_fo, blk_lo;
     dbuf<pos_t> blk_mk, blk_ser, blk_ss;
+    dbuf<u32> sss_tot;  // |S| partial sums of the stripe kernels (csrc/sss.hip)
     dbuf<u64> blk_re, blk_rs;  // packed per-block run end / start (lce_dev.h run_tab::re / rs)
     u64 brk_nbk = 0;
     bool brk_valid = false;
@@ -207,10 +222,12 @@ struct engine {
     dbuf<u8> dec_out;
     u32 dec_rounds = 0;
     u64 num_fact = 0;
-    int last_fact_mode = -1;  // fact_mode of the last factorize call (-1: none for the loaded text)
-    // the factors in HBM are a factorization of the loaded text (lz77sss_session_verify)
+    int last_fact_mode = -1;  // fact_mode of the last factorize call (-1: none yet)
+    // lz77sss_session_verify checks the factors in HBM against the text in HBM: a factorization must
+    // exist and be one (a skip_phrases stream is not).  Loading another text keeps the factors, so
+    // the check then reports where they do not reproduce it (tests corrupt the text this way)
     void check_verifiable() const {
-        if (last_fact_mode == -1) throw error(LZ77SSS_EINVAL, "no factorization of the loaded text to verify");
+        if (last_fact_mode == -1) throw error(LZ77SSS_EINVAL, "no factorization in the session to verify");
         if (last_fact_mode == LZ77SSS_SKIP_PHRASES)
             throw error(LZ77SSS_EINVAL, "a skip_phrases stream is not a factorization (nothing to verify)");
     }

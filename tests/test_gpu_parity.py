@@ -565,3 +565,34 @@ def test_greedy_window_chain_reaches_tail(session, orc, window, max_outer, run_l
     # stats[23]: windows walked again as the last one (the sequential completion also re-walks
     # a window whose hand-over point an LPF factor carried past n - 64)
     assert s.stats()[23] >= 1 if crosses else (max_outer == 0 or s.stats()[23] == 0)
+
+
+@pytest.mark.parametrize("kind,mib", [("rr", 64), ("rr", 3), ("periods", 8)])
+def test_block_run_records_vs_scan_form(session, orc, lz, kind, mib, monkeypatch):
+    """The per-block run records' segment ends / starts (k_blk_seg_tiles + k_blk_seg_info, ballot masks
+    per 64-block group) equal the marker + min/max-scan formulation entry by entry (LZ77SSS_BLK_CHECK
+    raises on any difference), and the stream equals the oracle's with and without the records and
+    with every stopped stripe sent through the Q-anchor path (LZ77SSS_NO_RUNS_KERNEL)."""
+    n = mib << 20
+    if kind == "periods":
+        rng = np.random.default_rng(5)
+        parts, tot = [], 0
+        while tot < n:  # runs of random periods 1..200 and lengths up to 2 MiB, random glue between
+            p = int(rng.integers(1, 201))
+            unit = rng.integers(97, 101, p, dtype=np.uint8)
+            ln = int(rng.integers(1, 2 << 20))
+            parts += [np.resize(unit, ln), rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8)]
+            tot += ln
+        T = np.concatenate(parts)[:n]
+    else:
+        T = lz.gen_random_repetitive(n, n, 31 + mib, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    monkeypatch.setenv("LZ77SSS_BLK_CHECK", "1")
+    _, F1 = run(session, T)
+    assert F1.shape == F_ref.shape and np.array_equal(F1, F_ref)
+    monkeypatch.delenv("LZ77SSS_BLK_CHECK")
+    for knob in ("LZ77SSS_NO_BLKREC", "LZ77SSS_NO_RUNS_KERNEL"):
+        monkeypatch.setenv(knob, "1")
+        _, F2 = run(session, T)
+        assert np.array_equal(F2, F_ref), knob
+        monkeypatch.delenv(knob)

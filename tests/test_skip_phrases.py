@@ -65,9 +65,10 @@ def test_gpu_skip_c1(session, orc, lz, seed):
 
 
 @pytest.mark.gpu
-def test_verify_refuses_skip_stream_and_stale_factors(session, lz):
-    """lz77sss_session_verify checks a factorization of the loaded text: after a skip_phrases call, or
-    after load() of another text, it refuses (LZ77SSS_EINVAL) instead of reporting bad positions."""
+def test_verify_refuses_skip_stream(session, lz):
+    """lz77sss_session_verify checks a factorization against the text in HBM: after a skip_phrases call
+    it refuses (LZ77SSS_EINVAL) instead of reporting bad positions; a later factorization is checked
+    again; another loaded text is checked against the kept factors (it differs)."""
     T = lz.gen_random_repetitive(10000, 200000, 4)
     s = session(T.size)
     s.load(T)
@@ -79,5 +80,4 @@ def test_verify_refuses_skip_stream_and_stale_factors(session, lz):
     s.factorize()
     assert s.verify() == 0
     s.load(T[::-1].copy())
-    with pytest.raises(lz.Lz77SssError):
-        s.verify()
+    assert s.verify() > 0
