@@ -19,9 +19,11 @@ collective, the barrier/max-over-ranks timing only (weak scaling).
 
 Also reported:
   roofline      the SSS kernel sequence (k_sss_stream pass 1 with the periodicity
-                filter, the exact Q pass on marked tiles, the re-run of stripes that
-                see Q windows), algorithmic bytes n + 4|S| per call over its HIP-event
-                time on the library's own stream,
+                filter, k_sss_runs on the stripes pass 1 stopped, the exact Q pass on
+                marked tiles and the re-run of stripes that see Q windows, the run-record
+                segments, the compaction of S), algorithmic bytes n + 4|S| per call over
+                its HIP-event time on the library's own stream (two windows: the
+                phase's one host read is not kernel time),
                 against the 8 TB/s HBM3E peak; ``traffic`` from the committed
                 rocprofv3 PMC summary (profiles/) when one exists for this
                 workload, else null.
@@ -66,7 +68,7 @@ def aggregate(dt_local: float, n_per_rank: int, world: int, dist=None, device="c
 
 # the SSS kernel set the roofline covers; a PMC summary counts only if it measured
 # all of them (older summaries predate k_sss_runs and cover a different kernel sequence)
-SSS_KERNELS = ("k_sss_stream<false, true>", "k_sss_runs", "k_q_anchors", "k_sss_stream<true, false>")
+SSS_KERNELS = ("k_sss_stream<false, true>", "k_sss_runs", "k_sss_compact_scan")
 
 
 def pmc_traffic(workload: str, n: int, mode: str = "approx"):
@@ -304,7 +306,9 @@ def main():
                 "huffman_container": {"bytes": hbytes, "ms_incl_d2h": round(t_h * 1e3, 3)},
             },
             "roofline": {
-                "kernel": "SSS kernels: k_sss_stream pass 1 .. k_sss_stream re-run + k_blk_seg_tiles/info (DESIGN.md 4.1)",
+                "kernel": "SSS phase kernels (DESIGN.md 4.1): k_sss_stream pass 1, k_sss_runs, [Q-anchor pass + re-run "
+                          "where a tile is marked], k_blk_seg_tiles/info, compaction; HIP events in two windows "
+                          "around the phase's one host read",
                 "bound": "hbm",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,

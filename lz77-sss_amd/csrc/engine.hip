@@ -47,9 +47,10 @@ void engine::load(const u8* h_text, u64 n_) {
 }
 
 void engine::destroy() {
-    if (sss_ev0) (void)hipEventDestroy(sss_ev0);
-    if (sss_ev1) (void)hipEventDestroy(sss_ev1);
-    sss_ev0 = sss_ev1 = nullptr;
+    for (hipEvent_t* e : {&sss_ev0, &sss_ev1, &sss_evA, &sss_evB}) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+    }
     if (d_text) (void)hipFree(d_text);
     if (d_text_rev) (void)hipFree(d_text_rev);
     d_text = d_text_rev = nullptr;

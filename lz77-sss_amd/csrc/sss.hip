@@ -723,7 +723,9 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
         // prologue: Hp for blocks 0 and 1, Phi'(block 0)
         u32 carry = 0;
         const u64 B0 = load8(0), B1 = load8(1);
-        u64 Ba = load8(2), Bb = load8(3);
+        // bytes of blocks c + 2 .. c + 5 in flight at step c (four blocks ahead: a lone wave at the
+        // kernel's tail otherwise waits on every load)
+        u64 Ba = load8(2), Bb = load8(3), Bc = load8(4), Bd = load8(5);
         const uint4 qa = loadq(0);
         uint4 qb = loadq(1);
         u32 hA[8], hB[8], xA[8], xB[8];
@@ -820,21 +822,23 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
         // stripe's decisions reach two blocks past its end); a hit in a decision block ends
         // the stripe (it is re-run)
         for (u32 c = 0; c < nblk; c += 2) {
-            u64 Bn = load8(c + 4);  // prefetch (the text pad covers the stripe's end)
+            const u64 N0 = load8(c + 6);  // prefetch (the text pad covers the stripe's end)
             if constexpr (PASS1) {
                 filt(c + 2, Ba);
                 if (dirty) break;
             }
             step(c, xA, xB, hB, hA, Ba, qb, fA, fB, loadq(c + 2));
-            Ba = Bn;
             if (c + 1 >= nblk) break;
-            Bn = load8(c + 5);
+            const u64 N1 = load8(c + 7);
             if constexpr (PASS1) {
                 filt(c + 3, Bb);
                 if (dirty) break;
             }
             step(c + 1, xB, xA, hA, hB, Bb, qb, fB, fA, loadq(c + 3));
-            Bb = Bn;
+            Ba = Bc;
+            Bb = Bd;
+            Bc = N0;
+            Bd = N1;
         }
     }
 stripe_done:
@@ -2060,6 +2064,7 @@ void engine::build_sss(const u8* T) {
     s = 0;
     has_runs = false;
     sss_kernel_ms = 0;
+    sss_ev_pending = false;
     sss_kernel_bytes = 0;
     runs_valid = false;
     stats_fallback_lanes = 0;
@@ -2097,10 +2102,8 @@ void engine::build_sss(const u8* T) {
     // test knob: a lower overflow threshold sends more stripes down the exact fallback
     const char* scap_env = std::getenv("LZ77SSS_TEST_SCAP");
     const u32 scap = scap_env ? (u32)std::min<long>(SCAP, std::max<long>(0, std::atol(scap_env))) : (u32)SCAP;
-    if (!sss_ev0) {
-        LZ_HIP(hipEventCreate(&sss_ev0));
-        LZ_HIP(hipEventCreate(&sss_ev1));
-    }
+    if (!sss_ev0)
+        for (hipEvent_t* e : {&sss_ev0, &sss_ev1, &sss_evA, &sss_evB}) LZ_HIP(hipEventCreate(e));
     sss_ev_pending = false;
     LZ_HIP(hipEventRecord(sss_ev0, st));
     // per-block run records (0: unknown), cleared by pass 1
@@ -2124,6 +2127,7 @@ void engine::build_sss(const u8* T) {
     // need the Q-anchor pass (a hit in a stripe pass 1 ran through, or a stripe k_sss_runs could not
     // settle); |S| as 64 partial sums (final unless the Q-anchor pass re-runs stripes)
     u32 hc[6], htot[64];
+    LZ_HIP(hipEventRecord(sss_evA, st));
     {
         hread rb(st);
         rb.add(hc, (const u32*)ctr, 6);
@@ -2131,6 +2135,7 @@ void engine::build_sss(const u8* T) {
         rb.sync();
     }
     const u32 need_marks = hc[5], any_rec = hc[4];
+    LZ_HIP(hipEventRecord(sss_evB, st));
     u32 ndirty = 0;
     if (need_marks || !runs_kernel) {
         // tiles the filter marked (the stopped stripes k_sss_runs settled have no hit bits left)
@@ -2228,9 +2233,6 @@ void engine::build_sss(const u8* T) {
             }
         }
     }
-    // sss_kernel_ms: pass 1 through the re-run (the phase's kernels and its one host read)
-    LZ_HIP(hipEventRecord(sss_ev1, st));
-    sss_ev_pending = true;
 
     u32 hp[3];
     u32 total = 0;
@@ -2250,6 +2252,8 @@ void engine::build_sss(const u8* T) {
         pos_t* dS = S.get((u64)s + 1);
         k_sss_compact_scan<<<cdiv(nlanes, CC_SPB), CC_T, 0, st>>>(lo, lc, nlanes, dS);
         LZ_HIP(hipGetLastError());
+        LZ_HIP(hipEventRecord(sss_ev1, st));  // sss_kernel_ms: the two windows (engine.h sss_ms)
+        sss_ev_pending = true;
         return;
     }
     // exclusive scan of stripe counts -> offsets; total = |S|
@@ -2292,6 +2296,8 @@ void engine::build_sss(const u8* T) {
     pos_t* dS = S.get((u64)s + 1);
     k_sss_compact<<<capped_grid(nlanes * 64, 256), 256, 0, st>>>(lo, lc, off, lf, ovf_slot, ovf_out, nlanes, dS);
     LZ_HIP(hipGetLastError());
+    LZ_HIP(hipEventRecord(sss_ev1, st));  // (this path's second window also holds its reads)
+    sss_ev_pending = true;
 }
 
 // ---------------------------------------------------------------------------

@@ -67,15 +67,18 @@ struct engine {
     bool has_runs = false;
     // dominant kernel (SSS phase) duration: HIP events recorded around the phase's kernels, read
     // when asked (sss_ms), so the phase needs no synchronization of its own for them
+    // Two windows: pass 1 .. k_sss_runs, and after the phase's one host read the rest through the
+    // compaction (the read's round trip is not kernel time)
     mutable double sss_kernel_ms = 0;
-    hipEvent_t sss_ev0 = nullptr, sss_ev1 = nullptr;
+    hipEvent_t sss_ev0 = nullptr, sss_ev1 = nullptr, sss_evA = nullptr, sss_evB = nullptr;
     mutable bool sss_ev_pending = false;
     double sss_ms() const {
         if (sss_ev_pending) {
-            float ms = 0;
+            float a = 0, b = 0;
             LZ_HIP(hipEventSynchronize(sss_ev1));
-            LZ_HIP(hipEventElapsedTime(&ms, sss_ev0, sss_ev1));
-            sss_kernel_ms = ms;
+            LZ_HIP(hipEventElapsedTime(&a, sss_ev0, sss_evA));
+            LZ_HIP(hipEventElapsedTime(&b, sss_evB, sss_ev1));
+            sss_kernel_ms = (double)a + (double)b;
             sss_ev_pending = false;
         }
         return sss_kernel_ms;
