@@ -140,6 +140,29 @@ def cpu_baseline(lz, workload: str, sample_mib: int, phr_mode: int = 2, runs: in
             "greedy_parallel": par}
 
 
+CHR19_SAMPLE_N = (1 << 32) + (3 << 20) + 12345  # the instance tests/golden/stream_hashes.json pins (chr19_4gib_u64)
+
+
+def cpu_baseline_chr19(lz, n: int):
+    """configs[3]'s CPU leg: the oracle (pos_t = uint64_t) at p = the host's OpenMP threads on a chr19-style
+    instance of n bytes (default the 4 GiB + 3 MiB one whose p = 1 stream is SHA-pinned), one run."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle  # the CPU port (test/bench infrastructure only)
+
+    buf = lz.gen_genome_pos(n, 59 << 20, 0.001, 7, pad=4096)
+    p = oracle.num_threads()
+    print(f"cpu_baseline chr19 p={p}: n={n} ...", file=sys.stderr, flush=True)
+    z, sec, _, par = oracle.factorize_timed_p64(buf[:n], p, buf=buf)
+    print(f"cpu_baseline chr19 p={p}: {sec:.1f} s z={z}", file=sys.stderr, flush=True)
+    greedy = ("the reference's racy parallel greedy, greedy_parallel.cpp:31-285, selected as lz77_sss.hpp:467-474"
+              if par else "sequential greedy")
+    return {"value": round(n / sec / 1e6, 2), "unit": "MB/s", "cores": p, "kind": "port", "cpu_model": cpu_model(),
+            "runs": 1, "sample": f"chr19-style (59 MiB ACGT block, 0.1% mutations, position-hashed as the GPU's), "
+                                 f"n={n} ({n / GIB:.3f} GiB, pos_t=uint64), oracle factorize_approximate<greedy,lpf_opt> "
+                                 f"at p={p}: {sec:.1f} s, z={z} ({greedy})",
+            "greedy_parallel": par}
+
+
 def cpu_baseline_exact(lz, workload: str, sample_mib: int):
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # the CPU port (test/bench infrastructure only)
@@ -250,6 +273,7 @@ def main():
     dt, value = aggregate((t1 - t0) / args.steps, n, world, dist, device="cuda")
 
     phases = sess.phase_times()
+    pmem = sess.phase_mem()
     st = sess.stats()
     # PCIe-inclusive rate of one call (host text in, factors out), reported beside the HBM-resident value
     t_out0 = time.perf_counter()
@@ -304,6 +328,7 @@ def main():
                 "device_decode": {"mismatches": int(mism), "ms": round(dec_ms, 3), "jump_rounds": int(dec_rounds),
                                   "mbps": round(n / (dec_ms * 1e-3) / 1e6, 1)},
                 "huffman_container": {"bytes": hbytes, "ms_incl_d2h": round(t_h * 1e3, 3)},
+                "phase_mem_gib": {ph: {k: round(v / GIB, 3) for k, v in m.items()} for ph, m in pmem.items()},
             },
             "roofline": {
                 "kernel": "SSS phase kernels (DESIGN.md 4.1): k_sss_stream pass 1, k_sss_runs, [Q-anchor pass + re-run "
@@ -399,6 +424,10 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
     t1 = time.perf_counter()
     barrier()
     dt, _ = aggregate((t1 - t0) / args.steps, n, world, dist, device="cuda")  # max over ranks
+    mem = {}
+    for key in ("mem_prepare", "mem_greedy"):
+        for ph, m in (tm.pop(key, None) or {}).items():
+            mem[ph] = {k: round(v / GIB, 2) for k, v in m.items()}
     phases = {k: (round(v * 1e3, 3) if isinstance(v, float) else v) for k, v in tm.items()}
     z = int(F.shape[0])
     same = None
@@ -440,11 +469,20 @@ def main_shard(args, lz, torch, dist, world, rank, local_rank):
                                       f"LZ77SSS_SPECULATE=1), gathered emission",
                        "factors": z, "equals_one_gpu_stream": same, "verify_in_hbm": verified,
                        "sss_size": int(st[0]) if st else None, "lpf_phrases": int(st[2]) if st else None,
-                       "text_gen_s": round(t_gen, 3), "rank0_phase_ms": phases},
+                       "text_gen_s": round(t_gen, 3), "rank0_phase_ms": phases,
+                       "rank0_phase_mem_gib": {"note": "per phase: the session's device buffers when the phase was "
+                                                       "enqueued (held) and their peak in it (peak), text excluded; "
+                                                       "the GPU's free memory then (hbm_free)", **mem}},
             "roofline": None, "cpu_baseline": None,
         }
+        if chr19 and world == 1 and not args.no_cpu_baseline:
+            sess.close()  # (the host copy of the sample needs no device memory; free it anyway)
+            sess = None
+            out["cpu_baseline"] = cpu_baseline_chr19(lz, args.cpu_sample_mib << 20 if args.cpu_sample_mib > 0
+                                                     else CHR19_SAMPLE_N)
         print(json.dumps(out), flush=True)
-    sess.close()
+    if sess is not None:
+        sess.close()
     if dist is not None:
         dist.destroy_process_group()
 

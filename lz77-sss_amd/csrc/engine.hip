@@ -111,6 +111,10 @@ u64 engine::emit_skip_phrases() {
 
 void engine::prepare_phrases(int phr_mode, bool external_sss) {
     const bool dbg = debug_enabled();
+    const char* lean_env = std::getenv("LZ77SSS_LEAN");
+    const bool lean_mode = lean_env ? lean_env[0] != '0' : n >= (1ull << 33);
+    lean = lean_mode;
+    if (lean_mode) release_greedy_buffers();  // the last call's emitter buffers go before the phases grow
     phr_info.valid = false;
     if (std::getenv("LZ77SSS_LCE_DEBUG") && !lce_dbg) {
         LZ_HIP(hipMalloc(&lce_dbg, 8 * sizeof(unsigned long long)));
@@ -153,6 +157,57 @@ void engine::prepare_phrases(int phr_mode, bool external_sss) {
         build_lpf_lnf(phr_mode == LZ77SSS_LPF_LNF_OPT ? 1 : 0);
         trace("lpf_lnf");
     }
+    // large texts: the phases' own scratch goes back before the emitter allocates its base set
+    // (grow-only buffers otherwise keep every phase's peak: 2.5 GiB of 288 GiB were left free
+    // after a 50 GiB factorization in round 4).  Small texts keep them for the next call.
+    if (lean_mode) release_phase_scratch();
+}
+
+// the emitter's buffers of the last call (lean mode, before the phases of the next one grow)
+void engine::release_greedy_buffers() {
+    fact.release(); tmp_greedy.release(); chunk_buf.release(); chunk_buf2.release(); rem_buf.release();
+    add_keys32.release(); add_pos.release(); dirty_in.release(); dirty_out.release(); dirty_sorted.release();
+    tmp_greedy2.release(); tmp_greedy3.release(); add_keys.release(); add_keys2.release();
+    seg_in_buf.release(); seg_out_buf.release(); seg_ids.release(); irank.release(); ekeys.release();
+    evals.release(); ekeys2.release(); evals2.release(); occ_buf.release(); ist.release(); iend.release();
+    ipos_buf.release(); iposr_buf.release(); tail_ins_buf.release(); seg_offs.release();
+    g_sin.release(); g_sout.release(); g_valid.release(); g_cs.release(); g_tailc.release();
+    g_succ.release(); g_seg_at.release(); g_ids.release(); g_chain.release(); g_dist[0].release(); g_dist[1].release();
+    g_cbv.release(); g_bmI.release(); g_bmI2.release(); g_bmIb.release(); g_bmT.release();
+    g_tmp1.release(); g_tmp2.release(); g_tmp3.release(); g_tmp4.release(); g_tmp5.release(); g_tmp6.release();
+    g_tmp7.release(); g_tmp8.release(); g_ark.release(); g_ast.release(); g_aen.release(); g_offs.release();
+    g_predk.release(); g_wk.release(); g_ids2.release(); g_brev.release(); g_bsum.release(); g_bincl.release();
+    g_pbtmp.release(); g_pbcur.release(); g_pbm.release(); g_pwp.release(); g_pcnt.release(); g_sdk.release();
+    g_dstart.release(); g_pflag.release(); g_bstart.release(); g_abeg.release(); g_abeg2.release(); g_bmA.release();
+    g_x32.release(); g_xpos.release(); g_stash.release(); g_H.release(); g_Hs.release(); g_hsused.release();
+    g_hsave.release(); g_htrue.release(); g_specbad.release(); fact_acc.release(); g_cut.release();
+    g_xk.release(); g_xk2.release(); g_ls_h.release(); g_ls_g.release(); g_lng.release(); g_pbw.release();
+    num_fact = 0;  // (the factors went with fact; the callers set last_fact_mode when they write new ones)
+    negpow_key = {};  // the influence tables lived in tmp_greedy
+    negpow_dev = nullptr;
+    seg_at_clean = false;
+    seg_at_n = 0;
+}
+
+// the buffers the phases before the emitter use only while they run: the SSS pass's stripe
+// outputs, filter words, tile lists and run-record inputs, SA_S's rank levels and sort scratch,
+// LPF's sparse tables over SA, PSV/NSV, candidates and pointer-doubling levels, the shared scratch.  Kept: the text, S, SA / ISA / LCP and its RMQ
+// levels, the successor table, the run tables and block records (the LCE's view), the phrases.
+void engine::release_phase_scratch() {
+    lane_out.release(); lane_cnt.release(); lane_flag.release(); sss_ovf.release();
+    sss_hitw.release(); sss_tflag.release(); sss_tiles.release(); sss_sflag.release(); sss_slist.release();
+    sss_fcnt.release(); sss_tot.release(); q_info.release();
+    blk_p.release(); blk_fo.release(); blk_lo.release(); blk_mk.release(); blk_ser.release(); blk_ss.release();
+    run_scan_a.release(); run_scan_b.release(); S64.release(); s64 = 0;
+    for (auto& b : rank_lv) b.release();
+    nlev_rank = 0;
+    for (auto& b : sa_min) b.release();
+    for (auto& b : jump) b.release();  // (the emitter's segment linking grows its own levels again)
+    PSV.release(); NSV.release(); cand.release(); p_Em.release(); p_lst.release(); p_ph3.release();
+    key_len.release(); sa_tmp1.release(); sa_tmp2.release(); sa_tmp3.release();
+    tmp_bytes.release(); tmp_bytes2.release(); tmp_bytes3.release(); scan_tmp.release();
+    u64a.release(); u64b.release(); u32a.release(); u32b.release(); u32c.release(); u32d.release(); u32e.release();
+    stats_released_scratch++;
 }
 
 void engine::set_sss(const pos_t* S_any, u64 count, bool runs) {
@@ -258,6 +313,7 @@ static u64 block_run(engine& E, u32 rk_seed, int log2_override, u64* st) {
     b.seed = (st[3] & 2) != 0;
     b.end = (pos_t)st[4];
     E.timer.begin(E.st);
+    E.last_fact_mode = LZ77SSS_GREEDY;
     E.num_fact = E.n ? E.factorize_greedy(E.d_text, rk_seed, log2_override, &b) : 0;
     E.timer.mark("greedy");
     LZ_HIP(hipStreamSynchronize(E.st));
@@ -833,6 +889,20 @@ LZ77SSS_API int lz77sss_session_phase_times(lz77sss_session* s, double* ms, cons
         }
     });
     return rc ? rc : k;
+}
+
+// device memory per phase, in the order of lz77sss_session_phase_times
+LZ77SSS_API int lz77sss_session_phase_mem(lz77sss_session* s, uint64_t* held, uint64_t* peak, uint64_t* hbm_free,
+                                          int cap) {
+    if (!s) return LZ77SSS_EINVAL;
+    const lz::phase_timer& t = s->E64 ? s->E64->timer() : s->E.timer;
+    int k = 0;
+    for (size_t i = 1; i < t.mem.size() && k < cap; i++, k++) {
+        if (held) held[k] = t.mem[i].held;
+        if (peak) peak[k] = t.mem[i].peak;
+        if (hbm_free) hbm_free[k] = t.mem[i].hbm_free;
+    }
+    return k;
 }
 
 LZ77SSS_API int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap) {

@@ -410,6 +410,15 @@ void engine::build_lpf_opt(const u8* T) {
         sa_min_levels_build(st, SA.p, s, sa_min, M);
         k_psv_nsv<<<g, 256, 0, st>>>(SA.p, s, M, PSV.get(s), NSV.get(s));
     }
+    // (lean mode: each table goes as soon as it has been read, so the phase's peak is not the sum
+    // of all of them: the sparse table over SA here, the doubling levels and the expansion
+    // buffers after the expansion, PSV / NSV after the candidates)
+    auto drop = [&](auto&... b) {
+        if (!lean) return;
+        LZ_HIP(hipStreamSynchronize(st));  // (the launches that read them have run)
+        (b.release(), ...);
+    };
+    for (auto& b : sa_min) drop(b);
     // 2. candidates
     pos_t* cd = cand.get((u64)s * CREC);
     k_lpf_candidates<<<cdiv(2ull * s, 256), 256, 0, st>>>(view(T), SA.p, PSV.p, NSV.p, cd);
@@ -427,6 +436,8 @@ void engine::build_lpf_opt(const u8* T) {
     u32* mark = u32c.get(s);
     LZ_HIP(hipMemsetAsync(mark, 0, (size_t)s * 4, st));
     k_mark<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, s, mark);
+    drop(PSV, NSV, u32a, u32b);
+    for (auto& b : jump) drop(b);
     // running max_end before each processed index
     pos_t* Em = p_Em.get(s);
     k_masked_E<<<g, 256, 0, st>>>(cd, mark, s, Em);

@@ -268,6 +268,10 @@ struct engine {
     u64 factorize(int phr_mode, u32 rk_seed, int log2_override, bool log, int fact_mode = 1);
     void log_summary(std::chrono::steady_clock::time_point t_start) const;  // lz77_sss.hpp:345-353
     void prepare_phrases(int phr_mode, bool external_sss);  // the phases before the emitter
+    void release_phase_scratch();                           // (large texts, LZ77SSS_LEAN: engine.hip)
+    void release_greedy_buffers();
+    bool lean = false;  // this call releases scratch as it goes (prepare_phrases)
+    u64 stats_released_scratch = 0;
     u64 carried_entries(int log2_override);                 // slots of the gap index (carried table size)
     u64 emit_skip_phrases();  // fact_mode = skip_phrases (csrc/engine.hip)
     u64 ssszip_gapped();      // csrc/ssszip.hip

@@ -147,10 +147,14 @@ struct error : std::runtime_error {
 // device bytes held by dbufs in this process, and their peak (the "peak memory consumption"
 // line of a logged factorization, lz77_sss.hpp:345-353)
 inline std::atomic<uint64_t> g_dev_bytes{0}, g_dev_peak{0};
+// the peak since the last phase mark (phase_timer: device bytes held per phase)
+inline std::atomic<uint64_t> g_phase_peak{0};
 inline void dev_bytes_add(int64_t b) {
     const uint64_t v = g_dev_bytes.fetch_add((uint64_t)b) + (uint64_t)b;
     uint64_t pk = g_dev_peak.load();
     while (b > 0 && v > pk && !g_dev_peak.compare_exchange_weak(pk, v)) {}
+    uint64_t pp = g_phase_peak.load();
+    while (b > 0 && v > pp && !g_phase_peak.compare_exchange_weak(pp, v)) {}
 }
 
 // grow-only device buffer

@@ -8,9 +8,15 @@
 
 namespace lz {
 
+struct phase_mem {
+    uint64_t held = 0;      // device bytes of the session's buffers when the phase was enqueued
+    uint64_t peak = 0;      // their peak during the phase
+    uint64_t hbm_free = 0;  // free device memory then (hipMemGetInfo: the whole GPU)
+};
 struct phase_timer {
     hipStream_t st = nullptr;
     std::vector<std::pair<std::string, hipEvent_t>> marks;
+    std::vector<phase_mem> mem;  // per mark (the allocations are host-side: exact at enqueue time)
     std::vector<hipEvent_t> pool;  // events are reused across calls (created once)
     size_t used = 0;
     void begin(hipStream_t s) {
@@ -27,9 +33,17 @@ struct phase_timer {
         hipEvent_t e = pool[used++];
         LZ_HIP(hipEventRecord(e, st));
         marks.emplace_back(name, e);
+        phase_mem m;
+        m.held = g_dev_bytes.load();
+        m.peak = g_phase_peak.exchange(m.held);
+        if (m.peak < m.held) m.peak = m.held;
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess) m.hbm_free = fr;
+        mem.push_back(m);
     }
     void clear() {
         marks.clear();
+        mem.clear();
         used = 0;
     }
     // (name, ms since previous mark)

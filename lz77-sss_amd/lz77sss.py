@@ -89,6 +89,7 @@ _SYMBOLS = {
     "lz77sss_session_get_sa_s": (ctypes.c_int, [_P, _P, _P, _U64]),
     "lz77sss_session_get_lpf": (ctypes.c_int, [_P, _P, _U64, ctypes.POINTER(_U64)]),
     "lz77sss_session_phase_times": (ctypes.c_int, [_P, _P, _P, ctypes.c_int]),
+    "lz77sss_session_phase_mem": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int]),
     "lz77sss_session_stats": (ctypes.c_int, [_P, _P, ctypes.c_int]),
     "lz77sss_session_sss_kernel_time": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     "lz77sss_session_destroy": (None, [_P]),
@@ -383,6 +384,18 @@ class Session:
         if k < 0:
             _check(k)
         return {names[i].decode(): ms[i] for i in range(k)}
+
+    def phase_mem(self) -> dict[str, dict[str, int]]:
+        """Per phase of the last call (lz77sss_session_phase_mem): device bytes the session's buffers
+        held when the phase was enqueued, their peak during it, and the GPU's free memory then."""
+        names = list(self.phase_times())
+        h, p, f = (np.zeros(32, np.uint64) for _ in range(3))
+        k = load_library().lz77sss_session_phase_mem(self._h, h.ctypes.data_as(_P), p.ctypes.data_as(_P),
+                                                      f.ctypes.data_as(_P), 32)
+        if k < 0:
+            _check(k)
+        return {names[i]: {"held": int(h[i]), "peak": int(p[i]), "hbm_free": int(f[i])}
+                for i in range(min(k, len(names)))}
 
     def sss_kernel_time(self):
         ms, b = ctypes.c_double(), _U64()

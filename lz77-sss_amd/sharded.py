@@ -322,6 +322,8 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     # (2) replicated SA_S / LCP / LPF phrases
     tab_bytes = sess.prepare(external_sss=True, **params)
     t2 = time.perf_counter()
+    if timings is not None and hasattr(sess, "phase_mem"):
+        timings["mem_prepare"] = sess.phase_mem()
     # (3) the greedy chain.  With speculation (world > 1) every rank r > 0 first walks its block
     # concurrently from a speculated entry: a lead-in walk of the text before g_r from a table
     # of the gap positions before it gives the chain state at the first hand-over point >= g_r
@@ -471,6 +473,8 @@ def factorize_sharded_resident(sess, n: int, rank: int, world: int, device: int,
     t3 = time.perf_counter()
     if timings is not None:
         timings.update(spec_walk=t_spec, chain_wait=t3 - t_wait, spec_accepted=accepted)
+        if hasattr(sess, "phase_mem"):
+            timings["mem_greedy"] = sess.phase_mem()
     # (4) emission: the blocks' factors gathered in rank order
     blocks = keep + ([F_rest] if F_rest is not None else [])
     F = torch.cat(blocks) if blocks else torch.empty(0, dtype=torch.int64, device=dev)

@@ -46,6 +46,8 @@ def lib():
         L.oracle_factorize_timed_p.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64),
                                                ctypes.POINTER(ctypes.c_int)]
+        L.oracle_factorize_timed_p64.restype = ctypes.c_int64
+        L.oracle_factorize_timed_p64.argtypes = L.oracle_factorize_timed_p.argtypes
         L.oracle_factorize_p.restype = ctypes.c_int64
         L.oracle_factorize_p.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, _P, _U64,
                                          ctypes.POINTER(ctypes.c_int)]
@@ -199,6 +201,20 @@ def factorize_timed_p(T, threads: int, phr_mode: int = LPF_OPT, rk_seed: int = 4
     sec, h, par = ctypes.c_double(), _U64(), ctypes.c_int()
     z = lib().oracle_factorize_timed_p(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, threads, ctypes.byref(sec),
                                        ctypes.byref(h), ctypes.byref(par))
+    return int(z), sec.value, h.value, bool(par.value)
+
+
+def factorize_timed_p64(T, threads: int, phr_mode: int = LPF_OPT, rk_seed: int = 42, buf=None):
+    """factorize_timed_p with pos_t = uint64_t (texts past 4 GiB, configs[3]); `buf` may be a pre-padded
+    copy -> (z, seconds, hash, parallel_greedy_ran)."""
+    n = _u8(T).size
+    if buf is None:
+        buf = _padded(T)
+    sec, h, par = ctypes.c_double(), _U64(), ctypes.c_int()
+    z = lib().oracle_factorize_timed_p64(buf.ctypes.data_as(_P), n, phr_mode, rk_seed, threads, ctypes.byref(sec),
+                                         ctypes.byref(h), ctypes.byref(par))
+    if z < 0:
+        raise RuntimeError("oracle factorization failed")
     return int(z), sec.value, h.value, bool(par.value)
 
 

@@ -215,6 +215,35 @@ int64_t oracle_factorize_timed_p(uint8_t* T, uint64_t n, int phr_mode, uint32_t 
     return (int64_t)k;
 }
 
+// The same CPU baseline with pos_t = uint64_t (configs[3]'s chr19-style text past 4 GiB): every
+// OpenMP stage on p threads, LPF in p partitions, the greedy sequential unless lz77_sss.hpp:467-474
+// selects the reference's parallel one.  Timing only.
+int64_t oracle_factorize_timed_p64(uint8_t* T, uint64_t n, int phr_mode, uint32_t rk_seed, int p,
+                                   double* seconds, uint64_t* stream_hash, int* par) {
+    try {
+        const int prev = omp_get_max_threads();
+        omp_set_num_threads(std::max(1, p));
+        uint64_t k = 0, h = 1469598103934665603ull;
+        approx_stats st;
+        auto t0 = std::chrono::steady_clock::now();
+        factorize_approximate<u64>(T, (u64)n, phr_mode, rk_seed, [&](factor_t<u64> f) {
+            k++;
+            const uint64_t w[2] = {f.src, f.len};
+            const uint8_t* q = (const uint8_t*)w;
+            for (int i = 0; i < 16; i++) { h ^= q[i]; h *= 1099511628211ull; }
+        }, &st, 1, std::max(1, p));
+        auto t1 = std::chrono::steady_clock::now();
+        omp_set_num_threads(prev);
+        if (par) *par = st.greedy_parallel;
+        if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+        if (stream_hash) *stream_hash = h;
+        return (int64_t)k;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -1;
+    }
+}
+
 // SSS only.  Returns |S| (or -1 if cap too small); *has_runs set.
 int64_t oracle_sss(const uint8_t* T, uint64_t n, uint32_t* out, uint64_t cap, int* has_runs) {
     bool hr = false;

@@ -596,3 +596,24 @@ def test_block_run_records_vs_scan_form(session, orc, lz, kind, mib, monkeypatch
         _, F2 = run(session, T)
         assert np.array_equal(F2, F_ref), knob
         monkeypatch.delenv(knob)
+
+
+@pytest.mark.parametrize("kind,mib", [("rr", 32), ("genome", 16)])
+def test_lean_release_of_phase_scratch(session, orc, lz, kind, mib, monkeypatch):
+    """Large texts release the phases' own scratch before the emitter (engine::release_phase_scratch;
+    LZ77SSS_LEAN=1 forces it at any size): the stream equals the oracle's, repeated calls on the same
+    session (buffers grown again) stay equal, and the per-phase device memory shows the drop."""
+    n = mib << 20
+    T = lz.gen_genome(n, 2 << 20, 0.001, 23) if kind == "genome" else lz.gen_random_repetitive(n, n, 29, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    s, F0 = run(session, T)
+    held_full = s.phase_mem()["greedy"]["held"]
+    monkeypatch.setenv("LZ77SSS_LEAN", "1")
+    for _ in range(2):
+        z = s.factorize()
+        F = s.factors(z)
+        assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
+    pm = s.phase_mem()
+    assert set(pm) >= {"sss", "sa_s", "lcp_rmq", "lpf", "greedy"}
+    assert pm["greedy"]["held"] < held_full  # (the release follows the "lpf" mark)
+    assert all(m["peak"] >= m["held"] for m in pm.values())

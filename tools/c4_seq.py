@@ -32,13 +32,20 @@ with lz.Session(n, pos64=True) as s:
     tm = {}
     F1 = sharded.factorize_sharded_resident(s, n, 0, 1, 0, timings=tm)
     torch.cuda.synchronize()
+    pm_p, pm_g = tm.pop("mem_prepare", {}), tm.pop("mem_greedy", {})
     print(f"[c4_seq] sharded (world 1): z={F1.shape[0]} {time.time() - t:.2f} s {tm}", flush=True)
+    for ph, m in list(pm_p.items()) + list(pm_g.items()):
+        print(f"[c4_seq]   sharded phase {ph}: held {m['held'] / 2**30:.1f} GiB, peak {m['peak'] / 2**30:.1f} GiB, "
+              f"HBM free {m['hbm_free'] / 2**30:.1f} GiB", flush=True)
     mem("after sharded")
     bad1 = s.verify()
     print(f"[c4_seq] sharded stream verify: bad positions {bad1}", flush=True)
     t = time.time()
     z = s.factorize()
     print(f"[c4_seq] plain factorize: z={z} {time.time() - t:.2f} s phases={s.phase_times()}", flush=True)
+    for ph, m in s.phase_mem().items():
+        print(f"[c4_seq]   plain phase {ph}: held {m['held'] / 2**30:.1f} GiB, peak {m['peak'] / 2**30:.1f} GiB, "
+              f"HBM free {m['hbm_free'] / 2**30:.1f} GiB", flush=True)
     mem("after plain")
     F2 = torch.empty(max(z, 1) * 2, dtype=torch.int64, device="cuda:0")
     if z:
