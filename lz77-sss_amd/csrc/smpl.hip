@@ -2,7 +2,6 @@
 // configs[4] (lz77_sss<>::factorizer::exact_factorizer, include/lz77_sss/lz77_sss.hpp:558-709;
 // transform_to_exact/{common,naive,without_samples,with_samples}.cpp; the sample index of
 // data_structures/sample_index/{sample_index.hpp,construction.cpp,queries.cpp}; the
-// Rabin-Karp substring fingerprints of data_structures/rabin_karp_substring.hpp; the
 // decomposed static weighted square grid of decomposed_range.hpp and
 // static_weighted_range/static_weighted_square_grid.hpp).
 //
@@ -14,28 +13,33 @@
 //            lz77_sss.hpp:326); consecutive samples are at most delta apart
 //   PA, SA   sample ids by left context (at most delta + 1 characters, lce_l_64
 //            semantics) and by suffix (sample_index.hpp:317-353): a radix sort by a
-//            57-bit key of 7 characters, then a comparison merge sort whose comparator
-//            falls back to the text (leftward LCE / the SSS-backed LCE of lce_dev.h)
+//            64-bit key packing as many characters as the text's alphabet allows, then a
+//            comparison merge sort whose comparator falls back to the text (leftward LCE /
+//            the SSS-backed LCE of lce_dev.h)
 //   points   (x = PA rank, y = SA rank, weight = sample id); Pi, Psi (common.cpp:114-182)
 //   grid     per first character (decomposed_range.hpp:82-130) cells of >= SG_WIN ranks per side
 //            ranks, points sorted by (cell, weight) (static_weighted_square_grid.hpp:67-104)
-//   RKS      prefix fingerprints mod 2^31 - 1 every RKS_RATE characters
-//            (rabin_karp_substring.hpp:77-172); with_samples: hash tables of the PA / SA
-//            intervals of the sampled pattern lengths (construction.cpp:108-305)
+//   orders   per order (PA, SA): 16-byte context keys by rank, the adjacent LCEs
+//            (construction.cpp:118-129) with sparse-table minima, and sparse-table minima
+//            of the weights.  They replace with_samples' interval samples
+//            (construction.cpp:108-305): any interval of any pattern length comes from one
+//            insertion rank by binary lifting, and the nearest lighter samples in SA order
+//            bound every right extension
 //   phrases  one wave per phrase start i; lane j in [i, i + delta) finds the PA interval
 //            of T[i..j] (extend_left, queries.cpp:67-275) and the longest right extension
 //            lce_r whose SA interval holds a point lighter than the first sample >= j
-//            (exp/binary search over lce_r, intersect of common.cpp:258-358, decided for
-//            the whole wave one query at a time: the Pi / Psi scan below SCAN_T ranks,
-//            the grid above); the wave keeps the longest, the smallest j on ties
-//   chain    chunk walks: one wave per chunk of ~32 approximate phrases walks the greedy
-//            chain from the chunk start (a task per phrase, in a hash table) until it meets
-//            another walk's task or passes its chunk end; bridges walk on from every chunk
-//            exit until they meet a task; the chain from position 0 is then marked in order
-//            by pointer doubling + top-down expansion over the successor tasks
+//            (intersect, common.cpp:258-358: the lightest point of either interval on the
+//            lane, else the Pi / Psi scan below SCAN_T ranks or the grid, for the whole wave
+//            one query at a time); the wave keeps the longest, the smallest j on ties
+//   chain    chunk walks: one wave per chunk of SMPL_CHUNK approximate phrases walks the
+//            greedy chain from the chunk's first phrase start (a task per phrase, in a hash
+//            table) until it meets another walk's task or passes its chunk end; bridges walk on
+//            from every chunk exit until they meet a task; the chain from position 0 is then
+//            marked in order by pointer doubling + top-down expansion over the successor tasks
 //
 // Lengths are the canonical greedy LZ77 lengths (every leftmost occurrence of a phrase
-// contains a sample within its first delta characters: DESIGN.md 4.8); sources are the
+// contains a sample within its first delta characters: DESIGN.md 4.8); the three transform
+// modes give the same lengths (naive skips the approximate lower bound).  Sources are the
 // lighter points found, not the reference's visit order (whose PA / SA tie order comes from
 // an unstable parallel sort).
 #include "../../include/lz77sss.h"
@@ -60,11 +64,15 @@ constexpr u32 SMALL_T = 32;          // intersect queries scanned by their own l
 constexpr u32 SG_WIN = LZ_SG_WIN;    // smallest grid cell width in ranks (the reference: 16384 on a CPU core)
 constexpr u32 SG_GMAX = 512;         // cells per side at most: wider blocks get wider cells
 constexpr u32 SG_LV = 10;            // row sparse-table levels (2^9 = SG_GMAX / 1)
-constexpr u32 RKS_RATE = 16;         // lz77_sss.hpp:82 rks_sample_rate
-constexpr u32 RKS_P = 0x7FFFFFFFu;   // Mersenne prime 2^31 - 1 (rabin_karp_substring<31>)
-constexpr u32 RKS_B = 0x2545F491u % RKS_P;  // fixed base (the reference draws one per run)
 constexpr u32 SWPB = 4;              // waves per workgroup of the phrase kernels
-constexpr u32 NSMPL = 24;            // sampled pattern lengths per side at most (with_samples)
+constexpr u32 SMPL_CHUNK = 32;       // approximate phrases per chunk walk
+
+// ---------------------------------------------------------------------------
+// rank intervals of an order by its adjacent LCEs (mn[0][r] = LCE of ranks r - 1, r) and their
+// sparse-table minima (mn[l][i] = min adj[i .. i + 2^l)): an interval's ends by binary lifting
+// (iv_around); a linear scan took seconds on repetitive text, where one interval spans millions
+// of samples
+struct iv_levels { const u32* mn[MAX_LV]; u32 nlv; };
 
 // ---------------------------------------------------------------------------
 // device view
@@ -91,38 +99,19 @@ struct smpl_view {
     u32 za;
     int mode;                // LZ77SSS_TRANSF_*
     u32 small_t;             // intersect queries with a side of at most this many ranks run on their own lane
-    // with_samples: RKS + interval samples
-    const u32* rks;          // fps[k] = fp(T[0 .. k * RKS_RATE))
-    const u32* pw_lo;        // b^e, e <= sq
-    const u32* pw_hi;        // b^(sq * e)
-    u32 sq;
-    const u64* hkey;         // interval hash: (side << 63 | len idx << 40 | fp) + 1, 0 empty
-    const u64* hval;         // (b << 32 | e)
-    u64 hmask;
-    u32 nlen[2];             // sampled lengths per side (0 = LEFT, 1 = RIGHT), the first two are 1, 2
-    u32 slen[2][NSMPL];
+    iv_levels sM;            // SA order: adjacent sample-suffix LCEs (sM.mn[0][r] = LCE of ranks r - 1, r) and their
+                             // sparse-table minima; the SA interval of any right extension by binary lifting
+    iv_levels pM;            // PA order: the same over the left contexts (capped at delta)
+    const u32* PAR;          // PA / SA rank of a sample id
+    const u32* SAR;
+    const u32* wPA[MAX_LV];  // sparse-table minima of the weights (sample ids) by PA rank: min PA[x .. x + 2^k)
+    const u32* wSA[MAX_LV];  // the same by SA rank (level 0: PA / SA themselves)
+    u32 wlv;                 // levels
+    const ulonglong2* kSA;   // context keys by SA rank (key_right) and by PA rank (key_left)
+    const ulonglong2* kPA;
+    unsigned long long* cyc;  // debug (LZ77SSS_SMPL_PROF): per-section clock and query counters, or null
+    u32 prof_split;           // debug: phrases before / after this position counted apart
 };
-
-__device__ __forceinline__ u32 mod31(u64 v) {
-    v = (v >> 31) + (v & RKS_P);
-    v = (v >> 31) + (v & RKS_P);
-    return (u32)(v >= RKS_P ? v - RKS_P : v);
-}
-__device__ __forceinline__ u32 rks_pow(const smpl_view& V, u64 e) {
-    return mod31((u64)V.pw_hi[e / V.sq] * V.pw_lo[e % V.sq]);
-}
-// fingerprint of T[0 .. x) (rabin_karp_substring.hpp:223-230)
-__device__ __forceinline__ u32 rks_upto(const smpl_view& V, u64 x) {
-    const u64 blk = x / RKS_RATE;
-    u32 fp = V.rks[blk];
-    for (u64 p = blk * RKS_RATE; p < x; p++) fp = mod31((u64)fp * RKS_B + V.L.T[p]);
-    return fp;
-}
-// fingerprint of T[pos .. pos + len) (rabin_karp_substring.hpp:232-239)
-__device__ __forceinline__ u32 rks_sub(const smpl_view& V, u64 pos, u64 len) {
-    const u32 a = mod31((u64)rks_upto(V, pos) * rks_pow(V, len)), b = rks_upto(V, pos + len);
-    return b >= a ? b - a : RKS_P - (a - b);
-}
 
 // ---- comparisons of a pattern (text position pp) with sample contexts -----------------
 // left: T[pp - len + 1 .. pp] against the context ending at pm; the LCE starts from a
@@ -146,100 +135,6 @@ __device__ __forceinline__ bool less_right(const smpl_view& V, u32 pm, u32 pp, u
     if (pm == pp) return false;
     if ((u64)max(pm, pp) + l >= V.L.n) return pm > pp;
     return V.L.T[(u64)pm + l] < V.L.T[(u64)pp + l];
-}
-
-// extend (queries.cpp:67-275 without interval samples): the ranks [b, e] of the order
-// (left: PA, right: SA) whose sample contexts match the pattern at pp of length len,
-// searched inside [b, e] whose contexts share lb / le characters with the pattern at
-// the two ends.  Returns false if none matches.
-template <bool LEFT>
-__device__ bool extend_iv(const smpl_view& V, u32 pp, u32 len, u32& b, u32& e, u32& lb, u32& le) {
-    const u32* X = LEFT ? V.PA : V.SA;
-    auto lce_at = [&](u32 r, u32 offs) -> u32 {
-        const u32 pm = V.C[X[r]];
-        if (LEFT) return lce_left_offs(V, pm, pp, offs, len);
-        return min(lce_right_offs(V, pm, pp, offs), max(len, offs));
-    };
-    auto less_at = [&](u32 r, u32 l) -> bool {
-        const u32 pm = V.C[X[r]];
-        return LEFT ? less_left(V, pm, pp, l) : less_right(V, pm, pp, l);
-    };
-    if (lb < len) lb = lce_at(b, lb);
-    if (le < len) le = (e == b) ? lb : lce_at(e, le);
-    // first matching rank: l "less than the pattern", r "matching or greater"
-    u32 nb, nlb;
-    if (lb >= len) {
-        nb = b;
-        nlb = lb;
-    } else {
-        if (!less_at(b, lb)) return false;              // every rank greater
-        if (le < len && less_at(e, le)) return false;   // every rank less
-        u32 l = b, r = e, ll = lb, lr = le;
-        while (r - l > 1) {
-            const u32 m = l + (r - l) / 2;
-            const u32 lm = lce_at(m, min(ll, lr));
-            if (lm < len && less_at(m, lm)) {
-                l = m;
-                ll = lm;
-            } else {
-                r = m;
-                lr = lm;
-            }
-        }
-        if (lr < len) return false;
-        nb = r;
-        nlb = lr;
-    }
-    // last matching rank: l matching, r not
-    u32 ne, nle;
-    if (le >= len) {
-        ne = e;
-        nle = le;
-    } else {
-        u32 l = nb, r = e, ll = nlb, lr = le;
-        while (r - l > 1) {
-            const u32 m = l + (r - l) / 2;
-            const u32 lm = lce_at(m, min(ll, lr));
-            if (lm >= len) {
-                l = m;
-                ll = lm;
-            } else {
-                r = m;
-                lr = lm;
-            }
-        }
-        ne = l;
-        nle = ll;
-    }
-    b = nb;
-    e = ne;
-    lb = nlb;
-    le = nle;
-    return true;
-}
-
-// interval samples (sxa_interval, queries.cpp:31-65): the interval of the sampled length
-// index k at pp, by fingerprint, verified against the interval's first sample
-template <bool LEFT>
-__device__ bool sampled_iv(const smpl_view& V, u32 k, u32 pp, u32 fp, u32& b, u32& e) {
-    const u32 len = V.slen[LEFT ? 0 : 1][k];
-    const u64 key = (((u64)(LEFT ? 0 : 1) << 63) | ((u64)k << 40) | fp) + 1;
-    u64 h = (key * 0x9E3779B97F4A7C15ull) >> 20;
-    for (u32 probe = 0; probe <= V.hmask; probe++, h++) {
-        const u64 kk = V.hkey[h & V.hmask];
-        if (kk == 0) return false;
-        if (kk != key) continue;
-        const u64 v = V.hval[h & V.hmask];
-        const u32 rb = (u32)(v >> 32), re = (u32)v;
-        const u32 pm = V.C[(LEFT ? V.PA : V.SA)[rb]];
-        const u32 l = LEFT ? lce_left_offs(V, pm, pp, 0, len) : min(lce_right_offs(V, pm, pp, 0), len);
-        if (l >= len) {
-            b = rb;
-            e = re;
-            return true;
-        }
-    }
-    return false;
 }
 
 // ---- intersect (common.cpp:258-358), one query of the wave at a time -----------------
@@ -410,31 +305,313 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
     }
 }
 
-// first sample index x with C[x] >= j (adjust_xc, common.cpp:184-196)
-__device__ __forceinline__ u32 first_sample_geq(const smpl_view& V, u32 j) {
-    u32 lo = 0, hi = V.c;
-    while (lo < hi) {
-        const u32 m = (lo + hi) >> 1;
-        if (V.C[m] < j) lo = m + 1; else hi = m;
+// ---- context keys ------------------------------------------------------------------------
+// 15 context bytes and their count in 16: the right key of p holds T[p .. p + 15) (zero past n)
+// big-endian in its top 15 bytes and min(n - p, 15) in its low byte; the left key T[p], T[p - 1],
+// .., T[p - 14] (zero before 0) and min(p + 1, 15).  Two keys give the contexts' common prefix
+// below 15 and their order (key_lcp / key_less_at), so most steps of an insertion search are
+// one 16-byte load with no text access.
+__device__ __forceinline__ ulonglong2 key_right(const u8* T, u64 n, u64 p) {
+    ulonglong2 k;
+    if (p + 16 <= n) {
+        k.x = __builtin_bswap64(ldu64(T + p));
+        k.y = (__builtin_bswap64(ldu64(T + p + 8)) & ~0xFFull) | 15u;
+        return k;
     }
-    return lo;
+    u64 h = 0, l = 0;
+    for (u32 t = 0; t < 15; t++) {
+        const u64 b = p + t < n ? T[p + t] : 0u;
+        if (t < 8) h |= b << (56 - 8 * t);
+        else l |= b << (56 - 8 * (t - 8));
+    }
+    k.x = h;
+    k.y = l | (n - p < 15 ? n - p : 15ull);
+    return k;
+}
+__device__ __forceinline__ ulonglong2 key_left(const u8* T, u64 p) {
+    ulonglong2 k;
+    if (p >= 15) {
+        k.x = ldu64(T + p - 7);                        // T[p] in the top byte .. T[p - 7]
+        k.y = (ldu64(T + p - 15) & ~0xFFull) | 15u;    // T[p - 8] .. T[p - 14]
+        return k;
+    }
+    u64 h = 0, l = 0;
+    for (u32 t = 0; t < 15; t++) {
+        const u64 b = t <= p ? T[p - t] : 0u;
+        if (t < 8) h |= b << (56 - 8 * t);
+        else l |= b << (56 - 8 * (t - 8));
+    }
+    k.x = h;
+    k.y = l | (p + 1 < 15 ? p + 1 : 15ull);
+    return k;
+}
+// the common prefix of the two contexts, or 15 when both hold 15 equal bytes (the rest unknown)
+__device__ __forceinline__ u32 key_lcp(const ulonglong2& a, const ulonglong2& b) {
+    const u64 x = a.x ^ b.x, y = (a.y ^ b.y) & ~0xFFull;
+    const u32 d = x ? (u32)(__builtin_clzll(x) >> 3) : (y ? 8u + (u32)(__builtin_clzll(y) >> 3) : 15u);
+    return min(d, (u32)min(a.y & 0xFF, b.y & 0xFF));
+}
+__device__ __forceinline__ u32 key_byte(const ulonglong2& a, u32 e) {
+    return (u32)((e < 8 ? a.x >> (56 - 8 * e) : a.y >> (56 - 8 * (e - 8))) & 0xFF);
+}
+// context a sorts before b, given their common prefix e < 15: a shorter context is smaller
+__device__ __forceinline__ bool key_less_at(const ulonglong2& a, const ulonglong2& b, u32 e) {
+    const u32 ca = (u32)(a.y & 0xFF), cb = (u32)(b.y & 0xFF);
+    if (e < ca && e < cb) return key_byte(a, e) < key_byte(b, e);
+    return e == ca && e < cb;
+}
+__global__ void k_ctx_keys(const u8* __restrict__ T, u64 n, const u32* __restrict__ C, const u32* __restrict__ X, u32 c,
+                           int left, ulonglong2* __restrict__ out) {
+    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= c) return;
+    const u32 pm = C[X[r]];
+    out[r] = left ? key_left(T, pm) : key_right(T, n, pm);
 }
 
+// min of the adjacent LCEs over ranks [a, b] (a <= b)
+__device__ __forceinline__ u32 adj_min(const iv_levels& M, u32 a, u32 b) {
+    const u32 k = 31 - __builtin_clz(b - a + 1);
+    return min(M.mn[k][a], M.mn[k][b + 1 - (1u << k)]);
+}
+// LCE of the sample suffix at SA rank y with the suffix whose insertion rank is rs (LCEs hlo /
+// hhi with ranks rs - 1 / rs)
+__device__ __forceinline__ u32 lce_of_rank(const iv_levels& M, u32 y, u32 rs, u32 hlo, u32 hhi) {
+    if (y < rs) return y + 1 == rs ? hlo : min(hlo, adj_min(M, y + 1, rs - 1));
+    return y == rs ? hhi : min(hhi, adj_min(M, rs + 1, y));
+}
+// the lightest point (smallest sample id) with rank in [a, b] of an order (PA: V.wPA, SA: V.wSA)
+__device__ __forceinline__ u32 min_weight(const u32* const* Wl, u32 a, u32 b) {
+    const u32 k = 31 - __builtin_clz(b - a + 1);
+    return min(Wl[k][a], Wl[k][b + 1 - (1u << k)]);
+}
+
+
+// the rank interval [b, e] around insertion rank rs whose LCEs with the pattern are >= len
+// (hlo / hhi: the LCEs of ranks rs - 1 / rs): the four adjacent LCEs either side first (most
+// intervals of a phrase search are a few ranks wide), then binary lifting (iv_begin / iv_end),
+// both ends' loads issued together
+__device__ __forceinline__ void iv_around(const iv_levels& M, u32 c, u32 rs, u32 hlo, u32 hhi, u32 len, u32& b,
+                                          u32& e) {
+    const u32* a = M.mn[0];
+    const bool db = hlo >= len, de = hhi >= len;  // the interval reaches below / above rs
+    b = rs;
+    e = rs - 1;
+    u32 vb[4], ve[4];
+#pragma unroll
+    for (u32 t = 0; t < 4; t++) {
+        vb[t] = db && t + 1 <= rs - 1 ? a[rs - 1 - t] : 0u;  // adj[r] links ranks r - 1, r
+        ve[t] = de && rs + 1 + t <= c ? a[rs + 1 + t] : 0u;
+    }
+    bool lb = db, le = de;  // still extending
+    if (db) b = rs - 1;
+    if (de) e = rs;
+#pragma unroll
+    for (u32 t = 0; t < 4; t++) {
+        if (lb) {
+            if (vb[t] < len) lb = false;
+            else b = rs - 2 - t;
+        }
+        if (le) {
+            if (ve[t] < len) le = false;
+            else e = rs + 1 + t;
+        }
+    }
+    // b: adj[b + 1 .. rs - 1] >= len so far; e: adj[rs + 1 .. e] >= len so far
+    for (int l = (int)M.nlv - 1; l >= 0 && (lb || le); l--) {
+        const u32 w = 1u << l;
+        const bool tb = lb && b >= w, te = le && e + 1 + w <= c;
+        u32 x = 0, y = 0;
+        if (tb) x = M.mn[l][b + 1 - w];
+        if (te) y = M.mn[l][e + 1];
+        if (tb && x >= len) b -= w;
+        if (te && y >= len) e += w;
+    }
+}
+
+// what is known about position j, whatever phrase it serves: the insertion ranks of its left
+// context (PA, capped at delta) and of its suffix (SA) with the LCEs of their neighbours, the
+// first sample W at or after j, and the nearest SA ranks either side of rsR holding a sample
+// lighter than W (the earlier sample suffixes sharing the most with the suffix at j) with their
+// LCEs, uA >= uB
+struct pos_info {
+    u32 rsL, hloL, hhiL;
+    u32 rsR, hloR, hhiR;
+    u32 w;
+    u32 yA, uA, yB, uB;
+};
+__device__ __forceinline__ void key_step(const ulonglong2& km, const ulonglong2& kp, u32 D, bool left, u32& lm,
+                                         bool& ls, bool& text) {
+    const u32 el = key_lcp(km, kp);
+    text = false;
+    if (left && el >= D) {
+        lm = D;
+        ls = false;
+    } else if (el < 15) {
+        lm = el;
+        ls = key_less_at(km, kp, el);
+    } else {
+        text = true;  // 15 equal bytes: the text decides
+    }
+}
+// the three binary searches (PA / SA insertion ranks, W) advance together, one load each per
+// step; then the two nearest-lighter searches together
+__device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_info& P) {
+    const u8* T = V.L.T;
+    const ulonglong2 kpL = key_left(T, j), kpR = key_right(T, V.L.n, j);
+    u32 lL = cb, rL = ce, hlL = 1, hrL = 1;
+    u32 lR = cb, rR = ce, hlR = 1, hrR = 1;
+    u32 lW = 0, hW = V.c;
+    P.hloL = P.hhiL = P.hloR = P.hhiR = 0;
+    while (lL < rL || lR < rR || lW < hW) {
+        const bool aL = lL < rL, aR = lR < rR, aW = lW < hW;
+        const u32 mL = lL + (rL - lL) / 2, mR = lR + (rR - lR) / 2, mW = (lW + hW) >> 1;
+        ulonglong2 kL = make_ulonglong2(0, 0), kR = make_ulonglong2(0, 0);
+        u32 cW = 0;
+        if (aL) kL = V.kPA[mL];
+        if (aR) kR = V.kSA[mR];
+        if (aW) cW = V.C[mW];
+        if (aL) {
+            u32 lm;
+            bool ls, text;
+            key_step(kL, kpL, D, true, lm, ls, text);
+            if (text) {
+                const u32 pm = V.C[V.PA[mL]];
+                lm = lce_left_offs(V, pm, j, max(min(hlL, hrL), 15u), D);
+                ls = lm < D && less_left(V, pm, j, lm);
+            }
+            if (ls) {
+                lL = mL + 1;
+                hlL = P.hloL = lm;
+            } else {
+                rL = mL;
+                hrL = P.hhiL = lm;
+            }
+        }
+        if (aR) {
+            u32 lm;
+            bool ls, text;
+            key_step(kR, kpR, 0, false, lm, ls, text);
+            if (text) {
+                const u32 pm = V.C[V.SA[mR]];
+                lm = lce_right_offs(V, pm, j, max(min(hlR, hrR), 15u));
+                ls = less_right(V, pm, j, lm);
+            }
+            if (ls) {
+                lR = mR + 1;
+                hlR = P.hloR = lm;
+            } else {
+                rR = mR;
+                hrR = P.hhiR = lm;
+            }
+        }
+        if (aW) {
+            if (cW < j) lW = mW + 1;
+            else hW = mW;
+        }
+    }
+    P.rsL = lL;
+    P.rsR = lR;
+    P.w = lW;  // the first sample index x with C[x] >= j (adjust_xc, common.cpp:184-196)
+    // nearest lighter ranks: the four ranks either side first, then binary lifting over the
+    // weight minima, both sides at once
+    const u32 c = V.c, rs = lR, W = lW;
+    u32 vb[4], vf[4];
+#pragma unroll
+    for (u32 t = 0; t < 4; t++) {
+        vb[t] = t < rs ? V.SA[rs - 1 - t] : NONE;
+        vf[t] = rs + t < c ? V.SA[rs + t] : NONE;
+    }
+    u32 yb = NONE, yf = NONE;
+#pragma unroll
+    for (int t = 3; t >= 0; t--) {
+        if (vb[t] < W) yb = rs - 1 - t;
+        if (vf[t] < W) yf = rs + t;
+    }
+    const bool sb = yb == NONE && rs > 4, sf = yf == NONE && rs + 4 < c;
+    u32 pb = rs - 4, pf = rs + 4;  // ranks [pb, rs) / [rs, pf) hold no lighter sample
+    for (int l = (int)V.wlv - 1; l >= 0 && (sb || sf); l--) {
+        const u32 w = 1u << l;
+        const bool tb = sb && pb >= w, tf = sf && pf + w <= c;
+        u32 x = 0, y = 0;
+        if (tb) x = V.wSA[l][pb - w];
+        if (tf) y = V.wSA[l][pf];
+        if (tb && x >= W) pb -= w;
+        if (tf && y >= W) pf += w;
+    }
+    if (sb) yb = pb == 0 ? NONE : pb - 1;
+    if (sf) yf = pf >= c ? NONE : pf;
+    u32 ub = 0, uf = 0;
+    if (yb != NONE) ub = lce_of_rank(V.sM, yb, rs, P.hloR, P.hhiR);
+    if (yf != NONE) uf = lce_of_rank(V.sM, yf, rs, P.hloR, P.hhiR);
+    if (uf > ub) {
+        P.yA = yf;
+        P.uA = uf;
+        P.yB = yb;
+        P.uB = ub;
+    } else {
+        P.yA = yb;
+        P.uA = ub;
+        P.yB = yf;
+        P.uB = uf;
+    }
+}
+
+// the walk's memory of the positions of the last phrase's first window (base .. base + 63, a
+// lane each): the next phrase starts less than 64 positions later and takes them over by a lane
+// shift (pos_info depends on the position only)
+struct lane_cache {
+    u32 base;     // NONE: empty
+    u32 ak;       // the approximate phrase holding the last phrase start, or NONE
+    pos_info P;   // valid if has
+    bool has;
+};
+
 // ---- one exact phrase at i (transform_to_exact_{naive,without_samples,with_samples}) --
-// executed by a whole wave; returns (src, len) in every lane
-__device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u32 lane) {
+// executed by a whole wave; returns (src, len) in every lane.
+// Lane j in [i, i + delta) (64 at a time) looks for the longest phrase T[i .. j + x) whose
+// occurrence contains a sample at j: the PA interval of T[i .. j] (the sample contexts that end
+// with it; extend<LEFT>, queries.cpp:67-275) and, for right extensions x, the SA interval of
+// T[j .. j + x) (extend<RIGHT>; with_samples narrows both by interval samples,
+// with_samples.cpp:35-122), then a point in both lighter than the first sample >= j
+// (intersect, common.cpp:258-358).  Both intervals come from the insertion ranks of j's
+// context / suffix (pos_probe, once per position of a walk) and the adjacent LCEs around them
+// (binary lifting over V.pM / V.sM): the same rank sets the reference's LCE binary searches
+// find, so every decision is the same.  x is bounded by the nearest lighter samples in SA order
+// (no earlier sample shares more with the suffix at j), starts from the best witness among
+// them and the lightest point of the PA interval, then runs the largest candidate, an
+// exponential search and bisection; the predicate is monotone in x, so the result is the
+// reference's whatever the probe order.
+__device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u32 lane, lane_cache& K) {
     const u32 n = (u32)V.L.n;
     const u32 e = n;  // one section: p = 1
     const u8* T = V.L.T;
+    u64 cy[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // clocks: left, right insertion, intersect; probes, coop queries,
+                                           // queries, phrases; clocks: probe intervals
+    u64 ct = V.cyc ? clock64() : 0;
+    auto tick = [&](int k) {
+        if (V.cyc) {
+            const u64 t = clock64();
+            cy[k] += t - ct;
+            ct = t;
+        }
+    };
     // lower bound: the approximate phrase covering i, cut at i (without_samples.cpp:64-77)
     f_src = T[i];
     f_len = 0;
     if (V.mode != LZ77SSS_TRANSF_NAIVE) {
-        u32 lo = 0, hi = V.za;  // largest k with afst[k] <= i
+        // largest k with afst[k] <= i: the walk's last one and the 63 after it first
+        u32 lo = 0, hi = V.za;
+        if (K.ak != NONE) {
+            const u32 k = K.ak + 1 + lane;
+            const u64 bal = __ballot(k < V.za && V.afst[k] <= i);
+            lo = K.ak + (u32)__popcll(bal);  // afst increases: the lanes below i are a prefix
+            if (bal != ~0ull) hi = lo + 1;
+        }
         while (hi - lo > 1) {
             const u32 m = (lo + hi) >> 1;
             if (V.afst[m] <= i) lo = m; else hi = m;
         }
+        K.ak = lo;
         const u32 alen = V.afact[2 * lo + 1];
         if (alen != 0) {
             const u32 nxt = V.afst[lo + 1];
@@ -444,86 +621,150 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         }
     }
     const u32 max_j = min<u32>(e, i + V.delta);
+    const u32 D = V.delta;  // left contexts: pattern lengths j - i + 1 <= delta
+    {
+        // the cached window shifted to start at i
+        const u32 d = (K.base != NONE && i >= K.base && i - K.base < 64) ? i - K.base : 64u;
+        const u32 sl = (lane + d) & 63;
+        const bool h = __shfl((int)K.has, sl, 64) != 0;
+        K.P.rsL = __shfl(K.P.rsL, sl, 64);
+        K.P.hloL = __shfl(K.P.hloL, sl, 64);
+        K.P.hhiL = __shfl(K.P.hhiL, sl, 64);
+        K.P.rsR = __shfl(K.P.rsR, sl, 64);
+        K.P.hloR = __shfl(K.P.hloR, sl, 64);
+        K.P.hhiR = __shfl(K.P.hhiR, sl, 64);
+        K.P.w = __shfl(K.P.w, sl, 64);
+        K.P.yA = __shfl(K.P.yA, sl, 64);
+        K.P.uA = __shfl(K.P.uA, sl, 64);
+        K.P.yB = __shfl(K.P.yB, sl, 64);
+        K.P.uB = __shfl(K.P.uB, sl, 64);
+        K.has = lane + d < 64 && h;
+        K.base = i;
+    }
     for (u32 j0 = i; j0 < max_j; j0 += 64) {
         const u32 j = j0 + lane;
         const bool act = j < max_j;
+        const bool first = j0 == i;  // the window the cache holds
         const u32 lce_l = j - i + 1;
         const u32 ch = act ? T[j] : 0u;
-        // PA interval of T[i..j] (extend_left; with_samples: the sampled lengths by fingerprint)
-        u32 xb = V.CS[ch], xe = V.CS[ch + 1] - 1, xlb = 1, xle = 1;
-        bool okl = act && V.CS[ch + 1] > V.CS[ch];
-        if (okl && lce_l > 1) {
-            if (V.mode == LZ77SSS_TRANSF_WITH_SAMPLES) {
-                // the longest sampled length <= lce_l narrows the search (extend<LEFT> with samples)
-                u32 k = 0;
-                while (k + 1 < V.nlen[0] && V.slen[0][k + 1] <= lce_l) k++;
-                if (k >= 2) {
-                    u32 b2, e2;
-                    const u32 L0 = V.slen[0][k];
-                    if (sampled_iv<true>(V, k, j, rks_sub(V, j + 1 - L0, L0), b2, e2)) {
-                        xb = b2;
-                        xe = e2;
-                        xlb = xle = L0;
-                    } else {
-                        okl = false;
-                    }
+        const u32 cb = V.CS[ch], ce = V.CS[ch + 1];
+        pos_info P{};
+        const bool have = act && ce > cb;
+        if (have) {
+            if (first && K.has) {
+                P = K.P;
+            } else {
+                pos_probe(V, j, D, cb, ce, P);
+                if (first) {
+                    K.P = P;
+                    K.has = true;
                 }
             }
-            if (okl) okl = extend_iv<true>(V, j, lce_l, xb, xe, xlb, xle);
         }
-        // right extensions: max lce_r in [lce_r_min, e - j] with a lighter point (exp search,
-        // then binary search; common.cpp intersect decides each probe)
+        // PA interval of T[i..j]: the ranks around j's insertion rank whose contexts share lce_l
+        u32 xb = 0, xe = 0;
+        const bool okl = have && (P.hloL >= lce_l || P.hhiL >= lce_l);
+        if (okl) iv_around(V.pM, V.c, P.rsL, P.hloL, P.hhiL, lce_l, xb, xe);
+        tick(0);
+        // right extensions: max lce_r in [lce_r_min, e - j] with a lighter point
         const u32 lrmin = (f_len < j - i) ? 0u : (i + f_len - j);
         const u32 lrmax = e - j;
         u32 lo = lrmin, hi = lrmax + 1, step = 1;
         bool bin = false;
         bool run = okl && lo < lrmax;
-        u32 yb = V.CS[ch], ye = V.CS[ch + 1] - 1, ylb = 1, yle = 1;
-        const u32 W = act ? first_sample_geq(V, j) : 0u;
+        const u32 rs = P.rsR, h_lo = P.hloR, h_hi = P.hhiR, W = P.w, yA = P.yA, uA = P.uA, yB = P.yB, uB = P.uB;
+        // no sample before j shares more than uA characters with the suffix at j
+        hi = min(hi, uA + 1);
+        if (hi - lo <= 1) run = false;
         u32 best_y = 0;
-        bool got = false;
-        while (__ballot(run)) {
-            u32 x = 0, nb = yb, ne = ye, nlb = ylb, nle = yle;
-            bool cand = false;
-            if (run) {
-                x = bin ? lo + (hi - lo) / 2 : min(lo + step, hi - 1);
-                cand = true;
-                if (V.mode == LZ77SSS_TRANSF_WITH_SAMPLES) {
-                    // extend_right_with_samples (with_samples.cpp:35-122): the longest sampled
-                    // length <= x beyond the known match narrows the interval by fingerprint
-                    u32 k = 0;
-                    while (k + 1 < V.nlen[1] && V.slen[1][k + 1] <= x) k++;
-                    const u32 L1 = V.slen[1][k];
-                    if (k >= 2 && L1 > min(nlb, nle)) {
-                        u32 b2, e2;
-                        if (sampled_iv<false>(V, k, j, rks_sub(V, j, L1), b2, e2)) {
-                            nb = b2;
-                            ne = e2;
-                            nlb = nle = L1;
-                        } else {
-                            cand = false;
-                        }
+        bool got = false, top = true;
+        if (run) {
+            // witnesses: the two nearest lighter ranks, when their contexts end with T[i..j]; else
+            // the lightest point of the PA interval (none lighter than W ends the lane's search)
+            const u32 xA = V.PAR[V.SA[yA]];
+            if (xA >= xb && xA <= xe) {
+                lo = uA;  // the largest possible
+                best_y = yA;
+                got = true;
+                run = false;
+            } else {
+                if (yB != NONE && uB > lo) {
+                    const u32 xB = V.PAR[V.SA[yB]];
+                    if (xB >= xb && xB <= xe) {
+                        lo = uB;
+                        best_y = yB;
+                        got = true;
                     }
                 }
-                if (cand) cand = extend_iv<false>(V, j, x, nb, ne, nlb, nle);
+                const u32 s0 = min_weight(V.wPA, xb, xe);
+                if (s0 >= W) {
+                    run = false;
+                    got = false;
+                } else {
+                    const u32 y0 = V.SAR[s0], l0 = lce_of_rank(V.sM, y0, rs, h_lo, h_hi);
+                    if (l0 > lo) {
+                        lo = l0;
+                        best_y = y0;
+                        got = true;
+                    }
+                }
+                if (hi - lo <= 1) run = false;
             }
-            bool f;
-            u32 py;
-            wave_intersect(V, cand, xb, xe, nb, ne, W, ch, f, py, lane);
+        }
+        tick(1);
+        while (__ballot(run)) {
+            u32 x = 0, nb = 0, ne = 0;
+            bool cand = false;
+            if (run) {
+                // the largest possible x first (its intervals are the narrowest, and it is often
+                // the answer), then the exponential search up from lo and bisection: the predicate
+                // is monotone in x, so the answer is the reference's
+                x = bin ? lo + (hi - lo) / 2 : top ? hi - 1 : min(lo + step, hi - 1);
+                cand = h_lo >= x || h_hi >= x;
+                if (cand) iv_around(V.sM, V.c, rs, h_lo, h_hi, x, nb, ne);
+            }
+            tick(7);
+            if (V.cyc) {
+                cy[3]++;
+                cy[4] += __popcll(__ballot(cand && min(xe - xb, ne - nb) + 1 > V.small_t));
+                cy[5] += __popcll(__ballot(cand));
+            }
+            // the lightest point of the SA interval decides most probes on the lane itself
+            bool f = false, open = false;
+            u32 py = 0;
+            if (cand) {
+                const u32 s1 = min_weight(V.wSA, nb, ne);
+                if (s1 < W) {
+                    const u32 x1 = V.PAR[s1];
+                    if (x1 >= xb && x1 <= xe) {
+                        f = true;
+                        py = V.SAR[s1];
+                    } else {
+                        open = true;
+                    }
+                }
+            }
+            {
+                bool f2;
+                u32 py2;
+                wave_intersect(V, open, xb, xe, nb, ne, W, ch, f2, py2, lane);
+                if (open) {
+                    f = f2;
+                    py = py2;
+                }
+            }
+            tick(2);
             if (run) {
                 if (cand && f) {
-                    lo = x;
-                    yb = nb;
-                    ye = ne;
-                    ylb = nlb;
-                    yle = nle;
+                    lo = lce_of_rank(V.sM, py, rs, h_lo, h_hi);  // >= x: the point is a witness up to it
                     best_y = py;
                     got = true;
-                    if (!bin) step *= 2;
+                    if (!bin && !top) step *= 2;
                 } else {
                     hi = x;
-                    bin = true;
+                    if (!top) bin = true;
                 }
+                top = false;
                 if (hi - lo <= 1) run = false;
             }
             // a lane whose longest possible phrase (lce_l + hi - 2) cannot beat the wave's
@@ -560,6 +801,11 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         }
     }
     if (f_len > e - i) f_len = e - i;
+    if (V.cyc && lane == 0) {
+        cy[6] = 1;
+        const u32 bank = i < V.prof_split ? 0 : 8;
+        for (int k = 0; k < 8; k++) atomicAdd(&V.cyc[bank + k], (unsigned long long)cy[k]);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -591,17 +837,41 @@ __global__ void k_smpl_fill(const u32* __restrict__ F, const u32* __restrict__ a
     C[o] = prev + g;
 }
 // 57-bit keys: 7 characters (c + 1, 0 past the text) going left from C (PA) or right (SA)
+// the characters the text uses (one flag per byte value)
+__global__ void k_text_alpha(const u8* __restrict__ T, u64 n, u32* __restrict__ used) {
+    __shared__ u32 f[256];
+    f[threadIdx.x] = 0;
+    __syncthreads();
+    const u64 nw = n / 16;
+    for (u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x; k < nw; k += (u64)gridDim.x * blockDim.x) {
+        const uint4 v = ((const uint4*)T)[k];
+        const u32 w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) f[(w[q] >> (8 * b)) & 0xFF] = 1;
+    }
+    for (u64 k = nw * 16 + (u64)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (u64)gridDim.x * blockDim.x)
+        f[T[k]] = 1;
+    __syncthreads();
+    if (f[threadIdx.x]) used[threadIdx.x] = 1;
+}
+// sort keys of the sample contexts: kc characters of `bits` bits each (the character's rank in
+// the text's alphabet), the first one in the top bits; past the text's end (right) or start
+// (left) the code 0, the smallest character's, so that a shorter context never gets a larger key
+// than a context it is a prefix of (key order implies context order; equal keys go to the
+// comparator).  Left contexts take at most cap + 1 characters, all the comparator looks at.
 __global__ void k_smpl_keys(const u8* __restrict__ T, u64 n, const u32* __restrict__ C, u32 c, int left,
-                            u64* __restrict__ key, u32* __restrict__ id) {
+                            const u8* __restrict__ code, u32 bits, u32 kc, u64* __restrict__ key, u32* __restrict__ id) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= c) return;
     const u64 p = C[k];
     u64 v = 0;
-    for (int t = 0; t < 7; t++) {
+    for (u32 t = 0; t < kc; t++) {
         u64 d;
-        if (left) d = p >= (u64)t ? (u64)T[p - t] + 1 : 0;
-        else d = p + t < n ? (u64)T[p + t] + 1 : 0;
-        v = v * 257 + d;
+        if (left) d = p >= (u64)t ? code[T[p - t]] : 0u;
+        else d = p + t < n ? code[T[p + t]] : 0u;
+        v = (v << bits) | d;
     }
     key[k] = v;
     id[k] = (u32)k;
@@ -702,28 +972,6 @@ __global__ void k_cell_rowmin(const u32* __restrict__ prev, const u32* __restric
     out[t] = x + half < gw ? min(prev[t], prev[t + half]) : prev[t];
 }
 
-// RKS block fingerprints: (fp(T[16k .. 16k + 16)), b^len) per block, then an inclusive scan
-// with the concatenation (fa, pa) . (fb, pb) = (fa pb + fb, pa pb) (rabin_karp_substring.hpp:205-208)
-__global__ void k_rks_blocks(const u8* __restrict__ T, u64 n, u64 nb, u64* __restrict__ out) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nb) return;
-    u32 fp = 0, pw = 1;
-    for (u64 p = k * RKS_RATE; p < (k + 1) * RKS_RATE && p < n; p++) {
-        fp = mod31((u64)fp * RKS_B + T[p]);
-        pw = mod31((u64)pw * RKS_B);
-    }
-    out[k] = ((u64)pw << 32) | fp;
-}
-struct rks_cat {
-    __device__ u64 operator()(const u64& a, const u64& b) const {
-        const u32 fa = (u32)a, pa = (u32)(a >> 32), fb = (u32)b, pb = (u32)(b >> 32);
-        return ((u64)mod31((u64)pa * pb) << 32) | mod31((u64)fa * pb + fb);
-    }
-};
-__global__ void k_rks_shift(const u64* __restrict__ incl, u64 nb, u32* __restrict__ fps) {
-    const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k <= nb) fps[k] = k == 0 ? 0u : (u32)incl[k - 1];
-}
 // adjacent context LCEs of an order (LCP_S / LCS_S of construction.cpp:118-129)
 __global__ void k_adj_lce(lce_view L, const u32* __restrict__ C, const u32* __restrict__ X, u32 c, u32 cap, int left,
                           u32* __restrict__ out) {
@@ -733,43 +981,10 @@ __global__ void k_adj_lce(lce_view L, const u32* __restrict__ C, const u32* __re
     const u32 a = C[X[r - 1]], b = C[X[r]];
     out[r] = left ? (u32)dev_lce_left(L.T, L.R, a, b, cap) : (u32)min<u64>(dev_lce(L, a, b), 0xFFFFFFFFull);
 }
-// interval samples of one sampled length (construction.cpp:265-305): every maximal rank
-// interval whose adjacent LCEs are >= len, keyed by the fingerprint of its context
-// the interval's end: the last e with adj[r + 1 .. e] >= len, by binary lifting over the
-// sparse-table minima of adj (levels mn[l][i] = min adj[i .. i + 2^l)); a linear scan took
-// seconds on repetitive text, where one interval spans millions of samples
-struct iv_levels { const u32* mn[MAX_LV]; u32 nlv; };
-__device__ __forceinline__ u32 iv_end(const iv_levels& M, const u32* adj, u32 c, u32 r, u32 len) {
-    u64 pos = (u64)r + 1;  // adj[r + 1 .. pos) are all >= len
-    for (int l = (int)M.nlv - 1; l >= 0; l--) {
-        const u64 w = 1ull << l;
-        if (pos + w <= c && M.mn[l][pos] >= len) pos += w;
-    }
-    return (u32)(pos - 1);
-}
+// sparse-table level of the adjacent LCEs: out[k] = min(prev[k], prev[k + half])
 __global__ void k_iv_min_level(const u32* __restrict__ prev, u64 cnt, u64 half, u32* __restrict__ out) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < cnt) out[k] = min(prev[k], prev[k + half]);
-}
-__global__ void k_iv_insert(const smpl_view V, const u32* __restrict__ X, const u32* __restrict__ adj, u32 c,
-                            int left, u32 k, u32 len, u64* __restrict__ hkey, u64* __restrict__ hval, u64 hmask,
-                            iv_levels M) {
-    const u64 r = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= c) return;
-    if (r > 0 && adj[r] >= len) return;  // not an interval start
-    const u32 e = iv_end(M, adj, c, (u32)r, len);
-    const u32 pm = V.C[X[r]];
-    if (left ? pm + 1 < len : (u64)pm + len > V.L.n) return;  // context shorter than len
-    const u32 fp = left ? rks_sub(V, pm + 1 - len, len) : rks_sub(V, pm, len);
-    const u64 key = (((u64)(left ? 0 : 1) << 63) | ((u64)k << 40) | fp) + 1;
-    u64 h = (key * 0x9E3779B97F4A7C15ull) >> 20;
-    for (;; h++) {
-        const u64 old = atomicCAS((unsigned long long*)&hkey[h & hmask], 0ull, (unsigned long long)key);
-        if (old == 0) {
-            hval[h & hmask] = ((u64)r << 32) | e;
-            return;
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -817,13 +1032,15 @@ __device__ u32 task_find(const task_tab& Tt, u32 p) {
     return NONE;
 }
 // ---- the chain by chunk walks + bridges (replaces one hop per launch) ----------------
-// Chunk k's wave walks the greedy chain from k * CS, inserting a task per phrase, until it
+// Chunk k's wave walks the greedy chain from its first approximate phrase, inserting a task per phrase, until it
 // meets a task another walk inserted (merged) or passes its chunk end (its exit is kept).
 // A bridge walks from every exit until it meets a task.  Every task's successor position
 // then holds a task (a walk inserts it, finds it, or hands it to a bridge), so the chain
 // from position 0 lies in the table; it is marked by pointer doubling.
-__device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p, u64 stop, u32 lane, u32* __restrict__ full) {
+__device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p, u64 stop, u32 lane, u32* __restrict__ full,
+                                         u32& nph) {
     const u64 n = V.L.n;
+    lane_cache K{NONE, NONE, pos_info{}, false};
     for (;;) {
         if (p >= n) return NONE;
         if (p >= stop) return (u32)p;
@@ -835,7 +1052,8 @@ __device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p
         t = (u32)__shfl((int)t, 0);
         if (t == NONE) return NONE;  // merged (or out of room: reported)
         u32 src, len;
-        wave_phrase(V, (u32)p, src, len, lane);
+        wave_phrase(V, (u32)p, src, len, lane, K);
+        nph++;
         if (lane == 0) {
             Tt.src[t] = src;
             Tt.len[t] = len;
@@ -843,20 +1061,40 @@ __device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p
         p += max(1u, len);
     }
 }
-__global__ __launch_bounds__(64 * SWPB) void k_chunk_walks(const smpl_view V, task_tab Tt, u64 CS, u32 nch,
-                                                          u32* __restrict__ ex, u32* __restrict__ full) {
+// Chunk k starts at approximate phrase k * cp (so every walk has about cp phrases to parse,
+// whatever the text's local compressibility) and ends at phrase (k + 1) * cp.  prof (debug,
+// LZ77SSS_SMPL_PROF): per walk, its clock ticks and phrase count.
+__global__ __launch_bounds__(64 * SWPB, 4) void k_chunk_walks(const smpl_view V, task_tab Tt, u32 cp, u32 nch,
+                                                          u32* __restrict__ ex, u32* __restrict__ full,
+                                                          u32* __restrict__ prof) {
     const u32 lane = threadIdx.x & 63;
     const u32 k = blockIdx.x * SWPB + (threadIdx.x >> 6);
     if (k >= nch) return;
-    const u32 e = wave_walk(V, Tt, (u64)k * CS, min<u64>(V.L.n, (u64)(k + 1) * CS), lane, full);
-    if (lane == 0) ex[k] = e;
+    const u64 a = (u64)k * cp, b = min<u64>(V.za, a + cp);
+    const u64 t0 = prof ? wall_clock64() : 0;
+    u32 nph = 0;
+    const u32 e = wave_walk(V, Tt, V.afst[a], V.afst[b], lane, full, nph);
+    if (lane == 0) {
+        ex[k] = e;
+        if (prof) {
+            prof[2 * k] = (u32)(wall_clock64() - t0);
+            prof[2 * k + 1] = nph;
+        }
+    }
 }
-__global__ __launch_bounds__(64 * SWPB) void k_bridge_walks(const smpl_view V, task_tab Tt, u32 nch,
-                                                           const u32* __restrict__ ex, u32* __restrict__ full) {
+__global__ __launch_bounds__(64 * SWPB, 4) void k_bridge_walks(const smpl_view V, task_tab Tt, u32 nch,
+                                                           const u32* __restrict__ ex, u32* __restrict__ full,
+                                                           u32* __restrict__ prof) {
     const u32 lane = threadIdx.x & 63;
     const u32 k = blockIdx.x * SWPB + (threadIdx.x >> 6);
     if (k >= nch || ex[k] == NONE) return;
-    wave_walk(V, Tt, ex[k], ~0ull, lane, full);
+    const u64 t0 = prof ? wall_clock64() : 0;
+    u32 nph = 0;
+    wave_walk(V, Tt, ex[k], ~0ull, lane, full, nph);
+    if (lane == 0 && prof) {
+        prof[2 * k] = (u32)(wall_clock64() - t0);
+        prof[2 * k + 1] = nph;
+    }
 }
 // successor task of every task (ntask = the end); a missing successor is reported
 __global__ void k_task_next(task_tab Tt, u32 ntask, u32 n, u32* __restrict__ nxt, u32* __restrict__ bad) {
@@ -901,15 +1139,6 @@ __global__ void k_path_emit(task_tab Tt, const u32* __restrict__ C, u32 z, u32* 
 
 // ---------------------------------------------------------------------------
 // host side
-static u32 pow31_host(u64 b, u64 e) {
-    u64 r = 1 % RKS_P, x = b % RKS_P;
-    while (e) {
-        if (e & 1) r = r * x % RKS_P;
-        x = x * x % RKS_P;
-        e >>= 1;
-    }
-    return (u32)r;
-}
 
 u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int log2_override, bool log) {
     LZ_HIP(hipSetDevice(device));
@@ -957,7 +1186,27 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     u32* C = e_C.p;
     timer.mark("smpl_set");
     const lce_view LV = view(d_text);
-    // PA / SA (sample_index.hpp:317-353): radix sort by 7 characters, merge sort by the text
+    // PA / SA (sample_index.hpp:317-353): radix sort by as many characters as 64 bits hold in
+    // the text's alphabet (32 of a 4-letter text), merge sort by the text
+    u32 bits = 1, kc_max = 64;
+    u8* code = (u8*)e_alpha.get(64 + 256);
+    {
+        u32* used = (u32*)code + 64;
+        LZ_HIP(hipMemsetAsync(used, 0, 1024, st));
+        k_text_alpha<<<std::min<u64>(std::max<u64>(1, cdiv(n / 16, 256)), 2048), 256, 0, st>>>(d_text, n, used);
+        u32 hu[256];
+        LZ_HIP(hipMemcpyAsync(hu, used, 1024, hipMemcpyDeviceToHost, st));
+        LZ_HIP(hipStreamSynchronize(st));
+        u8 hc[256];
+        u32 sigma = 0;
+        for (int ch = 0; ch < 256; ch++) {
+            hc[ch] = (u8)sigma;
+            sigma += hu[ch] ? 1u : 0u;
+        }
+        while ((1u << bits) < sigma) bits++;
+        kc_max = 64 / bits;
+        LZ_HIP(hipMemcpyAsync(code, hc, 256, hipMemcpyHostToDevice, st));
+    }
     u32* PA = e_PA.get(c);
     u32* SA = e_SA.get(c);
     u32* PAR = e_PAR.get(c);
@@ -970,12 +1219,14 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         u32* tmp = e_tmp2.get(c);
         for (int left = 1; left >= 0; left--) {
             u32* X = left ? PA : SA;
-            k_smpl_keys<<<cdiv(c, 256), 256, 0, st>>>(d_text, n, C, c, left, key, id);
+            const u32 kc = left ? std::min<u32>(kc_max, delta + 1) : kc_max;
+            k_smpl_keys<<<cdiv(c, 256), 256, 0, st>>>(d_text, n, C, c, left, code, bits, kc, key, id);
             LZ_HIP(hipMemcpyAsync(keyid, key, (size_t)c * 8, hipMemcpyDeviceToDevice, st));
+            const int kbits = (int)(bits * kc);
             size_t tb = 0;
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, id, X, (int)c, 0, 57, st));
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, id, X, (int)c, 0, kbits, st));
             u8* t = scan_tmp.get(tb);
-            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key2, id, X, (int)c, 0, 57, st));
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key2, id, X, (int)c, 0, kbits, st));
             merge_sort_u32(X, tmp, c, smpl_less{LV, C, keyid, delta, left}, st);
             k_rank_of<<<cdiv(c, 256), 256, 0, st>>>(X, c, left ? PAR : SAR);
         }
@@ -1050,6 +1301,8 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.SA = SA;
     V.Pi = Pi;
     V.Psi = Psi;
+    V.PAR = PAR;
+    V.SAR = SAR;
     V.CS = dCS;
     V.gcb = dCS + 257;
     V.gwd = dCS + 514;
@@ -1065,16 +1318,26 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.mode = transf_mode;
     V.small_t = SMALL_T;
     if (const char* e = std::getenv("LZ77SSS_SMPL_SMALL")) V.small_t = (u32)std::max(0L, std::atol(e));
-    V.nlen[0] = V.nlen[1] = 0;
-    if (transf_mode == LZ77SSS_TRANSF_WITH_SAMPLES) build_interval_samples(V, n, za64);
+    build_adjacent(V);
+    V.cyc = nullptr;
+    if (std::getenv("LZ77SSS_SMPL_PROF")) {
+        V.cyc = (unsigned long long*)e_cyc.get(16);
+        LZ_HIP(hipMemsetAsync(V.cyc, 0, 128, st));
+        const char* sp = std::getenv("LZ77SSS_SMPL_PROF_SPLIT");
+        V.prof_split = sp ? (u32)std::atoll(sp) : 0u;
+    }
     // the chain (chunk walks + bridges, then the path from position 0 by pointer doubling).
-    // Chunks hold about 32 approximate phrases each (the walks re-synchronise with the true
-    // chain within a few phrases).
-    const u64 CS = std::max<u64>(256, std::min<u64>(1ull << 26, 32 * (n / std::max<u64>(1, za64))));
-    const u32 nch = (u32)((n + CS - 1) / CS);
+    // Chunks hold SMPL_CHUNK approximate phrases each (the walks re-synchronise with the true
+    // chain within a few phrases); cut by phrase count, not bytes, so a low-compressibility
+    // stretch (short phrases) does not give a few walks most of the work.
+    u32 cp = SMPL_CHUNK;
+    if (const char* e = std::getenv("LZ77SSS_SMPL_CHUNK")) cp = (u32)std::max(1L, std::atol(e));
+    const u32 nch = (u32)(((u64)za + cp - 1) / cp);
     // task capacity: the chain (z <= z_approx) plus the walks before they merge; a full
     // table is detected and the walks rerun with four times the room
     u64 tcap64 = std::min<u64>(0x7FFFFFF0ull, 3 * (u64)za + 64 * (u64)nch + 65536);
+    const bool prof_on = std::getenv("LZ77SSS_SMPL_PROF") != nullptr;
+    u32* prof = prof_on ? e_tmp2.get(4 * (u64)nch + 4) : nullptr;
     task_tab Tt{};
     u32* ctr = counters.get(16);
     u32* full = ctr + 9;
@@ -1097,10 +1360,11 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         Tt.ntask = ctr + 8;
         LZ_HIP(hipMemsetAsync(Tt.keys, 0, (size_t)hsz * 4, st));
         LZ_HIP(hipMemsetAsync(ctr + 8, 0, 16, st));
-        k_chunk_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, CS, nch, ex, full);
+        if (prof) LZ_HIP(hipMemsetAsync(prof, 0, (4 * (size_t)nch + 4) * 4, st));
+        k_chunk_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, cp, nch, ex, full, prof);
         LZ_HIP(hipGetLastError());
         timer.mark("smpl_tasks");
-        k_bridge_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full);
+        k_bridge_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full, prof ? prof + 2 * (u64)nch : nullptr);
         LZ_HIP(hipGetLastError());
         LZ_HIP(hipMemcpyAsync(hc, ctr + 8, 8, hipMemcpyDeviceToHost, st));
         LZ_HIP(hipStreamSynchronize(st));
@@ -1109,6 +1373,47 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         tcap64 = std::min<u64>(0x7FFFFFF0ull, 4 * tcap64);
     }
     const u32 ntask = hc[0];
+    if (V.cyc) {
+        u64 hcy[16];
+        LZ_HIP(hipMemcpy(hcy, V.cyc, 128, hipMemcpyDeviceToHost));
+        for (int bank = 0; bank < 2; bank++) {
+            const u64* h = hcy + 8 * bank;
+            const double tot = (double)(h[0] + h[1] + h[2] + h[7]) + 1e-9, ph = (double)std::max<u64>(1, h[6]);
+            std::fprintf(stderr,
+                         "[lz77sss] smpl %s %u: phrases=%llu clocks/phrase=%.0f: position probes + PA interval %.1f%%, witnesses %.1f%%, "
+                         "probe intervals %.1f%%, intersect %.1f%%; probes/phrase=%.2f queries/probe=%.2f coop "
+                         "queries/probe=%.2f\n",
+                         bank ? "at/after" : "before", V.prof_split, (unsigned long long)h[6], tot / ph,
+                         100 * h[0] / tot, 100 * h[1] / tot, 100 * h[7] / tot, 100 * h[2] / tot, h[3] / ph,
+                         (double)h[5] / std::max<u64>(1, h[3]), (double)h[4] / std::max<u64>(1, h[3]));
+        }
+    }
+    if (prof) {
+        // per-walk profile (wall clock at 100 MHz): the slowest walks and the phrase totals
+        std::vector<u32> hp(4 * (size_t)nch);
+        LZ_HIP(hipMemcpy(hp.data(), prof, hp.size() * 4, hipMemcpyDeviceToHost));
+        for (int br = 0; br < 2; br++) {
+            std::vector<u32> tk(nch);
+            u64 ph = 0, sum = 0;
+            u32 mph = 0;
+            for (u32 k = 0; k < nch; k++) {
+                tk[k] = hp[2 * ((u64)br * nch + k)];
+                const u32 q = hp[2 * ((u64)br * nch + k) + 1];
+                ph += q;
+                mph = std::max(mph, q);
+                sum += tk[k];
+            }
+            std::vector<u32> s2 = tk;
+            std::sort(s2.begin(), s2.end());
+            const u32 kmax = (u32)(std::max_element(tk.begin(), tk.end()) - tk.begin());
+            std::fprintf(stderr,
+                         "[lz77sss] smpl %s: walks=%u phrases=%llu max_phrases=%u ticks sum=%.1f ms p50=%.1f us "
+                         "p99=%.1f us max=%.1f us (walk %u, %u phrases, at %u)\n",
+                         br ? "bridges" : "chunks", nch, (unsigned long long)ph, mph, sum / 1e5, s2[nch / 2] / 100.0,
+                         s2[(u64)nch * 99 / 100] / 100.0, s2.back() / 100.0, kmax, hp[2 * ((u64)br * nch + kmax) + 1],
+                         br ? 0u : kmax * cp);
+        }
+    }
     timer.mark("smpl_bridges");
     // the path from the task at position 0: pointer doubling + top-down expansion (in order)
     u32 T_lv = 0;
@@ -1154,116 +1459,52 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     return z;
 }
 
-// interval samples of with_samples (build_xa_s_1_2_intervals + build_samples,
-// construction.cpp:31-305): the RKS prefix fingerprints, adjacent context LCEs of PA and SA,
-// the sampled pattern lengths (quantiles of the adjacent LCEs), one hash entry per interval
-void engine::build_interval_samples(smpl_view& V, u64 nn, u64 za) {
-    // RKS (rabin_karp_substring.hpp:77-172)
-    const u64 nb = (nn + RKS_RATE - 1) / RKS_RATE;
-    u32* fps = e_rks.get(nb + 2);
-    {
-        u64* blk = e_key.get(nb + 1);
-        u64* incl = e_key2.get(nb + 1);
-        k_rks_blocks<<<cdiv(nb, 256), 256, 0, st>>>(d_text, nn, nb, blk);
-        rks_cat op{};
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, tb, blk, incl, op, (int)nb, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceScan::InclusiveScan(t, tb, blk, incl, op, (int)nb, st));
-        k_rks_shift<<<cdiv(nb + 1, 256), 256, 0, st>>>(incl, nb, fps);
-    }
-    // the last block is partial: fps[nb] must be fp(T[0..n)); fp(T[0..16 nb)) with zero
-    // padding differs, so rks_upto never reads fps[nb] past n (x / 16 <= (n - 1) / 16 < nb
-    // for x < n; x = n reads fps[n / 16] only when n % 16 == 0, where it is exact)
-    u32 sq = 1;
-    while ((u64)sq * sq < nn + 1) sq++;
-    std::vector<u32> lo(sq + 1), hi(sq + 2);
-    lo[0] = 1;
-    for (u32 e = 1; e <= sq; e++) lo[e] = (u32)((u64)lo[e - 1] * RKS_B % RKS_P);
-    hi[0] = 1;
-    for (u32 e = 1; e <= sq + 1; e++) hi[e] = (u32)((u64)hi[e - 1] * lo[sq] % RKS_P);
-    u32* dpw = e_rkspw.get(2 * (u64)sq + 4);
-    LZ_HIP(hipMemcpyAsync(dpw, lo.data(), (sq + 1) * 4, hipMemcpyHostToDevice, st));
-    LZ_HIP(hipMemcpyAsync(dpw + sq + 1, hi.data(), (sq + 2) * 4, hipMemcpyHostToDevice, st));
-    V.rks = fps;
-    V.pw_lo = dpw;
-    V.pw_hi = dpw + sq + 1;
-    V.sq = sq;
-    // adjacent LCEs and sampled lengths per side
+// the phrase searches' structures per order (PA: left contexts, SA: suffixes): the 16-byte
+// context keys by rank, the adjacent LCEs (LCS_S / LCP_S of construction.cpp:118-129; left
+// capped at delta) and their sparse-table minima
+void engine::build_adjacent(smpl_view& V) {
     const u32 c = V.c;
-    const u64 max_smpl_right = (u64)std::llround((double)nn / za * (1.0 + 0.5 * std::exp(-(double)nn / za / 1000.0)));
-    // the adjacent LCEs are sorted on the device (a radix sort of c - 1 keys) and only the
-    // sorted column goes to the host for the quantile picks (a host sort took 0.6 s per side
-    // on the genome-like text's 2^24+ samples)
-    std::vector<u32> srth[2];
-    u32* adj[2] = {e_adjL.get((u64)c + 1), e_adjR.get((u64)c + 1)};
-    u32* srtd = e_adjS.get((u64)c + 1);
     for (int side = 0; side < 2; side++) {
-        k_adj_lce<<<cdiv((u64)c + 1, 256), 256, 0, st>>>(V.L, V.C, side == 0 ? V.PA : V.SA, c, V.delta, side == 0,
-                                                        adj[side]);
-        srth[side].resize(c > 1 ? (size_t)c - 1 : 0);
-        if (c > 1) {
-            size_t tb = 0;
-            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, adj[side] + 1, srtd, (int)(c - 1), 0, 32, st));
-            u8* t = scan_tmp.get(tb);
-            LZ_HIP(hipcub::DeviceRadixSort::SortKeys(t, tb, adj[side] + 1, srtd, (int)(c - 1), 0, 32, st));
-            LZ_HIP(hipMemcpyAsync(srth[side].data(), srtd, ((size_t)c - 1) * 4, hipMemcpyDeviceToHost, st));
-            LZ_HIP(hipStreamSynchronize(st));  // srtd is reused by the other side
-        }
-    }
-    u64 total_iv = 0;
-    for (int side = 0; side < 2; side++) {
-        // construction.cpp:136-199: quantiles of the sorted adjacent LCEs in [3, max]
-        const std::vector<u32>& srt = srth[side];
-        const u64 maxlen = side == 0 ? V.delta : std::min<u64>(srt.empty() ? 0 : srt.back(), max_smpl_right);
-        V.slen[side][0] = 1;
-        V.slen[side][1] = 2;
-        u32 k = 2;
-        if (!srt.empty() && maxlen > 3) {
-            const u64 rmin = std::lower_bound(srt.begin(), srt.end(), 3u) - srt.begin();
-            const u64 rmax = std::lower_bound(srt.begin(), srt.end(), (u32)maxlen) - srt.begin();
-            if (rmin < rmax) {
-                const u64 want = std::min<u64>(NSMPL, std::min<u64>(maxlen - 2, 2 + (u64)std::floor(4.0 * c / (double)(rmin + rmax))));
-                for (u64 q = 2; q < want && k < NSMPL; q++) {
-                    const double rel = (q - 1) / (double)(want - 2);
-                    const u64 rk = (u64)std::floor(rmin + rel * (double)(rmax - rmin));
-                    const u32 len = std::max<u32>(srt[std::min<u64>(rk, srt.size() - 1)], V.slen[side][k - 1] + 1);
-                    if (len > maxlen) break;
-                    V.slen[side][k++] = len;
-                }
-            }
-        }
-        V.nlen[side] = k;
-        for (u32 q = 2; q < k; q++) {
-            const u32 len = V.slen[side][q];
-            total_iv += 1 + (u64)(std::upper_bound(srt.begin(), srt.end(), len - 1) - srt.begin());
-        }
-    }
-    u64 hs = 1024;
-    while (hs < 2 * total_iv + 1024) hs <<= 1;
-    u64* hkey = e_hkey.get(hs);
-    u64* hval = e_hval.get(hs);
-    LZ_HIP(hipMemsetAsync(hkey, 0, hs * 8, st));
-    V.hkey = hkey;
-    V.hval = hval;
-    V.hmask = hs - 1;
-    for (int side = 0; side < 2; side++) {
-        // sparse-table minima of adj[0 .. c) (level 0 is adj itself) for the interval ends
+        const bool left = side == 0;
+        const u32* X = left ? V.PA : V.SA;
+        ulonglong2* keys = (ulonglong2*)(left ? e_kPA : e_kSA).get(2 * (u64)c + 2);
+        k_ctx_keys<<<cdiv(c, 256), 256, 0, st>>>(d_text, n, V.C, X, c, left, keys);
         iv_levels M{};
-        M.mn[0] = adj[side];
+        u32* adj = (left ? e_adjL : e_adjR).get((u64)c + 1);
+        k_adj_lce<<<cdiv((u64)c + 1, 256), 256, 0, st>>>(V.L, V.C, X, c, V.delta, left, adj);
+        M.mn[0] = adj;
         M.nlv = 1;
+        dbuf<u32>* lv = left ? e_ivminL : e_ivmin;
         while ((2ull << (M.nlv - 1)) <= c && M.nlv < (u32)MAX_LV) {
             const u64 half = 1ull << (M.nlv - 1), cnt = (u64)c - 2 * half + 1;
-            u32* out = e_ivmin[M.nlv].get(cnt);
+            u32* out = lv[M.nlv].get(cnt);
             k_iv_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(M.mn[M.nlv - 1], cnt, half, out);
             M.mn[M.nlv++] = out;
         }
-        for (u32 q = 2; q < V.nlen[side]; q++)
-            k_iv_insert<<<cdiv(c, 256), 256, 0, st>>>(V, side == 0 ? V.PA : V.SA, adj[side], c, side == 0, q,
-                                                     V.slen[side][q], hkey, hval, hs - 1, M);
+        if (left) {
+            V.pM = M;
+            V.kPA = keys;
+        } else {
+            V.sM = M;
+            V.kSA = keys;
+        }
+    }
+    // minima of the weights (sample ids) by PA / SA rank
+    V.wPA[0] = V.PA;
+    V.wSA[0] = V.SA;
+    V.wlv = 1;
+    while ((2ull << (V.wlv - 1)) <= c && V.wlv < (u32)MAX_LV) {
+        const u64 half = 1ull << (V.wlv - 1), cnt = (u64)c - 2 * half + 1;
+        u32* o1 = e_wPA[V.wlv].get(cnt);
+        u32* o2 = e_wSA[V.wlv].get(cnt);
+        k_iv_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(V.wPA[V.wlv - 1], cnt, half, o1);
+        k_iv_min_level<<<cdiv(cnt, 256), 256, 0, st>>>(V.wSA[V.wlv - 1], cnt, half, o2);
+        V.wPA[V.wlv] = o1;
+        V.wSA[V.wlv] = o2;
+        V.wlv++;
     }
     LZ_HIP(hipGetLastError());
-    timer.mark("smpl_ivs");
+    timer.mark("smpl_adj");
 }
 
 }  // namespace LZ_NS

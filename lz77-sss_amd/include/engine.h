@@ -211,13 +211,17 @@ struct engine {
     const u32* sa_full = nullptr;    // suffix array of the text (x_sa) after build_sa_full
     u32 x_rounds = 0;
     // exact-smpl mode (csrc/smpl.hip): approximate factors, samples, PA / SA, grid, RKS,
-    // interval samples, phrase tasks
+    // exact-smpl (csrc/smpl.hip): samples, PA / SA orders, grid, phrase tasks
     dbuf<u32> e_afact, e_afst, e_tmp1, e_tmp2, e_C, e_PA, e_SA, e_PAR, e_SAR, e_Pi, e_Psi, e_CS;
-    dbuf<u32> e_gx, e_gy, e_gw, e_cell, e_rks, e_rkspw, e_adjL, e_adjR, e_adjS;
+    dbuf<u32> e_alpha;  // exact-smpl: the character codes of the sort keys and the text's character flags
+    dbuf<u64> e_cyc;  // exact-smpl debug counters (LZ77SSS_SMPL_PROF)
+    dbuf<u32> e_gx, e_gy, e_gw, e_cell, e_adjL, e_adjR;
     dbuf<u32> e_rst[10];  // exact-smpl: row sparse tables of the grid cells' lightest weights
-    dbuf<u32> e_ivmin[MAX_LV];  // with_samples: sparse-table minima of the adjacent LCEs (interval ends)
+    dbuf<u32> e_ivmin[MAX_LV], e_ivminL[MAX_LV];  // sparse-table minima of the SA / PA adjacent LCEs (interval ends)
+    dbuf<u64> e_kSA, e_kPA;                      // 16-byte context keys by SA / PA rank
+    dbuf<u32> e_wPA[MAX_LV], e_wSA[MAX_LV];      // minima of the PA / SA weights per sparse-table level
     dbuf<u32> e_tpos, e_tlen, e_tsrc, e_thop, e_tkeys, e_tvals;
-    dbuf<u64> e_key, e_key2, e_key3, e_hkey, e_hval;
+    dbuf<u64> e_key, e_key2, e_key3;
     // device decode (csrc/decode.hip)
     dbuf<u32> dec_fid, dec_fid2;
     dbuf<pos_t> dec_ref, dec_ref2;
@@ -279,7 +283,7 @@ struct engine {
     void build_sa_full(const u8* T);
     u64 factorize_exact(bool log);  // csrc/exact.hip (full suffix array, LZ77SSS_TRANSF_FULL_SA)
     u64 factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int log2_override, bool log);  // csrc/smpl.hip
-    void build_interval_samples(smpl_view& V, u64 nn, u64 za);                                         // csrc/smpl.hip
+    void build_adjacent(smpl_view& V);                                                                 // csrc/smpl.hip
     u64 decode_device(const pos_t* F, u64 nf, u64 n_out, u8* out, const u8* cmp);
     u64 verify_factors(const pos_t* F, u64 nf, u64 n_out, const u8* T, u64* first_bad = nullptr);  // csrc/decode.hip
     void debug_verify_phrases(const char* what);  // LZ77SSS_DEBUG_VERIFY (csrc/decode.hip)
