@@ -56,7 +56,7 @@
 namespace LZ_NS {
 
 constexpr u32 SMPL_MAX_DELTA = 256;  // lz77_sss.hpp:81 max_delta
-constexpr u32 SCAN_T = 4096;         // lz77_sss.hpp:83 range_scan_threshold
+constexpr u32 SCAN_T = 1024;         // lz77_sss.hpp:83 range_scan_threshold (4096 on a CPU core)
 constexpr u32 SMALL_T = 32;          // intersect queries scanned by their own lane (no wave round trip)
 #ifndef LZ_SG_WIN
 #define LZ_SG_WIN 2048
@@ -65,7 +65,8 @@ constexpr u32 SG_WIN = LZ_SG_WIN;    // smallest grid cell width in ranks (the r
 constexpr u32 SG_GMAX = 512;         // cells per side at most: wider blocks get wider cells
 constexpr u32 SG_LV = 10;            // row sparse-table levels (2^9 = SG_GMAX / 1)
 constexpr u32 SWPB = 4;              // waves per workgroup of the phrase kernels
-constexpr u32 SMPL_CHUNK = 32;       // approximate phrases per chunk walk
+constexpr u32 SMPL_CHUNK = 1024;     // approximate phrases per chunk walk at most
+constexpr u32 SMPL_WALKS = 16384;    // chunk walks wanted
 
 // ---------------------------------------------------------------------------
 // rank intervals of an order by its adjacent LCEs (mn[0][r] = LCE of ranks r - 1, r) and their
@@ -99,6 +100,7 @@ struct smpl_view {
     u32 za;
     int mode;                // LZ77SSS_TRANSF_*
     u32 small_t;             // intersect queries with a side of at most this many ranks run on their own lane
+    u32 scan_t;              // the wave scans a side of at most this many ranks (else the grid)
     iv_levels sM;            // SA order: adjacent sample-suffix LCEs (sM.mn[0][r] = LCE of ranks r - 1, r) and their
                              // sparse-table minima; the SA interval of any right extension by binary lifting
     iv_levels pM;            // PA order: the same over the left contexts (capped at delta)
@@ -107,6 +109,11 @@ struct smpl_view {
     const u32* wPA[MAX_LV];  // sparse-table minima of the weights (sample ids) by PA rank: min PA[x .. x + 2^k)
     const u32* wSA[MAX_LV];  // the same by SA rank (level 0: PA / SA themselves)
     u32 wlv;                 // levels
+    const u32* pre[2];       // PA / SA: the first rank per value of a context's first 16 key bits [65537]
+    const u8* code;          // the characters' codes in the sort keys
+    u32 kbits_ch;            // bits per character in the sort keys
+    u32 kc[2];               // characters per sort key (PA, SA)
+    const u32* wblk;         // the first sample index x with C[x] >= 256 b, per 256-position block b
     const ulonglong2* kSA;   // context keys by SA rank (key_right) and by PA rank (key_left)
     const ulonglong2* kPA;
     unsigned long long* cyc;  // debug (LZ77SSS_SMPL_PROF): per-section clock and query counters, or null
@@ -181,7 +188,7 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
         bool f = false;
         u32 y = 0;
         const u32 rx = qxe - qxb + 1, ry = qye - qyb + 1;
-        if (V.mode != LZ77SSS_TRANSF_NAIVE && min(rx, ry) <= SCAN_T) {
+        if (V.mode != LZ77SSS_TRANSF_NAIVE && min(rx, ry) <= V.scan_t) {
             // scan the smaller interval through Pi / Psi
             if (rx <= ry) {
                 for (u32 base = qxb; base <= qxe; base += 64) {
@@ -430,14 +437,14 @@ __device__ __forceinline__ void iv_around(const iv_levels& M, u32 c, u32 rs, u32
 
 // what is known about position j, whatever phrase it serves: the insertion ranks of its left
 // context (PA, capped at delta) and of its suffix (SA) with the LCEs of their neighbours, the
-// first sample W at or after j, and the nearest SA ranks either side of rsR holding a sample
-// lighter than W (the earlier sample suffixes sharing the most with the suffix at j) with their
-// LCEs, uA >= uB
+// first sample W at or after j, and of the nearest SA ranks either side of rsR holding a sample
+// lighter than W (the earlier sample suffixes sharing the most with the suffix at j) the one with
+// the larger LCE uA (no earlier sample shares more)
 struct pos_info {
     u32 rsL, hloL, hhiL;
     u32 rsR, hloR, hhiR;
     u32 w;
-    u32 yA, uA, yB, uB;
+    u32 yA, uA;
 };
 __device__ __forceinline__ void key_step(const ulonglong2& km, const ulonglong2& kp, u32 D, bool left, u32& lm,
                                          bool& ls, bool& text) {
@@ -453,14 +460,64 @@ __device__ __forceinline__ void key_step(const ulonglong2& km, const ulonglong2&
         text = true;  // 15 equal bytes: the text decides
     }
 }
+// the range of first-16-bit values of the sort keys (k_smpl_keys: kc characters of `bits` bits)
+// of the contexts that agree with the context at p on its first characters: all the key's
+// characters in 16 bits, at most D of a left context (the comparator looks no further)
+__device__ __forceinline__ void ctx_pre16(const smpl_view& V, u64 p, bool left, u32 D, u32& vlo, u32& vhi) {
+    const u32 bits = V.kbits_ch, kc = left ? V.kc[0] : V.kc[1];
+    const u32 q = min(kc, (16 + bits - 1) / bits), qa = left ? min(q, D) : q, qb = qa * bits;
+    u32 v = 0;
+    for (u32 t = 0; t < qa; t++) {
+        u32 d;
+        if (left) d = p >= (u64)t ? V.code[V.L.T[p - t]] : 0u;
+        else d = p + t < V.L.n ? V.code[V.L.T[p + t]] : 0u;
+        v = (v << bits) | d;
+    }
+    if (qb >= 16) {
+        vlo = vhi = v >> (qb - 16);
+    } else {
+        vlo = v << (16 - qb);
+        vhi = vlo | ((1u << (16 - qb)) - 1);
+    }
+}
+// one comparison of an insertion search: the LCE lm of the context at rank m with the pattern
+// (capped at D on the left) and whether it sorts below the pattern; keys first, the text past 15
+// equal bytes (lower bound hb)
+template <bool LEFT>
+__device__ __forceinline__ void rank_cmp(const smpl_view& V, u32 j, u32 D, const ulonglong2& km, const ulonglong2& kp,
+                                         u32 m, u32 hb, u32& lm, bool& ls) {
+    bool text;
+    key_step(km, kp, D, LEFT, lm, ls, text);
+    if (text) {
+        const u32 pm = V.C[(LEFT ? V.PA : V.SA)[m]];
+        if (LEFT) {
+            lm = lce_left_offs(V, pm, j, max(hb, 15u), D);
+            ls = lm < D && less_left(V, pm, j, lm);
+        } else {
+            lm = lce_right_offs(V, pm, j, max(hb, 15u));
+            ls = less_right(V, pm, j, lm);
+        }
+    }
+}
 // the three binary searches (PA / SA insertion ranks, W) advance together, one load each per
-// step; then the two nearest-lighter searches together
-__device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_info& P) {
+// step: the insertion searches inside the ranks of the pattern's first 16 key bits (V.pre), W
+// inside the samples of j's 256-position block (V.wblk); then the two nearest-lighter searches
+// together
+template <bool PROF>
+__device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_info& P, u64* cy) {
     const u8* T = V.L.T;
+    u64 t0 = PROF ? clock64() : 0;
+    if constexpr (PROF) cy[13] += __popcll(__ballot(true));
     const ulonglong2 kpL = key_left(T, j), kpR = key_right(T, V.L.n, j);
-    u32 lL = cb, rL = ce, hlL = 1, hrL = 1;
-    u32 lR = cb, rR = ce, hlR = 1, hrR = 1;
-    u32 lW = 0, hW = V.c;
+    u32 vL0, vL1, vR0, vR1;
+    ctx_pre16(V, j, true, D, vL0, vL1);
+    ctx_pre16(V, j, false, 0, vR0, vR1);
+    const u32 bL = V.pre[0][vL0], eL = V.pre[0][vL1 + 1], bR = V.pre[1][vR0], eR = V.pre[1][vR1 + 1];  // in [cb, ce]
+    u32 lW = V.wblk[j >> 8], hW = V.wblk[(j >> 8) + 1];
+    // one rank more either side (inside the character's block): the search then compares the
+    // pattern with both neighbours of its insertion rank, whose LCEs it returns
+    u32 lL = bL > cb ? bL - 1 : bL, rL = eL < ce ? eL + 1 : eL, hlL = 1, hrL = 1;
+    u32 lR = bR > cb ? bR - 1 : bR, rR = eR < ce ? eR + 1 : eR, hlR = 1, hrR = 1;
     P.hloL = P.hhiL = P.hloR = P.hhiR = 0;
     while (lL < rL || lR < rR || lW < hW) {
         const bool aL = lL < rL, aR = lR < rR, aW = lW < hW;
@@ -472,13 +529,8 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
         if (aW) cW = V.C[mW];
         if (aL) {
             u32 lm;
-            bool ls, text;
-            key_step(kL, kpL, D, true, lm, ls, text);
-            if (text) {
-                const u32 pm = V.C[V.PA[mL]];
-                lm = lce_left_offs(V, pm, j, max(min(hlL, hrL), 15u), D);
-                ls = lm < D && less_left(V, pm, j, lm);
-            }
+            bool ls;
+            rank_cmp<true>(V, j, D, kL, kpL, mL, min(hlL, hrL), lm, ls);
             if (ls) {
                 lL = mL + 1;
                 hlL = P.hloL = lm;
@@ -489,13 +541,8 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
         }
         if (aR) {
             u32 lm;
-            bool ls, text;
-            key_step(kR, kpR, 0, false, lm, ls, text);
-            if (text) {
-                const u32 pm = V.C[V.SA[mR]];
-                lm = lce_right_offs(V, pm, j, max(min(hlR, hrR), 15u));
-                ls = less_right(V, pm, j, lm);
-            }
+            bool ls;
+            rank_cmp<false>(V, j, D, kR, kpR, mR, min(hlR, hrR), lm, ls);
             if (ls) {
                 lR = mR + 1;
                 hlR = P.hloR = lm;
@@ -508,12 +555,19 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
             if (cW < j) lW = mW + 1;
             else hW = mW;
         }
+        if constexpr (PROF) cy[12]++;
+    }
+    if constexpr (PROF) {
+        const u64 t = clock64();
+        cy[8] += t - t0;
+        t0 = t;
     }
     P.rsL = lL;
     P.rsR = lR;
     P.w = lW;  // the first sample index x with C[x] >= j (adjust_xc, common.cpp:184-196)
-    // nearest lighter ranks: the four ranks either side first, then binary lifting over the
-    // weight minima, both sides at once
+    // nearest lighter ranks, both sides at once: the four ranks either side first, then blocks
+    // of 2^l ranks over the weight minima, l growing while the blocks hold no lighter sample
+    // and falling once one does (2 log d steps for a lighter sample d ranks away)
     const u32 c = V.c, rs = lR, W = lW;
     u32 vb[4], vf[4];
 #pragma unroll
@@ -527,32 +581,58 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
         if (vb[t] < W) yb = rs - 1 - t;
         if (vf[t] < W) yf = rs + t;
     }
-    const bool sb = yb == NONE && rs > 4, sf = yf == NONE && rs + 4 < c;
+    bool sb = yb == NONE && rs > 4, sf = yf == NONE && rs + 4 < c;
     u32 pb = rs - 4, pf = rs + 4;  // ranks [pb, rs) / [rs, pf) hold no lighter sample
-    for (int l = (int)V.wlv - 1; l >= 0 && (sb || sf); l--) {
-        const u32 w = 1u << l;
-        const bool tb = sb && pb >= w, tf = sf && pf + w <= c;
+    int lb = 2, lf = 2;            // block levels
+    bool ub_ = true, uf_ = true;   // growing
+    const int top = (int)V.wlv - 1;
+    while (sb || sf) {
+        const u32 wb = 1u << max(lb, 0), wf = 1u << max(lf, 0);
+        const bool tb = sb && lb >= 0 && lb <= top && pb >= wb, tf = sf && lf >= 0 && lf <= top && pf + wf <= c;
         u32 x = 0, y = 0;
-        if (tb) x = V.wSA[l][pb - w];
-        if (tf) y = V.wSA[l][pf];
-        if (tb && x >= W) pb -= w;
-        if (tf && y >= W) pf += w;
+        if (tb) x = V.wSA[lb][pb - wb];
+        if (tf) y = V.wSA[lf][pf];
+        if (sb) {
+            if (tb && x >= W) {
+                pb -= wb;
+                if (ub_ && lb < top) lb++;
+                else if (!ub_) lb--;
+            } else if (ub_) {
+                ub_ = false;
+                lb--;
+            } else {
+                lb--;
+            }
+            if (lb < 0) sb = false;
+        }
+        if (sf) {
+            if (tf && y >= W) {
+                pf += wf;
+                if (uf_ && lf < top) lf++;
+                else if (!uf_) lf--;
+            } else if (uf_) {
+                uf_ = false;
+                lf--;
+            } else {
+                lf--;
+            }
+            if (lf < 0) sf = false;
+        }
+        if constexpr (PROF) cy[11]++;
     }
-    if (sb) yb = pb == 0 ? NONE : pb - 1;
-    if (sf) yf = pf >= c ? NONE : pf;
+    if (yb == NONE && rs > 4) yb = pb == 0 ? NONE : pb - 1;
+    if (yf == NONE && rs + 4 < c) yf = pf >= c ? NONE : pf;
+    if constexpr (PROF) cy[9] += clock64() - t0;
     u32 ub = 0, uf = 0;
     if (yb != NONE) ub = lce_of_rank(V.sM, yb, rs, P.hloR, P.hhiR);
     if (yf != NONE) uf = lce_of_rank(V.sM, yf, rs, P.hloR, P.hhiR);
     if (uf > ub) {
         P.yA = yf;
         P.uA = uf;
-        P.yB = yb;
-        P.uB = ub;
     } else {
         P.yA = yb;
         P.uA = ub;
-        P.yB = yf;
-        P.uB = uf;
+
     }
 }
 
@@ -565,6 +645,8 @@ struct lane_cache {
     pos_info P;   // valid if has
     bool has;
 };
+
+constexpr u32 LANE_SCAN = 8;   // PA intervals scanned whole on the lane
 
 // ---- one exact phrase at i (transform_to_exact_{naive,without_samples,with_samples}) --
 // executed by a whole wave; returns (src, len) in every lane.
@@ -581,15 +663,15 @@ struct lane_cache {
 // them and the lightest point of the PA interval, then runs the largest candidate, an
 // exponential search and bisection; the predicate is monotone in x, so the result is the
 // reference's whatever the probe order.
-__device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u32 lane, lane_cache& K) {
+template <bool PROF>
+__device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u32 lane, lane_cache& K, u64* cy) {
     const u32 n = (u32)V.L.n;
     const u32 e = n;  // one section: p = 1
     const u8* T = V.L.T;
-    u64 cy[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // clocks: left, right insertion, intersect; probes, coop queries,
-                                           // queries, phrases; clocks: probe intervals
-    u64 ct = V.cyc ? clock64() : 0;
+    // PROF (LZ77SSS_SMPL_PROF): clocks and counts per walk in cy, printed by factorize_exact_smpl
+    u64 ct = PROF ? clock64() : 0;
     auto tick = [&](int k) {
-        if (V.cyc) {
+        if constexpr (PROF) {
             const u64 t = clock64();
             cy[k] += t - ct;
             ct = t;
@@ -636,8 +718,6 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         K.P.w = __shfl(K.P.w, sl, 64);
         K.P.yA = __shfl(K.P.yA, sl, 64);
         K.P.uA = __shfl(K.P.uA, sl, 64);
-        K.P.yB = __shfl(K.P.yB, sl, 64);
-        K.P.uB = __shfl(K.P.uB, sl, 64);
         K.has = lane + d < 64 && h;
         K.base = i;
     }
@@ -654,7 +734,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
             if (first && K.has) {
                 P = K.P;
             } else {
-                pos_probe(V, j, D, cb, ce, P);
+                pos_probe<PROF>(V, j, D, cb, ce, P, cy);
                 if (first) {
                     K.P = P;
                     K.has = true;
@@ -664,43 +744,56 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         // PA interval of T[i..j]: the ranks around j's insertion rank whose contexts share lce_l
         u32 xb = 0, xe = 0;
         const bool okl = have && (P.hloL >= lce_l || P.hhiL >= lce_l);
-        if (okl) iv_around(V.pM, V.c, P.rsL, P.hloL, P.hhiL, lce_l, xb, xe);
         tick(0);
+        if (okl) iv_around(V.pM, V.c, P.rsL, P.hloL, P.hhiL, lce_l, xb, xe);
+        tick(14);
         // right extensions: max lce_r in [lce_r_min, e - j] with a lighter point
         const u32 lrmin = (f_len < j - i) ? 0u : (i + f_len - j);
         const u32 lrmax = e - j;
         u32 lo = lrmin, hi = lrmax + 1, step = 1;
         bool bin = false;
         bool run = okl && lo < lrmax;
-        const u32 rs = P.rsR, h_lo = P.hloR, h_hi = P.hhiR, W = P.w, yA = P.yA, uA = P.uA, yB = P.yB, uB = P.uB;
+        const u32 rs = P.rsR, h_lo = P.hloR, h_hi = P.hhiR, W = P.w, yA = P.yA, uA = P.uA;
         // no sample before j shares more than uA characters with the suffix at j
         hi = min(hi, uA + 1);
         if (hi - lo <= 1) run = false;
         u32 best_y = 0;
         bool got = false, top = true;
+        // the answer is the largest LCE with j of a lighter sample whose context ends with
+        // T[i..j].  Few such contexts (a PA interval below LANE_SCAN ranks): all of them, on the
+        // lane.  Else the nearest lighter sample in SA order, whose LCE bounds the answer, when
+        // its context ends with T[i..j]; the probes below finish between the bounds.
+        bool done = !run;
         if (run) {
-            // witnesses: the two nearest lighter ranks, when their contexts end with T[i..j]; else
-            // the lightest point of the PA interval (none lighter than W ends the lane's search)
-            const u32 xA = V.PAR[V.SA[yA]];
-            if (xA >= xb && xA <= xe) {
-                lo = uA;  // the largest possible
-                best_y = yA;
-                got = true;
-                run = false;
-            } else {
-                if (yB != NONE && uB > lo) {
-                    const u32 xB = V.PAR[V.SA[yB]];
-                    if (xB >= xb && xB <= xe) {
-                        lo = uB;
-                        best_y = yB;
-                        got = true;
+            if (xe - xb < LANE_SCAN) {
+                for (u32 x = xb; x <= xe; x++) {
+                    if (V.PA[x] < W) {
+                        const u32 y = V.Pi[x], l = lce_of_rank(V.sM, y, rs, h_lo, h_hi);
+                        if (l > lo) {
+                            lo = l;
+                            best_y = y;
+                            got = true;
+                        }
                     }
                 }
+                done = true;
+            } else if (yA == NONE || uA <= lo) {
+                done = true;  // no lighter sample shares more than lo
+            } else {
+                const u32 xx = V.PAR[V.SA[yA]];
+                if (xx >= xb && xx <= xe) {
+                    lo = uA;
+                    best_y = yA;
+                    got = true;
+                    done = true;
+                }
+            }
+        }
+        if (run) {
+            if (!done) {
+                // the lightest point of the PA interval is a witness up to its LCE
                 const u32 s0 = min_weight(V.wPA, xb, xe);
-                if (s0 >= W) {
-                    run = false;
-                    got = false;
-                } else {
+                if (s0 < W) {
                     const u32 y0 = V.SAR[s0], l0 = lce_of_rank(V.sM, y0, rs, h_lo, h_hi);
                     if (l0 > lo) {
                         lo = l0;
@@ -708,8 +801,8 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
                         got = true;
                     }
                 }
-                if (hi - lo <= 1) run = false;
             }
+            if (done || hi - lo <= 1) run = false;
         }
         tick(1);
         while (__ballot(run)) {
@@ -724,35 +817,14 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
                 if (cand) iv_around(V.sM, V.c, rs, h_lo, h_hi, x, nb, ne);
             }
             tick(7);
-            if (V.cyc) {
+            if constexpr (PROF) {
                 cy[3]++;
                 cy[4] += __popcll(__ballot(cand && min(xe - xb, ne - nb) + 1 > V.small_t));
                 cy[5] += __popcll(__ballot(cand));
             }
-            // the lightest point of the SA interval decides most probes on the lane itself
-            bool f = false, open = false;
-            u32 py = 0;
-            if (cand) {
-                const u32 s1 = min_weight(V.wSA, nb, ne);
-                if (s1 < W) {
-                    const u32 x1 = V.PAR[s1];
-                    if (x1 >= xb && x1 <= xe) {
-                        f = true;
-                        py = V.SAR[s1];
-                    } else {
-                        open = true;
-                    }
-                }
-            }
-            {
-                bool f2;
-                u32 py2;
-                wave_intersect(V, open, xb, xe, nb, ne, W, ch, f2, py2, lane);
-                if (open) {
-                    f = f2;
-                    py = py2;
-                }
-            }
+            bool f;
+            u32 py;
+            wave_intersect(V, cand, xb, xe, nb, ne, W, ch, f, py, lane);
             tick(2);
             if (run) {
                 if (cand && f) {
@@ -801,11 +873,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         }
     }
     if (f_len > e - i) f_len = e - i;
-    if (V.cyc && lane == 0) {
-        cy[6] = 1;
-        const u32 bank = i < V.prof_split ? 0 : 8;
-        for (int k = 0; k < 8; k++) atomicAdd(&V.cyc[bank + k], (unsigned long long)cy[k]);
-    }
+    if constexpr (PROF) cy[6]++;
 }
 
 // ---------------------------------------------------------------------------
@@ -875,6 +943,31 @@ __global__ void k_smpl_keys(const u8* __restrict__ T, u64 n, const u32* __restri
     }
     key[k] = v;
     id[k] = (u32)k;
+}
+// the first 16 bits of a sort key of kbits bits
+__device__ __forceinline__ u32 key_pre16(u64 key, u32 kbits) {
+    return kbits >= 16 ? (u32)(key >> (kbits - 16)) : (u32)(key << (16 - kbits));
+}
+// out[u] = the first rank whose sorted key starts with 16 bits >= u, u in [0, 65536]
+__global__ void k_pre_table(const u64* __restrict__ sorted, u32 c, u32 kbits, u32* __restrict__ out) {
+    const u32 u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u > 65536) return;
+    u32 lo = 0, hi = c;
+    while (lo < hi) {
+        const u32 m = (lo + hi) >> 1;
+        if (key_pre16(sorted[m], kbits) < u) lo = m + 1; else hi = m;
+    }
+    out[u] = lo;
+}
+// out[b] = the first sample index x with C[x] >= 256 b (b in [0, nblk)); consecutive samples
+// are at most delta <= 256 apart, so each sample fills at most two blocks
+__global__ void k_wblk(const u32* __restrict__ C, u32 c, u64 nblk, u32* __restrict__ out) {
+    const u64 x = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= c) return;
+    const u64 b0 = x == 0 ? 0 : ((u64)C[x - 1] >> 8) + 1, b1 = (u64)C[x] >> 8;
+    for (u64 b = b0; b <= b1 && b < nblk; b++) out[b] = (u32)x;
+    if (x == c - 1)
+        for (u64 b = b1 + 1; b < nblk; b++) out[b] = c;
 }
 struct smpl_less {
     lce_view L;
@@ -1037,8 +1130,9 @@ __device__ u32 task_find(const task_tab& Tt, u32 p) {
 // A bridge walks from every exit until it meets a task.  Every task's successor position
 // then holds a task (a walk inserts it, finds it, or hands it to a bridge), so the chain
 // from position 0 lies in the table; it is marked by pointer doubling.
+template <bool PROF>
 __device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p, u64 stop, u32 lane, u32* __restrict__ full,
-                                         u32& nph) {
+                                         u32& nph, u64* cy) {
     const u64 n = V.L.n;
     lane_cache K{NONE, NONE, pos_info{}, false};
     for (;;) {
@@ -1052,7 +1146,7 @@ __device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p
         t = (u32)__shfl((int)t, 0);
         if (t == NONE) return NONE;  // merged (or out of room: reported)
         u32 src, len;
-        wave_phrase(V, (u32)p, src, len, lane, K);
+        wave_phrase<PROF>(V, (u32)p, src, len, lane, K, cy);
         nph++;
         if (lane == 0) {
             Tt.src[t] = src;
@@ -1061,9 +1155,20 @@ __device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p
         p += max(1u, len);
     }
 }
+// PROF (LZ77SSS_SMPL_PROF): per walk its clock ticks and phrase count in prof, the section
+// clocks and counts summed into V.cyc (walks starting before / at or after V.prof_split apart)
+template <bool PROF>
+__device__ __forceinline__ void walk_prof(const smpl_view& V, u64 start, u64 t0, u32 nph, const u64* cy, u32 lane,
+                                          u32* __restrict__ slot) {
+    if (lane != 0) return;
+    slot[0] = (u32)(wall_clock64() - t0);
+    slot[1] = nph;
+    const u32 bank = start < V.prof_split ? 0 : 16;
+    for (int k = 0; k < 16; k++) atomicAdd(&V.cyc[bank + k], (unsigned long long)cy[k]);
+}
 // Chunk k starts at approximate phrase k * cp (so every walk has about cp phrases to parse,
-// whatever the text's local compressibility) and ends at phrase (k + 1) * cp.  prof (debug,
-// LZ77SSS_SMPL_PROF): per walk, its clock ticks and phrase count.
+// whatever the text's local compressibility) and ends at phrase (k + 1) * cp.
+template <bool PROF>
 __global__ __launch_bounds__(64 * SWPB, 4) void k_chunk_walks(const smpl_view V, task_tab Tt, u32 cp, u32 nch,
                                                           u32* __restrict__ ex, u32* __restrict__ full,
                                                           u32* __restrict__ prof) {
@@ -1071,30 +1176,26 @@ __global__ __launch_bounds__(64 * SWPB, 4) void k_chunk_walks(const smpl_view V,
     const u32 k = blockIdx.x * SWPB + (threadIdx.x >> 6);
     if (k >= nch) return;
     const u64 a = (u64)k * cp, b = min<u64>(V.za, a + cp);
-    const u64 t0 = prof ? wall_clock64() : 0;
+    const u64 t0 = PROF ? wall_clock64() : 0;
     u32 nph = 0;
-    const u32 e = wave_walk(V, Tt, V.afst[a], V.afst[b], lane, full, nph);
-    if (lane == 0) {
-        ex[k] = e;
-        if (prof) {
-            prof[2 * k] = (u32)(wall_clock64() - t0);
-            prof[2 * k + 1] = nph;
-        }
-    }
+    u64 cy[16] = {};
+    const u64 start = V.afst[a];
+    const u32 e = wave_walk<PROF>(V, Tt, start, V.afst[b], lane, full, nph, cy);
+    if (lane == 0) ex[k] = e;
+    if constexpr (PROF) walk_prof<PROF>(V, start, t0, nph, cy, lane, prof + 2 * (u64)k);
 }
+template <bool PROF>
 __global__ __launch_bounds__(64 * SWPB, 4) void k_bridge_walks(const smpl_view V, task_tab Tt, u32 nch,
                                                            const u32* __restrict__ ex, u32* __restrict__ full,
                                                            u32* __restrict__ prof) {
     const u32 lane = threadIdx.x & 63;
     const u32 k = blockIdx.x * SWPB + (threadIdx.x >> 6);
     if (k >= nch || ex[k] == NONE) return;
-    const u64 t0 = prof ? wall_clock64() : 0;
+    const u64 t0 = PROF ? wall_clock64() : 0;
     u32 nph = 0;
-    wave_walk(V, Tt, ex[k], ~0ull, lane, full, nph);
-    if (lane == 0 && prof) {
-        prof[2 * k] = (u32)(wall_clock64() - t0);
-        prof[2 * k + 1] = nph;
-    }
+    u64 cy[16] = {};
+    wave_walk<PROF>(V, Tt, ex[k], ~0ull, lane, full, nph, cy);
+    if constexpr (PROF) walk_prof<PROF>(V, ex[k], t0, nph, cy, lane, prof + 2 * (u64)k);
 }
 // successor task of every task (ntask = the end); a missing successor is reported
 __global__ void k_task_next(task_tab Tt, u32 ntask, u32 n, u32* __restrict__ nxt, u32* __restrict__ bad) {
@@ -1188,7 +1289,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     const lce_view LV = view(d_text);
     // PA / SA (sample_index.hpp:317-353): radix sort by as many characters as 64 bits hold in
     // the text's alphabet (32 of a 4-letter text), merge sort by the text
-    u32 bits = 1, kc_max = 64;
+    u32 bits = 1, kc_max = 64, kc_side[2] = {0, 0};
     u8* code = (u8*)e_alpha.get(64 + 256);
     {
         u32* used = (u32*)code + 64;
@@ -1229,6 +1330,8 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key2, id, X, (int)c, 0, kbits, st));
             merge_sort_u32(X, tmp, c, smpl_less{LV, C, keyid, delta, left}, st);
             k_rank_of<<<cdiv(c, 256), 256, 0, st>>>(X, c, left ? PAR : SAR);
+            k_pre_table<<<cdiv(65537, 256), 256, 0, st>>>(key2, c, (u32)kbits, (left ? e_preL : e_preR).get(65537));
+            kc_side[left ? 0 : 1] = kc;
         }
     }
     u32* Pi = e_Pi.get(c);
@@ -1303,6 +1406,18 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.Psi = Psi;
     V.PAR = PAR;
     V.SAR = SAR;
+    V.pre[0] = e_preL.p;
+    V.pre[1] = e_preR.p;
+    V.code = code;
+    V.kbits_ch = bits;
+    V.kc[0] = kc_side[0];
+    V.kc[1] = kc_side[1];
+    {
+        const u64 nblk = (n >> 8) + 2;
+        u32* wb = e_wblk.get(nblk);
+        k_wblk<<<cdiv(c, 256), 256, 0, st>>>(C, c, nblk, wb);
+        V.wblk = wb;
+    }
     V.CS = dCS;
     V.gcb = dCS + 257;
     V.gwd = dCS + 514;
@@ -1318,19 +1433,22 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.mode = transf_mode;
     V.small_t = SMALL_T;
     if (const char* e = std::getenv("LZ77SSS_SMPL_SMALL")) V.small_t = (u32)std::max(0L, std::atol(e));
+    V.scan_t = SCAN_T;
+    if (const char* e = std::getenv("LZ77SSS_SMPL_SCAN")) V.scan_t = (u32)std::max(0L, std::atol(e));
     build_adjacent(V);
     V.cyc = nullptr;
     if (std::getenv("LZ77SSS_SMPL_PROF")) {
-        V.cyc = (unsigned long long*)e_cyc.get(16);
-        LZ_HIP(hipMemsetAsync(V.cyc, 0, 128, st));
+        V.cyc = (unsigned long long*)e_cyc.get(32);
+        LZ_HIP(hipMemsetAsync(V.cyc, 0, 256, st));
         const char* sp = std::getenv("LZ77SSS_SMPL_PROF_SPLIT");
         V.prof_split = sp ? (u32)std::atoll(sp) : 0u;
     }
     // the chain (chunk walks + bridges, then the path from position 0 by pointer doubling).
-    // Chunks hold SMPL_CHUNK approximate phrases each (the walks re-synchronise with the true
-    // chain within a few phrases); cut by phrase count, not bytes, so a low-compressibility
-    // stretch (short phrases) does not give a few walks most of the work.
-    u32 cp = SMPL_CHUNK;
+    // Chunks hold cp approximate phrases each (the walks re-synchronise with the true chain
+    // within a few phrases, so longer chunks leave less to the bridges); cut by phrase count, not
+    // bytes, so a low-compressibility stretch (short phrases) does not give a few walks most of
+    // the work; at least SMPL_WALKS walks (four per wave slot of the chip) while cp >= 32
+    u32 cp = (u32)std::max<u64>(32, std::min<u64>(SMPL_CHUNK, za / SMPL_WALKS));
     if (const char* e = std::getenv("LZ77SSS_SMPL_CHUNK")) cp = (u32)std::max(1L, std::atol(e));
     const u32 nch = (u32)(((u64)za + cp - 1) / cp);
     // task capacity: the chain (z <= z_approx) plus the walks before they merge; a full
@@ -1361,10 +1479,12 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         LZ_HIP(hipMemsetAsync(Tt.keys, 0, (size_t)hsz * 4, st));
         LZ_HIP(hipMemsetAsync(ctr + 8, 0, 16, st));
         if (prof) LZ_HIP(hipMemsetAsync(prof, 0, (4 * (size_t)nch + 4) * 4, st));
-        k_chunk_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, cp, nch, ex, full, prof);
+        if (prof) k_chunk_walks<true><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, cp, nch, ex, full, prof);
+        else k_chunk_walks<false><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, cp, nch, ex, full, nullptr);
         LZ_HIP(hipGetLastError());
         timer.mark("smpl_tasks");
-        k_bridge_walks<<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full, prof ? prof + 2 * (u64)nch : nullptr);
+        if (prof) k_bridge_walks<true><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full, prof + 2 * (u64)nch);
+        else k_bridge_walks<false><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full, nullptr);
         LZ_HIP(hipGetLastError());
         LZ_HIP(hipMemcpyAsync(hc, ctr + 8, 8, hipMemcpyDeviceToHost, st));
         LZ_HIP(hipStreamSynchronize(st));
@@ -1374,18 +1494,21 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     }
     const u32 ntask = hc[0];
     if (V.cyc) {
-        u64 hcy[16];
-        LZ_HIP(hipMemcpy(hcy, V.cyc, 128, hipMemcpyDeviceToHost));
+        u64 hcy[32];
+        LZ_HIP(hipMemcpy(hcy, V.cyc, 256, hipMemcpyDeviceToHost));
         for (int bank = 0; bank < 2; bank++) {
-            const u64* h = hcy + 8 * bank;
-            const double tot = (double)(h[0] + h[1] + h[2] + h[7]) + 1e-9, ph = (double)std::max<u64>(1, h[6]);
+            const u64* h = hcy + 16 * bank;
+            const double tot = (double)(h[0] + h[1] + h[2] + h[7] + h[14]) + 1e-9, ph = (double)std::max<u64>(1, h[6]);
             std::fprintf(stderr,
-                         "[lz77sss] smpl %s %u: phrases=%llu clocks/phrase=%.0f: position probes + PA interval %.1f%%, witnesses %.1f%%, "
-                         "probe intervals %.1f%%, intersect %.1f%%; probes/phrase=%.2f queries/probe=%.2f coop "
-                         "queries/probe=%.2f\n",
+                         "[lz77sss] smpl %s %u: phrases=%llu clocks/phrase=%.0f: position probes %.1f%% (searches "
+                         "%.1f%%, %.1f steps; lighter %.1f%%, %.1f steps; %.1f lanes/phrase), PA interval %.1f%%, "
+                         "witnesses %.1f%%, probe intervals %.1f%%, intersect %.1f%%; probes/phrase=%.2f "
+                         "queries/probe=%.2f coop queries/probe=%.2f (left to the wave %.2f)\n",
                          bank ? "at/after" : "before", V.prof_split, (unsigned long long)h[6], tot / ph,
-                         100 * h[0] / tot, 100 * h[1] / tot, 100 * h[7] / tot, 100 * h[2] / tot, h[3] / ph,
-                         (double)h[5] / std::max<u64>(1, h[3]), (double)h[4] / std::max<u64>(1, h[3]));
+                         100 * h[0] / tot, 100 * h[8] / tot, (double)h[12] / ph, 100 * h[9] / tot, (double)h[11] / ph,
+                         (double)h[13] / ph, 100 * h[14] / tot, 100 * h[1] / tot, 100 * h[7] / tot, 100 * h[2] / tot,
+                         h[3] / ph, (double)h[5] / std::max<u64>(1, h[3]), (double)h[4] / std::max<u64>(1, h[3]),
+                         (double)h[15] / std::max<u64>(1, h[3]));
         }
     }
     if (prof) {

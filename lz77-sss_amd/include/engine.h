@@ -214,6 +214,7 @@ struct engine {
     // exact-smpl (csrc/smpl.hip): samples, PA / SA orders, grid, phrase tasks
     dbuf<u32> e_afact, e_afst, e_tmp1, e_tmp2, e_C, e_PA, e_SA, e_PAR, e_SAR, e_Pi, e_Psi, e_CS;
     dbuf<u32> e_alpha;  // exact-smpl: the character codes of the sort keys and the text's character flags
+    dbuf<u32> e_preL, e_preR, e_wblk;  // exact-smpl: first ranks per 16-bit key prefix (PA, SA); first sample per 256-block
     dbuf<u64> e_cyc;  // exact-smpl debug counters (LZ77SSS_SMPL_PROF)
     dbuf<u32> e_gx, e_gy, e_gw, e_cell, e_adjL, e_adjR;
     dbuf<u32> e_rst[10];  // exact-smpl: row sparse tables of the grid cells' lightest weights
