@@ -191,8 +191,8 @@ def main():
                     help="approx = configs[1]/[2] (3-aprx); exact = configs[4] (exact factorization); "
                          "sss = the sharded pos_t=uint64 sync-set pass of configs[3] (chr19-style text)")
     ap.add_argument("--transf-mode", default="with_samples", choices=["naive", "with_samples", "without_samples", "full_sa"],
-                    help="--mode exact: factorize_exact's transform_mode (configs[4]: with_samples, the sample index "
-                         "with interval sampling; full_sa is the device extension)")
+                    help="--mode exact: factorize_exact's transform_mode (configs[4]: with_samples, the sample index; "
+                         "full_sa is the device extension)")
     ap.add_argument("--size-gib", type=float, default=50.0,
                     help="--mode sss / --workload chr19: text size in GiB (configs[3]: 50)")
     ap.add_argument("--cpu-sample-mib", type=int, default=-1,

@@ -101,6 +101,7 @@ struct smpl_view {
     int mode;                // LZ77SSS_TRANSF_*
     u32 small_t;             // intersect queries with a side of at most this many ranks run on their own lane
     u32 scan_t;              // the wave scans a side of at most this many ranks (else the grid)
+    u32 lane_scan;           // a lane scans PA intervals of fewer ranks for the answer
     iv_levels sM;            // SA order: adjacent sample-suffix LCEs (sM.mn[0][r] = LCE of ranks r - 1, r) and their
                              // sparse-table minima; the SA interval of any right extension by binary lifting
     iv_levels pM;            // PA order: the same over the left contexts (capped at delta)
@@ -646,7 +647,7 @@ struct lane_cache {
     bool has;
 };
 
-constexpr u32 LANE_SCAN = 8;   // PA intervals scanned whole on the lane
+constexpr u32 LANE_SCAN = 32;  // PA intervals scanned whole on the lane
 
 // ---- one exact phrase at i (transform_to_exact_{naive,without_samples,with_samples}) --
 // executed by a whole wave; returns (src, len) in every lane.
@@ -765,7 +766,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         // its context ends with T[i..j]; the probes below finish between the bounds.
         bool done = !run;
         if (run) {
-            if (xe - xb < LANE_SCAN) {
+            if (xe - xb < V.lane_scan) {
                 for (u32 x = xb; x <= xe; x++) {
                     if (V.PA[x] < W) {
                         const u32 y = V.Pi[x], l = lce_of_rank(V.sM, y, rs, h_lo, h_hi);
@@ -1433,6 +1434,8 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     V.mode = transf_mode;
     V.small_t = SMALL_T;
     if (const char* e = std::getenv("LZ77SSS_SMPL_SMALL")) V.small_t = (u32)std::max(0L, std::atol(e));
+    V.lane_scan = LANE_SCAN;
+    if (const char* e = std::getenv("LZ77SSS_SMPL_LSCAN")) V.lane_scan = (u32)std::max(0L, std::atol(e));
     V.scan_t = SCAN_T;
     if (const char* e = std::getenv("LZ77SSS_SMPL_SCAN")) V.scan_t = (u32)std::max(0L, std::atol(e));
     build_adjacent(V);
