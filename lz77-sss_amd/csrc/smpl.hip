@@ -65,6 +65,12 @@ constexpr u32 SG_WIN = LZ_SG_WIN;    // smallest grid cell width in ranks (the r
 constexpr u32 SG_GMAX = 512;         // cells per side at most: wider blocks get wider cells
 constexpr u32 SG_LV = 10;            // row sparse-table levels (2^9 = SG_GMAX / 1)
 constexpr u32 SWPB = 4;              // waves per workgroup of the phrase kernels
+#ifndef SMPL_OCC
+#define SMPL_OCC 6                   // waves per SIMD the walk kernels are register-bounded for: the walks
+                                     // are bound by L2-miss traffic, more waves in flight beat the spills
+                                     // (genome 1 GiB k_chunk_walks: 4 -> 981 ms, 5 -> 922, 6 -> 832, 7 -> 860,
+                                     // 8 -> 883)
+#endif
 constexpr u32 SMPL_CHUNK = 1024;     // approximate phrases per chunk walk at most
 constexpr u32 SMPL_WALKS = 16384;    // chunk walks wanted
 
@@ -1170,7 +1176,7 @@ __device__ __forceinline__ void walk_prof(const smpl_view& V, u64 start, u64 t0,
 // Chunk k starts at approximate phrase k * cp (so every walk has about cp phrases to parse,
 // whatever the text's local compressibility) and ends at phrase (k + 1) * cp.
 template <bool PROF>
-__global__ __launch_bounds__(64 * SWPB, 4) void k_chunk_walks(const smpl_view V, task_tab Tt, u32 cp, u32 nch,
+__global__ __launch_bounds__(64 * SWPB, SMPL_OCC) void k_chunk_walks(const smpl_view V, task_tab Tt, u32 cp, u32 nch,
                                                           u32* __restrict__ ex, u32* __restrict__ full,
                                                           u32* __restrict__ prof) {
     const u32 lane = threadIdx.x & 63;
@@ -1186,7 +1192,7 @@ __global__ __launch_bounds__(64 * SWPB, 4) void k_chunk_walks(const smpl_view V,
     if constexpr (PROF) walk_prof<PROF>(V, start, t0, nph, cy, lane, prof + 2 * (u64)k);
 }
 template <bool PROF>
-__global__ __launch_bounds__(64 * SWPB, 4) void k_bridge_walks(const smpl_view V, task_tab Tt, u32 nch,
+__global__ __launch_bounds__(64 * SWPB, SMPL_OCC) void k_bridge_walks(const smpl_view V, task_tab Tt, u32 nch,
                                                            const u32* __restrict__ ex, u32* __restrict__ full,
                                                            u32* __restrict__ prof) {
     const u32 lane = threadIdx.x & 63;
