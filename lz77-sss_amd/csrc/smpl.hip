@@ -653,6 +653,7 @@ struct lane_cache {
     bool has;
 };
 
+constexpr u32 BISECT_T = 128;   // right-extension bounds this close are bisected at once
 constexpr u32 LANE_SCAN = 32;  // PA intervals scanned whole on the lane
 
 // ---- one exact phrase at i (transform_to_exact_{naive,without_samples,with_samples}) --
@@ -817,9 +818,11 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
             bool cand = false;
             if (run) {
                 // the largest possible x first (its intervals are the narrowest, and it is often
-                // the answer), then the exponential search up from lo and bisection: the predicate
-                // is monotone in x, so the answer is the reference's
-                x = bin ? lo + (hi - lo) / 2 : top ? hi - 1 : min(lo + step, hi - 1);
+                // the answer), then bisection between the witness and the failed probes when they
+                // are at most BISECT_T apart (its probes stay well above lo, where the intervals
+                // are narrow), else an exponential search up from lo first: the predicate is
+                // monotone in x, so the answer is the reference's upward exponential search's
+                x = top ? hi - 1 : bin ? lo + (hi - lo) / 2 : min(lo + step, hi - 1);
                 cand = h_lo >= x || h_hi >= x;
                 if (cand) iv_around(V.sM, V.c, rs, h_lo, h_hi, x, nb, ne);
             }
@@ -841,7 +844,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
                     if (!bin && !top) step *= 2;
                 } else {
                     hi = x;
-                    if (!top) bin = true;
+                    if (!top || hi - lo <= BISECT_T) bin = true;
                 }
                 top = false;
                 if (hi - lo <= 1) run = false;
