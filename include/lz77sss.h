@@ -116,8 +116,9 @@ int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_
  * reference's exact modes produce at p = 1.  transf_mode naive, with_samples and
  * without_samples run the reference's exact-smpl path on the device (csrc/smpl.hip:
  * the 3-approximation, the sample index over its phrase ends and delta-samples, the
- * decomposed weighted square grid; with_samples adds the RKS fingerprints and the
- * interval samples; lz77_sss.hpp:558-709, transform_to_exact/{naive,with_samples,without_samples}.cpp); their sources are
+ * decomposed weighted square grid, and per order keyed insertion ranks over adjacent-LCE
+ * and weight sparse tables, which answer every interval query with_samples' interval
+ * samples would; lz77_sss.hpp:558-709, transform_to_exact/{naive,with_samples,without_samples}.cpp); their sources are
  * the lighter points the range queries find.  LZ77SSS_TRANSF_FULL_SA computes the
  * same lengths from LPF over the full suffix array of the text (csrc/exact.hip; 44 B
  * per character, n < 2^31) with the PSV/NSV source rule.  The sample-index modes require

@@ -49,7 +49,7 @@ def test_full_size_stream_hash(lz, name):
         else:  # generated in HBM (the host generator of make_stream_hashes.py makes the same bytes)
             s.gen_genome(n, a["base_len"], a["mut"], a["seed"])
         mode = e.get("mode", "lpf_opt")
-        if mode == "exact_lengths":  # configs[4]: the sample-index path with interval samples
+        if mode == "exact_lengths":  # configs[4]: the sample-index path (transf_mode with_samples)
             z = s.factorize_exact(transf_mode=lz.WITH_SAMPLES)
             F = s.factors(z)
             assert s.verify() == 0
