@@ -233,9 +233,13 @@ int lz77sss_session_get_lpf64(lz77sss_session* s, uint64_t* out3, uint64_t cap, 
 /* Per-phase times (ms, hipEvent-timed) of the last call; returns the count. */
 int lz77sss_session_phase_times(lz77sss_session* s, double* ms, const char** names, int cap);
 /* Device memory per phase of the last call, in the order of lz77sss_session_phase_times: the
- * bytes the session's buffers held when the phase was enqueued (held), their peak during the phase
- * (peak), and the GPU's free memory then (hbm_free, hipMemGetInfo).  The text itself (n + 64 KiB)
- * is not in held/peak.  Returns the number of phases (or a negative error). */
+ * bytes the process's engine buffers held when the phase was enqueued (held), their peak during the
+ * phase (peak), and the GPU's free memory then (hbm_free: hipMemGetInfo at the call's start, later
+ * phases derived from the process's allocations since; every phase queried when LZ77SSS_PHASE_MEM is
+ * set).  held / peak are process-wide: with several sessions in one process they count all of them.
+ * A lean call (texts of 8 GiB and more) starts with a "release" phase that frees the last call's
+ * emitter buffers, so the later peaks do not include them.  The text itself (n + 64 KiB) is not in
+ * held/peak.  Returns the number of phases (or a negative error). */
 int lz77sss_session_phase_mem(lz77sss_session* s, uint64_t* held, uint64_t* peak, uint64_t* hbm_free, int cap);
 /* Statistics of the last factorize call: [size_sss, has_runs, num_lpf, len_lpf_phr,
  * num_gaps, patt_lens[5], roll_threshold, log2_size_h, greedy_rounds, fixups, ...]. */

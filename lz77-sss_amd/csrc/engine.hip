@@ -114,7 +114,10 @@ void engine::prepare_phrases(int phr_mode, bool external_sss) {
     const char* lean_env = std::getenv("LZ77SSS_LEAN");
     const bool lean_mode = lean_env ? lean_env[0] != '0' : n >= (1ull << 33);
     lean = lean_mode;
-    if (lean_mode) release_greedy_buffers();  // the last call's emitter buffers go before the phases grow
+    if (lean_mode) {
+        release_greedy_buffers();  // the last call's emitter buffers go before the phases grow
+        timer.mark("release");     // (the phases after it report peaks without those buffers)
+    }
     phr_info.valid = false;
     if (std::getenv("LZ77SSS_LCE_DEBUG") && !lce_dbg) {
         LZ_HIP(hipMalloc(&lce_dbg, 8 * sizeof(unsigned long long)));

@@ -2203,6 +2203,16 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
     G.negpow = d_negpow;
     u32 zmask0 = 0;
     for (int x = 0; x < 5; x++) zmask0 |= (G.lens[x] >= N) ? (1u << x) : 0u;  // reinit(0) at construction
+    // test knobs of the chain-insert kernels, read once per call: a small long-range list and a
+    // short "long" range make the overflow path run
+    const u32 knob_lng_cap = [] {
+        const char* e = std::getenv("LZ77SSS_TEST_LNG_CAP");
+        return e ? (u32)std::max<long>(0, std::atol(e)) : 0xFFFFFFFFu;
+    }();
+    const u32 knob_long_words = [] {
+        const char* e = std::getenv("LZ77SSS_TEST_LONG_WORDS");
+        return e ? (u32)std::max<long>(1, std::atol(e)) : 2048u;
+    }();
     const char* ch_env = std::getenv("LZ77SSS_GAP_CHUNK");  // tuning knob (walk length per segment)
     const u32 CH = std::getenv("LZ77SSS_NO_CHUNK") ? 0x0FFFFFFFu : ch_env ? (u32)std::max(16, std::atoi(ch_env)) : 512u;
     const char* mo_env = std::getenv("LZ77SSS_GREEDY_MAX_OUTER");  // test knob (0: sequential only)
@@ -2943,14 +2953,8 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     // whole grid instead
                     constexpr u32 LNG_CAP = 1024;
                     // test knobs: a small list and a short "long" range make the overflow path run
-                    const u32 lng_cap = [&] {
-                        const char* e = std::getenv("LZ77SSS_TEST_LNG_CAP");
-                        return e ? (u32)std::min<long>(LNG_CAP, std::max<long>(0, std::atol(e))) : LNG_CAP;
-                    }();
-                    const u32 long_words = [] {
-                        const char* e = std::getenv("LZ77SSS_TEST_LONG_WORDS");
-                        return e ? (u32)std::max<long>(1, std::atol(e)) : 2048u;
-                    }();
+                    const u32 lng_cap = std::min(LNG_CAP, knob_lng_cap);
+                    const u32 long_words = knob_long_words;
                     u32* lng = (u32*)g_lng.get(2 + 4 * LNG_CAP);
                     LZ_HIP(hipMemsetAsync(lng, 0, 8, st));
                     k_chain_inserts<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2,

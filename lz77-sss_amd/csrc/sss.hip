@@ -496,7 +496,28 @@ __device__ __forceinline__ u32 min3u(u32 a, u32 b, u32 c) {
 // such a multiple).  The chance 16-byte repeats of a random ACGT text then pass only at d close to
 // 170, where the stretch is short (all inside the block: A + 186 <= 442, compared from the
 // registers by cross-lane moves).
-__device__ __forceinline__ u64 shfl64(u64 v, u32 src);
+// 8 bytes at byte offset 8 lane + p of the 1024-byte concatenation [Bx, By] of two blocks in
+// registers (p <= 170): the lane's words lane + p/8 and lane + p/8 + 1, by cross-lane moves
+__device__ __forceinline__ u64 shfl64(u64 v, u32 src) {
+    return ((u64)(u32)__shfl((int)(u32)(v >> 32), (int)src, 64) << 32) | (u32)__shfl((int)(u32)v, (int)src, 64);
+}
+// the same from the blocks' word rotations a = shfl64(Bx, (lane + p/8) & 63), c = shfl64(By, ...)
+// (a streaming caller rotates every block once and uses it for two blocks)
+__device__ __forceinline__ u64 shifted8_rot(u64 a, u64 c, u64 By, u32 p, u32 lane) {
+    const u32 q = p >> 3, sh = 8 * (p & 7);
+    const u64 w0 = lane + q >= 64 ? c : a;
+    if (!sh) return w0;
+    // word lane + q + 1: lane + 1's w0; for lane 63 word 64 + q, i.e. By's lane q
+    u64 w1 = ((u64)dpp<0x130>(0u, (u32)(w0 >> 32)) << 32) | dpp<0x130>(0u, (u32)w0);
+    if (lane == 63)
+        w1 = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(By >> 32), (int)q) << 32) |
+             (u32)__builtin_amdgcn_readlane((int)(u32)By, (int)q);
+    return (w0 >> sh) | (w1 << (64 - sh));
+}
+__device__ __forceinline__ u64 shifted8(u64 Bx, u64 By, u32 p, u32 lane) {
+    const u32 src = (lane + (p >> 3)) & 63;
+    return shifted8_rot(shfl64(Bx, src), shfl64(By, src), By, p, lane);
+}
 __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
     const u32 lo = (u32)B, hi = (u32)(B >> 32);
     const u32 li = lane & 31, grp = lane >> 5;
@@ -532,10 +553,12 @@ __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
                   ? 1u << k : 0u;
     if (li >= (u32)FA_LANES) hk = 0;
     u32 res = 0;
-    for (u64 hm = __ballot(hk != 0); hm; hm &= hm - 1) {
+    // (a confirmed half drops its other candidate lanes at once: on run-heavy text every even shift
+    // of a period-2 run is a candidate, and skipping them one by one cost ~600 SALU per block)
+    for (u64 hm = __ballot(hk != 0); hm;) {
         const u32 L = (u32)__builtin_ctzll(hm);
         const u32 g = L >> 5;
-        if (res & (1u << g)) continue;
+        hm &= hm - 1;
         const u64 x = shfl64(B, (32 * g + lane) & 63);  // bytes A + 8 lane .. + 7
         for (u32 bits = (u32)__builtin_amdgcn_readlane((int)hk, (int)L); bits; bits &= bits - 1) {
             const u32 d = 84 + 4 * (L & 31) + (u32)__builtin_ctz(bits);
@@ -555,11 +578,98 @@ __device__ __forceinline__ u32 sss_filter(u64 B, u32 lane) {
             }
             if (!__ballot(bad)) {
                 res |= 1u << g;
+                hm &= g ? 0ull : 0xFFFFFFFF00000000ull;
                 break;
             }
         }
     }
     return res;
+}
+
+// The smallest period q <= 170 of a 512-byte block Bx (lane L: bytes 8L .. 8L + 7) whose next
+// block is By: the smallest q with T[z] == T[z + q] for the block's 512 positions (0: none).  A
+// period of the block is a shift at which its first 8 bytes recur, so only those shifts are
+// verified, in increasing order (lane L finds the recurrences at q = 3L + 1 .. 3L + 3 from its
+// words j0 .. j0 + 2; one ballot per verified candidate instead of one per shift)
+__device__ __forceinline__ u32 smallest_period(u64 Bx, u64 By, u32 lane) {
+    const u64 A = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(Bx >> 32), 0) << 32) |
+                  (u32)__builtin_amdgcn_readlane((int)(u32)Bx, 0);
+    const u32 j0 = (3 * lane + 1) >> 3;
+    const u64 w0 = shfl64(Bx, j0 & 63), w1 = shfl64(Bx, (j0 + 1) & 63), w2 = shfl64(Bx, (j0 + 2) & 63);
+    u64 m[3];
+#pragma unroll
+    for (u32 k = 0; k < 3; k++) {
+        const u32 q = 3 * lane + 1 + k, r = q - 8 * j0;  // r <= 9
+        const u64 v = r == 0 ? w0 : r < 8 ? (w0 >> (8 * r)) | (w1 << (64 - 8 * r))
+                                 : r == 8 ? w1 : (w1 >> (8 * (r - 8))) | (w2 << (64 - 8 * (r - 8)));
+        m[k] = __ballot(q <= QL && v == A);
+    }
+    for (;;) {
+        u32 best = 0xFFFFu;
+#pragma unroll
+        for (u32 k = 0; k < 3; k++)
+            if (m[k]) best = min(best, 3u * (u32)__builtin_ctzll(m[k]) + 1 + k);
+        if (best > QL) return 0;
+        m[(best - 1) % 3] &= ~(1ull << ((best - 1) / 3));
+        if (!__ballot(shifted8(Bx, By, best, lane) != Bx)) return best;
+    }
+}
+
+// Run scan of a stripe pass 1 stopped (the first phase of k_sss_runs): blocks 0 .. 65 streamed
+// through the wave's LDS ring (chunks of 8 blocks; three register buffers, the loads of chunk g + 2
+// issued before chunk g is stored, so 16 blocks stay in flight through each store's wait; the loop
+// is unrolled, so nothing is copied -- a copy of a loading register waits for its load), each
+// compared with its bytes P ahead, P = the smallest period <= 170 of block 1 (0: none).  Returns
+// whether all 66 blocks have it (a pure run: every window of the stripe's decisions P-periodic, in
+// Q, none of its decisions in S); clean = the blocks before the first chunk with a break (they all
+// have the period P).  Stops at the first such chunk.  Full stripes only
+// (loads reach block 71: inside the text pad for every stripe but the last).
+// (tools/microbench/stream_runs.hip k_pure_v1: this loop alone reads the 1 GiB rr text at 5.6 TB/s)
+constexpr u32 RM_CH = 8;
+__device__ __forceinline__ bool run_scan(const u8* __restrict__ Tw, u64* __restrict__ ring, u32 rs, u32 lane,
+                                         u32& P, u32& clean) {
+    auto load8 = [&](u32 k) -> u64 { return *(const u64*)(Tw + (u64)k * TAU); };
+    u64 Q[3][RM_CH];
+#pragma unroll
+    for (u32 d = 0; d < 2; d++)
+#pragma unroll
+        for (u32 e = 0; e < RM_CH; e++) Q[d][e] = load8(d * RM_CH + e);
+    u32 ol = 0, sh = 0;
+    P = 0;
+    clean = 0;
+#pragma unroll
+    for (u32 g = 0; g <= 9; g++) {
+        const u32 c = RM_CH * g;
+        if (g + 2 <= 8) {
+#pragma unroll
+            for (u32 e = 0; e < RM_CH; e++) Q[(g + 2) % 3][e] = load8(c + 2 * RM_CH + e);
+        }
+        if (g <= 8) {
+#pragma unroll
+            for (u32 e = 0; e < RM_CH; e++) ring[((c + e) % rs) * 64 + lane] = Q[g % 3][e];
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (g == 0) {
+            // the period of block 1 (blocks 1, 2 in the ring)
+            P = smallest_period(ring[64 + lane], ring[128 + lane], lane);
+            if (!P) return false;
+            ol = lane + (P >> 3);
+            sh = 8 * (P & 7);
+            continue;
+        }
+        u64 acc = 0;
+#pragma unroll
+        for (u32 j = 0; j < RM_CH; j++) {
+            const u32 k = c - RM_CH + j;
+            if (k > 65) break;
+            const u32 o = (k % rs) * 64;
+            const u64 lo = ring[(o + ol) % (rs * 64)], hi = ring[(o + ol + 1) % (rs * 64)];
+            acc |= ring[o + lane] ^ (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo);
+        }
+        if (__ballot(acc != 0)) return false;
+        clean = min(c, 66u);
+    }
+    return true;
 }
 
 template <bool QSKIP, bool PASS1>
@@ -734,7 +844,8 @@ __global__ __launch_bounds__(64 * SWAVES, 5) void k_sss_stream(const u8* __restr
             filt(1, B1);
         }
         // a stripe with a hit in its decision blocks is re-run; it stops here and build_sss
-        // marks all of its anchors' tiles for the exact Q pass
+        // marks all of its anchors' tiles for the exact Q pass (k_sss_runs settles
+        // most such stripes first)
         if (dirty) goto stripe_done;
         block_prefix(B0, carry, hA);
         block_prefix(B1, carry, hB);
@@ -855,23 +966,10 @@ stripe_done:
             if (!dirty && (hw0 | hw1 | hw2) && __hip_atomic_load(mark_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
                 atomicOr(mark_flag, 1u);
         }
-        // the anchors past the last stripe's own (its halo and the read pad) start out empty too
-        if (w + 1 == nstripes) {
-            const u64 nanch = (n - TAU) / QA + 2, t_tail = w * (u64)(SD / QA) + 4 * nblk;
-            for (u64 t = t_tail + lane; t < nanch + 64; t += 64) {
-                q_init[t] = 0xFF00;
-                if (t < nanch) rp_init[t] = 0;
-            }
-        }
-        // Q intervals and periods of the stripe's own anchors start out empty (k_q_anchors
-        // overwrites the tiles the filter marked)
-        if (lane < nblk) {
-            const u64 t = w * (u64)(SD / QA) + 4 * lane;
-            *(u64*)(q_init + t) = 0xFF00FF00FF00FF00ull;
-            *(u32*)(rp_init + t) = 0u;
-        }
-        // the per-block run records start out unknown (k_sss_runs writes the stripes it settles);
-        // the last stripe also clears the blocks past its own, up to nbk inclusive
+        // (the Q intervals and periods of the anchors are not cleared here: build_sss clears
+        // them only when some tile needs the Q-anchor pass, or a stripe the fallback)
+        // the per-block run records start out unknown (k_sss_runs writes the stripes it
+        // settles); the last stripe also clears the blocks past its own, up to nbk inclusive
         {
             const u64 gk = w * (u64)SNB + lane;
             if (gk <= nbk) {
@@ -964,50 +1062,44 @@ __device__ u32 q_classify(u64 pd0, u64 pd1, u32 p, u32 lane, u32& u) {
     u = ~per & ~(longA | longB) & 0xFFu;
     return per;
 }
-// the smallest period q <= 170 of T[j..j+512) (0: none).  Lane l tests q = base + l; wrong
-// candidates fail at their first differing word
+// the smallest period q <= 170 of the window T[j..j+512) (0: none): T[z] == T[z + q] for z in
+// [j, j + 512 - q).  Candidates are the shifts at which the window's first 8 bytes recur (as in
+// smallest_period), each verified by one masked compare of the window's words (lane L: bytes
+// 8L .. 8L + 7) against the shifted ones
 __device__ u32 find_period(const u8* __restrict__ T, u64 j, u32 lane) {
-    for (u32 base = 1; base <= QL; base += 64) {
-        const u32 q = base + lane;
-        bool ok = q <= QL;
-        if (ok) {
-            const u32 len = TAU - q;
-            for (u32 o = 0; o < len; o += 8) {
-                u64 a = ldu64(T + j + o), c = ldu64(T + j + q + o);
-                const u32 r = len - o;
-                if (r < 8) {
-                    const u64 m = (1ull << (8 * r)) - 1;
-                    a &= m;
-                    c &= m;
-                }
-                if (a != c) {
-                    ok = false;
-                    break;
-                }
-            }
-        }
-        const u64 bal = __ballot(ok);
-        if (bal) return base + (u32)__builtin_ctzll(bal);
+    const u64 W = ldu64(T + j + 8 * lane), W2 = ldu64(T + j + TAU + 8 * lane);
+    const u64 A = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(W >> 32), 0) << 32) |
+                  (u32)__builtin_amdgcn_readlane((int)(u32)W, 0);
+    const u32 j0 = (3 * lane + 1) >> 3;
+    const u64 w0 = shfl64(W, j0 & 63), w1 = shfl64(W, (j0 + 1) & 63), w2 = shfl64(W, (j0 + 2) & 63);
+    u64 m[3];
+#pragma unroll
+    for (u32 k = 0; k < 3; k++) {
+        const u32 q = 3 * lane + 1 + k, r = q - 8 * j0;  // r <= 9
+        const u64 v = r == 0 ? w0 : r < 8 ? (w0 >> (8 * r)) | (w1 << (64 - 8 * r))
+                                 : r == 8 ? w1 : (w1 >> (8 * (r - 8))) | (w2 << (64 - 8 * (r - 8)));
+        m[k] = __ballot(q <= QL && v == A);
     }
-    return 0;
-}
-// 8 bytes at byte offset 8 lane + p of the 1024-byte concatenation [Bx, By] of two blocks in
-// registers (p <= 170): the lane's words lane + p/8 and lane + p/8 + 1, by cross-lane moves
-__device__ __forceinline__ u64 shfl64(u64 v, u32 src) {
-    return ((u64)(u32)__shfl((int)(u32)(v >> 32), (int)src, 64) << 32) | (u32)__shfl((int)(u32)v, (int)src, 64);
-}
-__device__ __forceinline__ u64 shifted8(u64 Bx, u64 By, u32 p, u32 lane) {
-    const u32 q = p >> 3, sh = 8 * (p & 7);
-    const u32 src = (lane + q) & 63;
-    const u64 a = shfl64(Bx, src), c = shfl64(By, src);
-    const u64 w0 = lane + q >= 64 ? c : a;
-    if (!sh) return w0;
-    // word lane + q + 1: lane + 1's w0; for lane 63 word 64 + q, i.e. By's lane q
-    u64 w1 = ((u64)dpp<0x130>(0u, (u32)(w0 >> 32)) << 32) | dpp<0x130>(0u, (u32)w0);
-    if (lane == 63)
-        w1 = ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(By >> 32), (int)q) << 32) |
-             (u32)__builtin_amdgcn_readlane((int)(u32)By, (int)q);
-    return (w0 >> sh) | (w1 << (64 - sh));
+    for (;;) {
+        u32 q = 0xFFFFu;
+#pragma unroll
+        for (u32 k = 0; k < 3; k++)
+            if (m[k]) q = min(q, 3u * (u32)__builtin_ctzll(m[k]) + 1 + k);
+        if (q > QL) return 0;
+        m[(q - 1) % 3] &= ~(1ull << ((q - 1) / 3));
+        const u32 len = TAU - q, o = 8 * lane;
+        u64 a = W, c = shifted8(W, W2, q, lane);
+        bool bad = false;
+        if (o < len) {
+            if (len - o < 8) {
+                const u64 mk = (1ull << (8 * (len - o))) - 1;
+                a &= mk;
+                c &= mk;
+            }
+            bad = a != c;
+        }
+        if (!__ballot(bad)) return q;
+    }
 }
 // first / last nonzero byte of a wave's 512 p-differences (block offsets), -1 if none
 __device__ __forceinline__ int first_diff(u64 d) {
@@ -1029,25 +1121,64 @@ __device__ __forceinline__ int last_diff(u64 d) {
 
 // (113 VGPRs = 4 waves per SIMD; bounding it to the 5 its LDS allows spills 17 VGPRs and was
 // slower on rr: 0.518 vs 0.483 ms for the SSS kernels, tools/gpu_r03b.sh)
-__global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restrict__ T, u64 n, u64 last_i, u64 nstripes,
+// (one wave per workgroup: a workgroup's slot is held until its slowest wave ends, and a stripe
+// with run boundaries walks several times longer than a pure run)
+constexpr int RWAVES = 1;
+__global__ __launch_bounds__(64 * RWAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_sss_runs(const u8* __restrict__ T, u64 n, u64 last_i, u64 nstripes,
                                                         pos_t* __restrict__ s_out, u32* __restrict__ s_cnt,
                                                         u32* __restrict__ s_flag, u32* __restrict__ ovf_ctr, u32 b,
                                                         sss_pow32 PW, u32 scap, u64* __restrict__ hitw,
                                                         u8* __restrict__ blk_p, u16* __restrict__ blk_fo,
                                                         u16* __restrict__ blk_lo, u64 nbk, u32* __restrict__ any_q,
-                                                        u32* __restrict__ dbg, u32* __restrict__ tot) {
+                                                        u32* __restrict__ dbg, u32* __restrict__ tot,
+                                                        u32* __restrict__ prof, int scan) {
     // a ring of RSL blocks per wave in LDS: the bytes at offset p of a block are two aligned word
     // reads (the block after it follows in the ring).  The text arrives RCH blocks at a time in
     // registers, loaded one chunk ahead (a register rotation per block would make every load
     // wait for the one before: one load in flight)
     constexpr u32 RSL = 16, RCH = 8;
-    __shared__ u64 s_ring[SWAVES][RSL * 64];
+    __shared__ u64 s_ring[RWAVES][RSL * 64];
     const u32 lane = threadIdx.x & 63;
     u64* ring = s_ring[threadIdx.x >> 6];
-    const u64 w = (u64)blockIdx.x * SWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const u64 w = (u64)blockIdx.x * RWAVES + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (w >= nstripes) return;
     if (!(hitw[3 * w + 2] >> 63)) return;  // settled by pass 1
+    const u64 t_start = prof ? (u64)clock64() : 0;  // LZ77SSS_RUNS_PROF: per-stripe clocks and counts
+    u32 n_phi = 0, n_cross = 0;
     const u64 i0 = w * (u64)SD;
+    // phase 1 (full stripes but the last): the run scan.  A pure run is settled here with the
+    // records and flags the walk below would produce for it (block 0: period P, first break
+    // unknown; blocks 1 .. 63: period P, no break; some window in Q; no sync position); any other
+    // stripe keeps its run map for the walk's crossings
+    const bool map_ok = scan && w + 1 < nstripes;
+    u32 mp = 0, m64 = 0, m65 = 0;
+    if (map_ok) {
+        u32 P0, clean;
+        const bool pure = run_scan(T + i0 + 8 * lane, ring, RSL, lane, P0, clean);
+        // the run map for the walk's crossings: the blocks before `clean` have the period P0
+        mp = lane < clean ? P0 : 0u;
+        m64 = clean > 64 ? P0 : 0u;
+        m65 = clean > 65 ? P0 : 0u;
+        if (pure) {
+            const u64 gk = w * (u64)SNB + lane;  // < nbk (not the last stripe)
+            blk_p[gk] = (u8)P0;
+            blk_fo[gk] = lane ? (u16)0xFFFFu : (u16)0;
+            blk_lo[gk] = 0;
+            if (prof && lane == 0) {
+                prof[4 * w] = (u32)t_start;
+                prof[4 * w + 1] = 0;
+            }
+            if (lane == 0) {
+                hitw[3 * w] = 0;
+                hitw[3 * w + 1] = 0;
+                hitw[3 * w + 2] = 1ull << 62;  // settled
+                if (__hip_atomic_load(any_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(any_q, 1u);
+                if (__hip_atomic_load(any_q + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(any_q + 4, 1u);
+            }
+            return;
+        }
+        __builtin_amdgcn_wave_barrier();  // (the walk's prologue refills the ring)
+    }
     const u64 jmax = n - TAU;
     const u64 ilim = min<u64>(last_i - i0, (u64)SD - 1);
     const u32 nblk = (u32)min<u64>((u64)SNB, ilim / TAU + 1);
@@ -1112,11 +1243,7 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
         return (hits & 4) ? 0xFFu : 0u;
     };
     // the smallest p <= 170 with T[z] == T[z+p] for every z of ring block k (bytes Bx), 0 if none
-    auto block_period = [&](u32 k, u64 Bx) -> u32 {
-        for (u32 q = 1; q <= QL; q++)
-            if (!__ballot(ring_shift(k, q) != Bx)) return q;
-        return 0;
-    };
+    auto block_period = [&](u32 k, u64 Bx) -> u32 { return smallest_period(Bx, ring[((k + 1) % RSL) * 64 + lane], lane); };
 
     u32 p = 1;  // the period of the current run
     bool fail = false, anyq = false;
@@ -1213,7 +1340,7 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
     u64 R[RCH];
     auto load_chunk = [&](u32 k0) {
 #pragma unroll
-        for (u32 e = 0; e < RCH; e++) R[e] = k0 + e < lend ? load8(k0 + e) : 0ull;
+        for (u32 e = 0; e < RCH; e++) R[e] = load8(k0 + e);  // unconditional (in the pad): no phi copies
     };
     auto store_chunk = [&](u32 k0) {
 #pragma unroll
@@ -1255,12 +1382,22 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
         }
     }
     const bool fail_pro = fail;  // block 0 unsettled
+    // the ring and the loading chunk as after refill(c), for a crossing that jumped to c
+    auto seek = [&](u32 c) {
+        const u32 cb = c & ~(RCH - 1);
+        load_chunk(cb);
+        store_chunk(cb);
+        load_chunk(cb + RCH);
+        store_chunk(cb + RCH);
+        load_chunk(cb + 2 * RCH);
+        ring_sync();
+    };
     auto refill = [&](u32 c) {
         if (c % RCH == 0 && c) {
             // blocks c + RCH .. c + 2 RCH - 1 replace c - RCH .. c - 1 (read no more); the next
             // chunk loads for RCH iterations
             store_chunk(c + RCH);
-            if (c + 2 * RCH < lend) load_chunk(c + 2 * RCH);
+            load_chunk(c + 2 * RCH);
             ring_sync();
         }
     };
@@ -1289,6 +1426,27 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
                 return ring[o + lane] ^ (sh ? ((lo >> sh) | (hi << (64 - sh))) : lo);
             };
             for (;;) {
+                if (map_ok) {
+                    // the run map: blocks whose entry is p have the period p, so the run goes on
+                    // up to the first other one (t) without reading them; jump when that saves a
+                    // chunk of loads (the blocks from t on are compared below as before)
+                    const u64 cm = __ballot(mp == p);
+                    const u32 from = c + 2;
+                    u32 t = from;
+                    if (from < 64) {
+                        const u64 nc = ~cm & (~0ull << from);
+                        t = nc ? (u32)__builtin_ctzll(nc) : 64u;
+                    }
+                    if (t == 64 && m64 == p) t = 65;
+                    if (t == 65 && m65 == p) t = 66;
+                    const u32 jt = min(t - 2, nblk);
+                    if (jt >= c + RCH) {
+                        n_cross += jt - c;
+                        c = jt;
+                        seek(c);
+                        if (c >= nblk) break;
+                    }
+                }
                 u32 f = RB;  // first block of the round with a p-break (uniform)
 #pragma unroll
                 for (u32 j = 0; j < RB; j++)
@@ -1298,6 +1456,7 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
                 if (f < lim) d = pdiff(c + 2 + f);  // (read again: no array of RB values held live)
                 for (u32 j = 1; j <= adv; j++) refill(c + j);
                 c += adv;
+                n_cross += adv;
                 if (f < RB || c >= nblk) break;
             }
             if (c > cs) {
@@ -1347,6 +1506,7 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
 #pragma unroll
             for (int e = 0; e < 8; e++) hc[e] = hn[e];
             hk = (int)k + 1;
+            n_phi++;
         }
         // decisions of block c from Phi'(c) = x and Phi'(c+1) = y
         if (!(fx && allk)) {
@@ -1412,9 +1572,7 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
             u64 pd = B0x ^ shifted8(B0x, B1x, p, lane);
             const int fo = first_diff(pd);
             if (__ballot(pd != 0)) {
-                u32 p2 = 0;
-                for (u32 q = 1; q <= QL && !p2; q++)
-                    if (!__ballot(shifted8(B0x, B1x, q, lane) != B0x)) p2 = q;
+                const u32 p2 = smallest_period(B0x, B1x, lane);
                 if (p2) {
                     p = p2;
                     pd = 0;
@@ -1438,6 +1596,13 @@ __global__ __launch_bounds__(64 * SWAVES, 4) void k_sss_runs(const u8* __restric
     // intervals of k_q_anchors)
     const bool ovf = !fail && nout > scap;
     if (ovf) fail = true;
+    if (prof && lane == 0) {
+        const u64 t_end = clock64();
+        prof[4 * w] = (u32)t_start;
+        prof[4 * w + 1] = (u32)(t_end - t_start);
+        prof[4 * w + 2] = min(n_cls, 0xFFFFu) | (min(n_find, 0xFFFFu) << 16) | (fail ? 0x80000000u : 0u);
+        prof[4 * w + 3] = min(n_phi, 0xFFFFu) | (min(n_cross, 0xFFFFu) << 16);
+    }
     if (lane == 0) {
         if (dbg) {  // (same-address atomics from every wave serialize: debug runs only)
             atomicAdd(dbg + 0, n_cls);
@@ -2111,17 +2276,26 @@ void engine::build_sss(const u8* T) {
     u8* bp = blk_p.get(nbk + 1);
     u16* bfo = blk_fo.get(nbk + 1);
     u16* blo = blk_lo.get(nbk + 1);
+    const bool runs_kernel = !std::getenv("LZ77SSS_NO_RUNS_KERNEL");  // test knob: every stopped stripe through the Q-anchor path
+    // test knob: pure runs through k_sss_runs as well (pass 1 does not settle them)
+    const bool pure_runs = runs_kernel && !std::getenv("LZ77SSS_NO_PURE_RUNS");
     k_sss_stream<false, true><<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(
         T, n, last_i, qi, nlanes, lo, lc, lf, ctr + 1, (u32)SSS_BASE, PW, scap, hw, qi, rp, nullptr, nullptr, bp, bfo,
         blo, nbk, ctr + 5, tot);
     LZ_HIP(hipGetLastError());
     // the stripes pass 1 stopped: settled in one pass where their periodic windows are runs
     // (k_sss_runs), which also writes the per-block run records of the LCE
-    const bool runs_kernel = !std::getenv("LZ77SSS_NO_RUNS_KERNEL");  // test knob: every stopped stripe through the Q-anchor path
+    // LZ77SSS_RUNS_PROF: per-stripe clocks and counters of k_sss_runs, summarized on stderr
+    u32* runs_prof = nullptr;
+    if (std::getenv("LZ77SSS_RUNS_PROF")) {
+        runs_prof = (u32*)u64a.get(2 * nlanes + 2);
+        LZ_HIP(hipMemsetAsync(runs_prof, 0, 16 * nlanes, st));
+    }
     if (runs_kernel)
-        k_sss_runs<<<cdiv(nlanes, SWAVES), 64 * SWAVES, 0, st>>>(T, n, last_i, nlanes, lo, lc, lf, ctr + 1,
+        k_sss_runs<<<cdiv(nlanes, RWAVES), 64 * RWAVES, 0, st>>>(T, n, last_i, nlanes, lo, lc, lf, ctr + 1,
                                                                 (u32)SSS_BASE, PW, scap, hw, bp, bfo, blo, nbk, ctr + 0,
-                                                                debug_enabled() ? ctr + 8 : nullptr, tot);
+                                                                debug_enabled() ? ctr + 8 : nullptr, tot, runs_prof,
+                                                                pure_runs ? 1 : 0);
     LZ_HIP(hipGetLastError());
     // one read: any Q window, overflowing stripes, does any block have a run record, does any tile
     // need the Q-anchor pass (a hit in a stripe pass 1 ran through, or a stripe k_sss_runs could not
@@ -2135,9 +2309,48 @@ void engine::build_sss(const u8* T) {
         rb.sync();
     }
     const u32 need_marks = hc[5], any_rec = hc[4];
+    if (runs_prof) {
+        std::vector<u32> hp4(4 * nlanes);
+        LZ_HIP(hipMemcpy(hp4.data(), runs_prof, 16 * nlanes, hipMemcpyDeviceToHost));
+        std::vector<std::pair<u32, u64>> dur;
+        u64 t0 = ~0ull, sum_phi = 0, sum_cross = 0, sum_cls = 0;
+        for (u64 w = 0; w < nlanes; w++)
+            if (hp4[4 * w + 1]) {
+                dur.push_back({hp4[4 * w + 1], w});
+                t0 = std::min<u64>(t0, hp4[4 * w]);
+                sum_phi += hp4[4 * w + 3] & 0xFFFF;
+                sum_cross += hp4[4 * w + 3] >> 16;
+                sum_cls += hp4[4 * w + 2] & 0xFFFF;
+            }
+        std::sort(dur.begin(), dur.end());
+        const size_t m = dur.size();
+        std::fprintf(stderr, "[lz77sss-runs-prof] stripes run %zu of %llu: blocks hashed %llu crossed %llu classifications %llu\n", m,
+                     (unsigned long long)nlanes, (unsigned long long)sum_phi, (unsigned long long)sum_cross, (unsigned long long)sum_cls);
+        if (m) {
+            std::fprintf(stderr, "[lz77sss-runs-prof] clocks p50 %u p90 %u p99 %u max %u\n", dur[m / 2].first, dur[m * 9 / 10].first,
+                         dur[m * 99 / 100].first, dur[m - 1].first);
+            for (size_t i = m; i > 0 && i + 12 > m; i--) {
+                const u64 w = dur[i - 1].second;
+                std::fprintf(stderr, "[lz77sss-runs-prof]   stripe %llu: clocks %u start %llu cls %u find %u fail %u hashed %u crossed %u\n",
+                             (unsigned long long)w, hp4[4 * w + 1], (unsigned long long)(hp4[4 * w] - (u32)t0), hp4[4 * w + 2] & 0xFFFF,
+                             (hp4[4 * w + 2] >> 16) & 0x7FFF, hp4[4 * w + 2] >> 31, hp4[4 * w + 3] & 0xFFFF, hp4[4 * w + 3] >> 16);
+            }
+        }
+    }
     LZ_HIP(hipEventRecord(sss_evB, st));
     u32 ndirty = 0;
+    // the per-anchor Q intervals and run periods start out empty when something reads them (the
+    // Q-anchor pass and its re-run, the fallback); pass 1 no longer clears them (25 MB of stores
+    // per GiB that only run-free or settled texts skipped reading)
+    bool anchors_cleared = false;
+    auto clear_anchors = [&]() {
+        if (anchors_cleared) return;
+        LZ_HIP(hipMemsetD16Async((hipDeviceptr_t)qi, 0xFF00, nanch + 64, st));
+        LZ_HIP(hipMemsetAsync(rp, 0, nanch, st));
+        anchors_cleared = true;
+    };
     if (need_marks || !runs_kernel) {
+        clear_anchors();
         // tiles the filter marked (the stopped stripes k_sss_runs settled have no hit bits left)
         const u64 nblk_last = std::min<u64>(SNB, (last_i - (nlanes - 1) * SD) / TAU + 1);
         const u64 t_tail = (nlanes - 1) * (SD / QA) + 4 * nblk_last, q_end = nanch + 64;
@@ -2172,7 +2385,7 @@ void engine::build_sss(const u8* T) {
             ctr + 3, nullptr, nullptr, nullptr, 0, nullptr, tot);
         LZ_HIP(hipGetLastError());
     }
-    runs_valid = true;  // period 0 outside the marked tiles
+    runs_valid = ndirty != 0;  // the anchor run table: period 0 outside the marked tiles (none: not read)
     brk_valid = false;
     if (any_rec) {
         // run-record segments -> packed per-block run end / start (two launches)
@@ -2281,6 +2494,7 @@ void engine::build_sss(const u8* T) {
         LZ_HIP(hipMemcpy(ovf_slot, slot.data(), nlanes * 4, hipMemcpyHostToDevice));
         u32* scratch = (u32*)u64a.get((lanes.size() * 3 * (SD + TAU) + 1) / 2);
         ovf_out = sss_ovf.get(lanes.size() * SD);
+        clear_anchors();  // (Q intervals: empty outside the marked tiles)
         k_sss_fallback<<<(unsigned)lanes.size(), FB_T, 0, st>>>(T, n, last_i, qi, d_lanes, scratch, ovf_out, lc,
                                                                 (u32)SSS_BASE, bpow);
         LZ_HIP(hipGetLastError());

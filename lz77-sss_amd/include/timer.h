@@ -2,14 +2,17 @@
 #pragma once
 #include "lz77sss_internal.h"
 
+#include <cstdlib>
 #include <string>
 #include <utility>
 #include <vector>
 
 namespace lz {
 
+// (held / peak count the device allocations of every session in the process: g_dev_bytes and
+// g_phase_peak are process-wide, lz77sss.h lz77sss_session_phase_mem)
 struct phase_mem {
-    uint64_t held = 0;      // device bytes of the session's buffers when the phase was enqueued
+    uint64_t held = 0;      // device bytes of the process's buffers when the phase was enqueued
     uint64_t peak = 0;      // their peak during the phase
     uint64_t hbm_free = 0;  // free device memory then (hipMemGetInfo: the whole GPU)
 };
@@ -37,8 +40,17 @@ struct phase_timer {
         m.held = g_dev_bytes.load();
         m.peak = g_phase_peak.exchange(m.held);
         if (m.peak < m.held) m.peak = m.held;
-        size_t fr = 0, tot = 0;
-        if (hipMemGetInfo(&fr, &tot) == hipSuccess) m.hbm_free = fr;
+        // the driver's free-memory query is a host call between phases: once per call (at the start
+        // mark), later marks derive it from this process's own allocations since then, unless
+        // LZ77SSS_PHASE_MEM asks for a query at every mark
+        static const bool query_all = std::getenv("LZ77SSS_PHASE_MEM") != nullptr;
+        if (mem.empty() || query_all) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess) m.hbm_free = fr;
+        } else {
+            const phase_mem& m0 = mem.front();
+            m.hbm_free = m0.hbm_free + m0.held >= m.held ? m0.hbm_free + m0.held - m.held : 0;
+        }
         mem.push_back(m);
     }
     void clear() {

@@ -377,18 +377,30 @@ class Session:
         k = load_library().lz77sss_session_stats(self._h, out.ctypes.data_as(_P), 28)
         return [int(x) for x in out[:max(k, 0)]]
 
-    def phase_times(self) -> dict[str, float]:
+    def _phase_list(self) -> list[tuple[str, float]]:
+        """(name, ms) per phase of the last call, in order; a repeated name (a phase run again, e.g.
+        a retried task table) is kept as name#2, name#3, ..."""
         ms = (ctypes.c_double * 32)()
         names = (ctypes.c_char_p * 32)()
         k = load_library().lz77sss_session_phase_times(self._h, ms, names, 32)
         if k < 0:
             _check(k)
-        return {names[i].decode(): ms[i] for i in range(k)}
+        out, seen = [], {}
+        for i in range(k):
+            nm = names[i].decode()
+            seen[nm] = seen.get(nm, 0) + 1
+            out.append((nm if seen[nm] == 1 else f"{nm}#{seen[nm]}", ms[i]))
+        return out
+
+    def phase_times(self) -> dict[str, float]:
+        return dict(self._phase_list())
 
     def phase_mem(self) -> dict[str, dict[str, int]]:
-        """Per phase of the last call (lz77sss_session_phase_mem): device bytes the session's buffers
-        held when the phase was enqueued, their peak during it, and the GPU's free memory then."""
-        names = list(self.phase_times())
+        """Per phase of the last call (lz77sss_session_phase_mem): device bytes the process's buffers
+        held when the phase was enqueued, their peak during it, and the GPU's free memory then (all
+        process-wide: every session of the process counts).  Names pair with the C API's entries by
+        position, duplicates kept as name#k."""
+        names = [nm for nm, _ in self._phase_list()]
         h, p, f = (np.zeros(32, np.uint64) for _ in range(3))
         k = load_library().lz77sss_session_phase_mem(self._h, h.ctypes.data_as(_P), p.ctypes.data_as(_P),
                                                       f.ctypes.data_as(_P), 32)
