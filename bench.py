@@ -15,7 +15,11 @@ Workloads:
 
 Multi-GPU (``--gpus N`` under torch.distributed.run): the texts are
 independent objects, one 1 GiB text per rank (seed 42 + rank); no data-path
-collective, the barrier/max-over-ranks timing only (weak scaling).
+collective, the barrier/max-over-ranks timing only (weak scaling).  The same
+line carries ``strong_scaling_one_text``: rank 0's text split over all ranks
+through the sharded path's collectives (sync set by block + all-gather,
+rank-ordered chain blocks with the state hand-over, gathered emission;
+strong scaling, max over ranks), checked against rank 0's one-GPU stream.
 
 Also reported:
   roofline      the SSS kernel sequence (k_sss_stream pass 1 with the periodicity
@@ -60,6 +64,8 @@ def aggregate(dt_local: float, n_per_rank: int, world: int, dist=None, device="c
     if dist is not None and world > 1:
         import torch
 
+        if dist.get_backend() != "nccl":
+            device = "cpu"  # (gloo rehearsal runs: host tensors)
         t = torch.tensor([dt_local], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -207,6 +213,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, gloo between the ranks
+    # (LZ77SSS_BENCH_SHARE_GPU=1); the driver's runs use one GPU per rank and RCCL
+    share_gpu = os.environ.get("LZ77SSS_BENCH_SHARE_GPU") == "1"
+    if share_gpu:
+        local_rank = 0
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
@@ -217,7 +228,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     if args.mode == "sss":
         return main_sss(args, lz, torch, dist, world, rank, local_rank)
@@ -275,6 +289,15 @@ def main():
     phases = sess.phase_times()
     pmem = sess.phase_mem()
     st = sess.stats()
+    # N > 1: also ONE text (rank 0's, seed 42) split over all ranks through the sharded path's
+    # collectives (sync set by block + all-gather, rank-ordered chain blocks with the
+    # state hand-over, gathered emission), timed the same way -- strong scaling beside the weak line
+    strong = None
+    if world > 1 and not exact and args.phr_mode == "lpf_opt" and not os.environ.get("LZ77SSS_BENCH_NO_STRONG"):
+        try:
+            strong = strong_scaling_line(args, lz, torch, dist, world, rank, local_rank, n, sess, int(z))
+        except Exception as e:  # (reported in the line; the weak measurement above stands)
+            strong = {"error": f"{type(e).__name__}: {e}"}
     # PCIe-inclusive rate of one call (host text in, factors out), reported beside the HBM-resident value
     t_out0 = time.perf_counter()
     F = sess.factors(z)
@@ -359,6 +382,8 @@ def main():
                 "bound": "hbm", "note": "text bytes per step over the whole pipeline's phase time",
                 "achieved": round(n / (pipe * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(n / (pipe * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ms": round(pipe, 3)}
+        if strong is not None:
+            out["strong_scaling_one_text"] = strong
         if world == 1 and not args.no_cpu_baseline:
             sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else args.size_mib
             if exact:
@@ -370,6 +395,49 @@ def main():
     sess.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def strong_scaling_line(args, lz, torch, dist, world, rank, local_rank, n, sess_weak, z_weak):
+    """The N > 1 extra of the default line: rank 0's text (seed 42) factorized by all ranks together
+    (sharded.factorize_sharded_resident: collectives (1)-(4) of SURVEY.md 8e), max step time over
+    ranks; rank 0 compares the stream with its own one-GPU factorization of that text (the weak run's
+    last step, still in its session).  Returns the dict rank 0 adds to the JSON line (else None)."""
+    import sharded
+
+    T0 = make_text(lz, args.workload, n, 0)
+    s2 = lz.Session(n, device=local_rank)
+    s2.load(T0)
+    del T0
+    steps = max(2, args.steps // 4)
+    F = None
+    for _ in range(max(args.warmup, 1)):
+        F = sharded.factorize_sharded_resident(s2, n, rank, world, local_rank)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        F = sharded.factorize_sharded_resident(s2, n, rank, world, local_rank)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    dist.barrier()
+    dt, _ = aggregate((t1 - t0) / steps, n, world, dist, device="cuda")
+    out = None
+    if rank == 0:
+        zw = int(F.shape[0])
+        ok = False
+        if zw == z_weak:
+            ref = torch.empty(max(zw, 1) * 2, dtype=torch.int32, device=f"cuda:{local_rank}")
+            if zw:
+                sess_weak.copy_factors(ref.data_ptr(), zw * 8)
+            ok = bool(torch.equal(ref[: 2 * zw].view(-1, 2), F))
+        out = {"value": round(n / dt / 1e6, 2), "unit": "MB/s", "ms_per_step": round(dt * 1e3, 3), "steps": steps,
+               "scaling": "strong", "n": n,
+               "workload": f"{args.workload} n={n}: rank 0's text split over {world} ranks",
+               "parallelism": f"sharded x{world}: S by block + all-gather, replicated phrases, rank-ordered greedy "
+                              f"blocks with the chain-state hand-over, gathered emission",
+               "factors": int(zw), "equals_one_gpu_stream": ok}
+    s2.close()
+    return out
 
 
 def main_shard(args, lz, torch, dist, world, rank, local_rank):
