@@ -924,14 +924,18 @@ static inline void greedy_parallel(const u8* T, Q n, const lce_structure<Q>& L, 
     }
 }
 
+// (Lout: the LCE structure of lpf_opt is built there and kept for the caller -- the exact transform
+// reuses the approximation's LCE as the reference's factorizer does, lz77_sss.hpp:333)
 template <class Q = u32, typename OUT>
 static inline void factorize_approximate(u8* T, Q n, int phr_mode, u32 rk_seed, OUT&& output,
-                                         approx_stats* st = nullptr, int fact_mode = 1, int lpf_parts = 1) {
+                                         approx_stats* st = nullptr, int fact_mode = 1, int lpf_parts = 1,
+                                         lce_structure<Q>* Lout = nullptr) {
     using lpf = lpf_t<Q>;
     using factor = factor_t<Q>;
     if (n == 0) return;
     std::vector<lpf> P;
-    lce_structure<Q> L;
+    lce_structure<Q> Lown;
+    lce_structure<Q>& L = (Lout && phr_mode == lpf_opt) ? *Lout : Lown;
     if (phr_mode == lpf_opt) {
         L.build(T, n);
         P = lpf_parts > 1 ? build_lpf_opt_par(T, n, L, lpf_parts) : build_lpf_opt(T, n, L);

@@ -73,6 +73,11 @@ def lib():
         L.oracle_factorize_exact.argtypes = [_P, _U64, _P, _U64]
         L.oracle_factorize_exact_timed.restype = ctypes.c_int64
         L.oracle_factorize_exact_timed.argtypes = [_P, _U64, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_factorize_exact_smpl.restype = ctypes.c_int64
+        L.oracle_factorize_exact_smpl.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _P, _U64]
+        L.oracle_factorize_exact_smpl_timed.restype = ctypes.c_int64
+        L.oracle_factorize_exact_smpl_timed.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int,
+                                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.oracle_factorize_approx64.restype = ctypes.c_int64
         L.oracle_factorize_approx64.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, _P, _U64, _P]
         L.oracle_sss64.restype = ctypes.c_int64
@@ -258,6 +263,34 @@ def factorize_exact(T):
         if cap >= n + 1:
             raise RuntimeError("oracle exact factorization failed")
         cap = n + 1
+
+
+WITH_SAMPLES, WITHOUT_SAMPLES = 1, 2
+
+
+def factorize_exact_smpl(T, mode=WITH_SAMPLES, p=1):
+    """The reference's exact transform restated (oracle_exact.hpp): factorize_exact<greedy, lpf_opt,
+    with_samples | without_samples> -> (z,2) u32 factors; p = 1 is the deterministic stream."""
+    buf = _padded(T)
+    n = _u8(T).size
+    cap = n // 64 + 65536
+    while True:
+        out = np.zeros((cap, 2), np.uint32)
+        z = lib().oracle_factorize_exact_smpl(buf.ctypes.data_as(_P), n, mode, p, out.ctypes.data_as(_P), cap)
+        if z >= 0:
+            return out[:z].copy()
+        if cap >= n + 1:
+            raise RuntimeError("oracle exact-smpl factorization failed")
+        cap = n + 1
+
+
+def factorize_exact_smpl_timed(T, mode=WITH_SAMPLES, p=1):
+    """Times the exact transform restatement -> (z, seconds, seconds of its approximation stage)."""
+    buf = _padded(T)
+    n = _u8(T).size
+    sec, sa = ctypes.c_double(), ctypes.c_double()
+    z = lib().oracle_factorize_exact_smpl_timed(buf.ctypes.data_as(_P), n, mode, p, ctypes.byref(sec), ctypes.byref(sa))
+    return int(z), sec.value, sa.value
 
 
 def factorize_exact_timed(T):

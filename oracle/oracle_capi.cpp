@@ -3,6 +3,7 @@
 // never linked into the product.  See oracle.hpp for what is restated and the
 // "parity unpinned" status.
 #include "oracle.hpp"
+#include "oracle_exact.hpp"
 
 #include <chrono>
 #include <cstdio>
@@ -171,6 +172,37 @@ int64_t oracle_factorize_exact_timed(const uint8_t* T, uint64_t n, double* secon
     std::vector<factor> F = factorize_exact(T, n);
     *seconds = omp_get_wtime() - t0;
     return (int64_t)F.size();
+}
+
+// The reference's exact transform restated (oracle_exact.hpp): factorize_exact<greedy, lpf_opt,
+// with_samples (mode 1) | without_samples (mode 2)> at p threads (p = 1: the deterministic stream).
+// Returns z or -1 (cap too small / error).
+int64_t oracle_factorize_exact_smpl(uint8_t* T, uint64_t n, int mode, int p, uint32_t* out, uint64_t cap) {
+    try {
+        if (n >= 0xFFFFFFF0ull) return -1;
+        std::vector<factor> F = factorize_exact_smpl(T, (u32)n, mode, p);
+        if (F.size() > cap) return -1;
+        for (size_t k = 0; k < F.size(); k++) { out[2 * k] = F[k].src; out[2 * k + 1] = F[k].len; }
+        return (int64_t)F.size();
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -1;
+    }
+}
+// Same, timed (cpu_baseline of bench.py --mode exact): factor count; seconds for the whole call and
+// for its approximation stage.
+int64_t oracle_factorize_exact_smpl_timed(uint8_t* T, uint64_t n, int mode, int p, double* seconds,
+                                          double* seconds_aprx) {
+    try {
+        if (n >= 0xFFFFFFF0ull) return -1;
+        const double t0 = omp_get_wtime();
+        std::vector<factor> F = factorize_exact_smpl(T, (u32)n, mode, p, seconds_aprx);
+        *seconds = omp_get_wtime() - t0;
+        return (int64_t)F.size();
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle error: %s\n", e.what());
+        return -1;
+    }
 }
 
 // Factor count and wall time only (cpu_baseline); also returns an FNV-1a hash of the stream.

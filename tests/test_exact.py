@@ -71,6 +71,46 @@ def test_exact_never_longer_than_approx(name):
     assert g["factors_exact"].shape[0] <= g["factors"].shape[0]
 
 
+SMPL_FIXTURES = ["c1_seed1", "c1_seed2", "c1_seed4", "periodic", "genome_small", "binary_30k", "zeros_10k",
+                 "edge_n1", "edge_n2", "edge_n511", "edge_n1025", "edge_n5000"]
+
+
+@pytest.mark.parametrize("transf_mode", [1, 2])
+@pytest.mark.parametrize("name", SMPL_FIXTURES)
+def test_oracle_exact_smpl_restatement(orc, name, transf_mode):
+    """The restatement of the reference's transform (oracle_exact.hpp) at p = 1: one section, so
+    its lengths are the canonical greedy ones (pinned by brute force above), and it decodes."""
+    g = load_golden(name)
+    F = orc.factorize_exact_smpl(g["text"], transf_mode, 1)
+    assert np.array_equal(F[:, 1], g["factors_exact"][:, 1])
+    check_valid(g["text"], F)
+    assert np.array_equal(orc.decode(F, g["text"].size), g["text"])
+
+
+@pytest.mark.parametrize("seed", [1, 5, 9, 13])
+def test_oracle_exact_smpl_c1_seeds(orc, lz, seed):
+    T = lz.gen_random_repetitive(10000, 200000, seed)
+    F_ref = orc.factorize_exact(T)
+    for tm in (1, 2):
+        F = orc.factorize_exact_smpl(T, tm, 1)
+        assert np.array_equal(F[:, 1], F_ref[:, 1])
+        check_valid(T, F)
+
+
+@pytest.mark.parametrize("p", [2, 3, 8])
+@pytest.mark.parametrize("name", ["binary_30k", "genome_small", "c1_seed1"])
+def test_oracle_exact_smpl_sections(orc, name, p):
+    """At p > 1 the reference splits the parse into 16 p sections that restart the greedy parse
+    (common.cpp:48-75; every extension stops at its section end e, with_samples.cpp:50-53): a
+    valid parse, never shorter than the canonical one."""
+    g = load_golden(name)
+    for tm in (1, 2):
+        F = orc.factorize_exact_smpl(g["text"], tm, p)
+        check_valid(g["text"], F)
+        assert np.array_equal(orc.decode(F, g["text"].size), g["text"])
+        assert F.shape[0] >= g["factors_exact"].shape[0]
+
+
 def run_exact(session, T, **kw):
     s = session(max(T.size, 1))
     s.load(T)
