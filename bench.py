@@ -169,17 +169,32 @@ def cpu_baseline_chr19(lz, n: int):
             "greedy_parallel": par}
 
 
-def cpu_baseline_exact(lz, workload: str, sample_mib: int):
+def cpu_baseline_exact(lz, workload: str, sample_mib: int, transf_mode: str):
+    """configs[4]'s CPU leg: the restatement of the reference's own transform (oracle/oracle_exact.hpp:
+    factorize_exact<greedy, lpf_opt, with_samples | without_samples>, its 3-approximation included) at
+    p = min(16, host threads) on the workload's text (default the full one), one run."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # the CPU port (test/bench infrastructure only)
 
     n = sample_mib << 20
     T = make_text(lz, workload, n, 0)
-    z, sec = oracle.factorize_exact_timed(T)
-    return {"value": round(n / sec / 1e6, 2), "unit": "MB/s", "cores": oracle.num_threads(), "kind": "port",
-            "sample": f"{workload}: {sample_mib} MiB instance of the same generator (n={n}, z={z}); the oracle's "
-                      f"exact greedy LZ77 restatement (prefix-doubling SA with a parallel comparison sort, "
-                      f"Kasai LCP, PSV/NSV), not the reference's sample-based transform, {sec:.2f} s"}
+    p = min(16, oracle.num_threads())
+    mode = oracle.WITHOUT_SAMPLES if transf_mode == "without_samples" else oracle.WITH_SAMPLES
+    mname = "without_samples" if mode == oracle.WITHOUT_SAMPLES else "with_samples"
+    print(f"cpu_baseline exact p={p}: n={n} {mname} ...", file=sys.stderr, flush=True)
+    z, sec, sec_aprx = oracle.factorize_exact_smpl_timed(T, mode, p)
+    print(f"cpu_baseline exact p={p}: {sec:.1f} s z={z}", file=sys.stderr, flush=True)
+    return {"value": round(n / sec / 1e6, 2), "unit": "MB/s", "cores": p, "kind": "port", "cpu_model": cpu_model(),
+            "runs": 1,
+            "sample": f"{workload}: {sample_mib} MiB instance of the same generator (n={n}); the restatement of "
+                      f"the reference's transform_to_exact_{mname} (oracle_exact.hpp: sample set, PA/SA by stable "
+                      f"sort, interval samples, decomposed weighted square grid, 16 p sections) after its "
+                      f"3-approximation, p={p}: {sec:.2f} s ({sec_aprx:.2f} s approximation), z={z} "
+                      f"(sections restart the greedy parse: z >= the canonical z)",
+            "device_transform": "one device implementation serves with_samples and without_samples (csrc/smpl.hip: "
+                                "sparse-table interval lifting replaces with_samples' interval samples), so the "
+                                "two modes time the same device code; naive drops the approximate lower bound "
+                                "and the Pi / Psi scans"}
 
 
 def main():
@@ -387,8 +402,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             sample = args.cpu_sample_mib if args.cpu_sample_mib > 0 else args.size_mib
             if exact:
-                out["cpu_baseline"] = cpu_baseline_exact(lz, args.workload, args.cpu_sample_mib
-                                                         if args.cpu_sample_mib > 0 else 4)
+                out["cpu_baseline"] = cpu_baseline_exact(lz, args.workload, sample, args.transf_mode)
             else:
                 out["cpu_baseline"] = cpu_baseline(lz, args.workload, sample, PHR[args.phr_mode])
         print(json.dumps(out), flush=True)

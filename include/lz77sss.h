@@ -242,7 +242,9 @@ int lz77sss_session_phase_times(lz77sss_session* s, double* ms, const char** nam
  * held/peak.  Returns the number of phases (or a negative error). */
 int lz77sss_session_phase_mem(lz77sss_session* s, uint64_t* held, uint64_t* peak, uint64_t* hbm_free, int cap);
 /* Statistics of the last factorize call: [size_sss, has_runs, num_lpf, len_lpf_phr,
- * num_gaps, patt_lens[5], roll_threshold, log2_size_h, greedy_rounds, fixups, ...]. */
+ * num_gaps, patt_lens[5], roll_threshold, log2_size_h, greedy_rounds, fixups, ...]; after an
+ * exact-smpl call 24..28 = samples, delta, phrase tasks, chunks << 32 | doubling levels, and 1 when
+ * the sources follow the reference's visit order. */
 int lz77sss_session_stats(lz77sss_session* s, uint64_t* out, int cap);
 void lz77sss_session_destroy(lz77sss_session* s);
 

@@ -55,6 +55,39 @@
 
 namespace LZ_NS {
 
+// LZ_SMPL_CHECK (debug builds only, tools/build_check.sh): every array index of the phrase
+// searches and walks is checked against its array's size; the first violation is recorded in
+// g_smpl_chk (site, index, limit) and the index replaced by 0, so the kernel completes and the
+// host prints the site
+#ifdef LZ_SMPL_CHECK
+__device__ u32* g_smpl_chk;
+__device__ u64 g_smpl_lim[8];  // c, ncell, nblk, za, n + pad, hash slots, task capacity, ncell2
+__device__ __forceinline__ u64 smpl_ck(u64 idx, u64 lim, u32 site) {
+    if (idx < lim) return idx;
+    u32* ck = g_smpl_chk;
+    if (ck && atomicCAS(ck, 0u, site) == 0u) {
+        ck[1] = (u32)idx;
+        ck[2] = (u32)(idx >> 32);
+        ck[3] = (u32)lim;
+        ck[4] = (u32)(lim >> 32);
+    }
+    return 0;
+}
+#define CK(idx, lim, site) smpl_ck((u64)(idx), (u64)(lim), (site))
+#define LIM(k) g_smpl_lim[k]
+// every phase synchronised and named on stderr: a fault then names its phase
+#define SMPL_STAGE(name)                                                                    \
+    do {                                                                                    \
+        const hipError_t e_ = hipStreamSynchronize(st);                                     \
+        std::fprintf(stderr, "[lz77sss] smpl stage %s: %s\n", name, hipGetErrorString(e_)); \
+        LZ_HIP(e_);                                                                         \
+    } while (0)
+#else
+#define CK(idx, lim, site) (idx)
+#define LIM(k) 0
+#define SMPL_STAGE(name) ((void)0)
+#endif
+
 constexpr u32 SMPL_MAX_DELTA = 256;  // lz77_sss.hpp:81 max_delta
 constexpr u32 SCAN_T = 1024;         // lz77_sss.hpp:83 range_scan_threshold (4096 on a CPU core)
 constexpr u32 SMALL_T = 32;          // intersect queries scanned by their own lane (no wave round trip)
@@ -63,7 +96,9 @@ constexpr u32 SMALL_T = 32;          // intersect queries scanned by their own l
 #endif
 constexpr u32 SG_WIN = LZ_SG_WIN;    // smallest grid cell width in ranks (the reference: 16384 on a CPU core)
 constexpr u32 SG_GMAX = 512;         // cells per side at most: wider blocks get wider cells
-constexpr u32 SG_LV = 10;            // row sparse-table levels (2^9 = SG_GMAX / 1)
+constexpr u32 RST_MAX = 18;          // row sparse-table levels at most (2^17 cells per side)
+constexpr u32 RG_WIN = 16384;        // the reference's window width (static_weighted_square_grid.hpp:69)
+constexpr u32 RG_SCAN = 4096;        // the reference's range_scan_threshold (lz77_sss.hpp:85)
 constexpr u32 SWPB = 4;              // waves per workgroup of the phrase kernels
 #ifndef SMPL_OCC
 #define SMPL_OCC 6                   // waves per SIMD the walk kernels are register-bounded for: the walks
@@ -97,7 +132,7 @@ struct smpl_view {
     const u32* gwd;          // [256] grid width per character (cells per side)
     const u32* gwin;         // [256] cell width in ranks per character
     const u32* cell;         // [ncells + 1] first point per cell
-    const u32* rst[SG_LV];   // per row of cells: min weight over cells [x, x + 2^k) of the row
+    const u32* rst[RST_MAX]; // per row of cells: min weight over cells [x, x + 2^k) of the row
     const u32* gx;           // points by (cell, weight): PA rank, SA rank, weight
     const u32* gy;
     const u32* gw;
@@ -166,8 +201,8 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
             qq = false;
             if (rx <= ry) {
                 for (u32 x = xb; x <= xe; x++) {
-                    const u32 yy = V.Pi[x];
-                    if (V.PA[x] < W && yy >= yb && yy <= ye) {
+                    const u32 yy = V.Pi[CK(x, LIM(0), 1)];
+                    if (V.PA[CK(x, LIM(0), 2)] < W && yy >= yb && yy <= ye) {
                         found = true;
                         py = yy;
                         break;
@@ -175,8 +210,8 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
                 }
             } else {
                 for (u32 yy = yb; yy <= ye; yy++) {
-                    const u32 xx = V.Psi[yy];
-                    if (V.SA[yy] < W && xx >= xb && xx <= xe) {
+                    const u32 xx = V.Psi[CK(yy, LIM(0), 3)];
+                    if (V.SA[CK(yy, LIM(0), 4)] < W && xx >= xb && xx <= xe) {
                         found = true;
                         py = yy;
                         break;
@@ -203,8 +238,8 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
                     u32 yy = 0;
                     bool ok = false;
                     if (x <= qxe) {
-                        yy = V.Pi[x];
-                        ok = V.PA[x] < qW && yy >= qyb && yy <= qye;
+                        yy = V.Pi[CK(x, LIM(0), 5)];
+                        ok = V.PA[CK(x, LIM(0), 6)] < qW && yy >= qyb && yy <= qye;
                     }
                     const u64 bal = __ballot(ok);
                     if (bal) {
@@ -218,8 +253,8 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
                     const u32 yy = base + lane;
                     bool ok = false;
                     if (yy <= qye) {
-                        const u32 xx = V.Psi[yy];
-                        ok = V.SA[yy] < qW && xx >= qxb && xx <= qxe;
+                        const u32 xx = V.Psi[CK(yy, LIM(0), 3)];
+                        ok = V.SA[CK(yy, LIM(0), 7)] < qW && xx >= qxb && xx <= qxe;
                     }
                     const u64 bal = __ballot(ok);
                     if (bal) {
@@ -247,7 +282,7 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
                     bool ok = false;
                     if (row < yi2) {
                         const u32 o = cb + row * gw;
-                        ok = min(R[o + xi1], R[o + xi2 - (1u << k)]) < qW;
+                        ok = min(R[CK(o + xi1, LIM(1) + 1, 8)], R[CK(o + xi2 - (1u << k), LIM(1) + 1, 9)]) < qW;
                     }
                     const u64 bal = __ballot(ok);
                     if (bal) {
@@ -255,11 +290,11 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
                         const u32 row1 = base + (u32)__builtin_ctzll(bal), o = cb + row1 * gw;
                         for (u32 xb = xi1; xb < xi2; xb += 64) {
                             const u32 cx = xb + lane;
-                            const bool hit = cx < xi2 && V.rst[0][o + cx] < qW;
+                            const bool hit = cx < xi2 && V.rst[0][CK(o + cx, LIM(1) + 1, 10)] < qW;
                             const u64 hb = __ballot(hit);
                             if (hb) {
                                 const u32 cid = o + xb + (u32)__builtin_ctzll(hb);
-                                y = V.gy[V.cell[cid]];
+                                y = V.gy[CK(V.cell[CK(cid, LIM(1) + 1, 11)], LIM(0), 12)];
                                 f = true;
                                 break;
                             }
@@ -268,35 +303,38 @@ __device__ void wave_intersect(const smpl_view& V, bool q, u32 xb, u32 xe, u32 y
                 }
             }
             if (!f) {
-                // border cells: full rows yw1 (< yi1) and yw2 (>= yi2) when not inner, and the
-                // columns xw1 (< xi1) and xw2 (>= xi2) of the inner rows (every cell when there
-                // is no inner part)
+                // border cells in the reference's row-major order (the first cell in it with a
+                // point decides which point answers): the full row yw1 (< yi1), the cells xw1
+                // (< xi1) and xw2 (>= xi2) of each inner row, the full row yw2 (>= yi2); every
+                // cell row by row when there is no inner part
                 const u32 nx = xw2 - xw1 + 1, ny = yw2 - yw1 + 1;
                 const bool full = !inner;
                 const u32 top = full ? ny : (yw1 < yi1 ? 1u : 0u), bot = full ? 0u : (yw2 >= yi2 ? 1u : 0u);
                 const u32 lc = (!full && xw1 < xi1) ? 1u : 0u, rc = (!full && xw2 >= xi2) ? 1u : 0u;
-                const u32 nin = full ? 0u : yi2 - yi1;
-                const u32 nrow = (top + bot) * nx, ncol = (lc + rc) * nin, nb = nrow + ncol;
+                const u32 nin = full ? 0u : yi2 - yi1, sides = lc + rc;
+                const u32 ntop = top * nx, nmid = sides * nin, nb = ntop + nmid + bot * nx;
                 for (u32 base = 0; base < nb && !f; base += 64) {
                     const u32 t = base + lane;
                     bool ok = false;
                     u32 yy = 0;
                     if (t < nb) {
                         u32 cx, cy;
-                        if (t < nrow) {
-                            const u32 r = t / nx;
-                            cy = r < top ? yw1 + r : yw2;
+                        if (t < ntop) {
+                            cy = yw1 + t / nx;
                             cx = xw1 + t % nx;
+                        } else if (t < ntop + nmid) {
+                            const u32 u = t - ntop, s = u % sides;
+                            cy = yi1 + u / sides;
+                            cx = (lc && s == 0) ? xw1 : xw2;
                         } else {
-                            const u32 u = t - nrow, side = lc ? u / nin : 1u;
-                            cy = yi1 + u % nin;
-                            cx = side == 0 ? xw1 : xw2;
+                            cy = yw2;
+                            cx = xw1 + (t - ntop - nmid);
                         }
                         const u32 cid = cb + cy * gw + cx;
-                        const u32 p1 = V.cell[cid + 1];
-                        for (u32 q = V.cell[cid]; q < p1; q++) {
-                            if (V.gw[q] >= qW) break;
-                            const u32 xx = V.gx[q], y3 = V.gy[q];
+                        const u32 p1 = V.cell[CK(cid + 1, LIM(1) + 1, 13)];
+                        for (u32 q = V.cell[CK(cid, LIM(1) + 1, 14)]; q < p1; q++) {
+                            if (V.gw[CK(q, LIM(0), 15)] >= qW) break;
+                            const u32 xx = V.gx[CK(q, LIM(0), 16)], y3 = V.gy[CK(q, LIM(0), 16)];
                             if (xx >= qxb && xx <= qxe && y3 >= qyb && y3 <= qye) {
                                 ok = true;
                                 yy = y3;
@@ -385,7 +423,8 @@ __global__ void k_ctx_keys(const u8* __restrict__ T, u64 n, const u32* __restric
 // min of the adjacent LCEs over ranks [a, b] (a <= b)
 __device__ __forceinline__ u32 adj_min(const iv_levels& M, u32 a, u32 b) {
     const u32 k = 31 - __builtin_clz(b - a + 1);
-    return min(M.mn[k][a], M.mn[k][b + 1 - (1u << k)]);
+    return min(M.mn[k][CK(a, k ? LIM(0) - (1u << k) + 1 : LIM(0) + 1, 20)],
+               M.mn[k][CK(b + 1 - (1u << k), k ? LIM(0) - (1u << k) + 1 : LIM(0) + 1, 21)]);
 }
 // LCE of the sample suffix at SA rank y with the suffix whose insertion rank is rs (LCEs hlo /
 // hhi with ranks rs - 1 / rs)
@@ -396,7 +435,7 @@ __device__ __forceinline__ u32 lce_of_rank(const iv_levels& M, u32 y, u32 rs, u3
 // the lightest point (smallest sample id) with rank in [a, b] of an order (PA: V.wPA, SA: V.wSA)
 __device__ __forceinline__ u32 min_weight(const u32* const* Wl, u32 a, u32 b) {
     const u32 k = 31 - __builtin_clz(b - a + 1);
-    return min(Wl[k][a], Wl[k][b + 1 - (1u << k)]);
+    return min(Wl[k][CK(a, k ? LIM(0) - (1u << k) + 1 : LIM(0), 22)], Wl[k][CK(b + 1 - (1u << k), k ? LIM(0) - (1u << k) + 1 : LIM(0), 23)]);
 }
 
 
@@ -413,8 +452,8 @@ __device__ __forceinline__ void iv_around(const iv_levels& M, u32 c, u32 rs, u32
     u32 vb[4], ve[4];
 #pragma unroll
     for (u32 t = 0; t < 4; t++) {
-        vb[t] = db && t + 1 <= rs - 1 ? a[rs - 1 - t] : 0u;  // adj[r] links ranks r - 1, r
-        ve[t] = de && rs + 1 + t <= c ? a[rs + 1 + t] : 0u;
+        vb[t] = db && t + 1 <= rs - 1 ? a[CK(rs - 1 - t, LIM(0) + 1, 24)] : 0u;  // adj[r] links ranks r - 1, r
+        ve[t] = de && rs + 1 + t <= c ? a[CK(rs + 1 + t, LIM(0) + 1, 25)] : 0u;
     }
     bool lb = db, le = de;  // still extending
     if (db) b = rs - 1;
@@ -435,8 +474,8 @@ __device__ __forceinline__ void iv_around(const iv_levels& M, u32 c, u32 rs, u32
         const u32 w = 1u << l;
         const bool tb = lb && b >= w, te = le && e + 1 + w <= c;
         u32 x = 0, y = 0;
-        if (tb) x = M.mn[l][b + 1 - w];
-        if (te) y = M.mn[l][e + 1];
+        if (tb) x = M.mn[l][CK(b + 1 - w, l ? LIM(0) - w + 1 : LIM(0) + 1, 26)];
+        if (te) y = M.mn[l][CK(e + 1, l ? LIM(0) - w + 1 : LIM(0) + 1, 27)];
         if (tb && x >= len) b -= w;
         if (te && y >= len) e += w;
     }
@@ -476,8 +515,8 @@ __device__ __forceinline__ void ctx_pre16(const smpl_view& V, u64 p, bool left, 
     u32 v = 0;
     for (u32 t = 0; t < qa; t++) {
         u32 d;
-        if (left) d = p >= (u64)t ? V.code[V.L.T[p - t]] : 0u;
-        else d = p + t < V.L.n ? V.code[V.L.T[p + t]] : 0u;
+        if (left) d = p >= (u64)t ? V.code[V.L.T[CK(p - t, LIM(4), 28)]] : 0u;
+        else d = p + t < V.L.n ? V.code[V.L.T[CK(p + t, LIM(4), 29)]] : 0u;
         v = (v << bits) | d;
     }
     if (qb >= 16) {
@@ -496,7 +535,7 @@ __device__ __forceinline__ void rank_cmp(const smpl_view& V, u32 j, u32 D, const
     bool text;
     key_step(km, kp, D, LEFT, lm, ls, text);
     if (text) {
-        const u32 pm = V.C[(LEFT ? V.PA : V.SA)[m]];
+        const u32 pm = V.C[CK((LEFT ? V.PA : V.SA)[CK(m, LIM(0), 30)], LIM(0), 31)];
         if (LEFT) {
             lm = lce_left_offs(V, pm, j, max(hb, 15u), D);
             ls = lm < D && less_left(V, pm, j, lm);
@@ -519,8 +558,9 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
     u32 vL0, vL1, vR0, vR1;
     ctx_pre16(V, j, true, D, vL0, vL1);
     ctx_pre16(V, j, false, 0, vR0, vR1);
-    const u32 bL = V.pre[0][vL0], eL = V.pre[0][vL1 + 1], bR = V.pre[1][vR0], eR = V.pre[1][vR1 + 1];  // in [cb, ce]
-    u32 lW = V.wblk[j >> 8], hW = V.wblk[(j >> 8) + 1];
+    const u32 bL = V.pre[0][CK(vL0, 65537, 32)], eL = V.pre[0][CK(vL1 + 1, 65537, 33)], bR = V.pre[1][CK(vR0, 65537, 34)],
+              eR = V.pre[1][CK(vR1 + 1, 65537, 35)];  // in [cb, ce]
+    u32 lW = V.wblk[CK(j >> 8, LIM(2), 36)], hW = V.wblk[CK((j >> 8) + 1, LIM(2), 37)];
     // one rank more either side (inside the character's block): the search then compares the
     // pattern with both neighbours of its insertion rank, whose LCEs it returns
     u32 lL = bL > cb ? bL - 1 : bL, rL = eL < ce ? eL + 1 : eL, hlL = 1, hrL = 1;
@@ -531,9 +571,9 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
         const u32 mL = lL + (rL - lL) / 2, mR = lR + (rR - lR) / 2, mW = (lW + hW) >> 1;
         ulonglong2 kL = make_ulonglong2(0, 0), kR = make_ulonglong2(0, 0);
         u32 cW = 0;
-        if (aL) kL = V.kPA[mL];
-        if (aR) kR = V.kSA[mR];
-        if (aW) cW = V.C[mW];
+        if (aL) kL = V.kPA[CK(mL, LIM(0), 38)];
+        if (aR) kR = V.kSA[CK(mR, LIM(0), 39)];
+        if (aW) cW = V.C[CK(mW, LIM(0) + 1, 40)];
         if (aL) {
             u32 lm;
             bool ls;
@@ -579,8 +619,8 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
     u32 vb[4], vf[4];
 #pragma unroll
     for (u32 t = 0; t < 4; t++) {
-        vb[t] = t < rs ? V.SA[rs - 1 - t] : NONE;
-        vf[t] = rs + t < c ? V.SA[rs + t] : NONE;
+        vb[t] = t < rs ? V.SA[CK(rs - 1 - t, LIM(0), 41)] : NONE;
+        vf[t] = rs + t < c ? V.SA[CK(rs + t, LIM(0), 42)] : NONE;
     }
     u32 yb = NONE, yf = NONE;
 #pragma unroll
@@ -597,8 +637,8 @@ __device__ void pos_probe(const smpl_view& V, u32 j, u32 D, u32 cb, u32 ce, pos_
         const u32 wb = 1u << max(lb, 0), wf = 1u << max(lf, 0);
         const bool tb = sb && lb >= 0 && lb <= top && pb >= wb, tf = sf && lf >= 0 && lf <= top && pf + wf <= c;
         u32 x = 0, y = 0;
-        if (tb) x = V.wSA[lb][pb - wb];
-        if (tf) y = V.wSA[lf][pf];
+        if (tb) x = V.wSA[lb][CK(pb - wb, lb ? LIM(0) - wb + 1 : LIM(0), 43)];
+        if (tf) y = V.wSA[lf][CK(pf, lf ? LIM(0) - wf + 1 : LIM(0), 44)];
         if (sb) {
             if (tb && x >= W) {
                 pb -= wb;
@@ -693,18 +733,18 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         u32 lo = 0, hi = V.za;
         if (K.ak != NONE) {
             const u32 k = K.ak + 1 + lane;
-            const u64 bal = __ballot(k < V.za && V.afst[k] <= i);
+            const u64 bal = __ballot(k < V.za && V.afst[CK(k, LIM(3) + 1, 45)] <= i);
             lo = K.ak + (u32)__popcll(bal);  // afst increases: the lanes below i are a prefix
             if (bal != ~0ull) hi = lo + 1;
         }
         while (hi - lo > 1) {
             const u32 m = (lo + hi) >> 1;
-            if (V.afst[m] <= i) lo = m; else hi = m;
+            if (V.afst[CK(m, LIM(3) + 1, 46)] <= i) lo = m; else hi = m;
         }
         K.ak = lo;
-        const u32 alen = V.afact[2 * lo + 1];
+        const u32 alen = V.afact[CK(2 * lo + 1, 2 * LIM(3), 47)];
         if (alen != 0) {
-            const u32 nxt = V.afst[lo + 1];
+            const u32 nxt = V.afst[CK(lo + 1, LIM(3) + 1, 48)];
             const u32 cut = alen - (nxt - i);
             f_len = alen - cut;
             f_src = V.afact[2 * lo] + cut;
@@ -775,8 +815,8 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         if (run) {
             if (xe - xb < V.lane_scan) {
                 for (u32 x = xb; x <= xe; x++) {
-                    if (V.PA[x] < W) {
-                        const u32 y = V.Pi[x], l = lce_of_rank(V.sM, y, rs, h_lo, h_hi);
+                    if (V.PA[CK(x, LIM(0), 50)] < W) {
+                        const u32 y = V.Pi[CK(x, LIM(0), 51)], l = lce_of_rank(V.sM, y, rs, h_lo, h_hi);
                         if (l > lo) {
                             lo = l;
                             best_y = y;
@@ -788,7 +828,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
             } else if (yA == NONE || uA <= lo) {
                 done = true;  // no lighter sample shares more than lo
             } else {
-                const u32 xx = V.PAR[V.SA[yA]];
+                const u32 xx = V.PAR[CK(V.SA[CK(yA, LIM(0), 52)], LIM(0), 53)];
                 if (xx >= xb && xx <= xe) {
                     lo = uA;
                     best_y = yA;
@@ -802,7 +842,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
                 // the lightest point of the PA interval is a witness up to its LCE
                 const u32 s0 = min_weight(V.wPA, xb, xe);
                 if (s0 < W) {
-                    const u32 y0 = V.SAR[s0], l0 = lce_of_rank(V.sM, y0, rs, h_lo, h_hi);
+                    const u32 y0 = V.SAR[CK(s0, LIM(0), 54)], l0 = lce_of_rank(V.sM, y0, rs, h_lo, h_hi);
                     if (l0 > lo) {
                         lo = l0;
                         best_y = y0;
@@ -867,7 +907,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         }
         // the longest of the wave (the smallest j on ties) improves f (intersect: lce > f.len)
         u32 len = got ? lce_l + lo - 1 : 0u;
-        u32 src = got ? V.C[V.SA[best_y]] - lce_l + 1 : 0u;
+        u32 src = got ? V.C[CK(V.SA[CK(best_y, LIM(0), 55)], LIM(0), 56)] - lce_l + 1 : 0u;
         u32 bj = got ? j : 0xFFFFFFFFu;
         for (int o = 32; o >= 1; o >>= 1) {
             const u32 l2 = __shfl_xor(len, o, 64), s2 = __shfl_xor(src, o, 64), j2 = __shfl_xor(bj, o, 64);
@@ -1249,7 +1289,154 @@ __global__ void k_path_emit(task_tab Tt, const u32* __restrict__ C, u32 z, u32* 
 }
 
 // ---------------------------------------------------------------------------
+// the source pass: the reference's source for every phrase of the chain.  The lengths are the
+// canonical ones whatever the probe order; the source is not: the reference keeps the first
+// factor it finds of the final length (intersect, common.cpp:341-346: only a strictly longer one
+// replaces f), so it is
+//   * the approximate phrase cut at i when that is already as long (without_samples.cpp:64-77,
+//     with_samples.cpp:146-160; naive starts from a literal, naive.cpp:57),
+//   * else the point that intersect returns for the first j in the transform's visit order whose
+//     intervals (T[i..j] in PA order, T[j..i+len) in SA order) hold a point lighter than the
+//     first sample >= j: j ascending (naive.cpp:60, without_samples.cpp:79), with_samples the
+//     sampled left lengths first, then the others (with_samples.cpp:162-185); intersect's point
+//     comes from the Pi / Psi scan below RG_SCAN ranks or the reference's grid
+//     (static_weighted_square_grid.hpp:116-185), both in their visit order (wave_intersect
+//     over a view holding the reference's grid).
+__global__ void k_fact_len1(const u32* __restrict__ F, u32 z, u32* __restrict__ out) {
+    const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < z) out[m] = max(1u, F[2 * m + 1]);
+    else if (m == z) out[m] = 0;
+}
+// histogram of the adjacent left-context LCEs in PA order, LCX[0 .. c) (LCX[0] = 0; values <= delta)
+__global__ void k_adj_hist(const u32* __restrict__ adj, u32 c, u32* __restrict__ hist) {
+    __shared__ u32 h[SMPL_MAX_DELTA + 1];
+    for (u32 t = threadIdx.x; t <= SMPL_MAX_DELTA; t += blockDim.x) h[t] = 0;
+    __syncthreads();
+    for (u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x; k < c; k += (u64)gridDim.x * blockDim.x)
+        atomicAdd(&h[min(adj[k], SMPL_MAX_DELTA)], 1u);
+    __syncthreads();
+    for (u32 t = threadIdx.x; t <= SMPL_MAX_DELTA; t += blockDim.x)
+        if (h[t]) atomicAdd(&hist[t], h[t]);
+}
+__global__ __launch_bounds__(64 * SWPB) void k_ref_sources(const smpl_view V, u32* __restrict__ F,
+                                                           const u32* __restrict__ pos, u32 z,
+                                                           const u32* __restrict__ smpld, u32* __restrict__ miss) {
+    const u32 lane = threadIdx.x & 63;
+    const u64 w = (u64)blockIdx.x * SWPB + (threadIdx.x >> 6);
+    if (w >= z) return;  // (wave-uniform)
+    const u32 i = pos[w], M = F[2 * w + 1];
+    if (M == 0) return;
+    const u32 n = (u32)V.L.n;
+    if (V.mode != LZ77SSS_TRANSF_NAIVE) {
+        u32 lo = 0, hi = V.za;  // largest k with afst[k] <= i
+        while (hi - lo > 1) {
+            const u32 m = (lo + hi) >> 1;
+            if (V.afst[m] <= i) lo = m; else hi = m;
+        }
+        const u32 alen = V.afact[2 * lo + 1];
+        if (alen != 0) {
+            const u32 rest = V.afst[lo + 1] - i;
+            if (rest >= M) {  // (== M: the lengths are maximal)
+                if (lane == 0) F[2 * w] = V.afact[2 * lo] + (alen - rest);
+                return;
+            }
+        }
+    }
+    const bool ws = V.mode == LZ77SSS_TRANSF_WITH_SAMPLES;
+    const u32 kmax = min(min(V.delta, n - i), M);  // j = i + k with k < kmax (lce_r = M - k >= 1)
+    u32 best = NONE, bsrc = 0;
+    for (u32 k0 = 0; k0 < kmax; k0 += 64) {
+        const u32 k = k0 + lane, j = i + k;
+        const bool act = k < kmax;
+        const u32 ch = act ? V.L.T[j] : 0u;
+        const u32 cb = V.CS[ch], ce = V.CS[ch + 1];
+        pos_info P{};
+        const bool have = act && ce > cb;
+        if (have) pos_probe<false>(V, j, V.delta, cb, ce, P, nullptr);
+        const u32 lce_l = k + 1, lce_r = M - k;
+        u32 xb = 1, xe = 0, nb = 1, ne = 0;
+        const bool okl = have && (P.hloL >= lce_l || P.hhiL >= lce_l);
+        const bool okr = have && (P.hloR >= lce_r || P.hhiR >= lce_r);
+        if (okl) iv_around(V.pM, V.c, P.rsL, P.hloL, P.hhiL, lce_l, xb, xe);
+        if (okr) iv_around(V.sM, V.c, P.rsR, P.hloR, P.hhiR, lce_r, nb, ne);
+        const bool cand = okl && okr;
+        bool f = false;
+        u32 py = 0;
+        wave_intersect(V, cand, xb, xe, nb, ne, P.w, ch, f, py, lane);
+        u32 key = NONE, src = 0;
+        if (cand && f) {
+            key = (ws && !smpld[lce_l]) ? SMPL_MAX_DELTA + k : k;
+            src = V.C[V.SA[py]] - lce_l + 1;
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            const u32 k2 = __shfl_xor(key, o, 64), s2 = __shfl_xor(src, o, 64);
+            if (k2 < key) {
+                key = k2;
+                src = s2;
+            }
+        }
+        if (key < best) {
+            best = key;
+            bsrc = src;
+        }
+        // later windows hold larger k: only a sampled length (with_samples) can still come first
+        if (best != NONE && (!ws || best < SMPL_MAX_DELTA)) break;
+    }
+    if (lane == 0) {
+        if (best != NONE) F[2 * w] = bsrc;
+        else atomicAdd(miss, 1u);  // (no j reaches the length: cannot happen for a canonical phrase)
+    }
+}
+
+// ---------------------------------------------------------------------------
 // host side
+
+// with_samples' sampled left pattern lengths (construction.cpp build_samples<LEFT>, max length
+// delta) from the histogram of LCX[0 .. c) (the adjacent left-context LCEs in PA order, <= delta):
+// the rank-interpolated lengths between the ranks of 3 and of the longest, then the short lengths
+// added while their ranks sum below 0.2 x 2c.  smpld[len] = 1 for every sampled length.
+static void sampled_left_lengths(const u32* hist, u32 c, u32 delta, u32* smpld) {
+    u64 cum[SMPL_MAX_DELTA + 2];  // cum[v] = number of values < v
+    cum[0] = 0;
+    for (u32 v = 0; v <= SMPL_MAX_DELTA; v++) cum[v + 1] = cum[v] + hist[v];
+    // the binary searches of the reference over the sorted values: the first index in [0, c - 1]
+    // whose value is >= v (c - 1 when none is)
+    auto rank_geq = [&](u32 v) -> u32 { return (u32)std::min<u64>(cum[std::min<u32>(v, SMPL_MAX_DELTA + 1)], c - 1); };
+    auto at = [&](u64 r) -> u32 {
+        u32 v = 0;
+        while (v < SMPL_MAX_DELTA && cum[v + 1] <= r) v++;
+        return v;
+    };
+    std::vector<u32> pl{1, 2};
+    const u32 msl = std::min<u32>(at(c - 1), delta);
+    const u32 rng_min = rank_geq(3), rng_max = rank_geq(msl);
+    if (rng_min < rng_max) {
+        const double max_num = 2.0 * c, rng = (double)rng_max - (double)rng_min;
+        const u64 num = std::min<u64>((u64)msl - 2, 2 + (u64)std::floor((2.0 * max_num) / (double)(rng_min + rng_max)));
+        std::vector<u32> ranks(std::max<u64>(num, 3), 0);
+        for (u64 i = 2; i < num; i++) {
+            const double rel = (double)(i - 1) / (double)(num - 2);
+            const u32 rnk = (u32)std::floor((double)rng_min + rel * rng);
+            const u32 len = std::max(at(rnk), pl.back() + 1);
+            if (len > msl) break;
+            pl.push_back(len);
+            ranks[i] = rank_geq(len);
+        }
+        const u32 max_add = (u32)(max_num * 0.2);
+        if (ranks[2] < max_add) {
+            u32 added = 0;
+            for (u32 len = 3; true; len++) {
+                if (std::find(pl.begin(), pl.end(), len) != pl.end()) continue;
+                const u32 rnk = rank_geq(len);
+                if (len > msl || added + rnk > max_add) break;
+                added += rnk;
+                pl.push_back(len);
+            }
+        }
+    }
+    for (u32 len : pl)
+        if (len <= SMPL_MAX_DELTA) smpld[len] = 1;
+}
 
 u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int log2_override, bool log) {
     LZ_HIP(hipSetDevice(device));
@@ -1258,6 +1445,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     if (log) g_dev_peak.store(g_dev_bytes.load());
     // the 3-approximation (compute_approximation, lz77_sss.hpp:324)
     const u64 za64 = factorize(phr_mode, rk_seed, log2_override, false, LZ77SSS_GREEDY);
+    SMPL_STAGE("approx");
     num_fact = 0;
     last_fact_mode = LZ77SSS_GREEDY;
     if (n == 0) return 0;
@@ -1295,7 +1483,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         k_smpl_fill<<<cdiv(za, 256), 256, 0, st>>>(afact, afst, za, delta, off, C);
     }
     u32* C = e_C.p;
-    timer.mark("smpl_set");
+    timer.mark("smpl_set"); SMPL_STAGE("smpl_set");
     const lce_view LV = view(d_text);
     // PA / SA (sample_index.hpp:317-353): radix sort by as many characters as 64 bits hold in
     // the text's alphabet (32 of a 4-letter text), merge sort by the text
@@ -1317,6 +1505,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         while ((1u << bits) < sigma) bits++;
         kc_max = 64 / bits;
         LZ_HIP(hipMemcpyAsync(code, hc, 256, hipMemcpyHostToDevice, st));
+        LZ_HIP(hipStreamSynchronize(st));  // (hc lives in this block)
     }
     u32* PA = e_PA.get(c);
     u32* SA = e_SA.get(c);
@@ -1338,7 +1527,9 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, id, X, (int)c, 0, kbits, st));
             u8* t = scan_tmp.get(tb);
             LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key2, id, X, (int)c, 0, kbits, st));
+            SMPL_STAGE(left ? "radix PA" : "radix SA");
             merge_sort_u32(X, tmp, c, smpl_less{LV, C, keyid, delta, left}, st);
+            SMPL_STAGE(left ? "merge PA" : "merge SA");
             k_rank_of<<<cdiv(c, 256), 256, 0, st>>>(X, c, left ? PAR : SAR);
             k_pre_table<<<cdiv(65537, 256), 256, 0, st>>>(key2, c, (u32)kbits, (left ? e_preL : e_preR).get(65537));
             kc_side[left ? 0 : 1] = kc;
@@ -1347,64 +1538,113 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     u32* Pi = e_Pi.get(c);
     u32* Psi = e_Psi.get(c);
     k_pi_psi<<<cdiv(c, 256), 256, 0, st>>>(PA, SA, PAR, SAR, c, Pi, Psi);
-    timer.mark("smpl_index");
+    timer.mark("smpl_index"); SMPL_STAGE("smpl_index");
     // the decomposed grid (decomposed_range.hpp:82-130, static_weighted_square_grid.hpp:67-104)
-    u32 hCS[257], hgcb[257], hgwd[256], hwin[256];
-    u32* dCS = e_CS.get(257 + 257 + 256 + 256);
+    u32 hh[256];
     {
         u32* hist = e_tmp1.get(256);
         LZ_HIP(hipMemsetAsync(hist, 0, 1024, st));
         k_char_hist<<<std::min<unsigned>(cdiv(c, 256), 1024), 256, 0, st>>>(d_text, C, c, hist);
-        u32 hh[256];
         LZ_HIP(hipMemcpyAsync(hh, hist, 1024, hipMemcpyDeviceToHost, st));
         LZ_HIP(hipStreamSynchronize(st));
+    }
+    // one grid per character block: the phrase searches' (cells of at least SG_WIN ranks, at most
+    // SG_GMAX per side) or, with ref = true, the reference's own (windows of exactly RG_WIN ranks,
+    // div_ceil(frq, RG_WIN) per side) for the source pass.  Returns false when the cells would
+    // take more than max_bytes.
+    struct grid_set {
+        const u32* cs;  // [CS 257 | first cell 257 | cells per side 256 | cell width 256]
+        const u32* cell;
+        const u32* gx;
+        const u32* gy;
+        const u32* gw;
+        const u32* rst[RST_MAX];
+        u32 ncell;
+    };
+    auto build_grid = [&](bool ref, dbuf<u32>& cs_b, dbuf<u32>& gx_b, dbuf<u32>& gy_b, dbuf<u32>& gw_b,
+                          dbuf<u32>& cell_b, dbuf<u32>* rst_b, u64 max_bytes, grid_set& G) -> bool {
+        u32 hCS[257], hgcb[257], hgwd[256], hwin[256];
+        u64 ncell64 = 0;
+        u32 wmax = 1;
         hCS[0] = 0;
         hgcb[0] = 0;
         for (int ch = 0; ch < 256; ch++) {
             hCS[ch + 1] = hCS[ch] + hh[ch];
-            // cells of at least SG_WIN ranks, at most SG_GMAX per side
-            hgwd[ch] = std::min<u32>((hh[ch] + SG_WIN - 1) / SG_WIN, SG_GMAX);
-            hwin[ch] = hgwd[ch] ? (hh[ch] + hgwd[ch] - 1) / hgwd[ch] : SG_WIN;
-            hgcb[ch + 1] = hgcb[ch] + hgwd[ch] * hgwd[ch];
+            if (ref) {
+                hgwd[ch] = (hh[ch] + RG_WIN - 1) / RG_WIN;
+                hwin[ch] = RG_WIN;
+            } else {
+                hgwd[ch] = std::min<u32>((hh[ch] + SG_WIN - 1) / SG_WIN, SG_GMAX);
+                hwin[ch] = hgwd[ch] ? (hh[ch] + hgwd[ch] - 1) / hgwd[ch] : SG_WIN;
+            }
+            ncell64 += (u64)hgwd[ch] * hgwd[ch];
+            if (ncell64 >= 0xFFFFFFF0ull) return false;
+            hgcb[ch + 1] = (u32)ncell64;
+            wmax = std::max(wmax, hgwd[ch]);
         }
+        u32 nlv = 1;  // row levels k with 2^k <= the widest row
+        while (nlv < RST_MAX && (2ull << (nlv - 1)) <= wmax) nlv++;
+        if ((2ull << (nlv - 1)) <= wmax) return false;
+        const u32 ncell = (u32)ncell64;
+        if ((u64)(ncell + 1) * 4 * (nlv + 1) > max_bytes) return false;
+        u32* dCS = cs_b.get(257 + 257 + 256 + 256);
         LZ_HIP(hipMemcpyAsync(dCS, hCS, 257 * 4, hipMemcpyHostToDevice, st));
         LZ_HIP(hipMemcpyAsync(dCS + 257, hgcb, 257 * 4, hipMemcpyHostToDevice, st));
         LZ_HIP(hipMemcpyAsync(dCS + 514, hgwd, 256 * 4, hipMemcpyHostToDevice, st));
         LZ_HIP(hipMemcpyAsync(dCS + 770, hwin, 256 * 4, hipMemcpyHostToDevice, st));
-    }
-    const u32 ncell = hgcb[256];
-    u32* gx = e_gx.get(c);
-    u32* gy = e_gy.get(c);
-    u32* gw = e_gw.get(c);
-    u32* cell = e_cell.get((u64)ncell + 1);
-    {
-        u64* key = e_key.get(c);
-        u64* key2 = e_key2.get(c);
-        u32* id = e_tmp1.get(c);
-        u32* id2 = e_tmp2.get(c);
-        k_grid_keys<<<cdiv(c, 256), 256, 0, st>>>(d_text, C, c, PAR, SAR, dCS, dCS + 257, dCS + 514, dCS + 770, key,
-                                                  id);
-        size_t tb = 0;
-        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, id, id2, (int)c, 0, 64, st));
-        u8* t = scan_tmp.get(tb);
-        LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key2, id, id2, (int)c, 0, 64, st));
-        k_grid_points<<<cdiv((u64)c + 1, 256), 256, 0, st>>>(key2, PAR, SAR, c, gx, gy, gw, cell, ncell);
-    }
-    // row sparse tables over the cells' lightest weights (levels 0 .. SG_LV - 1)
-    const u32* rst[SG_LV];
-    {
-        u32* lv0 = e_rst[0].get((u64)ncell + 1);
-        if (ncell) k_cell_min<<<cdiv(ncell, 256), 256, 0, st>>>(cell, gw, ncell, lv0);
-        rst[0] = lv0;
-        for (u32 k = 1; k < SG_LV; k++) {
-            u32* out = e_rst[k].get((u64)ncell + 1);
-            if (ncell)
-                k_cell_rowmin<<<cdiv(ncell, 256), 256, 0, st>>>(e_rst[k - 1].p, dCS + 514, dCS + 257, ncell, 1u << (k - 1),
-                                                                 out);
-            rst[k] = out;
+        LZ_HIP(hipStreamSynchronize(st));  // (the host arrays live in this frame)
+        u32* gx = gx_b.get(c);
+        u32* gy = gy_b.get(c);
+        u32* gw = gw_b.get(c);
+        u32* cell = cell_b.get((u64)ncell + 1);
+        {
+            u64* key = e_key.get(c);
+            u64* key2 = e_key2.get(c);
+            u32* id = e_tmp1.get(c);
+            u32* id2 = e_tmp2.get(c);
+            k_grid_keys<<<cdiv(c, 256), 256, 0, st>>>(d_text, C, c, PAR, SAR, dCS, dCS + 257, dCS + 514, dCS + 770,
+                                                      key, id);
+            size_t tb = 0;
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key, key2, id, id2, (int)c, 0, 64, st));
+            u8* t = scan_tmp.get(tb);
+            LZ_HIP(hipcub::DeviceRadixSort::SortPairs(t, tb, key, key2, id, id2, (int)c, 0, 64, st));
+            k_grid_points<<<cdiv((u64)c + 1, 256), 256, 0, st>>>(key2, PAR, SAR, c, gx, gy, gw, cell, ncell);
         }
-    }
-    timer.mark("smpl_grid");
+        // row sparse tables over the cells' lightest weights (levels 0 .. nlv - 1)
+        u32* lv0 = rst_b[0].get((u64)ncell + 1);
+        if (ncell) k_cell_min<<<cdiv(ncell, 256), 256, 0, st>>>(cell, gw, ncell, lv0);
+        G.rst[0] = lv0;
+        for (u32 k = 1; k < nlv; k++) {
+            u32* out = rst_b[k].get((u64)ncell + 1);
+            if (ncell)
+                k_cell_rowmin<<<cdiv(ncell, 256), 256, 0, st>>>(rst_b[k - 1].p, dCS + 514, dCS + 257, ncell,
+                                                                 1u << (k - 1), out);
+            G.rst[k] = out;
+        }
+        for (u32 k = nlv; k < RST_MAX; k++) G.rst[k] = nullptr;
+        G.cs = dCS;
+        G.ncell = ncell;
+        G.cell = cell;
+        G.gx = gx;
+        G.gy = gy;
+        G.gw = gw;
+        return true;
+    };
+    grid_set G1{};
+    if (!build_grid(false, e_CS, e_gx, e_gy, e_gw, e_cell, e_rst, ~0ull, G1))
+        throw error(LZ77SSS_EINTERNAL, "exact-smpl: grid too large");
+    auto set_grid = [](smpl_view& W, const grid_set& G) {
+        W.CS = G.cs;
+        W.gcb = G.cs + 257;
+        W.gwd = G.cs + 514;
+        W.gwin = G.cs + 770;
+        for (u32 k = 0; k < RST_MAX; k++) W.rst[k] = G.rst[k];
+        W.cell = G.cell;
+        W.gx = G.gx;
+        W.gy = G.gy;
+        W.gw = G.gw;
+    };
+    timer.mark("smpl_grid"); SMPL_STAGE("smpl_grid");
     smpl_view V{};
     V.L = LV;
     V.C = C;
@@ -1428,15 +1668,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         k_wblk<<<cdiv(c, 256), 256, 0, st>>>(C, c, nblk, wb);
         V.wblk = wb;
     }
-    V.CS = dCS;
-    V.gcb = dCS + 257;
-    V.gwd = dCS + 514;
-    V.gwin = dCS + 770;
-    for (u32 k = 0; k < SG_LV; k++) V.rst[k] = rst[k];
-    V.cell = cell;
-    V.gx = gx;
-    V.gy = gy;
-    V.gw = gw;
+    set_grid(V, G1);
     V.afst = afst;
     V.afact = afact;
     V.za = za;
@@ -1460,6 +1692,22 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     // within a few phrases, so longer chunks leave less to the bridges); cut by phrase count, not
     // bytes, so a low-compressibility stretch (short phrases) does not give a few walks most of
     // the work; at least SMPL_WALKS walks (four per wave slot of the chip) while cp >= 32
+#ifdef LZ_SMPL_CHECK
+    static u32* s_chk = nullptr;
+    if (!s_chk) LZ_HIP(hipMalloc(&s_chk, 64));
+    LZ_HIP(hipMemsetAsync(s_chk, 0, 64, st));
+    LZ_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_smpl_chk), &s_chk, sizeof(s_chk), 0, hipMemcpyHostToDevice, st));
+    u64 lims[8] = {c, G1.ncell, (n >> 8) + 2, za, n + TEXT_PAD, 0, 0, 0};
+    LZ_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_smpl_lim), lims, sizeof(lims), 0, hipMemcpyHostToDevice, st));
+    LZ_HIP(hipStreamSynchronize(st));
+    auto chk_report = [&](const char* where) {
+        u32 h[5];
+        LZ_HIP(hipMemcpy(h, s_chk, sizeof(h), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[lz77sss] smpl check %s: %s site %u index %llu limit %llu\n", where, h[0] ? "FAIL" : "ok",
+                     h[0], (unsigned long long)h[1] | ((unsigned long long)h[2] << 32),
+                     (unsigned long long)h[3] | ((unsigned long long)h[4] << 32));
+    };
+#endif
     u32 cp = (u32)std::max<u64>(32, std::min<u64>(SMPL_CHUNK, za / SMPL_WALKS));
     if (const char* e = std::getenv("LZ77SSS_SMPL_CHUNK")) cp = (u32)std::max(1L, std::atol(e));
     const u32 nch = (u32)(((u64)za + cp - 1) / cp);
@@ -1494,7 +1742,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         if (prof) k_chunk_walks<true><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, cp, nch, ex, full, prof);
         else k_chunk_walks<false><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, cp, nch, ex, full, nullptr);
         LZ_HIP(hipGetLastError());
-        timer.mark("smpl_tasks");
+        timer.mark("smpl_tasks"); SMPL_STAGE("smpl_tasks");
         if (prof) k_bridge_walks<true><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full, prof + 2 * (u64)nch);
         else k_bridge_walks<false><<<cdiv(nch, SWPB), 64 * SWPB, 0, st>>>(V, Tt, nch, ex, full, nullptr);
         LZ_HIP(hipGetLastError());
@@ -1505,6 +1753,9 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         tcap64 = std::min<u64>(0x7FFFFFF0ull, 4 * tcap64);
     }
     const u32 ntask = hc[0];
+#ifdef LZ_SMPL_CHECK
+    chk_report("walks");
+#endif
     if (V.cyc) {
         u64 hcy[32];
         LZ_HIP(hipMemcpy(hcy, V.cyc, 256, hipMemcpyDeviceToHost));
@@ -1549,7 +1800,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
                          br ? 0u : kmax * cp);
         }
     }
-    timer.mark("smpl_bridges");
+    timer.mark("smpl_bridges"); SMPL_STAGE("smpl_bridges");
     // the path from the task at position 0: pointer doubling + top-down expansion (in order)
     u32 T_lv = 0;
     while ((1ull << T_lv) < (u64)ntask + 1) T_lv++;
@@ -1577,9 +1828,62 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipStreamSynchronize(st));
     const u32 rounds = nch, walks = T_lv;
-    timer.mark("smpl_chain");
+    timer.mark("smpl_chain"); SMPL_STAGE("smpl_chain");
+    // the reference's sources (k_ref_sources) over its own grid, built now that the walks are
+    // done; LZ77SSS_SMPL_OWN_SOURCES=1 keeps the phrase searches' witnesses (valid, not the
+    // reference's), as does a reference grid that would not fit in half the free memory
+    bool ref_src = false;
+    if (z && !std::getenv("LZ77SSS_SMPL_OWN_SOURCES")) {
+        size_t free_b = 0, tot_b = 0;
+        LZ_HIP(hipMemGetInfo(&free_b, &tot_b));
+        grid_set G2{};
+        if (build_grid(true, e_CS2, e_gx2, e_gy2, e_gw2, e_cell2, e_rst2, (u64)free_b / 2, G2)) {
+            smpl_view V2 = V;
+            set_grid(V2, G2);
+#ifdef LZ_SMPL_CHECK
+            lims[1] = std::max(G1.ncell, G2.ncell);
+            LZ_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_smpl_lim), lims, sizeof(lims)));
+#endif
+            V2.scan_t = RG_SCAN;
+            V2.cyc = nullptr;
+            u32* vis = e_vis.get(2 * (SMPL_MAX_DELTA + 1));
+            u32 hsm[SMPL_MAX_DELTA + 1] = {};
+            if (transf_mode == LZ77SSS_TRANSF_WITH_SAMPLES) {
+                u32* hist = vis + SMPL_MAX_DELTA + 1;
+                LZ_HIP(hipMemsetAsync(hist, 0, (SMPL_MAX_DELTA + 1) * 4, st));
+                k_adj_hist<<<std::min<unsigned>(cdiv(c, 256), 1024), 256, 0, st>>>(V.pM.mn[0], c, hist);
+                u32 hh2[SMPL_MAX_DELTA + 1];
+                LZ_HIP(hipMemcpyAsync(hh2, hist, sizeof(hh2), hipMemcpyDeviceToHost, st));
+                LZ_HIP(hipStreamSynchronize(st));
+                sampled_left_lengths(hh2, c, delta, hsm);
+            }
+            LZ_HIP(hipMemcpyAsync(vis, hsm, sizeof(hsm), hipMemcpyHostToDevice, st));
+            // phrase starts: exclusive sum of max(1, len)
+            u32* lens = e_tmp1.get(z + 1);
+            u32* fpos = e_fpos.get(z + 1);
+            k_fact_len1<<<cdiv(z + 1, 256), 256, 0, st>>>(F, (u32)z, lens);
+            size_t tb = 0;
+            LZ_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, lens, fpos, (int)(z + 1), st));
+            u8* t = scan_tmp.get(tb);
+            LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, lens, fpos, (int)(z + 1), st));
+            u32* miss = ctr + 12;
+            LZ_HIP(hipMemsetAsync(miss, 0, 4, st));
+            k_ref_sources<<<cdiv(z, SWPB), 64 * SWPB, 0, st>>>(V2, F, fpos, (u32)z, vis, miss);
+            LZ_HIP(hipGetLastError());
+            u32 hm = 0;
+            LZ_HIP(hipMemcpyAsync(&hm, miss, 4, hipMemcpyDeviceToHost, st));
+            LZ_HIP(hipStreamSynchronize(st));
+            if (hm) throw error(LZ77SSS_EINTERNAL, "exact-smpl: a phrase without a source in the reference's order");
+            ref_src = true;
+#ifdef LZ_SMPL_CHECK
+            chk_report("sources");
+#endif
+        }
+        timer.mark("smpl_sources"); SMPL_STAGE("smpl_sources");
+    }
     num_fact = z;
-    stats.resize(28, 0);
+    stats.resize(29, 0);
+    stats[28] = ref_src ? 1 : 0;  // the sources follow the reference's visit order
     stats[24] = c;
     stats[25] = delta;
     stats[26] = ntask;
@@ -1639,7 +1943,7 @@ void engine::build_adjacent(smpl_view& V) {
         V.wlv++;
     }
     LZ_HIP(hipGetLastError());
-    timer.mark("smpl_adj");
+    timer.mark("smpl_adj"); SMPL_STAGE("smpl_adj");
 }
 
 }  // namespace LZ_NS

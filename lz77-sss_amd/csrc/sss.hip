@@ -1336,7 +1336,6 @@ __global__ __launch_bounds__(64 * RWAVES) __attribute__((amdgpu_waves_per_eu(4))
     // prologue: blocks 0 .. RSL - 1 in the ring, the chunk after them loading (blocks past
     // nblk + 4 are never read: the text pad covers up to there); block 0 classified, Phi'(0).
     // Iteration c reads ring blocks c .. c + 3
-    const u32 lend = nblk + 5;
     u64 R[RCH];
     auto load_chunk = [&](u32 k0) {
 #pragma unroll
@@ -1570,7 +1569,10 @@ __global__ __launch_bounds__(64 * RWAVES) __attribute__((amdgpu_waves_per_eu(4))
                 B1x = load8(kk + 1);
             }
             u64 pd = B0x ^ shifted8(B0x, B1x, p, lane);
-            const int fo = first_diff(pd);
+            // the first break of the period of the record before (a run's exact end): the failed
+            // block's classification may have left p at another period already
+            const u32 pr = prev_rec ? prev_rec : p;
+            const int fo = first_diff(pr == p ? pd : B0x ^ shifted8(B0x, B1x, pr, lane));
             if (__ballot(pd != 0)) {
                 const u32 p2 = smallest_period(B0x, B1x, lane);
                 if (p2) {
@@ -2421,6 +2423,27 @@ void engine::build_sss(const u8* T) {
         }
         brk_nbk = nbk;
         brk_valid = true;
+        if (const char* dp = std::getenv("LZ77SSS_DUMP_RUNS")) {
+            // debug knob: the raw records (period, first break, last break) and the packed
+            // end / start words, as five consecutive arrays of nbk entries
+            std::vector<u8> hp(nbk);
+            std::vector<u16> hf(nbk), hl(nbk);
+            std::vector<u64> he(nbk), hs(nbk);
+            LZ_HIP(hipStreamSynchronize(st));
+            LZ_HIP(hipMemcpy(hp.data(), bp, nbk, hipMemcpyDeviceToHost));
+            LZ_HIP(hipMemcpy(hf.data(), bfo, 2 * nbk, hipMemcpyDeviceToHost));
+            LZ_HIP(hipMemcpy(hl.data(), blo, 2 * nbk, hipMemcpyDeviceToHost));
+            LZ_HIP(hipMemcpy(he.data(), blk_re.p, 8 * nbk, hipMemcpyDeviceToHost));
+            LZ_HIP(hipMemcpy(hs.data(), blk_rs.p, 8 * nbk, hipMemcpyDeviceToHost));
+            if (FILE* f = std::fopen(dp, "wb")) {
+                std::fwrite(hp.data(), 1, nbk, f);
+                std::fwrite(hf.data(), 2, nbk, f);
+                std::fwrite(hl.data(), 2, nbk, f);
+                std::fwrite(he.data(), 8, nbk, f);
+                std::fwrite(hs.data(), 8, nbk, f);
+                std::fclose(f);
+            }
+        }
         if (debug_enabled()) {
             std::vector<u8> hb(nbk);
             LZ_HIP(hipMemcpy(hb.data(), bp, nbk, hipMemcpyDeviceToHost));

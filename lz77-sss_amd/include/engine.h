@@ -217,7 +217,11 @@ struct engine {
     dbuf<u32> e_preL, e_preR, e_wblk;  // exact-smpl: first ranks per 16-bit key prefix (PA, SA); first sample per 256-block
     dbuf<u64> e_cyc;  // exact-smpl debug counters (LZ77SSS_SMPL_PROF)
     dbuf<u32> e_gx, e_gy, e_gw, e_cell, e_adjL, e_adjR;
-    dbuf<u32> e_rst[10];  // exact-smpl: row sparse tables of the grid cells' lightest weights
+    dbuf<u32> e_rst[18];  // exact-smpl: row sparse tables of the grid cells' lightest weights
+    // exact-smpl source pass: the reference's grid (16384-rank windows), the phrase starts, the
+    // sampled left pattern lengths of with_samples
+    dbuf<u32> e_CS2, e_gx2, e_gy2, e_gw2, e_cell2, e_fpos, e_vis;
+    dbuf<u32> e_rst2[18];
     dbuf<u32> e_ivmin[MAX_LV], e_ivminL[MAX_LV];  // sparse-table minima of the SA / PA adjacent LCEs (interval ends)
     dbuf<u64> e_kSA, e_kPA;                      // 16-byte context keys by SA / PA rank
     dbuf<u32> e_wPA[MAX_LV], e_wSA[MAX_LV];      // minima of the PA / SA weights per sparse-table level

@@ -373,8 +373,8 @@ class Session:
         return out[:c.value]
 
     def stats(self) -> list[int]:
-        out = np.zeros(28, np.uint64)
-        k = load_library().lz77sss_session_stats(self._h, out.ctypes.data_as(_P), 28)
+        out = np.zeros(32, np.uint64)
+        k = load_library().lz77sss_session_stats(self._h, out.ctypes.data_as(_P), 32)
         return [int(x) for x in out[:max(k, 0)]]
 
     def _phase_list(self) -> list[tuple[str, float]]:

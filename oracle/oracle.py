@@ -265,7 +265,7 @@ def factorize_exact(T):
         cap = n + 1
 
 
-WITH_SAMPLES, WITHOUT_SAMPLES = 1, 2
+NAIVE, WITH_SAMPLES, WITHOUT_SAMPLES = 0, 1, 2
 
 
 def factorize_exact_smpl(T, mode=WITH_SAMPLES, p=1):

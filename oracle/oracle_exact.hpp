@@ -391,8 +391,11 @@ struct exact_smpl {
         if constexpr (dir == LEFT) {
             return skip + lce_left_w(T, q - skip, s - skip, len - skip);
         } else {
-            const u32 rest = len - skip;
-            if (rest <= 3 * TAU) return skip + (u32)naive_lce(T, n, (u64)q + skip, (u64)s + skip, rest);
+            // (the reference compares up to 3 tau characters directly; the same value, found here
+            // through the LCE structure once the first 64 characters agree)
+            const u32 rest = len - skip, head = std::min<u32>(rest, 64);
+            const u32 k = (u32)naive_lce(T, n, (u64)q + skip, (u64)s + skip, head);
+            if (k < head || rest == head) return skip + k;
             return std::min<u32>(rlce(q, s), len);
         }
     }
@@ -674,7 +677,8 @@ struct exact_smpl {
                 fa = Fa[fi++];
                 beg_nxt += std::max<u32>(1, fa.len);
             }
-            factor f = fa;
+            // (naive, naive.cpp:57: a literal to start from, no approximate lower bound)
+            factor f = naive ? factor{T[i], 0} : fa;
             const u32 max_j = std::min<u32>(e, i + delta);
             if (f.len != 0) {
                 const u32 cut = f.len - (beg_nxt - i);

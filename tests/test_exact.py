@@ -282,3 +282,86 @@ def test_gpu_exact_invalid_parameters(session, lz):
         s.factorize_exact(transf_mode=7)
     with pytest.raises(lz.Lz77SssError):
         s.factorize_exact(fact_mode=lz.SKIP_PHRASES)
+
+
+def check_reference_stream(orc, session, T, modes=SMPL_MODES):
+    """The device's whole exact-smpl stream, sources included, against the restatement of the
+    reference's transform at p = 1 (oracle_exact.hpp): the source pass (k_ref_sources) picks the
+    factor the reference's visit order keeps."""
+    for tm in modes:
+        s, F = run_exact(session, T, transf_mode=tm)
+        assert s.stats()[28] == 1  # the source pass ran
+        F_ref = orc.factorize_exact_smpl(T, tm, 1)
+        assert F.shape == F_ref.shape
+        bad = np.nonzero(np.any(F != F_ref, axis=1))[0]
+        assert bad.size == 0, (tm, int(bad[0]), F[bad[0]].tolist(), F_ref[bad[0]].tolist(), int(bad.size))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", golden_names())
+def test_gpu_exact_smpl_reference_sources_golden(session, orc, name):
+    check_reference_stream(orc, session, load_golden(name)["text"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(1, 17))
+def test_gpu_exact_smpl_reference_sources_c1(session, orc, lz, seed):
+    check_reference_stream(orc, session, lz.gen_random_repetitive(10000, 200000, seed))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["genome", "rr", "runs"])
+def test_gpu_exact_smpl_reference_sources_medium(session, orc, lz, kind):
+    """4 MiB texts: many grid queries (intervals above the 4 096-rank scan threshold)."""
+    n = 4 << 20
+    if kind == "genome":
+        T = lz.gen_genome(n, 1 << 20, 0.001, 3)
+    elif kind == "rr":
+        T = lz.gen_random_repetitive(n, n, 4, 0.5, 0.05)
+    else:
+        rng = np.random.Generator(np.random.PCG64(6))
+        T = np.tile(rng.integers(0, 4, 777, dtype=np.uint8), n // 777 + 1)[:n]
+        T[rng.integers(0, n, 200)] = 9
+    check_reference_stream(orc, session, T, modes=[1, 2])
+
+
+KNOBS = [{"LZ77SSS_SMPL_LSCAN": "0"}, {"LZ77SSS_SMPL_SCAN": "0"}, {"LZ77SSS_SMPL_SCAN": "1000000000"},
+         {"LZ77SSS_SMPL_SMALL": "0"}, {"LZ77SSS_SMPL_CHUNK": "1"}, {"LZ77SSS_SMPL_CHUNK": "7"},
+         {"LZ77SSS_SMPL_OWN_SOURCES": "1"}]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knob", KNOBS, ids=lambda k: ",".join(f"{a[13:]}={b}" for a, b in k.items()))
+def test_gpu_exact_smpl_knobs(session, orc, lz, monkeypatch, knob):
+    """The phrase searches' paths one at a time (lane scans off, every intersect by the grid or by the
+    Pi / Psi scan, the per-lane small scans off, one or seven phrases per chunk walk): the same
+    stream, sources included (the source pass decides them); with the source pass off, the
+    canonical lengths with valid sources."""
+    for k, v in knob.items():
+        monkeypatch.setenv(k, v)
+    texts = [load_golden(nm)["text"] for nm in ("c1_seed1", "genome_small", "binary_30k", "periodic")]
+    texts.append(lz.gen_random_repetitive(10000, 200000, 3))
+    for T in texts:
+        if "LZ77SSS_SMPL_OWN_SOURCES" in knob:
+            for tm in SMPL_MODES:
+                _, F = run_exact(session, T, transf_mode=tm)
+                check_exact(lz, T, F, orc.factorize_exact(T))
+        else:
+            check_reference_stream(orc, session, T)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sigma", [2, 256])
+def test_gpu_exact_smpl_alphabets(session, orc, lz, sigma):
+    """Sort-key packing at 1 bit (two symbols) and 8 bits (all 256 byte values) per character."""
+    rng = np.random.Generator(np.random.PCG64(sigma))
+    base = rng.integers(0, sigma, 3000, dtype=np.uint8)
+    parts = [base]
+    for _ in range(60):  # mutated copies: long phrases with sources to choose from
+        cp = base[rng.integers(0, 2000):][:rng.integers(200, 1000)].copy()
+        cp[rng.integers(0, cp.size, 3)] = rng.integers(0, sigma, 3, dtype=np.uint8)
+        parts.append(cp)
+    T = np.concatenate(parts)
+    if sigma == 256:
+        T[:256] = np.arange(256, dtype=np.uint8)
+    check_reference_stream(orc, session, T)

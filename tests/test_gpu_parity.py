@@ -617,3 +617,17 @@ def test_lean_release_of_phase_scratch(session, orc, lz, kind, mib, monkeypatch)
     assert set(pm) >= {"sss", "sa_s", "lcp_rmq", "lpf", "greedy"}
     assert pm["greedy"]["held"] < held_full  # (the release follows the "lpf" mark)
     assert all(m["peak"] >= m["held"] for m in pm.values())
+
+
+@pytest.mark.parametrize("seed", range(1, 13))
+def test_rr_4mib_seeds_vs_oracle(session, orc, lz, seed):
+    """Run-heavy 4 MiB texts (runs of period 1 next to runs of other periods): the LPF phrases and
+    the stream equal the oracle's.  Seed 4 once ended a period-1 run at the first break of the next
+    run's period (the record written after k_sss_runs gave the stripe to the Q-anchor path), and the
+    LCE's run skip stopped 343 bytes early."""
+    n = 4 << 20
+    T = lz.gen_random_repetitive(n, n, seed, 0.5, 0.05)
+    F_ref, _ = orc.factorize(T)
+    s, F = run(session, T)
+    assert np.array_equal(s.lpf(), orc.lpf_opt(T))
+    assert F.shape == F_ref.shape and np.array_equal(F, F_ref)
