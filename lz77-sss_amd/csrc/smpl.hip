@@ -712,7 +712,8 @@ constexpr u32 LANE_SCAN = 32;  // PA intervals scanned whole on the lane
 // exponential search and bisection; the predicate is monotone in x, so the result is the
 // reference's whatever the probe order.
 template <bool PROF>
-__device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u32 lane, lane_cache& K, u64* cy) {
+__device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u32& f_k, u32 lane, lane_cache& K,
+                            u64* cy) {
     const u32 n = (u32)V.L.n;
     const u32 e = n;  // one section: p = 1
     const u8* T = V.L.T;
@@ -728,6 +729,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
     // lower bound: the approximate phrase covering i, cut at i (without_samples.cpp:64-77)
     f_src = T[i];
     f_len = 0;
+    f_k = NONE;  // the phrase's j - i when a sample-anchored factor beats the lower bound
     if (V.mode != LZ77SSS_TRANSF_NAIVE) {
         // largest k with afst[k] <= i: the walk's last one and the 63 after it first
         u32 lo = 0, hi = V.za;
@@ -920,6 +922,7 @@ __device__ void wave_phrase(const smpl_view& V, u32 i, u32& f_src, u32& f_len, u
         if (len > f_len) {
             f_len = len;
             f_src = src;
+            f_k = bj - i;  // the smallest j reaching len (its lane is never stopped early)
         }
     }
     if (f_len > e - i) f_len = e - i;
@@ -1137,6 +1140,7 @@ struct task_tab {
     u32* len;
     u32* src;
     u32* hop;
+    u32* wk;     // the phrase's j - i (wave_phrase f_k): where the source pass starts
     u32* keys;   // position + 1, 0 empty
     u32* vals;   // task id
     u32 mask;
@@ -1195,12 +1199,13 @@ __device__ __forceinline__ u32 wave_walk(const smpl_view& V, task_tab& Tt, u64 p
         }
         t = (u32)__shfl((int)t, 0);
         if (t == NONE) return NONE;  // merged (or out of room: reported)
-        u32 src, len;
-        wave_phrase<PROF>(V, (u32)p, src, len, lane, K, cy);
+        u32 src, len, wk;
+        wave_phrase<PROF>(V, (u32)p, src, len, wk, lane, K, cy);
         nph++;
         if (lane == 0) {
             Tt.src[t] = src;
             Tt.len[t] = len;
+            Tt.wk[t] = wk;
         }
         p += max(1u, len);
     }
@@ -1280,12 +1285,13 @@ __global__ void k_path_len(const u32* __restrict__ C, u64 cnt, u32 ntask, u32* _
     const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (m < cnt && C[m] == ntask && (m == 0 || C[m - 1] != ntask)) *z = (u32)m;
 }
-__global__ void k_path_emit(task_tab Tt, const u32* __restrict__ C, u32 z, u32* __restrict__ F) {
+__global__ void k_path_emit(task_tab Tt, const u32* __restrict__ C, u32 z, u32* __restrict__ F, u32* __restrict__ wk) {
     const u64 m = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= z) return;
     const u32 t = C[m];
     F[2 * m] = Tt.src[t];
     F[2 * m + 1] = Tt.len[t];
+    wk[m] = Tt.wk[t];
 }
 
 // ---------------------------------------------------------------------------
@@ -1318,40 +1324,47 @@ __global__ void k_adj_hist(const u32* __restrict__ adj, u32 c, u32* __restrict__
     for (u32 t = threadIdx.x; t <= SMPL_MAX_DELTA; t += blockDim.x)
         if (h[t]) atomicAdd(&hist[t], h[t]);
 }
+// One lane per phrase.  The walk's phrase search kept, of the j reaching the final length, the
+// smallest (wk = j - i; NONE when the lower bound was kept, whose source is the reference's
+// already): the reference's first j in ascending order (naive, without_samples).  with_samples
+// visits the sampled left lengths first, so a sampled k in (wk, kmax) reaching the length comes
+// before wk: those are tried in ascending order, then wk (a sampled wk is the answer itself).
+// Each try is one position probe, two interval liftings and one intersect of the wave.
 __global__ __launch_bounds__(64 * SWPB) void k_ref_sources(const smpl_view V, u32* __restrict__ F,
-                                                           const u32* __restrict__ pos, u32 z,
-                                                           const u32* __restrict__ smpld, u32* __restrict__ miss) {
+                                                           const u32* __restrict__ pos, const u32* __restrict__ wk,
+                                                           u32 z, const u32* __restrict__ smpld,
+                                                           u32* __restrict__ miss) {
     const u32 lane = threadIdx.x & 63;
-    const u64 w = (u64)blockIdx.x * SWPB + (threadIdx.x >> 6);
-    if (w >= z) return;  // (wave-uniform)
-    const u32 i = pos[w], M = F[2 * w + 1];
-    if (M == 0) return;
+    const u64 m = ((u64)blockIdx.x * SWPB + (threadIdx.x >> 6)) * 64 + lane;
     const u32 n = (u32)V.L.n;
-    if (V.mode != LZ77SSS_TRANSF_NAIVE) {
-        u32 lo = 0, hi = V.za;  // largest k with afst[k] <= i
-        while (hi - lo > 1) {
-            const u32 m = (lo + hi) >> 1;
-            if (V.afst[m] <= i) lo = m; else hi = m;
-        }
-        const u32 alen = V.afact[2 * lo + 1];
-        if (alen != 0) {
-            const u32 rest = V.afst[lo + 1] - i;
-            if (rest >= M) {  // (== M: the lengths are maximal)
-                if (lane == 0) F[2 * w] = V.afact[2 * lo] + (alen - rest);
-                return;
-            }
+    const bool ws = V.mode == LZ77SSS_TRANSF_WITH_SAMPLES;
+    u32 i = 0, M = 0, k0 = NONE, kmax = 0;
+    if (m < z) {
+        k0 = wk[m];
+        if (k0 != NONE) {
+            i = pos[m];
+            M = F[2 * m + 1];
+            kmax = min(min(V.delta, n - i), M);
         }
     }
-    const bool ws = V.mode == LZ77SSS_TRANSF_WITH_SAMPLES;
-    const u32 kmax = min(min(V.delta, n - i), M);  // j = i + k with k < kmax (lce_r = M - k >= 1)
-    u32 best = NONE, bsrc = 0;
-    for (u32 k0 = 0; k0 < kmax; k0 += 64) {
-        const u32 k = k0 + lane, j = i + k;
-        const bool act = k < kmax;
-        const u32 ch = act ? V.L.T[j] : 0u;
+    // the lane's next candidate: with_samples' sampled k above k0 first (ascending), then k0
+    bool pend = k0 != NONE;
+    u32 k = k0;
+    bool after = false;  // k0 itself has been reached (the last candidate)
+    if (pend && ws && !smpld[k0 + 1]) {
+        u32 t = k0 + 1;
+        while (t < kmax && !smpld[t + 1]) t++;
+        if (t < kmax) k = t;
+        else after = true;
+    } else {
+        after = true;
+    }
+    while (__ballot(pend)) {
+        const u32 j = i + k;
+        const u32 ch = pend ? V.L.T[j] : 0u;
         const u32 cb = V.CS[ch], ce = V.CS[ch + 1];
         pos_info P{};
-        const bool have = act && ce > cb;
+        const bool have = pend && ce > cb;
         if (have) pos_probe<false>(V, j, V.delta, cb, ce, P, nullptr);
         const u32 lce_l = k + 1, lce_r = M - k;
         u32 xb = 1, xe = 0, nb = 1, ne = 0;
@@ -1363,33 +1376,26 @@ __global__ __launch_bounds__(64 * SWPB) void k_ref_sources(const smpl_view V, u3
         bool f = false;
         u32 py = 0;
         wave_intersect(V, cand, xb, xe, nb, ne, P.w, ch, f, py, lane);
-        u32 key = NONE, src = 0;
-        if (cand && f) {
-            key = (ws && !smpld[lce_l]) ? SMPL_MAX_DELTA + k : k;
-            src = V.C[V.SA[py]] - lce_l + 1;
-        }
-        for (int o = 32; o >= 1; o >>= 1) {
-            const u32 k2 = __shfl_xor(key, o, 64), s2 = __shfl_xor(src, o, 64);
-            if (k2 < key) {
-                key = k2;
-                src = s2;
+        if (pend) {
+            if (cand && f) {
+                F[2 * m] = V.C[V.SA[py]] - lce_l + 1;
+                pend = false;
+            } else if (after) {
+                atomicAdd(miss, 1u);  // (k0 reaches the length: cannot happen)
+                pend = false;
+            } else {
+                u32 t = k + 1;
+                while (t < kmax && !smpld[t + 1]) t++;
+                if (t < kmax) {
+                    k = t;
+                } else {
+                    k = k0;
+                    after = true;
+                }
             }
         }
-        if (key < best) {
-            best = key;
-            bsrc = src;
-        }
-        // later windows hold larger k: only a sampled length (with_samples) can still come first
-        if (best != NONE && (!ws || best < SMPL_MAX_DELTA)) break;
-    }
-    if (lane == 0) {
-        if (best != NONE) F[2 * w] = bsrc;
-        else atomicAdd(miss, 1u);  // (no j reaches the length: cannot happen for a canonical phrase)
     }
 }
-
-// ---------------------------------------------------------------------------
-// host side
 
 // with_samples' sampled left pattern lengths (construction.cpp build_samples<LEFT>, max length
 // delta) from the histogram of LCX[0 .. c) (the adjacent left-context LCEs in PA order, <= delta):
@@ -1731,6 +1737,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
         Tt.len = e_tlen.get(tcap);
         Tt.src = e_tsrc.get(tcap);
         Tt.hop = e_thop.get(tcap);
+        Tt.wk = e_twk.get(tcap);
         Tt.keys = e_tkeys.get(hsz);
         Tt.vals = e_tvals.get(hsz);
         Tt.mask = hsz - 1;
@@ -1824,7 +1831,8 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
     if (hc[0]) throw error(LZ77SSS_EINTERNAL, "exact-smpl: a task without its successor");
     const u64 z = hc[1];
     u32* F = fact.get(2 * z + 2);
-    if (z) k_path_emit<<<cdiv(z, 256), 256, 0, st>>>(Tt, PC, (u32)z, F);
+    u32* FWK = e_fwk.get(z + 1);
+    if (z) k_path_emit<<<cdiv(z, 256), 256, 0, st>>>(Tt, PC, (u32)z, F, FWK);
     LZ_HIP(hipGetLastError());
     LZ_HIP(hipStreamSynchronize(st));
     const u32 rounds = nch, walks = T_lv;
@@ -1868,7 +1876,7 @@ u64 engine::factorize_exact_smpl(int transf_mode, int phr_mode, u32 rk_seed, int
             LZ_HIP(hipcub::DeviceScan::ExclusiveSum(t, tb, lens, fpos, (int)(z + 1), st));
             u32* miss = ctr + 12;
             LZ_HIP(hipMemsetAsync(miss, 0, 4, st));
-            k_ref_sources<<<cdiv(z, SWPB), 64 * SWPB, 0, st>>>(V2, F, fpos, (u32)z, vis, miss);
+            k_ref_sources<<<cdiv(cdiv(z, 64), SWPB), 64 * SWPB, 0, st>>>(V2, F, fpos, FWK, (u32)z, vis, miss);
             LZ_HIP(hipGetLastError());
             u32 hm = 0;
             LZ_HIP(hipMemcpyAsync(&hm, miss, 4, hipMemcpyDeviceToHost, st));

@@ -220,7 +220,7 @@ struct engine {
     dbuf<u32> e_rst[18];  // exact-smpl: row sparse tables of the grid cells' lightest weights
     // exact-smpl source pass: the reference's grid (16384-rank windows), the phrase starts, the
     // sampled left pattern lengths of with_samples
-    dbuf<u32> e_CS2, e_gx2, e_gy2, e_gw2, e_cell2, e_fpos, e_vis;
+    dbuf<u32> e_CS2, e_gx2, e_gy2, e_gw2, e_cell2, e_fpos, e_vis, e_twk, e_fwk;
     dbuf<u32> e_rst2[18];
     dbuf<u32> e_ivmin[MAX_LV], e_ivminL[MAX_LV];  // sparse-table minima of the SA / PA adjacent LCEs (interval ends)
     dbuf<u64> e_kSA, e_kPA;                      // 16-byte context keys by SA / PA rank
