@@ -66,6 +66,47 @@ void engine::destroy() {
 // (approximate/factorize/skip_gaps.cpp:31-61): {beg of the first phrase, 0}, then
 // per phrase {src, len} followed by {gap length, 0} when the next phrase (or the
 // sentinel {n, n+1, 0}) starts after its end
+struct fill_batch {
+    u8* p[engine::FILL_MAX];
+    u64 bytes[engine::FILL_MAX];
+    u32 pat[engine::FILL_MAX];
+};
+// blockIdx.y = the fill; 32-bit stores over the aligned words, then the tail bytes
+__global__ void k_fills(fill_batch B) {
+    const u32 f = blockIdx.y;
+    u8* p = B.p[f];
+    const u64 nb = B.bytes[f];
+    const u32 pat = B.pat[f];
+    const u64 head = ((4 - ((uintptr_t)p & 3)) & 3) < nb ? ((4 - ((uintptr_t)p & 3)) & 3) : nb;
+    const u64 nw = (nb - head) / 4;
+    const u64 t0 = (u64)blockIdx.x * blockDim.x + threadIdx.x, str = (u64)gridDim.x * blockDim.x;
+    u32* w = (u32*)(p + head);
+    const u32 rot = 8 * (u32)(((uintptr_t)p + head) & 3);  // (0: the words are aligned)
+    const u32 wp = rot ? (pat >> rot) | (pat << (32 - rot)) : pat;
+    for (u64 k = t0; k < nw; k += str) w[k] = wp;
+    if (t0 < head) p[t0] = (u8)(pat >> (8 * ((uintptr_t)(p + t0) & 3)));
+    const u64 tail0 = head + 4 * nw;
+    if (t0 < nb - tail0) p[tail0 + t0] = (u8)(pat >> (8 * ((uintptr_t)(p + tail0 + t0) & 3)));
+}
+void engine::fills(std::initializer_list<fill_op> ops) {
+    fill_batch B{};
+    u32 nf = 0;
+    u64 wmax = 0;
+    for (const fill_op& o : ops) {
+        if (!o.bytes || !o.p) continue;
+        if (nf == (u32)FILL_MAX) throw error(LZ77SSS_EINTERNAL, "fills: too many");
+        B.p[nf] = (u8*)o.p;
+        B.bytes[nf] = o.bytes;
+        B.pat[nf] = o.pat;
+        wmax = std::max<u64>(wmax, o.bytes / 4 + 4);
+        nf++;
+    }
+    if (!nf) return;
+    const u32 gx = (u32)std::min<u64>(std::max<u64>(1, cdiv(wmax, 256)), 2048);
+    k_fills<<<dim3(gx, nf), 256, 0, st>>>(B);
+    LZ_HIP(hipGetLastError());
+}
+
 __global__ void k_skip_counts(const pos_t* __restrict__ P, u32 m, u32* __restrict__ cnt) {
     const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m) return;

@@ -2343,8 +2343,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
         u32* bmT = g_bmT.get(nw);
         // the superset goes straight into Ib (the first base set); the scratch bitmap is
         // always fully overwritten before it is read
-        LZ_HIP(hipMemsetAsync(bmI, 0, nw * 4, st));
-        LZ_HIP(hipMemsetAsync(bmIb, 0, nw * 4, st));
+        fills({{bmI, nw * 4, 0u}, {bmIb, nw * 4, 0u}});
         if (nseg0)
             k_gap_bitmaps<<<capped_grid((u64)nseg0 * 64, 256), 256, 0, st>>>(S, nseg0, N, G.nt, hi_ins, off, bmI, bmIb);
         k_gap_bitmaps_phr<<<cdiv(m + 1, 256), 256, 0, st>>>(P, m, N, G.nt, a, hi_ins, off, bmI, bmIb);
@@ -2561,19 +2560,18 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
             pos_t* ipos = ipos_buf.get(nb + 1);
             u32* pred5 = occ_buf.get(ne5 + 1);
             u8* rem = rem_buf.get(nb + 1);
-            LZ_HIP(hipMemsetAsync(rem, 0, nb + 1, st));
             bool dense = false, ls = false;
             u32 D = 0, dense_bits = 0;
             const u64 npw = ((u64)nslots + 31) / 32;
             u32* pbm = g_pbm.get(npw + 1);
             u32* pwp = g_pwp.get(npw + 1);
+            // distinct slots -> dense ids when that saves radix passes (tried below 2^28 entries:
+            // a base set that large comes from a non-repetitive text, whose slots are all in use);
+            // k_slots marks the present slots
+            const bool try_dense = nch && ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE");
+            u8* pf = try_dense ? (u8*)g_pflag.get(npw * 8) : nullptr;
+            fills({{rem, nb + 1, 0u}, {pf, pf ? npw * 32 : 0, 0u}});
             if (nch) {
-                // distinct slots -> dense ids when that saves radix passes
-                // (tried below 2^28 entries: a base set that large comes from a non-repetitive
-                // text, whose slots are all in use); k_slots marks the present slots
-                const bool try_dense = ne5 < (1ull << 28) && !std::getenv("LZ77SSS_NO_DENSE");
-                u8* pf = try_dense ? (u8*)g_pflag.get(npw * 8) : nullptr;
-                if (pf) LZ_HIP(hipMemsetAsync(pf, 0, npw * 32, st));
                 k_slots<<<cdiv(nch, SL_CH), SL_T, 0, st>>>(T, G, ch, nch, keys, nullptr, ipos, pf);
                 lap("base slots");
                 if (try_dense) {
@@ -2592,8 +2590,7 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                 ls = dense && !W.use_pred && !std::getenv("LZ77SSS_NO_LSD");
                 if (ls) {
                     u32* dstart = g_dstart.get((u64)D + 2);
-                    LZ_HIP(hipMemsetAsync(dstart, 0xFF, (u64)D * 4, st));
-                    k_set_u32x2<<<1, 1, 0, st>>>(dstart + D, (u32)ne5, 0u);
+                    fills({{dstart, (u64)D * 4, ~0u}, {dstart + D, 4, (u32)ne5}, {dstart + D + 1, 4, 0u}});
                     u64* pbw = (u64*)g_pbw.get(2 * npw);
                     k_pack_pbw<<<cdiv(npw, 256), 256, 0, st>>>(pbm, pwp, npw, pbw);
                     lsd_sort(ls_dense{keys, pbw}, ne5, dense_bits, skeys, vals, svals, dstart, D);
@@ -2945,18 +2942,16 @@ u64 engine::factorize_greedy(const u8* T, u32 rk_seed, int log2_override, greedy
                     fact.get(2 * chain_fact + 2);
                 }
                 // ---- the insert set the chain actually produced vs the speculation
-                LZ_HIP(hipMemsetAsync(bmI2, 0, nw * 4, st));
                 const bool fast = I_fresh && !std::getenv("LZ77SSS_NO_FAST_CHECK");
-                if (fast) LZ_HIP(hipMemsetAsync(i_cnt, 0, 8, st));
+                // a long gap is walked by one wave: with few chain nodes, the long ranges go to the
+                // whole grid instead
+                constexpr u32 LNG_CAP = 1024;
+                u32* lng = nchain ? (u32*)g_lng.get(2 + 4 * LNG_CAP) : nullptr;
+                fills({{bmI2, nw * 4, 0u}, {fast ? i_cnt : nullptr, 8, 0u}, {lng, 8, 0u}});
                 if (nchain) {
-                    // a long gap is walked by one wave: with few chain nodes, the long ranges go to the
-                    // whole grid instead
-                    constexpr u32 LNG_CAP = 1024;
                     // test knobs: a small list and a short "long" range make the overflow path run
                     const u32 lng_cap = std::min(LNG_CAP, knob_lng_cap);
                     const u32 long_words = knob_long_words;
-                    u32* lng = (u32*)g_lng.get(2 + 4 * LNG_CAP);
-                    LZ_HIP(hipMemsetAsync(lng, 0, 8, st));
                     k_chain_inserts<<<capped_grid((u64)nchain * 64, 256), 256, 0, st>>>(S, chain, nchain, hi_ins, off, bmI2,
                                                                                      bmI, fast ? i_cnt : nullptr, long_words,
                                                                                      lng, lng_cap);

@@ -430,11 +430,11 @@ void engine::build_lpf_opt(const u8* T) {
     jump_levels_build(st, m, T_lv, jump);
     u32* C = u32a.get(4ull << T_lv);
     u32* C2 = u32b.get(4ull << T_lv);
-    LZ_HIP(hipMemsetAsync(C, 0, 4, st));
+    u32* mark = u32c.get(s);
+    u64* acc = counters64.get(16) + 2;  // [2] total length, [3] gaps, [4] m (factorize_greedy's slots)
+    fills({{C, 4, 0u}, {mark, (u64)s * 4, 0u}, {acc, 16, 0u}});  // (none is read before its use below)
     C = path_expand(st, T_lv, jump, C, C2);
     const u32 cnt = 1u << T_lv;
-    u32* mark = u32c.get(s);
-    LZ_HIP(hipMemsetAsync(mark, 0, (size_t)s * 4, st));
     k_mark<<<cdiv(cnt, 256), 256, 0, st>>>(C, cnt, s, mark);
     drop(PSV, NSV, u32a, u32b);
     for (auto& b : jump) drop(b);
@@ -453,8 +453,6 @@ void engine::build_lpf_opt(const u8* T) {
     // one pass and one host read (the emitter reuses them: phr_info)
     pos_t* out = lpf.get((u64)(s + 1) * 3);
     k_compact3<<<g, 256, 0, st>>>(ph3, push, off, s, out);
-    u64* acc = counters64.get(16) + 2;  // [2] total length, [3] gaps, [4] m (factorize_greedy's slots)
-    LZ_HIP(hipMemsetAsync(acc, 0, 16, st));
     k_phrase_finish<<<cdiv((u64)s + 1, 256), 256, 0, st>>>(out, push, off, s, (pos_t)n, acc);
     LZ_HIP(hipGetLastError());
     u64 h3[3];

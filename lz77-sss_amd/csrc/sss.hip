@@ -2248,9 +2248,10 @@ void engine::build_sss(const u8* T) {
     pos_t* rlo = run_lo.get(nanch);
     u8* rcap = tmp_bytes.get(nanch);
     u32* ctr = counters.get(16);
-    LZ_HIP(hipMemsetAsync(ctr, 0, 12 * sizeof(u32), st));  // any Q, overflowing stripes, tiles, re-run stripes, any block record, marks needed; 8..11: k_sss_runs counters
-    u32* tot = sss_tot.get(64);  // |S| as 64 partial sums (stripe w adds to w & 63)
-    LZ_HIP(hipMemsetAsync(tot, 0, 64 * sizeof(u32), st));
+    // ctr: any Q, overflowing stripes, tiles, re-run stripes, any block record, marks needed;
+    // 8..11: k_sss_runs counters.  tot: |S| as 64 partial sums (stripe w adds to w & 63)
+    u32* tot = sss_tot.get(64);
+    fills({{ctr, 12 * sizeof(u32), 0u}, {tot, 64 * sizeof(u32), 0u}});
     pos_t* lo = lane_out.get(nlanes * SCAP);
     u32* lc = lane_cnt.get(nlanes + 1);
     u32* lf = lane_flag.get(nlanes);
@@ -2347,8 +2348,7 @@ void engine::build_sss(const u8* T) {
     bool anchors_cleared = false;
     auto clear_anchors = [&]() {
         if (anchors_cleared) return;
-        LZ_HIP(hipMemsetD16Async((hipDeviceptr_t)qi, 0xFF00, nanch + 64, st));
-        LZ_HIP(hipMemsetAsync(rp, 0, nanch, st));
+        fills({{qi, 2 * (nanch + 64), 0xFF00FF00u}, {rp, nanch, 0u}});
         anchors_cleared = true;
     };
     if (need_marks || !runs_kernel) {

@@ -1,6 +1,7 @@
 // engine.h -- the device-resident LZ77-SSS engine (one per session / GPU).
 // Data layout in HBM is documented in DESIGN.md section 5.
 #pragma once
+#include <initializer_list>
 #include "../../include/lz77sss.h"
 #include "lz77sss_internal.h"
 #include "lce_dev.h"
@@ -254,6 +255,14 @@ struct engine {
     u32* h_pin = nullptr;
     hipEvent_t ev_pin[2] = {nullptr, nullptr};
 
+    // several buffer fills in one launch (k_fills, csrc/engine.hip): a rocclr fill costs about 5 us
+    // of launch and gap however small the buffer, and a call has tens of them.  A fill writes the
+    // 32-bit pattern `pat` over `bytes` bytes (a byte value v: pat = v * 0x01010101; 16-bit
+    // patterns repeat in both halves); at most FILL_MAX per launch, in any order (they must not
+    // overlap)
+    struct fill_op { void* p; u64 bytes; u32 pat; };
+    static constexpr int FILL_MAX = 8;
+    void fills(std::initializer_list<fill_op> ops);
     void init(int dev, u64 maxn);
     void load(const u8* h_text, u64 n_);
     void destroy();
