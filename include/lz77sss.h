@@ -119,7 +119,10 @@ int lz77sss_factorize_approx_u64(const uint8_t* text, uint64_t n, const lz77sss_
  * decomposed weighted square grid, and per order keyed insertion ranks over adjacent-LCE
  * and weight sparse tables, which answer every interval query with_samples' interval
  * samples would; lz77_sss.hpp:558-709, transform_to_exact/{naive,with_samples,without_samples}.cpp); their sources are
- * the lighter points the range queries find.  LZ77SSS_TRANSF_FULL_SA computes the
+ * the reference's: of the factors of the final length, the first the transform's visit order
+ * meets, its point from the Pi / Psi scan or the reference's own 16384-rank grid (a source pass
+ * after the chain; with PA / SA ties in sample order, the stable-sort reading of the
+ * reference's ips4o).  LZ77SSS_TRANSF_FULL_SA computes the
  * same lengths from LPF over the full suffix array of the text (csrc/exact.hip; 44 B
  * per character, n < 2^31) with the PSV/NSV source rule.  The sample-index modes require
  * n < 2^32 - 16 and fewer than 2^31 samples (z_aprx + n/delta; LZ77SSS_EINVAL otherwise). */

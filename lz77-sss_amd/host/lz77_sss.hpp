@@ -37,7 +37,7 @@ enum transform_mode { naive, with_samples, without_samples };          // lz77_s
 // path (csrc/smpl.hip) always builds the default, a decomposed static weighted
 // square grid (decomposed_range.hpp:78-166, static_weighted_square_grid.hpp:67-185);
 // the factor lengths are the canonical greedy LZ77 ones whichever structure is
-// named, the sources are the lighter points that grid's queries find.
+// named, the sources those of the default structure's visit order.
 template <typename> struct static_weighted_kd_tree {};
 template <typename> struct static_weighted_square_grid {};
 template <typename> struct static_weighted_striped_square {};
