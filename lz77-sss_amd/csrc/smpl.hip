@@ -1040,9 +1040,38 @@ struct smpl_less {
             if (ca != cb) return ca < cb;
             return a < b;  // equal on cap + 1 characters
         }
-        const u64 l = dev_lce(L, pa, pb);
-        if ((u64)max(pa, pb) + l >= L.n) return pa > pb;
-        return L.T[pa + l] < L.T[pb + l];
+        return suffix_less(pa, pb);
+    }
+    // the suffix order of two text positions (dev_lce's cases): when both meet their next sync
+    // positions at the same offset d with equal text before them, the order is that of the sync
+    // suffixes (ISA), with no LCP range minimum and no text read after it
+    __device__ bool suffix_less(u64 i, u64 j) const {
+        const u64 l = min(i, j), r = max(i, j);
+        const u64 lmax = L.n - r, local = min<u64>(64, lmax);
+        u64 c = dev_naive_lce(L.T, l, r, local);
+        if (c < local || c == lmax) {
+            if (r + c >= L.n) return i > j;
+            return L.T[i + c] < L.T[j + c];
+        }
+        const u32 kl = dev_succ(L, l), kr = dev_succ(L, r);
+        if (kl != L.s && kr != L.s) {
+            const u64 dl = L.S[kl] - l, dr = L.S[kr] - r;
+            if (dl == dr && (sizeof(pos_t) == 4)) {
+                if (dl > c) {
+                    const u64 e = dev_lce_fwd(L.T, L.R, l + c, r + c, dl - c);
+                    if (e < dl - c) {
+                        const u64 m = c + e;
+                        return L.T[i + m] < L.T[j + m];
+                    }
+                }
+                // equal up to the sync positions S[kl] = l + d, S[kr] = r + d
+                const u32 a = L.ISA[kl], b = L.ISA[kr];
+                return (i == l) ? a < b : b < a;
+            }
+        }
+        const u64 e = dev_lce(L, i, j);
+        if (r + e >= L.n) return i > j;
+        return L.T[i + e] < L.T[j + e];
     }
 };
 __global__ void k_rank_of(const u32* __restrict__ X, u32 c, u32* __restrict__ R) {
